@@ -1,0 +1,276 @@
+"""Plain-PyTorch CPU restatement of SevenNet-0 energy/force/stress.
+
+TEST INFRASTRUCTURE ONLY -- see oracle/__init__.py.  Never imported by the
+product package.
+
+Follows the reference modules in pipeline order (sevenn/model_build.py:186-445
+assembles them; deploy.py:20-32 prepends EdgePreprocess and swaps in
+ForceStressOutput for the serial deployment):
+
+  EdgePreprocess            sevenn/nn/edge_embedding.py:24-77
+  EdgeEmbedding             sevenn/nn/edge_embedding.py:220-230
+    BesselBasis             :114-116   XPLORCutoff :163-173
+    SphericalEncoding       :177-198   (e3nn SH, component norm, normalize)
+  OnehotEmbedding + embed   sevenn/nn/node_embedding.py:39-48, linear.py:37-44
+  per layer t (interaction_blocks.py:22-86):
+    SelfConnectionLinearIntro  self_connection.py:42-62
+    IrrepsLinear si1           linear.py:46-49
+    IrrepsConvolution          convolution.py:36-123 (radial MLP, uvu TP,
+                               scatter-sum over edge_index[0], / denominator)
+    IrrepsLinear si2, SelfConnectionOutro (self_connection.py:106-109)
+    EquivariantGate            equivariant_gate.py:13-61
+  readout linears            model_build.py:374-408
+  SpeciesWiseRescale         scale.py:67-73,  AtomReduce linear.py:76-90
+  ForceStressOutput          force_output.py:74-130
+
+All arithmetic is in ``dtype`` (fp32 by default, fp64 for tight checks).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import torch
+
+from .cg import tp_cg
+
+_ASSETS = os.path.join(os.path.dirname(__file__), '..', 'sevennet_finetuning_amd',
+                       'assets', 'sevennet0')
+
+
+def parse_irreps(s):
+    """'128x0e+64x1e' -> [(128, 0), (64, 1)] (parity is even throughout)."""
+    out = []
+    for term in s.split('+'):
+        mul, ir = term.strip().split('x')
+        assert ir[-1] == 'e', 'SevenNet-0 path is even-parity only'
+        out.append((int(mul), int(ir[:-1])))
+    return out
+
+
+def irreps_dim(irreps):
+    return sum(m * (2 * l + 1) for m, l in irreps)
+
+
+def load_sevennet0(assets=_ASSETS):
+    with open(os.path.join(assets, 'manifest.json')) as f:
+        man = json.load(f)
+    flat = np.fromfile(os.path.join(assets, 'weights.bin'), dtype='<f4')
+    params = {}
+    for t in man['tensors']:
+        a = flat[t['offset']:t['offset'] + t['numel']].reshape(t['shape'])
+        params[t['name']] = a.copy()
+    return man, params
+
+
+# --------------------------------------------------------------- e3nn pieces
+def e3nn_linear(x, irreps_in, irreps_out, w_flat):
+    """e3nn o3.Linear (no bias, 'element' path normalisation).
+
+    Instructions = (i_in, i_out) pairs with equal irrep, in i_in-major order;
+    each weight block is (mul_in, mul_out) row-major in the flat parameter;
+    path weight 1/sqrt(sum of mul_in feeding that i_out) (linear.py:46-49).
+    """
+    n = x.shape[0]
+    ins = [(i, j) for i, (_, li) in enumerate(irreps_in)
+           for j, (_, lo) in enumerate(irreps_out) if li == lo]
+    fan = {j: sum(irreps_in[i][0] for i, jj in ins if jj == j) for _, j in ins}
+    in_off = np.cumsum([0] + [m * (2 * l + 1) for m, l in irreps_in])
+    out_off = np.cumsum([0] + [m * (2 * l + 1) for m, l in irreps_out])
+    outs = [torch.zeros(n, m, 2 * l + 1, dtype=x.dtype) for m, l in irreps_out]
+    woff = 0
+    for i, j in ins:
+        mi, l = irreps_in[i]
+        mo, _ = irreps_out[j]
+        w = torch.as_tensor(w_flat[woff:woff + mi * mo].reshape(mi, mo), dtype=x.dtype)
+        woff += mi * mo
+        xi = x[:, in_off[i]:in_off[i + 1]].reshape(n, mi, 2 * l + 1)
+        outs[j] = outs[j] + torch.einsum('zui,uw->zwi', xi, w) / math.sqrt(fan[j])
+    assert woff == w_flat.size
+    return torch.cat([o.reshape(n, -1) for o in outs], dim=1)
+
+
+def spherical_harmonics_l2(vec):
+    """e3nn SH lmax=2, normalize=True, 'component' (edge_embedding.py:177-198;
+    frozen polynomial in serial_code.py:43-71)."""
+    r = vec.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+    u = vec / r
+    x, y, z = u[:, 0], u[:, 1], u[:, 2]
+    s3 = math.sqrt(3.0)
+    sh = torch.stack([
+        torch.ones_like(x), x, y, z,
+        s3 * x * z, s3 * x * y, y * y - 0.5 * (x * x + z * z), s3 * y * z,
+        0.5 * s3 * (z * z - x * x)], dim=-1)
+    norm = torch.tensor([1.0] + [math.sqrt(3.0)] * 3 + [math.sqrt(5.0)] * 5,
+                        dtype=vec.dtype)
+    return sh * norm
+
+
+def conv_instructions(irreps_x, lmax_out):
+    """IrrepsConvolution.__init__ (convolution.py:72-95) for filter 0e+1e+2e.
+
+    Returns (instructions, irreps_mid_sorted, perm) where instructions are
+    (i_x, l_filter, l_out, mul) in weight order and ``perm[k]`` is the slot
+    of instruction k in the (stable-)sorted mid irreps (convolution.py:82-87).
+    """
+    ins = []
+    for i, (mul, l1) in enumerate(irreps_x):
+        for l2 in range(3):
+            for l3 in range(abs(l1 - l2), l1 + l2 + 1):
+                if l3 <= lmax_out:
+                    ins.append((i, l2, l3, mul))
+    order = sorted(range(len(ins)), key=lambda k: (ins[k][2], k))
+    perm = [0] * len(ins)
+    for slot, k in enumerate(order):
+        perm[k] = slot
+    mid = [(ins[k][3], ins[k][2]) for k in order]
+    return ins, mid, perm
+
+
+class SevenNet0Ref:
+    """Energy/force/stress of SevenNet-0 on one periodic cell."""
+
+    def __init__(self, dtype=torch.float32, assets=_ASSETS):
+        self.man, p = load_sevennet0(assets)
+        self.dtype = dtype
+        self.p = p
+        self.silu_norm = self.man['silu_norm']
+        self.cutoff = self.man['cutoff']
+        self.r_on = self.man['cutoff_function']['cutoff_on']
+        self.irreps = [parse_irreps(s) for s in self.man['irreps_manual']]
+        self.nlayer = self.man['num_convolution_layer']
+        self.symbols = self.man['chemical_symbols']
+
+    def t(self, name):
+        return torch.as_tensor(self.p[name], dtype=self.dtype)
+
+    def act(self, x):
+        return torch.nn.functional.silu(x) * self.silu_norm
+
+    def edge_embedding(self, r):
+        # BesselBasis (edge_embedding.py:114-116) * XPLORCutoff (:163-173)
+        rc, ron = self.cutoff, self.r_on
+        ur = r.unsqueeze(-1)
+        bessel = (2.0 / rc) * torch.sin(self.t('edge_embedding.basis_function.coeffs') * ur) / ur
+        r2 = r * r
+        env = torch.where(r < ron, torch.ones_like(r),
+                          (rc * rc - r2) ** 2 * (rc * rc + 2 * r2 - 3 * ron * ron)
+                          / (rc * rc - ron * ron) ** 3)
+        return bessel * env.unsqueeze(-1)
+
+    def gate_irreps(self, irreps_out):
+        """e3nn Gate.irreps_in = sorted+simplified(scalars + gates + gated)
+        (equivariant_gate.py:48-55): e.g. 224x0e+64x1e+32x2e, the first 128
+        scalars being the activated ones and the next 96 the gates."""
+        scal = [(m, l) for m, l in irreps_out if l == 0]
+        gated = [(m, l) for m, l in irreps_out if l > 0]
+        full = scal + [(m, 0) for m, _ in gated] + gated
+        simp = []
+        for m, l in sorted(full, key=lambda t: t[1]):
+            if simp and simp[-1][1] == l:
+                simp[-1] = (simp[-1][0] + m, l)
+            else:
+                simp.append((m, l))
+        return simp, scal, gated
+
+    def gate(self, x, irreps_out):
+        # e3nn nn.Gate (equivariant_gate.py:59-61; serial_code.py:256-347)
+        gin, scal, gated = self.gate_irreps(irreps_out)
+        n = x.shape[0]
+        ns = sum(m for m, _ in scal)
+        ng = sum(m for m, _ in gated)
+        s = self.act(x[:, :ns])
+        if ng == 0:
+            return s
+        g = self.act(x[:, ns:ns + ng])
+        outs, off, goff = [s], ns + ng, 0
+        for m, l in gated:
+            d = 2 * l + 1
+            blk = x[:, off:off + m * d].reshape(n, m, d)
+            outs.append((g[:, goff:goff + m].unsqueeze(-1) * blk).reshape(n, -1))
+            off += m * d
+            goff += m
+        return torch.cat(outs, dim=1)
+
+    def convolution(self, t, x, emb, sh, edge_src, edge_dst, irreps_x, lmax_out):
+        # IrrepsConvolution.forward (convolution.py:104-123)
+        pre = f'{t}_convolution'
+        h = self.act(emb @ (self.t(f'{pre}.weight_nn.layer0.weight') / math.sqrt(8)))
+        h = self.act(h @ (self.t(f'{pre}.weight_nn.layer1.weight') / 8.0))
+        w = h @ (self.t(f'{pre}.weight_nn.layer2.weight') / 8.0)
+        ins, mid, perm = conv_instructions(irreps_x, lmax_out)
+        xs = x[edge_src]
+        e = xs.shape[0]
+        x_off = np.cumsum([0] + [m * (2 * l + 1) for m, l in irreps_x])
+        sh_off = [0, 1, 4, 9]
+        outs = [None] * len(ins)
+        woff = 0
+        for k, (i, l2, l3, mul) in enumerate(ins):
+            l1 = irreps_x[i][1]
+            xi = xs[:, x_off[i]:x_off[i + 1]].reshape(e, mul, 2 * l1 + 1)
+            y = sh[:, sh_off[l2]:sh_off[l2 + 1]]
+            c = torch.as_tensor(tp_cg(l1, l2, l3), dtype=self.dtype)
+            wk = w[:, woff:woff + mul]
+            woff += mul
+            m = torch.einsum('eui,ej,ijk->euk', xi, y, c) * wk.unsqueeze(-1)
+            outs[perm[k]] = m.reshape(e, -1)
+        msg = torch.cat(outs, dim=1)
+        agg = torch.zeros(x.shape[0], msg.shape[1], dtype=self.dtype)
+        agg = agg.index_add(0, edge_dst, msg)
+        return agg / self.t(f'{pre}.denominator')[0], mid
+
+    def energy(self, pos, types, edge_index, shift, cell, with_stress=True):
+        """Returns dict with E (scalar), atomic_energy [N], and the autograd
+        graph inputs so forces/stress can be taken (force_output.py:74-130)."""
+        dt = self.dtype
+        pos = pos.to(dt)
+        cell = cell.to(dt)
+        strain = torch.zeros(3, 3, dtype=dt, requires_grad=with_stress)
+        sym = 0.5 * (strain + strain.t())
+        pos_s = pos + pos @ sym            # edge_embedding.py:50-60
+        cell_s = cell + cell @ sym
+        src, dst = edge_index[0], edge_index[1]
+        vec = pos_s[dst] - pos_s[src] + shift.to(dt) @ cell_s   # :62-76
+        r = vec.norm(dim=-1)
+        emb = self.edge_embedding(r)
+        sh = spherical_harmonics_l2(vec)
+        n = pos.shape[0]
+        onehot = torch.nn.functional.one_hot(types, len(self.symbols)).to(dt)
+        # embed: weight was divided by its path weight at build (linear.py:37-44)
+        nsp = len(self.symbols)
+        x = (onehot @ self.t('onehot_to_feature_x.linear.weight').reshape(nsp, -1)) \
+            / math.sqrt(nsp)
+        for t in range(self.nlayer):
+            irr_x, irr_out = self.irreps[t], self.irreps[t + 1]
+            last = t == self.nlayer - 1
+            gin, _, _ = self.gate_irreps(irr_out)
+            sc = e3nn_linear(x, irr_x, gin, self.p[f'{t}_self_connection_intro.linear.weight'])
+            h = e3nn_linear(x, irr_x, irr_x, self.p[f'{t}_self_interaction_1.linear.weight'])
+            # convolution uses edge_index[1] as source, [0] as target (convolution.py:111-113)
+            agg, mid = self.convolution(t, h, emb, sh, dst, src, irr_x, 0 if last else 2)
+            y = e3nn_linear(agg, mid, gin, self.p[f'{t}_self_interaction_2.linear.weight']) + sc
+            x = self.gate(y, irr_out)
+        hid = e3nn_linear(x, self.irreps[-1], [(x.shape[1] // 2, 0)],
+                          self.p['reduce_input_to_hidden.linear.weight'])
+        e_s = e3nn_linear(hid, [(hid.shape[1], 0)], [(1, 0)],
+                          self.p['reduce_hidden_to_energy.linear.weight'])
+        scale = self.t('rescale_atomic_energy.scale')[types]
+        shift_e = self.t('rescale_atomic_energy.shift')[types]
+        atomic = e_s[:, 0] * scale + shift_e
+        return {'energy': atomic.sum(), 'atomic_energy': atomic, 'pos': pos,
+                'strain': strain, 'edge_vec': vec}
+
+    def __call__(self, pos, types, edge_index, shift, cell, with_stress=True):
+        pos = pos.detach().to(self.dtype).requires_grad_(True)
+        out = self.energy(pos, types, edge_index, shift, cell, with_stress)
+        wrt = [pos, out['strain']] if with_stress else [pos]
+        grads = torch.autograd.grad(out['energy'], wrt, allow_unused=True)
+        res = {'energy': out['energy'].detach(),
+               'atomic_energy': out['atomic_energy'].detach(),
+               'forces': -grads[0]}
+        if with_stress:
+            vol = torch.abs(torch.det(cell.to(self.dtype)))
+            s = -grads[1] / vol
+            res['stress'] = torch.stack([s[0, 0], s[1, 1], s[2, 2],
+                                         s[0, 1], s[1, 2], s[0, 2]])
+        return res
