@@ -1,0 +1,192 @@
+"""Benchmark: atoms/s of one SevenNet-0 energy+force(+virial) evaluation.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` prints ONE
+JSON line on rank 0.  A step = one full evaluation through the C ABI
+(graph indices + edge embedding + 5 interaction blocks + readout + the
+complete force/virial backward) of a synthetic periodic Si diamond box
+(a = 5.43 A, 23^3 conventional cells = 97,336 atoms,
+default_rng(0) N(0, 0.05 A) displacements, rc = 5 A, 2,725,408 edges), with
+the inputs already resident in HBM.  Neighbour list built once on the host
+before timing ("graph prebuilt").
+
+N > 1: one process per GPU (torchrun); every rank evaluates its own 97k-atom
+box -- weak scaling with no collective on the data path (round-1 scope; the
+spatial decomposition with RCCL halo exchange lives in parallel.py).
+The timed region is bracketed by barrier + synchronize; the max over ranks
+is reported and value = total atoms / that time.
+
+Also reported: ``roofline`` for the dominant kernel class (HIP-event timed
+inside the library, on the stream the kernels run on) and ``cpu_baseline``
+(the oracle CPU restatement timed on this host on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 matrix = vector peak (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--cells', type=int, default=23, help='n for an n^3 conventional-cell box')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=15.0)
+    ap.add_argument('--profile-only', action='store_true',
+                    help='warmup + steps only, no stats pass (for rocprofv3)')
+    return ap.parse_args()
+
+
+def make_box(cells, device):
+    from sevennet_finetuning_amd.neighbor import neighbor_list
+    from sevennet_finetuning_amd.structures import si_diamond
+    pos, cell = si_diamond((cells,) * 3, sigma=0.05)
+    ei, sh = neighbor_list(pos, cell, 5.0)
+    vec = pos[ei[1]] + sh @ cell - pos[ei[0]]
+    return {
+        'n': len(pos), 'E': ei.shape[1],
+        'types': torch.full((len(pos),), 69, dtype=torch.int32, device=device),  # Si
+        'center': torch.tensor(ei[0], dtype=torch.int32, device=device),
+        'nbr': torch.tensor(ei[1], dtype=torch.int32, device=device),
+        'vec': torch.tensor(vec, dtype=torch.float32, device=device),
+    }
+
+
+def cpu_baseline(seconds):
+    """Oracle (plain-PyTorch CPU restatement of the reference) on a bounded
+    sample: 216-atom Si box (3x3x3 cells, same recipe), repeated until
+    ~`seconds` of CPU work, all host threads."""
+    from oracle.neighbor import neighbor_list
+    from oracle.sevennet_ref import SevenNet0Ref
+    from sevennet_finetuning_amd.structures import si_diamond
+    threads = len(os.sched_getaffinity(0))
+    torch.set_num_threads(threads)
+    ref = SevenNet0Ref(dtype=torch.float32)
+    pos, cell = si_diamond((3, 3, 3), sigma=0.05)
+    ei, sh = neighbor_list(pos, cell, 5.0)
+    args = (torch.tensor(pos, dtype=torch.float32), torch.full((len(pos),), 69),
+            torch.tensor(ei), torch.tensor(sh, dtype=torch.float32),
+            torch.tensor(cell, dtype=torch.float32))
+    ref(*args)  # warm
+    t0, n = time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        ref(*args)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {'value': round(n * len(pos) / dt, 2), 'unit': 'atoms/s', 'cores': threads,
+            'kind': 'port',
+            'sample': f'{n} energy+force+stress evals of a 216-atom Si box (3x3x3 cells, '
+                      f'6048 edges) in {dt:.1f} s, oracle/sevennet_ref.py fp32, torch CPU'}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    device = torch.device('cuda', local if world > 1 else 0)
+    torch.cuda.set_device(device)
+
+    from sevennet_finetuning_amd.model import E3GNNModel
+    model = E3GNNModel(device=device)
+    box = make_box(args.cells, device)
+    n, E = box['n'], box['E']
+
+    def step():
+        return model.energy_forces(box['types'], box['center'], box['nbr'], box['vec'])
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t)
+    ms = dt / args.steps * 1e3
+    value = world * n * args.steps / dt
+    energy = float(out['energy'])
+
+    roofline, kernels = None, None
+    if not args.profile_only:
+        model.set_timing(True)
+        model.reset_stats()
+        step()
+        stats = model.kernel_stats()
+        model.set_timing(False)
+        total = sum(s['ms'] for s in stats.values())
+        kernels = {k: {'ms': round(v['ms'], 3), 'launches': v['launches'],
+                       'tflops': round(v['flops'] / (v['ms'] * 1e9), 2) if v['ms'] else 0.0,
+                       'gbs': round(v['bytes'] / (v['ms'] * 1e6), 1) if v['ms'] else 0.0}
+                   for k, v in stats.items() if v['launches']}
+        dom = max(stats, key=lambda k: stats[k]['ms'])
+        d = stats[dom]
+        if d['flops'] > 0:
+            ach = d['flops'] / (d['ms'] * 1e9)
+            roofline = {'bound': 'mfma', 'kernel': dom, 'achieved': round(ach, 3),
+                        'peak': PEAK_FP32_TFLOPS, 'unit': 'TFLOP/s',
+                        'frac': round(ach / PEAK_FP32_TFLOPS, 4), 'traffic': None,
+                        'ms_per_launch': round(d['ms'] / d['launches'], 4),
+                        'share_of_step': round(d['ms'] / total, 3)}
+        else:
+            ach = d['bytes'] / (d['ms'] * 1e6)
+            roofline = {'bound': 'hbm', 'kernel': dom, 'achieved': round(ach, 1),
+                        'peak': PEAK_HBM_GBS, 'unit': 'GB/s', 'frac': round(ach / PEAK_HBM_GBS, 4),
+                        'traffic': None, 'ms_per_launch': round(d['ms'] / d['launches'], 4),
+                        'share_of_step': round(d['ms'] / total, 3)}
+        tot_flops = sum(v['flops'] for v in stats.values())
+        roofline['step_tflops'] = round(tot_flops / (ms * 1e9), 3)
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline and world == 1 and not args.profile_only:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            'metric': 'atoms/sec energy+force, SevenNet-0 lmax=2, 100k-atom box',
+            'value': round(value, 2), 'unit': 'atoms/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+            'data': 'synthetic Si diamond box, default_rng(0) 0.05 A displacements; '
+                    'SevenNet-0 weights (reference opt_params_sevenn.pt)',
+            'config': {'workload': f'SevenNet-0 energy+force+virial, {n}-atom periodic Si box '
+                                   f'({args.cells}^3 cells), {E} edges per rank',
+                       'atoms_per_rank': n, 'edges_per_rank': E,
+                       'parallelism': f'replicas x{world}' if world > 1 else 'single'},
+            'energy': energy,
+            'roofline': roofline,
+            'cpu_baseline': cpu,
+            'kernels': kernels,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,140 @@
+/*
+ * e3gnn.h -- C ABI of the MI355X-native SevenNet-0 energy/force library
+ * (libe3gnn_hip.so, built from sevennet_finetuning_amd/csrc/ for gfx950).
+ *
+ * This is the drop-in boundary for the reference's message-passing hot path.
+ * Every entry point names the reference interface it replaces:
+ *
+ *   reference (kskjs1203/SevenNet_finetuning)                      here
+ *   -----------------------------------------------------------   -------------------------
+ *   torch::jit::load(model.pt, _extra_files)                        e3gnn_load
+ *     pair_e3gnn.cpp:294-386 (coeff), deploy.py:15-51
+ *   model.forward(dict) + autograd forces/stress                    e3gnn_energy_forces
+ *     pair_e3gnn.cpp:205-256, force_output.py:74-130,
+ *     sevennet_calculator.py:119-157
+ *   segment forward model_list[i].forward(dict)                    e3gnn_graph_set +
+ *     pair_e3gnn_parallel.cpp:347-403                                e3gnn_layer_forward
+ *   inferred_total_energy / atomic_energy of the last segment        e3gnn_readout
+ *   torch::autograd::grad per segment                               e3gnn_layer_backward
+ *     pair_e3gnn_parallel.cpp:417-454
+ *   force/virial scatter of dE_dr                                   e3gnn_forces
+ *     pair_e3gnn_parallel.cpp:474-519
+ *   pack/unpack_{forward,reverse}_comm_gnn                          e3gnn_halo_pack/_unpack
+ *     pair_e3gnn_parallel.cpp:803-933
+ *   error->all(FLERR, msg)                                           return code +
+ *                                                                    e3gnn_last_error()
+ *
+ * Conventions (bit-for-bit those of the reference):
+ *   edge_center = edge_index[0] (aggregation target), sorted non-decreasing;
+ *   edge_nbr    = edge_index[1] (gathered source);
+ *   edge_vec    = x_j - x_i (+ periodic image), E x 3 fp32;
+ *   F_i += dE/dr_ij, F_j -= dE/dr_ij;
+ *   virial6 = -dE/dstrain = inferred_stress * volume, order (xx, yy, zz, xy, yz, zx);
+ *     LAMMPS order (xx,yy,zz,xy,xz,yz) is virial6[0,1,2,3,5,4] (pair_e3gnn.cpp:250-255).
+ *
+ * Memory: every array argument is caller-owned DEVICE memory of the model's
+ * device unless stated; the library owns its workspaces (grow-only).  Calls
+ * are asynchronous on `stream` (a hipStream_t; NULL = default stream) except
+ * where noted.  A context is not thread-safe; use one per host thread.
+ * Return value: 0 on success, else a nonzero E3GNN_ERR_* code with a message
+ * in e3gnn_last_error() (thread-local).
+ */
+#ifndef E3GNN_H_
+#define E3GNN_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define E3GNN_OK 0
+#define E3GNN_ERR_ARG 1   /* bad argument / shape */
+#define E3GNN_ERR_HIP 2   /* HIP runtime error */
+#define E3GNN_ERR_IO 3    /* model files */
+#define E3GNN_ERR_GRAPH 4 /* unsorted edge_center, index or species out of range */
+
+typedef struct e3gnn_model e3gnn_model;
+typedef struct e3gnn_ctx e3gnn_ctx;
+
+const char* e3gnn_last_error(void);
+int e3gnn_abi_version(void);
+
+/* Load weights.bin + manifest.json (this build's deploy format; replaces the
+ * TorchScript archive + _extra_files, deploy.py:34-51) onto HIP device
+ * `device`.  Returns NULL on failure. */
+e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int device);
+void e3gnn_free(e3gnn_model* m);
+/* _extra_files metadata: num_species, cutoff, number of interaction layers,
+ * comm_size (features exchanged per ghost atom between layers). */
+int e3gnn_model_info(const e3gnn_model* m, int* num_species, float* cutoff, int* num_layers,
+                     int* comm_size);
+
+e3gnn_ctx* e3gnn_ctx_create(e3gnn_model* m);
+void e3gnn_ctx_free(e3gnn_ctx* c);
+
+/* Whole energy+force(+virial) evaluation of one graph (serial pair_e3gnn /
+ * deployed_serial.pt).  type[n_atoms] (species index), edge_center/edge_nbr[E]
+ * int32, edge_vec[E*3].  Outputs (each nullable except energy): energy[1],
+ * atomic_energy[n_atoms], forces[n_atoms*3], virial6[6], edge_grad[E*3] =
+ * dE/dedge_vec.  Synchronises `stream` before returning. */
+int e3gnn_energy_forces(e3gnn_ctx* c, int64_t n_atoms, int64_t n_edges, const int32_t* type,
+                        const int32_t* edge_center, const int32_t* edge_nbr,
+                        const float* edge_vec, float* energy, float* atomic_energy,
+                        float* forces, float* virial6, float* edge_grad, void* stream);
+
+/* ---- segment API (pair_e3gnn_parallel): one rank's local + ghost graph ---- */
+/* Nodes [0, n_local) are owned (edge centres), [n_local, n_local+n_ghost) are
+ * ghosts.  Copies the inputs (device or host pointers), builds the CSR
+ * indices, edge embedding and layer-0 features.  Synchronises `stream` to
+ * validate the graph. */
+int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_edges,
+                    const int32_t* type, const int32_t* edge_center, const int32_t* edge_nbr,
+                    const float* edge_vec, void* stream);
+/* Interaction block `layer` (0..num_layers-1): reads features of layer
+ * `layer` on all n_local+n_ghost rows, writes features of layer+1 on the
+ * n_local owned rows (ghost rows are the caller's halo exchange). */
+int e3gnn_layer_forward(e3gnn_ctx* c, int layer, void* stream);
+/* Device pointer / row width of the features entering layer `layer`
+ * (0..num_layers); rows are n_local+n_ghost, contiguous, fp32. */
+float* e3gnn_feature_ptr(e3gnn_ctx* c, int layer);
+int e3gnn_feature_dim(const e3gnn_ctx* c, int layer);
+/* Readout of the owned atoms; energy[1] and atomic_energy[n_local] (nullable)
+ * receive the rank-local totals.  Also seeds the backward pass. */
+int e3gnn_readout(e3gnn_ctx* c, float* energy, float* atomic_energy, void* stream);
+/* Backward of block `layer` (num_layers-1 down to 0): reads dE/dfeatures of
+ * layer+1 on owned rows, writes dE/dfeatures of `layer` on all rows (ghost
+ * rows are the caller's reverse halo exchange, to be accumulated into the
+ * owners' rows before the next call). */
+int e3gnn_layer_backward(e3gnn_ctx* c, int layer, void* stream);
+float* e3gnn_grad_ptr(e3gnn_ctx* c, int layer);
+/* Forces on all n_local+n_ghost rows (ghost rows: reverse-communicate),
+ * rank-local virial6 and optional edge_grad[E*3]. */
+int e3gnn_forces(e3gnn_ctx* c, float* forces, float* virial6, float* edge_grad, void* stream);
+
+/* ---- halo kernels ---- */
+/* dst[r*dim + k] = src[idx[r]*src_stride + k], r < n */
+int e3gnn_halo_pack(const int32_t* idx, int64_t n, int dim, const float* src, int64_t src_stride,
+                    float* dst, void* stream);
+/* dst[idx[r]*dst_stride + k] (+)= src[r*dim + k]; idx entries must be unique */
+int e3gnn_halo_unpack(const int32_t* idx, int64_t n, int dim, const float* src, float* dst,
+                      int64_t dst_stride, int accumulate, void* stream);
+
+/* ---- diagnostics ---- */
+/* enable per-kernel-class HIP-event timing on the context */
+int e3gnn_set_timing(e3gnn_ctx* c, int enable);
+/* Number of kernel classes recorded; fills up to `max` entries: name (static
+ * string), total ms, launches, algorithmic FLOP and algorithmic HBM bytes. */
+int e3gnn_kernel_stats(e3gnn_ctx* c, const char** names, double* ms, int64_t* launches,
+                       double* flops, double* bytes, int max);
+int e3gnn_reset_stats(e3gnn_ctx* c);
+/* Dense coupling table C_{l1 l2 l3}[m1][m2][m3] * sqrt(2 l3 + 1) used by the
+ * kernels (host memory, (2l1+1)(2l2+1)(2l3+1) floats). */
+int e3gnn_cg_table(int l1, int l2, int l3, float* out);
+/* Bytes of device workspace currently held by the context. */
+int64_t e3gnn_workspace_bytes(const e3gnn_ctx* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* E3GNN_H_ */

@@ -219,9 +219,11 @@ class SevenNet0Ref:
         agg = agg.index_add(0, edge_dst, msg)
         return agg / self.t(f'{pre}.denominator')[0], mid
 
-    def energy(self, pos, types, edge_index, shift, cell, with_stress=True):
+    def energy(self, pos, types, edge_index, shift, cell, with_stress=True, trace=None):
         """Returns dict with E (scalar), atomic_energy [N], and the autograd
-        graph inputs so forces/stress can be taken (force_output.py:74-130)."""
+        graph inputs so forces/stress can be taken (force_output.py:74-130).
+        ``trace``: optional list receiving the node features after each
+        interaction block (layer-wise known answers for the HIP kernels)."""
         dt = self.dtype
         pos = pos.to(dt)
         cell = cell.to(dt)
@@ -250,6 +252,8 @@ class SevenNet0Ref:
             agg, mid = self.convolution(t, h, emb, sh, dst, src, irr_x, 0 if last else 2)
             y = e3nn_linear(agg, mid, gin, self.p[f'{t}_self_interaction_2.linear.weight']) + sc
             x = self.gate(y, irr_out)
+            if trace is not None:
+                trace.append(x)
         hid = e3nn_linear(x, self.irreps[-1], [(x.shape[1] // 2, 0)],
                           self.p['reduce_input_to_hidden.linear.weight'])
         e_s = e3nn_linear(hid, [(hid.shape[1], 0)], [(1, 0)],

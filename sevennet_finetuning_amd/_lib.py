@@ -1,0 +1,94 @@
+"""ctypes binding of libe3gnn_hip.so (the C ABI declared in include/e3gnn.h).
+
+This module is the only door from Python into the HIP path.  There is no
+fallback: if the library is missing or cannot be loaded, every entry point
+raises ``E3GNNError`` (build it with ``python -m sevennet_finetuning_amd.build_lib``).
+"""
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libe3gnn_hip.so')
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), 'include', 'e3gnn.h')
+
+_c_int, _c_i64, _c_f, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+_cp = ctypes.c_char_p
+_P = ctypes.POINTER
+
+# name -> (restype, argtypes); pointers to device memory are passed as void*
+SIGNATURES = {
+    'e3gnn_last_error': (_cp, []),
+    'e3gnn_abi_version': (_c_int, []),
+    'e3gnn_load': (_vp, [_cp, _cp, _c_int]),
+    'e3gnn_free': (None, [_vp]),
+    'e3gnn_model_info': (_c_int, [_vp, _P(_c_int), _P(_c_f), _P(_c_int), _P(_c_int)]),
+    'e3gnn_ctx_create': (_vp, [_vp]),
+    'e3gnn_ctx_free': (None, [_vp]),
+    'e3gnn_energy_forces': (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                     _vp, _vp, _vp]),
+    'e3gnn_graph_set': (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),
+    'e3gnn_layer_forward': (_c_int, [_vp, _c_int, _vp]),
+    'e3gnn_feature_ptr': (_vp, [_vp, _c_int]),
+    'e3gnn_feature_dim': (_c_int, [_vp, _c_int]),
+    'e3gnn_readout': (_c_int, [_vp, _vp, _vp, _vp]),
+    'e3gnn_layer_backward': (_c_int, [_vp, _c_int, _vp]),
+    'e3gnn_grad_ptr': (_vp, [_vp, _c_int]),
+    'e3gnn_forces': (_c_int, [_vp, _vp, _vp, _vp, _vp]),
+    'e3gnn_halo_pack': (_c_int, [_vp, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
+    'e3gnn_halo_unpack': (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_i64, _c_int, _vp]),
+    'e3gnn_set_timing': (_c_int, [_vp, _c_int]),
+    'e3gnn_kernel_stats': (_c_int, [_vp, _P(_cp), _P(ctypes.c_double), _P(_c_i64),
+                                    _P(ctypes.c_double), _P(ctypes.c_double), _c_int]),
+    'e3gnn_reset_stats': (_c_int, [_vp]),
+    'e3gnn_cg_table': (_c_int, [_c_int, _c_int, _c_int, _P(_c_f)]),
+    'e3gnn_workspace_bytes': (_c_i64, [_vp]),
+}
+
+
+class E3GNNError(RuntimeError):
+    """Error raised by the HIP library (maps the reference's error->all)."""
+
+
+_lib = None
+
+
+def header_symbols(path=HEADER_PATH):
+    """Function names declared in include/e3gnn.h."""
+    text = open(path).read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    return sorted(set(re.findall(r'\b(e3gnn_[a-z0-9_]+)\s*\(', text)))
+
+
+def load():
+    """Load (once) and return the configured ctypes library."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise E3GNNError(f'{LIB_PATH} is missing: the HIP path is not built '
+                         '(python -m sevennet_finetuning_amd.build_lib); there is no CPU fallback')
+    # torch's wheel bundles a HIP runtime with the same SONAME
+    # (libamdhip64.so.7); importing torch first makes the library bind to
+    # that one copy, so torch's device pointers and streams are ours too.
+    import torch  # noqa: F401
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        raise E3GNNError(f'e3gnn error {rc}: {load().e3gnn_last_error().decode()}')
+    return rc
+
+
+def cg_table(l1, l2, l3):
+    import numpy as np
+    out = np.zeros((2 * l1 + 1) * (2 * l2 + 1) * (2 * l3 + 1), dtype=np.float32)
+    check(load().e3gnn_cg_table(l1, l2, l3, out.ctypes.data_as(_P(_c_f))))
+    return out.reshape(2 * l1 + 1, 2 * l2 + 1, 2 * l3 + 1)

@@ -1,0 +1,58 @@
+"""Build libe3gnn_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+
+    python -m sevennet_finetuning_amd.build_lib [--force]
+
+The library is the product: the Python surface of this package only loads it
+(``_lib.py``) and fails loudly when it is missing.
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+INCLUDE = os.path.join(os.path.dirname(HERE), 'include')
+LIB = os.path.join(HERE, 'libe3gnn_hip.so')
+OBJDIR = os.path.join(HERE, 'csrc', 'build')
+SOURCES = ['api.cpp', 'gemm.hip', 'tp.hip', 'node.hip']
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', f'-I{INCLUDE}',
+         '-Wall', '-Wno-unused-function']
+
+
+def _deps_mtime():
+    files = [os.path.join(CSRC, f) for f in os.listdir(CSRC)
+             if f.endswith(('.h', '.hip', '.cpp'))]
+    files.append(os.path.join(INCLUDE, 'e3gnn.h'))
+    return max(os.path.getmtime(f) for f in files)
+
+
+def build(force=False, verbose=False):
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():
+        return LIB
+    os.makedirs(OBJDIR, exist_ok=True)
+
+    def compile_one(src):
+        obj = os.path.join(OBJDIR, src + '.o')
+        cmd = [HIPCC, *FLAGS, '-c', os.path.join(CSRC, src), '-o', obj]
+        if verbose:
+            print(' '.join(cmd))
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f'hipcc failed on {src}:\n{r.stdout}\n{r.stderr}')
+        return obj
+
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = LIB + '.tmp'
+    cmd = [HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', tmp, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f'link failed:\n{r.stdout}\n{r.stderr}')
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == '__main__':
+    print(build(force='--force' in sys.argv, verbose=True))

@@ -1,0 +1,983 @@
+// Host side of libe3gnn_hip.so: model loading (this build's deploy format),
+// workspace management and the per-layer orchestration of the SevenNet-0
+// energy + force evaluation, behind the C ABI of include/e3gnn.h.
+//
+// Pipeline (sevenn/model_build.py:186-445; deploy.py:20-32 for the serial
+// deployment, model_build.py:103-182 for the parallel segments):
+//   edge embedding -> onehot embed -> 5 x [self_connection_intro,
+//   self_interaction_1, IrrepsConvolution, self_interaction_2,
+//   self_connection_outro, gate] -> readout -> SpeciesWiseRescale -> sum
+// and the reverse-mode pass that ForceStressOutput gets from autograd
+// (force_output.py:74-130), written out explicitly.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/e3gnn.h"
+#include "cg_tables.h"
+#include "common.h"
+#include "minijson.h"
+#include "node.h"
+#include "tp.h"
+
+using namespace e3gnn;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess)                                                                     \
+      return fail(E3GNN_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));         \
+  } while (0)
+
+// ------------------------------------------------------------ irreps helpers
+struct Irr {
+  int mul, l;
+};
+using Irreps = std::vector<Irr>;
+
+Irreps parse_irreps(const std::string& s) {
+  Irreps out;
+  std::stringstream ss(s);
+  std::string term;
+  while (std::getline(ss, term, '+')) {
+    const auto x = term.find('x');
+    out.push_back({std::stoi(term.substr(0, x)), std::stoi(term.substr(x + 1))});
+  }
+  return out;
+}
+int irreps_dim(const Irreps& ir) {
+  int d = 0;
+  for (auto& i : ir) d += i.mul * (2 * i.l + 1);
+  return d;
+}
+// merge consecutive equal-l entries (the layouts are identical, see tp.h)
+Irreps merged(const Irreps& ir) {
+  Irreps out;
+  for (auto& i : ir) {
+    if (!out.empty() && out.back().l == i.l) out.back().mul += i.mul;
+    else out.push_back(i);
+  }
+  return out;
+}
+
+// ------------------------------------------------------------ device buffers
+struct DBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+    }
+    size_t b = bytes < 256 ? 256 : bytes;
+    hipError_t e = hipMalloc(&p, b);
+    if (e == hipSuccess) cap = b;
+    return e;
+  }
+  float* f() const { return (float*)p; }
+  int* i() const { return (int*)p; }
+};
+
+hipError_t upload(DBuf& b, const std::vector<float>& v) {
+  hipError_t e = b.ensure(v.size() * sizeof(float));
+  if (e != hipSuccess) return e;
+  return hipMemcpy(b.p, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice);
+}
+
+// e3nn o3.Linear on merged irreps: one block per l present in both.
+struct LinBlock {
+  int l, K, N, in_off, out_off, w_off, wt_off;
+};
+struct Linear {
+  std::vector<LinBlock> blocks;
+  DBuf W, WT;  // W: per block [K x N] row-major; WT: [N x K]
+  int din = 0, dout = 0;
+};
+
+}  // namespace
+
+// ------------------------------------------------------------ model
+struct e3gnn_model {
+  int device = 0;
+  int nsp = 0, nlayer = 0;
+  float cutoff = 5.f, r_on = 4.5f;
+  std::vector<Irreps> irreps;  // irreps_manual per layer boundary (merged)
+  std::vector<Irreps> gin, mid;
+  std::vector<int> W;          // radial weight numel per layer
+  std::vector<float> denom;
+  DBuf coeffs, embed, readout_v, scale, shift;
+  std::vector<std::unique_ptr<Linear>> sc, si1, si2;
+  struct Mlp {
+    DBuf w0, w1, w2, w0t, w1t, w2t;
+  };
+  std::vector<Mlp> mlp;
+};
+
+namespace {
+
+struct Stat {
+  double ms = 0, flops = 0, bytes = 0;
+  int64_t launches = 0;
+};
+struct Pending {
+  int cls;
+  hipEvent_t a, b;
+  double flops, bytes;
+};
+const char* kClassNames[] = {"graph_build", "edge_embed",  "node_linear", "radial_mlp_fwd",
+                             "tp_fwd",      "gate_fwd",    "readout",     "gate_bwd",
+                             "tp_bwd",      "radial_mlp_bwd", "gather_src", "edge_force",
+                             "atom_force",  "embed"};
+enum Cls {
+  C_GRAPH,
+  C_EMBED_EDGE,
+  C_LINEAR,
+  C_MLP_FWD,
+  C_TP_FWD,
+  C_GATE_FWD,
+  C_READOUT,
+  C_GATE_BWD,
+  C_TP_BWD,
+  C_MLP_BWD,
+  C_GATHER,
+  C_EDGE_FORCE,
+  C_ATOM_FORCE,
+  C_EMBED_NODE,
+  C_NCLS
+};
+
+// algorithmic per-edge FLOP of one TP forward
+double tp_flops_per_edge(int kind) {
+  return kind == 0 ? 3456.0 : (kind == 1 ? 16832.0 : 1184.0);
+}
+
+}  // namespace
+
+struct e3gnn_ctx {
+  e3gnn_model* m;
+  int64_t n = 0, nl = 0, E = 0;
+  // graph
+  DBuf type, center, nbr, vec, row_ptr, src_ptr, src_perm, cnt, err;
+  DBuf Y, emb, dY, demb, fe;
+  // per layer
+  std::vector<DBuf> x, grad, h, y, w, a1, a2;
+  DBuf H1, H2, agg, dw, dxc, dy, dh, eat, part, vpart, scratch6;
+  bool timing = false;
+  Stat stats[C_NCLS];
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> evpool;
+  int readout_done = 0;
+
+  hipEvent_t ev() {
+    if (!evpool.empty()) {
+      hipEvent_t e = evpool.back();
+      evpool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  void flush() {
+    for (auto& p : pending) {
+      (void)hipEventSynchronize(p.b);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, p.a, p.b);
+      stats[p.cls].ms += ms;
+      stats[p.cls].launches += 1;
+      stats[p.cls].flops += p.flops;
+      stats[p.cls].bytes += p.bytes;
+      evpool.push_back(p.a);
+      evpool.push_back(p.b);
+    }
+    pending.clear();
+  }
+  ~e3gnn_ctx() {
+    flush();
+    for (auto e : evpool) (void)hipEventDestroy(e);
+  }
+};
+
+namespace {
+
+// Timed region helper: brackets the enclosed launches with events when timing.
+struct Region {
+  e3gnn_ctx* c;
+  hipStream_t s;
+  int cls;
+  double flops, bytes;
+  hipEvent_t a = nullptr;
+  Region(e3gnn_ctx* c_, hipStream_t s_, int cls_, double f = 0, double b = 0)
+      : c(c_), s(s_), cls(cls_), flops(f), bytes(b) {
+    if (c->timing) {
+      a = c->ev();
+      (void)hipEventRecord(a, s);
+    }
+  }
+  ~Region() {
+    if (c->timing) {
+      hipEvent_t b = c->ev();
+      (void)hipEventRecord(b, s);
+      c->pending.push_back({cls, a, b, flops, bytes});
+    }
+  }
+};
+
+// ------------------------------------------------------------ linear → GEMM problems
+void add_prob(GemmBatch& b, const GemmProb& p) {
+  GemmProb q = p;
+  const int tm = (q.M + 63) / 64, tn = (q.N + 63) / 64;
+  if (tm == 0 || tn == 0) return;
+  q.tiles_n = tn;
+  q.tile_begin = b.total_tiles;
+  b.p[b.nprob++] = q;
+  b.total_tiles += tm * tn;
+}
+
+GemmProb base_prob() {
+  GemmProb p;
+  std::memset(&p, 0, sizeof(p));
+  p.R = 1;
+  return p;
+}
+
+// y[rows, dout] (+)= x[rows, din] @ lin    (row strides lda/ldc)
+GemmBatch lin_fwd(const Linear& L, const float* x, int64_t lda, float* y, int64_t ldc, int64_t rows,
+                  int beta) {
+  GemmBatch b;
+  std::memset(&b, 0, sizeof(b));
+  for (auto& k : L.blocks) {
+    GemmProb p = base_prob();
+    p.A = x;
+    p.B = L.W.f() + k.w_off;
+    p.C = y;
+    p.lda = lda;
+    p.ldc = ldc;
+    p.R = 2 * k.l + 1;
+    p.M = (int)(rows * p.R);
+    p.K = k.K;
+    p.N = k.N;
+    p.a_off = k.in_off;
+    p.c_off = k.out_off;
+    p.ldb = k.N;
+    p.beta = beta;
+    add_prob(b, p);
+  }
+  return b;
+}
+// dx[rows, din] (+)= dy[rows, dout] @ lin^T
+GemmBatch lin_bwd(const Linear& L, const float* dy, int64_t ldy, float* dx, int64_t ldx,
+                  int64_t rows, int beta) {
+  GemmBatch b;
+  std::memset(&b, 0, sizeof(b));
+  for (auto& k : L.blocks) {
+    GemmProb p = base_prob();
+    p.A = dy;
+    p.B = L.WT.f() + k.wt_off;
+    p.C = dx;
+    p.lda = ldy;
+    p.ldc = ldx;
+    p.R = 2 * k.l + 1;
+    p.M = (int)(rows * p.R);
+    p.K = k.N;
+    p.N = k.K;
+    p.a_off = k.out_off;
+    p.c_off = k.in_off;
+    p.ldb = k.K;
+    p.beta = beta;
+    add_prob(b, p);
+  }
+  return b;
+}
+double lin_flops(const Linear& L, int64_t rows) {
+  double f = 0;
+  for (auto& k : L.blocks) f += 2.0 * rows * (2 * k.l + 1) * k.K * k.N;
+  return f;
+}
+
+// ------------------------------------------------------------ model loading
+int build_linear(Linear& L, const Irreps& in, const Irreps& out, const float* w, size_t numel,
+                 double extra_scale_t) {
+  std::vector<float> W, WT;
+  int in_off = 0;
+  size_t woff = 0;
+  L.din = irreps_dim(in);
+  L.dout = irreps_dim(out);
+  for (auto& a : in) {
+    int out_off = 0;
+    for (auto& b : out) {
+      if (a.l == b.l) {
+        LinBlock k{a.l, a.mul, b.mul, in_off, out_off, (int)W.size(), (int)WT.size()};
+        // e3nn Linear 'element' path normalisation: 1/sqrt(fan_in), fan_in = mul_in
+        const double sc = 1.0 / std::sqrt((double)a.mul);
+        if (woff + (size_t)a.mul * b.mul > numel) return -1;
+        for (int u = 0; u < a.mul; ++u)
+          for (int v = 0; v < b.mul; ++v) W.push_back((float)(w[woff + (size_t)u * b.mul + v] * sc));
+        for (int v = 0; v < b.mul; ++v)
+          for (int u = 0; u < a.mul; ++u)
+            WT.push_back((float)(w[woff + (size_t)u * b.mul + v] * sc * extra_scale_t));
+        woff += (size_t)a.mul * b.mul;
+        L.blocks.push_back(k);
+      }
+      out_off += b.mul * (2 * b.l + 1);
+    }
+    in_off += a.mul * (2 * a.l + 1);
+  }
+  if (woff != numel) return -1;
+  if (upload(L.W, W) != hipSuccess || upload(L.WT, WT) != hipSuccess) return -2;
+  return 0;
+}
+
+// IrrepsConvolution instruction list (convolution.py:72-95) vs the kernel tables
+template <class LT>
+bool check_paths(const Irreps& x, int lmax_out) {
+  struct Ins {
+    int l1, l2, l3, mul, xoff;
+  };
+  std::vector<Ins> ins;
+  int xoff = 0;
+  for (auto& i : x) {
+    for (int l2 = 0; l2 <= 2; ++l2)
+      for (int l3 = std::abs(i.l - l2); l3 <= i.l + l2; ++l3)
+        if (l3 <= lmax_out) ins.push_back({i.l, l2, l3, i.mul, xoff});
+    xoff += i.mul * (2 * i.l + 1);
+  }
+  if ((int)ins.size() != LT::NP) return false;
+  // mid slots: stable sort by l3
+  std::vector<int> moff(ins.size());
+  int off = 0;
+  for (int l3 = 0; l3 <= 2; ++l3)
+    for (size_t k = 0; k < ins.size(); ++k)
+      if (ins[k].l3 == l3) {
+        moff[k] = off;
+        off += ins[k].mul * (2 * l3 + 1);
+      }
+  if (off != LT::DM) return false;
+  int woff = 0;
+  for (size_t k = 0; k < ins.size(); ++k) {
+    const PathDef& p = LT::P[k];
+    if (p.l1 != ins[k].l1 || p.l2 != ins[k].l2 || p.l3 != ins[k].l3 || p.mul != ins[k].mul ||
+        p.xoff != ins[k].xoff || p.woff != woff || p.moff != moff[k])
+      return false;
+    woff += ins[k].mul;
+  }
+  return woff == LT::W && xoff == LT::DX;
+}
+
+}  // namespace
+
+namespace {
+template <int A, int B, int C>
+void dense_cg(float* out) {
+  using T = CG<A, B, C>;
+  std::memset(out, 0, sizeof(float) * (2 * A + 1) * (2 * B + 1) * (2 * C + 1));
+  for (int q = 0; q < T::n; ++q)
+    out[(T::e[q].i * (2 * B + 1) + T::e[q].j) * (2 * C + 1) + T::e[q].k] = T::e[q].c;
+}
+}  // namespace
+
+extern "C" {
+
+const char* e3gnn_last_error(void) { return g_err.c_str(); }
+int e3gnn_abi_version(void) { return 1; }
+
+e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int device) {
+  auto m = std::make_unique<e3gnn_model>();
+  m->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    fail(E3GNN_ERR_HIP, "hipSetDevice failed");
+    return nullptr;
+  }
+  minijson::Value man;
+  {
+    std::ifstream f(manifest_path);
+    if (!f) {
+      fail(E3GNN_ERR_IO, std::string("cannot open manifest ") + manifest_path);
+      return nullptr;
+    }
+    std::stringstream ss;
+    ss << f.rdbuf();
+    std::string err;
+    if (!minijson::parse(ss.str(), man, err)) {
+      fail(E3GNN_ERR_IO, "manifest parse error: " + err);
+      return nullptr;
+    }
+  }
+  std::vector<float> flat;
+  {
+    std::ifstream f(weights_path, std::ios::binary | std::ios::ate);
+    if (!f) {
+      fail(E3GNN_ERR_IO, std::string("cannot open weights ") + weights_path);
+      return nullptr;
+    }
+    const std::streamsize sz = f.tellg();
+    f.seekg(0);
+    flat.resize(sz / 4);
+    f.read((char*)flat.data(), (std::streamsize)flat.size() * 4);
+  }
+  try {
+    if (man["model_type"].str() != "E3_equivariant_model")
+      throw std::runtime_error("unsupported model_type");
+    m->nsp = (int)man["num_species"].num();
+    m->cutoff = (float)man["cutoff"].num();
+    m->r_on = (float)man["cutoff_function"]["cutoff_on"].num();
+    if (man["cutoff_function"]["name"].str() != "XPLOR")
+      throw std::runtime_error("only the XPLOR cutoff of SevenNet-0 is implemented");
+    m->nlayer = (int)man["num_convolution_layer"].num();
+    if (std::abs(man["silu_norm"].num() - (double)SILU_NORM) > 1e-6)
+      throw std::runtime_error("silu_norm mismatch");
+    for (auto& s : man["irreps_manual"].arr()) m->irreps.push_back(merged(parse_irreps(s.str())));
+    if ((int)m->irreps.size() != m->nlayer + 1) throw std::runtime_error("irreps_manual length");
+    std::map<std::string, std::pair<size_t, size_t>> T;
+    for (auto& t : man["tensors"].arr())
+      T[t["name"].str()] = {(size_t)t["offset"].num(), (size_t)t["numel"].num()};
+    auto get = [&](const std::string& n, size_t expect = 0) -> const float* {
+      auto it = T.find(n);
+      if (it == T.end()) throw std::runtime_error("missing tensor " + n);
+      if (it->second.first + it->second.second > flat.size())
+        throw std::runtime_error("tensor out of file range " + n);
+      if (expect && it->second.second != expect) throw std::runtime_error("bad size " + n);
+      return flat.data() + it->second.first;
+    };
+    auto numel = [&](const std::string& n) { return T.at(n).second; };
+    if (m->nlayer != 5) throw std::runtime_error("kernel path tables are SevenNet-0's (5 layers)");
+    // geometry / embedding / readout
+    const float* cf = get("edge_embedding.basis_function.coeffs", 8);
+    if (upload(m->coeffs, std::vector<float>(cf, cf + 8)) != hipSuccess) throw std::runtime_error("upload");
+    const float* we = get("onehot_to_feature_x.linear.weight", (size_t)m->nsp * 128);
+    std::vector<float> emb((size_t)m->nsp * 128);
+    for (size_t i = 0; i < emb.size(); ++i) emb[i] = (float)(we[i] / std::sqrt((double)m->nsp));
+    if (upload(m->embed, emb) != hipSuccess) throw std::runtime_error("upload");
+    const float* wh = get("reduce_input_to_hidden.linear.weight", 128 * 64);
+    const float* wo = get("reduce_hidden_to_energy.linear.weight", 64);
+    std::vector<float> v(128);
+    for (int c = 0; c < 128; ++c) {
+      double s = 0;
+      for (int k = 0; k < 64; ++k) s += (double)wh[c * 64 + k] * wo[k];
+      v[c] = (float)(s / (std::sqrt(128.0) * 8.0));
+    }
+    if (upload(m->readout_v, v) != hipSuccess) throw std::runtime_error("upload");
+    const float* sc = get("rescale_atomic_energy.scale", m->nsp);
+    const float* sh = get("rescale_atomic_energy.shift", m->nsp);
+    if (upload(m->scale, std::vector<float>(sc, sc + m->nsp)) != hipSuccess ||
+        upload(m->shift, std::vector<float>(sh, sh + m->nsp)) != hipSuccess)
+      throw std::runtime_error("upload");
+    // interaction blocks
+    for (int t = 0; t < m->nlayer; ++t) {
+      const Irreps& xin = m->irreps[t];
+      const Irreps& xout = m->irreps[t + 1];
+      const bool last = t == m->nlayer - 1;
+      // gate irreps_in: scalars + gates (0e) + gated (equivariant_gate.py:48-55)
+      Irreps gin;
+      int nscal = 0, ngated = 0;
+      for (auto& i : xout) (i.l == 0 ? nscal : ngated) += i.mul;
+      gin.push_back({nscal + ngated, 0});
+      for (auto& i : xout)
+        if (i.l > 0) gin.push_back(i);
+      const int lmax_out = last ? 0 : 2;
+      bool ok = t == 0 ? check_paths<LayerFirst>(xin, lmax_out)
+                       : (last ? check_paths<LayerLast>(xin, lmax_out)
+                               : check_paths<LayerMid>(xin, lmax_out));
+      if (!ok) throw std::runtime_error("convolution path table mismatch at layer " + std::to_string(t));
+      // mid irreps merged by l (sorted), see tp.h
+      Irreps mid;
+      for (int l3 = 0; l3 <= lmax_out; ++l3) {
+        int mul = 0;
+        for (auto& i : xin)
+          for (int l2 = 0; l2 <= 2; ++l2)
+            if (std::abs(i.l - l2) <= l3 && l3 <= i.l + l2) mul += i.mul;
+        if (mul) mid.push_back({mul, l3});
+      }
+      m->gin.push_back(gin);
+      m->mid.push_back(mid);
+      const std::string p = std::to_string(t);
+      const float den = *get(p + "_convolution.denominator", 1);
+      m->denom.push_back(den);
+      auto mk = [&](const std::string& name, const Irreps& a, const Irreps& b, double extra) {
+        auto L = std::make_unique<Linear>();
+        if (build_linear(*L, a, b, get(name), numel(name), extra) != 0)
+          throw std::runtime_error("linear " + name);
+        return L;
+      };
+      m->sc.push_back(mk(p + "_self_connection_intro.linear.weight", xin, gin, 1.0));
+      m->si1.push_back(mk(p + "_self_interaction_1.linear.weight", xin, xin, 1.0));
+      // backward of si2 feeds dE/dagg_raw = dE/dagg / denominator (convolution.py:117-118)
+      m->si2.push_back(mk(p + "_self_interaction_2.linear.weight", mid, gin, 1.0 / den));
+      // radial MLP (e3nn FullyConnectedNet, weights / sqrt(fan_in))
+      const float* w0 = get(p + "_convolution.weight_nn.layer0.weight", 8 * 64);
+      const float* w1 = get(p + "_convolution.weight_nn.layer1.weight", 64 * 64);
+      const size_t n2 = numel(p + "_convolution.weight_nn.layer2.weight");
+      const float* w2 = get(p + "_convolution.weight_nn.layer2.weight");
+      const int W = (int)(n2 / 64);
+      const int Wexp = t == 0 ? LayerFirst::W : (last ? LayerLast::W : LayerMid::W);
+      if (W != Wexp) throw std::runtime_error("radial weight width mismatch");
+      m->W.push_back(W);
+      auto scaled = [](const float* a, int r, int c, double s, bool tr) {
+        std::vector<float> o((size_t)r * c);
+        for (int i = 0; i < r; ++i)
+          for (int j = 0; j < c; ++j) {
+            const float v = (float)(a[(size_t)i * c + j] * s);
+            if (tr) o[(size_t)j * r + i] = v;
+            else o[(size_t)i * c + j] = v;
+          }
+        return o;
+      };
+      e3gnn_model::Mlp M;
+      m->mlp.push_back(std::move(M));
+      auto& mm = m->mlp.back();
+      const double s0 = 1.0 / std::sqrt(8.0), s1 = 1.0 / 8.0, s2 = 1.0 / 8.0;
+      if (upload(mm.w0, scaled(w0, 8, 64, s0, false)) != hipSuccess ||
+          upload(mm.w1, scaled(w1, 64, 64, s1, false)) != hipSuccess ||
+          upload(mm.w2, scaled(w2, 64, W, s2, false)) != hipSuccess ||
+          upload(mm.w0t, scaled(w0, 8, 64, s0, true)) != hipSuccess ||
+          upload(mm.w1t, scaled(w1, 64, 64, s1, true)) != hipSuccess ||
+          upload(mm.w2t, scaled(w2, 64, W, s2, true)) != hipSuccess)
+        throw std::runtime_error("upload mlp");
+    }
+  } catch (const std::exception& ex) {
+    fail(E3GNN_ERR_IO, std::string("model load: ") + ex.what());
+    return nullptr;
+  }
+  return m.release();
+}
+
+void e3gnn_free(e3gnn_model* m) { delete m; }
+
+int e3gnn_model_info(const e3gnn_model* m, int* num_species, float* cutoff, int* num_layers,
+                     int* comm_size) {
+  if (!m) return fail(E3GNN_ERR_ARG, "null model");
+  if (num_species) *num_species = m->nsp;
+  if (cutoff) *cutoff = m->cutoff;
+  if (num_layers) *num_layers = m->nlayer;
+  if (comm_size) *comm_size = irreps_dim(m->irreps[1]);
+  return E3GNN_OK;
+}
+
+e3gnn_ctx* e3gnn_ctx_create(e3gnn_model* m) {
+  if (!m) {
+    fail(E3GNN_ERR_ARG, "null model");
+    return nullptr;
+  }
+  auto c = new e3gnn_ctx();
+  c->m = m;
+  const int L = m->nlayer;
+  c->x.resize(L + 1);
+  c->grad.resize(L + 1);
+  c->h.resize(L);
+  c->y.resize(L);
+  c->w.resize(L);
+  c->a1.resize(L);
+  c->a2.resize(L);
+  return c;
+}
+void e3gnn_ctx_free(e3gnn_ctx* c) { delete c; }
+
+int e3gnn_feature_dim(const e3gnn_ctx* c, int layer) {
+  if (!c || layer < 0 || layer > c->m->nlayer) return -1;
+  return irreps_dim(c->m->irreps[layer]);
+}
+float* e3gnn_feature_ptr(e3gnn_ctx* c, int layer) {
+  if (!c || layer < 0 || layer > c->m->nlayer) return nullptr;
+  return c->x[layer].f();
+}
+float* e3gnn_grad_ptr(e3gnn_ctx* c, int layer) {
+  if (!c || layer < 0 || layer > c->m->nlayer) return nullptr;
+  return c->grad[layer].f();
+}
+
+int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_edges,
+                    const int32_t* type, const int32_t* edge_center, const int32_t* edge_nbr,
+                    const float* edge_vec, void* stream) {
+  if (!c) return fail(E3GNN_ERR_ARG, "null context");
+  if (n_local < 0 || n_ghost < 0 || n_edges < 0) return fail(E3GNN_ERR_ARG, "negative size");
+  if (n_local + n_ghost > (1LL << 30) || n_edges > (1LL << 31) - 1)
+    return fail(E3GNN_ERR_ARG, "graph too large for int32 indices");
+  if ((n_local + n_ghost > 0 && !type) || (n_edges > 0 && (!edge_center || !edge_nbr || !edge_vec)))
+    return fail(E3GNN_ERR_ARG, "null input array");
+  e3gnn_model* m = c->m;
+  HIPCHK(hipSetDevice(m->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = n_local + n_ghost, nl = n_local, E = n_edges;
+  c->n = n;
+  c->nl = nl;
+  c->E = E;
+  c->readout_done = 0;
+  const size_t F = sizeof(float);
+  // workspace (grow-only)
+  HIPCHK(c->type.ensure(n * 4));
+  HIPCHK(c->center.ensure(E * 4));
+  HIPCHK(c->nbr.ensure(E * 4));
+  HIPCHK(c->vec.ensure(E * 3 * F));
+  HIPCHK(c->row_ptr.ensure((nl + 1) * 4));
+  HIPCHK(c->src_ptr.ensure((n + 1) * 4));
+  HIPCHK(c->src_perm.ensure(E * 4));
+  HIPCHK(c->cnt.ensure(n * 4));
+  HIPCHK(c->err.ensure(4));
+  HIPCHK(c->Y.ensure(E * 9 * F));
+  HIPCHK(c->emb.ensure(E * 8 * F));
+  HIPCHK(c->dY.ensure(E * 9 * F));
+  HIPCHK(c->demb.ensure(E * 8 * F));
+  HIPCHK(c->fe.ensure(E * 3 * F));
+  HIPCHK(c->H1.ensure(E * 64 * F));
+  HIPCHK(c->H2.ensure(E * 64 * F));
+  int maxW = 0, maxDM = 0;
+  for (int t = 0; t < m->nlayer; ++t) {
+    const int dx = irreps_dim(m->irreps[t]), dg = irreps_dim(m->gin[t]);
+    maxW = std::max(maxW, m->W[t]);
+    maxDM = std::max(maxDM, irreps_dim(m->mid[t]));
+    HIPCHK(c->x[t].ensure(std::max<int64_t>(n, 1) * dx * F));
+    HIPCHK(c->grad[t].ensure(std::max<int64_t>(n, 1) * dx * F));
+    HIPCHK(c->h[t].ensure(n * dx * F));
+    HIPCHK(c->y[t].ensure(nl * dg * F));
+    HIPCHK(c->w[t].ensure(E * m->W[t] * F));
+    HIPCHK(c->a1[t].ensure(E * 64 * F));
+    HIPCHK(c->a2[t].ensure(E * 64 * F));
+  }
+  const int dlast = irreps_dim(m->irreps[m->nlayer]);
+  HIPCHK(c->x[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
+  HIPCHK(c->grad[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
+  HIPCHK(c->agg.ensure(nl * maxDM * F));
+  HIPCHK(c->dw.ensure(E * maxW * F));
+  HIPCHK(c->dxc.ensure(E * 480 * F));
+  HIPCHK(c->dy.ensure(nl * 576 * F));
+  HIPCHK(c->dh.ensure(n * 480 * F));
+  HIPCHK(c->eat.ensure(std::max<int64_t>(nl, 1) * F));
+  HIPCHK(c->part.ensure((sum_blocks(nl) + 1) * F));
+  HIPCHK(c->vpart.ensure((edge_force_blocks(E) + 1) * 6 * F));
+  HIPCHK(c->scratch6.ensure(8 * F));
+
+  if (n > 0) HIPCHK(hipMemcpyAsync(c->type.p, type, n * 4, hipMemcpyDefault, s));
+  if (E > 0) {
+    HIPCHK(hipMemcpyAsync(c->center.p, edge_center, E * 4, hipMemcpyDefault, s));
+    HIPCHK(hipMemcpyAsync(c->nbr.p, edge_nbr, E * 4, hipMemcpyDefault, s));
+    HIPCHK(hipMemcpyAsync(c->vec.p, edge_vec, E * 3 * F, hipMemcpyDefault, s));
+  }
+  HIPCHK(hipMemsetAsync(c->err.p, 0, 4, s));
+  {
+    Region r(c, s, C_GRAPH, 0, (double)E * 24 + n * 12);
+    HIPCHK(launch_build_graph(E, (int)nl, (int)n, c->center.i(), c->nbr.i(), c->row_ptr.i(),
+                              c->src_ptr.i(), c->src_perm.i(), c->cnt.i(), c->err.i(), s));
+  }
+  {
+    Region r(c, s, C_EMBED_NODE, 0, (double)n * 128 * 4);
+    HIPCHK(launch_embed((int)n, c->type.i(), m->nsp, m->embed.f(), c->x[0].f(), c->err.i(), s));
+  }
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (err) {
+    std::string msg = "invalid graph:";
+    if (err & 1) msg += " edge_center not sorted non-decreasing;";
+    if (err & 2) msg += " edge_center out of [0, n_local);";
+    if (err & 4) msg += " edge_nbr out of [0, n_local+n_ghost);";
+    if (err & 8) msg += " species index out of range;";
+    return fail(E3GNN_ERR_GRAPH, msg);
+  }
+  {
+    Region r(c, s, C_EMBED_EDGE, 0, (double)E * (12 + 68));
+    HIPCHK(launch_edge_embed(E, c->vec.f(), m->coeffs.f(), m->cutoff, m->r_on, c->Y.f(),
+                             c->emb.f(), s));
+  }
+  if (E > 0) {
+    HIPCHK(hipMemsetAsync(c->dY.p, 0, E * 9 * F, s));
+    HIPCHK(hipMemsetAsync(c->demb.p, 0, E * 8 * F, s));
+  }
+  return E3GNN_OK;
+}
+
+int e3gnn_layer_forward(e3gnn_ctx* c, int t, void* stream) {
+  if (!c) return fail(E3GNN_ERR_ARG, "null context");
+  e3gnn_model* m = c->m;
+  if (t < 0 || t >= m->nlayer) return fail(E3GNN_ERR_ARG, "layer out of range");
+  HIPCHK(hipSetDevice(m->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = c->n, nl = c->nl, E = c->E;
+  const int dx = irreps_dim(m->irreps[t]), dg = irreps_dim(m->gin[t]);
+  const int dm = irreps_dim(m->mid[t]), W = m->W[t];
+  const bool last = t == m->nlayer - 1;
+  const int kind = t == 0 ? 0 : (last ? 2 : 1);
+  // self_interaction_1 on owned + ghost rows
+  {
+    Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], n));
+    HIPCHK(launch_gemm(lin_fwd(*m->si1[t], c->x[t].f(), dx, c->h[t].f(), dx, n, 0), s));
+  }
+  // radial MLP: emb -> 64 -> 64 -> W  (convolution.py:97-106)
+  {
+    Region r(c, s, C_MLP_FWD, 2.0 * E * (8 * 64 + 64 * 64 + 64 * W),
+             (double)E * 4 * (8 + 64 * 4 + 2 * 64 + W));
+    auto& mm = m->mlp[t];
+    GemmBatch b;
+    std::memset(&b, 0, sizeof(b));
+    GemmProb p = base_prob();
+    p.A = c->emb.f(); p.lda = 8; p.K = 8;
+    p.B = mm.w0.f(); p.ldb = 64; p.N = 64;
+    p.C = c->H1.f(); p.ldc = 64; p.M = (int)E;
+    p.act = 1; p.pre_out = c->a1[t].f();
+    add_prob(b, p);
+    HIPCHK(launch_gemm(b, s));
+    std::memset(&b, 0, sizeof(b));
+    p.A = c->H1.f(); p.lda = 64; p.K = 64;
+    p.B = mm.w1.f(); p.C = c->H2.f(); p.pre_out = c->a2[t].f();
+    add_prob(b, p);
+    HIPCHK(launch_gemm(b, s));
+    std::memset(&b, 0, sizeof(b));
+    p.A = c->H2.f(); p.B = mm.w2.f(); p.ldb = W; p.N = W;
+    p.C = c->w[t].f(); p.ldc = W; p.act = 0; p.pre_out = nullptr;
+    add_prob(b, p);
+    HIPCHK(launch_gemm(b, s));
+  }
+  // tensor product + segmented neighbour sum
+  {
+    Region r(c, s, C_TP_FWD, tp_flops_per_edge(kind) * E,
+             (double)E * 4 * (W + 9 + dx + 2) + nl * 4.0 * dm);
+    TpArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.row_ptr = c->row_ptr.i();
+    a.nbr = c->nbr.i();
+    a.Y = c->Y.f();
+    a.w = c->w[t].f();
+    a.h = c->h[t].f();
+    a.agg = c->agg.f();
+    a.n_centers = (int)nl;
+    a.denom = m->denom[t];
+    HIPCHK(launch_tp_fwd(kind, a, s));
+  }
+  // self_interaction_2 + self_connection (intro/outro)
+  {
+    Region r(c, s, C_LINEAR, lin_flops(*m->si2[t], nl) + lin_flops(*m->sc[t], nl));
+    HIPCHK(launch_gemm(lin_fwd(*m->si2[t], c->agg.f(), dm, c->y[t].f(), dg, nl, 0), s));
+    HIPCHK(launch_gemm(lin_fwd(*m->sc[t], c->x[t].f(), dx, c->y[t].f(), dg, nl, 1), s));
+  }
+  {
+    Region r(c, s, C_GATE_FWD, 0, nl * 4.0 * (dg + irreps_dim(m->irreps[t + 1])));
+    HIPCHK(launch_gate_fwd((int)nl, last, c->y[t].f(), c->x[t + 1].f(), s));
+  }
+  return E3GNN_OK;
+}
+
+int e3gnn_readout(e3gnn_ctx* c, float* energy, float* atomic_energy, void* stream) {
+  if (!c) return fail(E3GNN_ERR_ARG, "null context");
+  e3gnn_model* m = c->m;
+  HIPCHK(hipSetDevice(m->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nl = c->nl;
+  const int L = m->nlayer;
+  {
+    Region r(c, s, C_READOUT, 2.0 * nl * 128, nl * 4.0 * 130);
+    HIPCHK(launch_readout((int)nl, c->x[L].f(), m->readout_v.f(), c->type.i(), m->scale.f(),
+                          m->shift.f(), c->eat.f(), s));
+    HIPCHK(launch_sum(nl, c->eat.f(), c->part.f(), energy ? energy : c->scratch6.f(), s));
+    if (atomic_energy && nl > 0)
+      HIPCHK(hipMemcpyAsync(atomic_energy, c->eat.p, nl * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(launch_readout_bwd((int)nl, m->readout_v.f(), c->type.i(), m->scale.f(),
+                              c->grad[L].f(), s));
+  }
+  c->readout_done = 1;
+  return E3GNN_OK;
+}
+
+int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
+  if (!c) return fail(E3GNN_ERR_ARG, "null context");
+  e3gnn_model* m = c->m;
+  if (t < 0 || t >= m->nlayer) return fail(E3GNN_ERR_ARG, "layer out of range");
+  if (!c->readout_done) return fail(E3GNN_ERR_ARG, "e3gnn_readout must precede the backward");
+  HIPCHK(hipSetDevice(m->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = c->n, nl = c->nl, E = c->E;
+  const int dx = irreps_dim(m->irreps[t]), dg = irreps_dim(m->gin[t]);
+  const int dm = irreps_dim(m->mid[t]), W = m->W[t];
+  const bool last = t == m->nlayer - 1;
+  const int kind = t == 0 ? 0 : (last ? 2 : 1);
+  {
+    Region r(c, s, C_GATE_BWD, 0, nl * 4.0 * (2 * dg + irreps_dim(m->irreps[t + 1])));
+    HIPCHK(launch_gate_bwd((int)nl, last, c->y[t].f(), c->grad[t + 1].f(), c->dy.f(), s));
+  }
+  {
+    Region r(c, s, C_LINEAR, lin_flops(*m->si2[t], nl));
+    HIPCHK(launch_gemm(lin_bwd(*m->si2[t], c->dy.f(), dg, c->agg.f(), dm, nl, 0), s));
+  }
+  {
+    Region r(c, s, C_TP_BWD, 3.0 * tp_flops_per_edge(kind) * E,
+             (double)E * 4 * (2 * W + 2 * 9 + dx + (t > 0 ? dx : 0) + 2) + nl * 4.0 * dm);
+    TpArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.row_ptr = c->row_ptr.i();
+    a.nbr = c->nbr.i();
+    a.Y = c->Y.f();
+    a.w = c->w[t].f();
+    a.h = c->h[t].f();
+    a.gagg = c->agg.f();
+    a.dw = c->dw.f();
+    a.dxc = t > 0 ? c->dxc.f() : nullptr;
+    a.dYacc = c->dY.f();
+    a.n_centers = (int)nl;
+    HIPCHK(launch_tp_bwd(kind, a, s));
+  }
+  {
+    Region r(c, s, C_MLP_BWD, 2.0 * E * (64 * W + 64 * 64 + 64 * 8),
+             (double)E * 4 * (W + 64 * 6 + 16));
+    auto& mm = m->mlp[t];
+    GemmBatch b;
+    std::memset(&b, 0, sizeof(b));
+    GemmProb p = base_prob();
+    p.A = c->dw.f(); p.lda = W; p.K = W;
+    p.B = mm.w2t.f(); p.ldb = 64; p.N = 64;
+    p.C = c->H2.f(); p.ldc = 64; p.M = (int)E;
+    p.act = 2; p.pre_in = c->a2[t].f();
+    add_prob(b, p);
+    HIPCHK(launch_gemm(b, s));
+    std::memset(&b, 0, sizeof(b));
+    p.A = c->H2.f(); p.lda = 64; p.K = 64;
+    p.B = mm.w1t.f(); p.C = c->H1.f(); p.pre_in = c->a1[t].f();
+    add_prob(b, p);
+    HIPCHK(launch_gemm(b, s));
+    std::memset(&b, 0, sizeof(b));
+    p.A = c->H1.f(); p.B = mm.w0t.f(); p.ldb = 8; p.N = 8;
+    p.C = c->demb.f(); p.ldc = 8; p.act = 0; p.pre_in = nullptr; p.beta = 1;
+    add_prob(b, p);
+    HIPCHK(launch_gemm(b, s));
+  }
+  if (t > 0) {
+    {
+      Region r(c, s, C_GATHER, 0, (double)E * 4 * (dx + 1) + n * 4.0 * dx);
+      HIPCHK(launch_gather_rows((int)n, dx, c->src_ptr.i(), c->src_perm.i(), c->dxc.f(),
+                                c->dh.f(), s));
+    }
+    Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], n) + lin_flops(*m->sc[t], nl));
+    HIPCHK(launch_gemm(lin_bwd(*m->si1[t], c->dh.f(), dx, c->grad[t].f(), dx, n, 0), s));
+    HIPCHK(launch_gemm(lin_bwd(*m->sc[t], c->dy.f(), dg, c->grad[t].f(), dx, nl, 1), s));
+  }
+  return E3GNN_OK;
+}
+
+int e3gnn_forces(e3gnn_ctx* c, float* forces, float* virial6, float* edge_grad, void* stream) {
+  if (!c) return fail(E3GNN_ERR_ARG, "null context");
+  e3gnn_model* m = c->m;
+  HIPCHK(hipSetDevice(m->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = c->n, nl = c->nl, E = c->E;
+  {
+    Region r(c, s, C_EDGE_FORCE, 0, (double)E * 4 * (3 + 9 + 8 + 3));
+    HIPCHK(launch_edge_force(E, c->vec.f(), m->coeffs.f(), m->cutoff, m->r_on, c->dY.f(),
+                             c->demb.f(), c->fe.f(), c->vpart.f(), s));
+    HIPCHK(launch_final_sum(edge_force_blocks(E), 6, c->vpart.f(),
+                            virial6 ? virial6 : c->scratch6.f(), s));
+  }
+  if (forces) {
+    Region r(c, s, C_ATOM_FORCE, 0, (double)E * 4 * 2 * 4 + n * 12.0);
+    HIPCHK(launch_atom_force((int)n, (int)nl, c->row_ptr.i(), c->src_ptr.i(), c->src_perm.i(),
+                             c->fe.f(), forces, s));
+  }
+  if (edge_grad && E > 0)
+    HIPCHK(hipMemcpyAsync(edge_grad, c->fe.p, E * 12, hipMemcpyDeviceToDevice, s));
+  return E3GNN_OK;
+}
+
+int e3gnn_energy_forces(e3gnn_ctx* c, int64_t n_atoms, int64_t n_edges, const int32_t* type,
+                        const int32_t* edge_center, const int32_t* edge_nbr,
+                        const float* edge_vec, float* energy, float* atomic_energy,
+                        float* forces, float* virial6, float* edge_grad, void* stream) {
+  if (!energy) return fail(E3GNN_ERR_ARG, "energy output is required");
+  int rc = e3gnn_graph_set(c, n_atoms, 0, n_edges, type, edge_center, edge_nbr, edge_vec, stream);
+  if (rc) return rc;
+  const int L = c->m->nlayer;
+  for (int t = 0; t < L; ++t)
+    if ((rc = e3gnn_layer_forward(c, t, stream))) return rc;
+  if ((rc = e3gnn_readout(c, energy, atomic_energy, stream))) return rc;
+  for (int t = L - 1; t >= 0; --t)
+    if ((rc = e3gnn_layer_backward(c, t, stream))) return rc;
+  if ((rc = e3gnn_forces(c, forces, virial6, edge_grad, stream))) return rc;
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_halo_pack(const int32_t* idx, int64_t n, int dim, const float* src, int64_t src_stride,
+                    float* dst, void* stream) {
+  if (n < 0 || dim <= 0) return fail(E3GNN_ERR_ARG, "bad halo size");
+  HIPCHK(launch_pack(n, dim, idx, src, src_stride, dst, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+int e3gnn_halo_unpack(const int32_t* idx, int64_t n, int dim, const float* src, float* dst,
+                      int64_t dst_stride, int accumulate, void* stream) {
+  if (n < 0 || dim <= 0) return fail(E3GNN_ERR_ARG, "bad halo size");
+  HIPCHK(launch_unpack(n, dim, idx, src, dst, dst_stride, accumulate, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_set_timing(e3gnn_ctx* c, int enable) {
+  if (!c) return fail(E3GNN_ERR_ARG, "null context");
+  c->flush();
+  c->timing = enable != 0;
+  return E3GNN_OK;
+}
+int e3gnn_kernel_stats(e3gnn_ctx* c, const char** names, double* ms, int64_t* launches,
+                       double* flops, double* bytes, int max) {
+  if (!c) return -1;
+  c->flush();
+  for (int i = 0; i < C_NCLS && i < max; ++i) {
+    if (names) names[i] = kClassNames[i];
+    if (ms) ms[i] = c->stats[i].ms;
+    if (launches) launches[i] = c->stats[i].launches;
+    if (flops) flops[i] = c->stats[i].flops;
+    if (bytes) bytes[i] = c->stats[i].bytes;
+  }
+  return C_NCLS;
+}
+int e3gnn_reset_stats(e3gnn_ctx* c) {
+  if (!c) return fail(E3GNN_ERR_ARG, "null context");
+  c->flush();
+  for (auto& st : c->stats) st = Stat();
+  return E3GNN_OK;
+}
+
+int e3gnn_cg_table(int l1, int l2, int l3, float* out) {
+  if (!out) return fail(E3GNN_ERR_ARG, "null out");
+  const int key = l1 * 100 + l2 * 10 + l3;
+  switch (key) {
+#define CGCASE(a, b, c) \
+  case a * 100 + b * 10 + c: dense_cg<a, b, c>(out); return E3GNN_OK;
+    CGCASE(0, 0, 0) CGCASE(0, 1, 1) CGCASE(0, 2, 2) CGCASE(1, 0, 1) CGCASE(1, 1, 0)
+    CGCASE(1, 1, 1) CGCASE(1, 1, 2) CGCASE(1, 2, 1) CGCASE(1, 2, 2) CGCASE(2, 0, 2)
+    CGCASE(2, 1, 1) CGCASE(2, 1, 2) CGCASE(2, 2, 0) CGCASE(2, 2, 1) CGCASE(2, 2, 2)
+#undef CGCASE
+    default: return fail(E3GNN_ERR_ARG, "no coupling table for this (l1,l2,l3)");
+  }
+}
+
+int64_t e3gnn_workspace_bytes(const e3gnn_ctx* c) {
+  if (!c) return 0;
+  int64_t b = 0;
+  const DBuf* fixed[] = {&c->type, &c->center, &c->nbr, &c->vec, &c->row_ptr, &c->src_ptr,
+                         &c->src_perm, &c->cnt, &c->err, &c->Y, &c->emb, &c->dY, &c->demb,
+                         &c->fe, &c->H1, &c->H2, &c->agg, &c->dw, &c->dxc, &c->dy, &c->dh,
+                         &c->eat, &c->part, &c->vpart, &c->scratch6};
+  for (auto* d : fixed) b += (int64_t)d->cap;
+  for (auto* v : {&c->x, &c->grad, &c->h, &c->y, &c->w, &c->a1, &c->a2})
+    for (auto& d : *v) b += (int64_t)d.cap;
+  return b;
+}
+
+}  // extern "C"

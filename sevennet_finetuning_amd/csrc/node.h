@@ -1,0 +1,36 @@
+// Launchers of node.hip (edge geometry, graph indices, node ops, reductions).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace e3gnn {
+hipError_t launch_edge_embed(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
+                             float* Y, float* emb, hipStream_t s);
+int edge_force_blocks(int64_t E);
+hipError_t launch_edge_force(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
+                             const float* dY, const float* demb, float* fe, float* vir_part,
+                             hipStream_t s);
+hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, const int* src_ptr,
+                             const int* src_perm, const float* fe, float* F, hipStream_t s);
+hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* center,
+                              const int* nbr, int* row_ptr, int* src_ptr, int* src_perm,
+                              int* cnt, int* err, hipStream_t s);
+hipError_t launch_embed(int n, const int* type, int nsp, const float* W, float* x, int* err,
+                        hipStream_t s);
+hipError_t launch_gate_fwd(int n, bool last, const float* y, float* x, hipStream_t s);
+hipError_t launch_gate_bwd(int n, bool last, const float* y, const float* dx, float* dy,
+                           hipStream_t s);
+hipError_t launch_readout(int n, const float* x, const float* v, const int* type,
+                          const float* scale, const float* shift, float* eat, hipStream_t s);
+hipError_t launch_readout_bwd(int n, const float* v, const int* type, const float* scale,
+                              float* dx, hipStream_t s);
+int sum_blocks(int64_t n);
+hipError_t launch_sum(int64_t n, const float* a, float* part, float* out, hipStream_t s);
+hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStream_t s);
+hipError_t launch_gather_rows(int n, int D, const int* ptr, const int* perm, const float* src,
+                              float* dst, hipStream_t s);
+hipError_t launch_pack(int64_t n, int dim, const int* idx, const float* src, int64_t ss, float* dst,
+                       hipStream_t s);
+hipError_t launch_unpack(int64_t n, int dim, const int* idx, const float* src, float* dst,
+                         int64_t ds, int acc, hipStream_t s);
+}  // namespace e3gnn

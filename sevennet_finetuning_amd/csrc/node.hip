@@ -1,0 +1,482 @@
+// Edge geometry, graph index builders, node-wise ops and the force/virial
+// reduction of the SevenNet-0 energy+force path, gfx950.
+//
+// Every reduction here is deterministic: per-atom sums walk CSR lists in edge
+// order (no float atomics); scalar totals use a fixed two-level tree.
+#include "common.h"
+#include "node.h"
+
+namespace e3gnn {
+namespace {
+
+constexpr int TPB = 256;
+inline int nblk(int64_t n, int t = TPB) { return (int)((n + t - 1) / t); }
+
+// ------------------------------------------------------------ edge embedding
+// EdgeEmbedding.forward (sevenn/nn/edge_embedding.py:220-230): r = |r_ij|,
+// BesselBasis (:114-116) B_n = (2/rc) sin(c_n r) / r with trainable c_n,
+// XPLORCutoff (:163-173), SphericalEncoding (:177-198; e3nn SH lmax 2,
+// normalize=True, 'component'; polynomial of serial_code.py:50-70).
+__global__ void k_edge_embed(int64_t E, const float* __restrict__ vec, const float* __restrict__ coeffs,
+                             float rc, float ron, float* __restrict__ Y, float* __restrict__ emb) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const float vx = vec[3 * e], vy = vec[3 * e + 1], vz = vec[3 * e + 2];
+  const float r = sqrtf(vx * vx + vy * vy + vz * vz);
+  const float x = vx / r, y = vy / r, z = vz / r;
+  const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f;
+  float* yo = Y + 9 * e;
+  yo[0] = 1.f;
+  yo[1] = s3 * x;
+  yo[2] = s3 * y;
+  yo[3] = s3 * z;
+  yo[4] = s5 * (s3 * x * z);
+  yo[5] = s5 * (s3 * x * y);
+  yo[6] = s5 * (y * y - 0.5f * (x * x + z * z));
+  yo[7] = s5 * (s3 * y * z);
+  yo[8] = s5 * (0.5f * s3 * (z * z - x * x));
+  float env = 1.f;
+  if (r >= ron) {
+    const float rc2 = rc * rc, r2 = r * r, ron2 = ron * ron;
+    const float a = rc2 - r2, d = rc2 - ron2;
+    env = a * a * (rc2 + 2.f * r2 - 3.f * ron2) / (d * d * d);
+  }
+  float* eo = emb + 8 * e;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) eo[n] = (2.f / rc) * sinf(coeffs[n] * r) / r * env;
+}
+
+// dE/dr_ij from the accumulated dE/dY (all layers) and dE/demb (all layers):
+// the chain rule of the two functions above (force_output.py:83-130 obtains
+// the same through autograd).  Also writes per-block virial partials.
+__global__ void k_edge_force(int64_t E, const float* __restrict__ vec, const float* __restrict__ coeffs,
+                             float rc, float ron, const float* __restrict__ dY,
+                             const float* __restrict__ demb, float* __restrict__ fe,
+                             float* __restrict__ vir_part) {
+  __shared__ float red[6][TPB];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float v6[6] = {0, 0, 0, 0, 0, 0};
+  if (e < E) {
+    const float vx = vec[3 * e], vy = vec[3 * e + 1], vz = vec[3 * e + 2];
+    const float r = sqrtf(vx * vx + vy * vy + vz * vz);
+    const float x = vx / r, y = vy / r, z = vz / r;
+    const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f;
+    const float* g = dY + 9 * e;
+    // gradient w.r.t. the unit vector u
+    float gx = s3 * g[1], gy = s3 * g[2], gz = s3 * g[3];
+    const float c = s5 * s3;
+    gx += c * (z * g[4] + y * g[5]) - s5 * x * g[6] - c * x * g[8];
+    gy += c * (x * g[5] + z * g[7]) + 2.f * s5 * y * g[6];
+    gz += c * (x * g[4] + y * g[7]) - s5 * z * g[6] + c * z * g[8];
+    const float dot = gx * x + gy * y + gz * z;
+    float fx = (gx - dot * x) / r, fy = (gy - dot * y) / r, fz = (gz - dot * z) / r;
+    // radial part
+    float env = 1.f, denv = 0.f;
+    if (r >= ron) {
+      const float rc2 = rc * rc, r2 = r * r, ron2 = ron * ron;
+      const float a = rc2 - r2, d = rc2 - ron2, d3 = d * d * d;
+      env = a * a * (rc2 + 2.f * r2 - 3.f * ron2) / d3;
+      denv = 12.f * r * a * (ron2 - r2) / d3;
+    }
+    const float* ge = demb + 8 * e;
+    float dr = 0.f;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const float cn = coeffs[n];
+      const float sn = sinf(cn * r), cs = cosf(cn * r);
+      const float b = (2.f / rc) * sn / r;
+      const float db = (2.f / rc) * (cn * cs * r - sn) / (r * r);
+      dr += ge[n] * (db * env + b * denv);
+    }
+    fx += dr * x;
+    fy += dr * y;
+    fz += dr * z;
+    fe[3 * e] = fx;
+    fe[3 * e + 1] = fy;
+    fe[3 * e + 2] = fz;
+    // virial = -dE/dstrain (symmetric strain, ForceStressOutput force_output.py:83-130);
+    // equals inferred_stress * volume, the quantity pair_e3gnn.cpp:244-256 hands LAMMPS
+    v6[0] = -(vx * fx);
+    v6[1] = -(vy * fy);
+    v6[2] = -(vz * fz);
+    v6[3] = -0.5f * (vx * fy + vy * fx);
+    v6[4] = -0.5f * (vy * fz + vz * fy);
+    v6[5] = -0.5f * (vx * fz + vz * fx);
+  }
+#pragma unroll
+  for (int q = 0; q < 6; ++q) red[q][threadIdx.x] = v6[q];
+  __syncthreads();
+  for (int s = TPB / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) vir_part[(int64_t)blockIdx.x * 6 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// F_i = sum_{e: center=i} f_e - sum_{e: nbr=i} f_e  (pair_e3gnn_parallel.cpp:482-484)
+__global__ void k_atom_force(int n_nodes, int n_centers, const int* __restrict__ row_ptr,
+                             const int* __restrict__ src_ptr, const int* __restrict__ src_perm,
+                             const float* __restrict__ fe, float* __restrict__ F) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_nodes) return;
+  float fx = 0.f, fy = 0.f, fz = 0.f;
+  if (i < n_centers)
+    for (int e = row_ptr[i]; e < row_ptr[i + 1]; ++e) {
+      fx += fe[3 * e];
+      fy += fe[3 * e + 1];
+      fz += fe[3 * e + 2];
+    }
+  for (int q = src_ptr[i]; q < src_ptr[i + 1]; ++q) {
+    const int e = src_perm[q];
+    fx -= fe[3 * e];
+    fy -= fe[3 * e + 1];
+    fz -= fe[3 * e + 2];
+  }
+  F[3 * i] = fx;
+  F[3 * i + 1] = fy;
+  F[3 * i + 2] = fz;
+}
+
+// ------------------------------------------------------------ graph indices
+// row_ptr of the centre-sorted edge list + validation (edge_index[0] sorted,
+// indices in range).  err bits: 1 unsorted, 2 centre out of range, 4 nbr out of range.
+__global__ void k_row_ptr(int64_t E, int n_centers, int n_nodes, const int* __restrict__ center,
+                          const int* __restrict__ nbr, int* __restrict__ row_ptr,
+                          int* __restrict__ err) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int c = center[e];
+  const int j = nbr[e];
+  if (c < 0 || c >= n_centers) {
+    atomicOr(err, 2);
+    return;
+  }
+  if (j < 0 || j >= n_nodes) atomicOr(err, 4);
+  const int prev = e ? center[e - 1] : -1;
+  if (c < prev) {
+    atomicOr(err, 1);
+    return;
+  }
+  for (int q = prev + 1; q <= c; ++q) row_ptr[q] = (int)e;
+  if (e == E - 1)
+    for (int q = c + 1; q <= n_centers; ++q) row_ptr[q] = (int)E;
+}
+
+__global__ void k_fill_int(int n, int v, int* __restrict__ p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+__global__ void k_count_nbr(int64_t E, const int* __restrict__ nbr, int n_nodes,
+                            int* __restrict__ cnt) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int j = nbr[e];
+  if (j >= 0 && j < n_nodes) atomicAdd(cnt + j, 1);
+}
+
+// exclusive scan of cnt[0..n) into out[0..n], single workgroup of 1024.
+__global__ __launch_bounds__(1024) void k_scan(int n, const int* __restrict__ cnt,
+                                               int* __restrict__ out) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int chunk = (n + 1023) / 1024;
+  const int b = t * chunk, en = min(n, b + chunk);
+  int s = 0;
+  for (int i = b; i < en; ++i) s += cnt[i];
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = t ? part[t - 1] : 0;
+  for (int i = b; i < en; ++i) {
+    out[i] = run;
+    run += cnt[i];
+  }
+  if (t == 1023) out[n] = part[1023];
+}
+
+__global__ void k_scatter_perm(int64_t E, const int* __restrict__ nbr, int n_nodes,
+                               const int* __restrict__ ptr, int* __restrict__ cursor,
+                               int* __restrict__ perm) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int j = nbr[e];
+  if (j < 0 || j >= n_nodes) return;
+  const int slot = atomicAdd(cursor + j, 1);
+  perm[ptr[j] + slot] = (int)e;
+}
+
+// make each neighbour's edge list ascending in edge id (deterministic order)
+__global__ void k_sort_segments(int n, const int* __restrict__ ptr, int* __restrict__ perm) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int b = ptr[j], en = ptr[j + 1];
+  for (int i = b + 1; i < en; ++i) {
+    const int v = perm[i];
+    int k = i - 1;
+    while (k >= b && perm[k] > v) {
+      perm[k + 1] = perm[k];
+      --k;
+    }
+    perm[k + 1] = v;
+  }
+}
+
+// ------------------------------------------------------------ node ops
+// OnehotEmbedding + IrrepsLinear(is_embed) (node_embedding.py:39-48,
+// linear.py:37-44): row lookup of the pre-scaled embedding matrix.
+__global__ void k_embed(int n, const int* __restrict__ type, int nsp, const float* __restrict__ W,
+                        float* __restrict__ x, int* __restrict__ err) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)n * 128) return;
+  const int i = (int)(idx >> 7), c = (int)(idx & 127);
+  const int t = type[i];
+  if (t < 0 || t >= nsp) {
+    if (c == 0) atomicOr(err, 8);
+    x[idx] = 0.f;
+    return;
+  }
+  x[idx] = W[t * 128 + c];
+}
+
+// e3nn Gate (equivariant_gate.py:13-61; serial_code.py:256-347).
+// y: [224x0e (128 scalars | 96 gates) | 64x1e | 32x2e] -> x: [128x0e | 64x1e | 32x2e]
+__global__ void k_gate_fwd(int n, const float* __restrict__ y, float* __restrict__ x) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)n * 480) return;
+  const int64_t i = idx / 480;
+  const int c = (int)(idx - i * 480);
+  const float* yr = y + i * 576;
+  float v;
+  if (c < 128) v = act_fwd(yr[c]);
+  else if (c < 320) v = act_fwd(yr[128 + (c - 128) / 3]) * yr[224 + (c - 128)];
+  else v = act_fwd(yr[192 + (c - 320) / 5]) * yr[416 + (c - 320)];
+  x[idx] = v;
+}
+__global__ void k_gate_bwd(int n, const float* __restrict__ y, const float* __restrict__ dx,
+                           float* __restrict__ dy) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)n * 576) return;
+  const int64_t i = idx / 576;
+  const int c = (int)(idx - i * 576);
+  const float* yr = y + i * 576;
+  const float* dr = dx + i * 480;
+  float v;
+  if (c < 128) {
+    v = dr[c] * act_grad(yr[c]);
+  } else if (c < 192) {  // gate of 1e channel u
+    const int u = c - 128;
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) s += dr[128 + 3 * u + m] * yr[224 + 3 * u + m];
+    v = s * act_grad(yr[c]);
+  } else if (c < 224) {  // gate of 2e channel u
+    const int u = c - 192;
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < 5; ++m) s += dr[320 + 5 * u + m] * yr[416 + 5 * u + m];
+    v = s * act_grad(yr[c]);
+  } else if (c < 416) {
+    v = dr[128 + (c - 224)] * act_fwd(yr[128 + (c - 224) / 3]);
+  } else {
+    v = dr[320 + (c - 416)] * act_fwd(yr[192 + (c - 416) / 5]);
+  }
+  dy[idx] = v;
+}
+// last layer: 128 scalars, all activated
+__global__ void k_act_fwd(int64_t n, const float* __restrict__ y, float* __restrict__ x) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = act_fwd(y[i]);
+}
+__global__ void k_act_bwd(int64_t n, const float* __restrict__ y, const float* __restrict__ dx,
+                          float* __restrict__ dy) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dy[i] = dx[i] * act_grad(y[i]);
+}
+
+// readout (model_build.py:374-408) + SpeciesWiseRescale (scale.py:67-73):
+// E_i = scale[t] * <x_i, v> + shift[t], v = W_hidden @ W_energy (path weights folded)
+__global__ void k_readout(int n, const float* __restrict__ x, const float* __restrict__ v,
+                          const int* __restrict__ type, const float* __restrict__ scale,
+                          const float* __restrict__ shift, float* __restrict__ eat) {
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const float* xr = x + (int64_t)i * 128;
+  const float s = wave_sum(xr[lane] * v[lane] + xr[lane + 64] * v[lane + 64]);
+  if (lane == 0) {
+    const int t = type[i];
+    eat[i] = s * scale[t] + shift[t];
+  }
+}
+__global__ void k_readout_bwd(int n, const float* __restrict__ v, const int* __restrict__ type,
+                              const float* __restrict__ scale, float* __restrict__ dx) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)n * 128) return;
+  dx[idx] = scale[type[idx >> 7]] * v[idx & 127];
+}
+
+// per-block partial sums of a [n, stride] array's column `col` (fixed tree)
+__global__ void k_block_sum(int64_t n, const float* __restrict__ a, float* __restrict__ part) {
+  __shared__ float red[TPB];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  red[threadIdx.x] = i < n ? a[i] : 0.f;
+  __syncthreads();
+  for (int s = TPB / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+// out[q] = sum_b part[b * k + q], q < k, in block order (one thread per q)
+__global__ void k_final_sum(int nb, int k, const float* __restrict__ part, float* __restrict__ out) {
+  const int q = threadIdx.x;
+  if (q >= k) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * k + q];
+  out[q] = s;
+}
+
+// dh[j] = sum_{e: nbr[e] == j} dxc[e]  (transposed CSR, ascending edge order)
+__global__ void k_gather_rows(int n, int D, const int* __restrict__ ptr, const int* __restrict__ perm,
+                              const float* __restrict__ src, float* __restrict__ dst) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j >= n) return;
+  const int b = ptr[j], en = ptr[j + 1];
+  for (int c = lane; c < D; c += 64) {
+    float s = 0.f;
+    for (int q = b; q < en; ++q) s += src[(int64_t)perm[q] * D + c];
+    dst[(int64_t)j * D + c] = s;
+  }
+}
+
+// halo pack / unpack: rows by index (pair_e3gnn_parallel.cpp:803-933)
+__global__ void k_pack(int64_t n, int dim, const int* __restrict__ idx, const float* __restrict__ src,
+                       int64_t ss, float* __restrict__ dst) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * dim) return;
+  const int64_t r = t / dim;
+  const int c = (int)(t - r * dim);
+  dst[t] = src[(int64_t)idx[r] * ss + c];
+}
+__global__ void k_unpack(int64_t n, int dim, const int* __restrict__ idx, const float* __restrict__ src,
+                         float* __restrict__ dst, int64_t ds, int acc) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * dim) return;
+  const int64_t r = t / dim;
+  const int c = (int)(t - r * dim);
+  float* p = dst + (int64_t)idx[r] * ds + c;
+  *p = acc ? *p + src[t] : src[t];
+}
+
+}  // namespace
+
+#define LAUNCH(k, grid, ...)                                   \
+  do {                                                         \
+    if ((grid) > 0) hipLaunchKernelGGL(k, dim3(grid), dim3(TPB), 0, s, __VA_ARGS__); \
+  } while (0)
+
+hipError_t launch_edge_embed(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
+                             float* Y, float* emb, hipStream_t s) {
+  LAUNCH(k_edge_embed, nblk(E), E, vec, coeffs, rc, ron, Y, emb);
+  return hipGetLastError();
+}
+int edge_force_blocks(int64_t E) { return nblk(E); }
+hipError_t launch_edge_force(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
+                             const float* dY, const float* demb, float* fe, float* vir_part,
+                             hipStream_t s) {
+  LAUNCH(k_edge_force, nblk(E), E, vec, coeffs, rc, ron, dY, demb, fe, vir_part);
+  return hipGetLastError();
+}
+hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, const int* src_ptr,
+                             const int* src_perm, const float* fe, float* F, hipStream_t s) {
+  LAUNCH(k_atom_force, nblk(n_nodes), n_nodes, n_centers, row_ptr, src_ptr, src_perm, fe, F);
+  return hipGetLastError();
+}
+hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* center,
+                              const int* nbr, int* row_ptr, int* src_ptr, int* src_perm,
+                              int* cnt, int* err, hipStream_t s) {
+  LAUNCH(k_fill_int, nblk(n_centers + 1), n_centers + 1, 0, row_ptr);
+  LAUNCH(k_row_ptr, nblk(E), E, n_centers, n_nodes, center, nbr, row_ptr, err);
+  LAUNCH(k_fill_int, nblk(n_nodes), n_nodes, 0, cnt);
+  LAUNCH(k_count_nbr, nblk(E), E, nbr, n_nodes, cnt);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, n_nodes, cnt, src_ptr);
+  LAUNCH(k_fill_int, nblk(n_nodes), n_nodes, 0, cnt);
+  LAUNCH(k_scatter_perm, nblk(E), E, nbr, n_nodes, src_ptr, cnt, src_perm);
+  LAUNCH(k_sort_segments, nblk(n_nodes), n_nodes, src_ptr, src_perm);
+  return hipGetLastError();
+}
+hipError_t launch_embed(int n, const int* type, int nsp, const float* W, float* x, int* err,
+                        hipStream_t s) {
+  LAUNCH(k_embed, nblk((int64_t)n * 128), n, type, nsp, W, x, err);
+  return hipGetLastError();
+}
+hipError_t launch_gate_fwd(int n, bool last, const float* y, float* x, hipStream_t s) {
+  if (last) LAUNCH(k_act_fwd, nblk((int64_t)n * 128), (int64_t)n * 128, y, x);
+  else LAUNCH(k_gate_fwd, nblk((int64_t)n * 480), n, y, x);
+  return hipGetLastError();
+}
+hipError_t launch_gate_bwd(int n, bool last, const float* y, const float* dx, float* dy,
+                           hipStream_t s) {
+  if (last) LAUNCH(k_act_bwd, nblk((int64_t)n * 128), (int64_t)n * 128, y, dx, dy);
+  else LAUNCH(k_gate_bwd, nblk((int64_t)n * 576), n, y, dx, dy);
+  return hipGetLastError();
+}
+hipError_t launch_readout(int n, const float* x, const float* v, const int* type,
+                          const float* scale, const float* shift, float* eat, hipStream_t s) {
+  if (n > 0)
+    hipLaunchKernelGGL(k_readout, dim3((n + 3) / 4), dim3(256), 0, s, n, x, v, type, scale, shift,
+                       eat);
+  return hipGetLastError();
+}
+hipError_t launch_readout_bwd(int n, const float* v, const int* type, const float* scale,
+                              float* dx, hipStream_t s) {
+  LAUNCH(k_readout_bwd, nblk((int64_t)n * 128), n, v, type, scale, dx);
+  return hipGetLastError();
+}
+int sum_blocks(int64_t n) { return nblk(n); }
+hipError_t launch_sum(int64_t n, const float* a, float* part, float* out, hipStream_t s) {
+  const int nb = nblk(n);
+  if (nb == 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(float), s);
+    return hipGetLastError();
+  }
+  LAUNCH(k_block_sum, nb, n, a, part);
+  hipLaunchKernelGGL(k_final_sum, dim3(1), dim3(64), 0, s, nb, 1, part, out);
+  return hipGetLastError();
+}
+hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStream_t s) {
+  if (nb == 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(float) * k, s);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_final_sum, dim3(1), dim3(64), 0, s, nb, k, part, out);
+  return hipGetLastError();
+}
+hipError_t launch_gather_rows(int n, int D, const int* ptr, const int* perm, const float* src,
+                              float* dst, hipStream_t s) {
+  if (n > 0)
+    hipLaunchKernelGGL(k_gather_rows, dim3((n + 3) / 4), dim3(256), 0, s, n, D, ptr, perm, src,
+                       dst);
+  return hipGetLastError();
+}
+hipError_t launch_pack(int64_t n, int dim, const int* idx, const float* src, int64_t ss, float* dst,
+                       hipStream_t s) {
+  LAUNCH(k_pack, nblk(n * dim), n, dim, idx, src, ss, dst);
+  return hipGetLastError();
+}
+hipError_t launch_unpack(int64_t n, int dim, const int* idx, const float* src, float* dst,
+                         int64_t ds, int acc, hipStream_t s) {
+  LAUNCH(k_unpack, nblk(n * dim), n, dim, idx, src, dst, ds, acc);
+  return hipGetLastError();
+}
+
+}  // namespace e3gnn

@@ -1,0 +1,300 @@
+// uvu Clebsch-Gordan tensor product + neighbor segmented sum (forward) and its
+// input-gradient backward, gfx950.
+//
+// Reference: IrrepsConvolution.forward (sevenn/nn/convolution.py:104-123):
+//   msg[e] = TP(x[edge_index[1][e]], Y[e], w[e])      (e3nn uvu, per-edge weights)
+//   agg[i] = sum_{e: edge_index[0][e] == i} msg[e] / denominator   (message_gather :19-32)
+// with instruction order / sorted mid layout of convolution.py:72-95 (see the
+// path tables below; the weight slice of path p is w[e, woff + u], its message
+// slot mid[moff + u*(2*l3+1) + k]).
+//
+// Layout & mapping.  Edges are CSR-sorted by centre.  One wave owns one centre
+// (deterministic, no atomics): it walks the centre's edges in order, gathers the
+// neighbour row of the node features, and keeps the centre's message sums in
+// registers, lane = channel u (128-multiplicity block: 2 channels per lane;
+// 32-multiplicity block: the two half-waves take alternate edges).
+// The backward (gradients w.r.t. w, Y and the gathered x) is the transposed
+// contraction with the same mapping; d/dx is written per edge (dxc) and summed
+// per neighbour by the transposed-CSR gather in node.hip (deterministic).
+#include "common.h"
+#include "cg_tables.h"
+#include "tp.h"
+
+#include <type_traits>
+#include <utility>
+
+namespace e3gnn {
+namespace {
+
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+constexpr int yoff(int l) { return l == 0 ? 0 : (l == 1 ? 1 : 4); }
+
+template <class L, int L1>
+constexpr int part_mul() {
+  for (int p = 0; p < L::NP; ++p)
+    if (L::P[p].l1 == L1) return L::P[p].mul;
+  return 0;
+}
+template <class L, int L1>
+constexpr int part_xoff() {
+  for (int p = 0; p < L::NP; ++p)
+    if (L::P[p].l1 == L1) return L::P[p].xoff;
+  return 0;
+}
+
+// acc[k] += w * sum_ij C[i][j][k] x[i] y[j]
+template <int L1, int L2, int L3>
+__device__ __forceinline__ void tp_acc(const float* x, const float* y, float w, float* acc) {
+  float t[2 * L3 + 1];
+#pragma unroll
+  for (int k = 0; k < 2 * L3 + 1; ++k) t[k] = 0.f;
+  using C = CG<L1, L2, L3>;
+#pragma unroll
+  for (int q = 0; q < C::n; ++q) t[C::e[q].k] += C::e[q].c * (x[C::e[q].i] * y[C::e[q].j]);
+#pragma unroll
+  for (int k = 0; k < 2 * L3 + 1; ++k) acc[k] += w * t[k];
+}
+
+// ------------------------------------------------------------------ forward
+template <class L, int L1>
+__device__ __forceinline__ void fwd_part(int lane, int beg, int end, const int* __restrict__ nbr,
+                                         const float* __restrict__ Y, const float* __restrict__ w,
+                                         const float* __restrict__ h, float* __restrict__ out,
+                                         float denom) {
+  constexpr int MUL = part_mul<L, L1>();
+  if constexpr (MUL == 0) {
+    return;
+  } else {
+    constexpr int D1 = 2 * L1 + 1;
+    constexpr int XOFF = part_xoff<L, L1>();
+    constexpr bool PAIR = MUL == 32;
+    constexpr int UPL = MUL == 128 ? 2 : 1;
+    float acc[L::NP][UPL][5];
+    static_for<L::NP>([&](auto pi) {
+#pragma unroll
+      for (int s = 0; s < UPL; ++s)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) acc[pi][s][k] = 0.f;
+    });
+    const int u0 = PAIR ? (lane & 31) : lane;
+    constexpr int STEP = PAIR ? 2 : 1;
+    for (int e0 = beg; e0 < end; e0 += STEP) {
+      const int e = PAIR ? e0 + (lane >> 5) : e0;
+      if (PAIR && e >= end) continue;
+      const int j = nbr[e];
+      float y[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) y[q] = Y[(int64_t)e * 9 + q];
+      const float* wr = w + (int64_t)e * L::W;
+      const float* hr = h + (int64_t)j * L::DX + XOFF;
+#pragma unroll
+      for (int s = 0; s < UPL; ++s) {
+        const int u = u0 + 64 * s;
+        float x[D1];
+#pragma unroll
+        for (int i = 0; i < D1; ++i) x[i] = hr[u * D1 + i];
+        static_for<L::NP>([&](auto pi) {
+          constexpr PathDef p = L::P[pi];
+          if constexpr (p.l1 == L1) {
+            tp_acc<p.l1, p.l2, p.l3>(x, y + yoff(p.l2), wr[p.woff + u], acc[pi][s]);
+          }
+        });
+      }
+    }
+    static_for<L::NP>([&](auto pi) {
+      constexpr PathDef p = L::P[pi];
+      if constexpr (p.l1 == L1) {
+        constexpr int D3 = 2 * p.l3 + 1;
+#pragma unroll
+        for (int s = 0; s < UPL; ++s) {
+#pragma unroll
+          for (int k = 0; k < D3; ++k) {
+            float v = acc[pi][s][k];
+            if (PAIR) v += __shfl_down(v, 32, 64);
+            if (!PAIR || lane < 32) out[p.moff + (u0 + 64 * s) * D3 + k] = v / denom;
+          }
+        }
+      }
+    });
+  }
+}
+
+template <class L>
+__global__ __launch_bounds__(256) void k_tp_fwd(const int* __restrict__ row_ptr,
+                                                const int* __restrict__ nbr,
+                                                const float* __restrict__ Y,
+                                                const float* __restrict__ w,
+                                                const float* __restrict__ h,
+                                                float* __restrict__ agg, int n_centers,
+                                                float denom) {
+  const int c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (c >= n_centers) return;
+  const int lane = threadIdx.x & 63;
+  const int beg = row_ptr[c], end = row_ptr[c + 1];
+  float* out = agg + (int64_t)c * L::DM;
+  fwd_part<L, 0>(lane, beg, end, nbr, Y, w, h, out, denom);
+  fwd_part<L, 1>(lane, beg, end, nbr, Y, w, h, out, denom);
+  fwd_part<L, 2>(lane, beg, end, nbr, Y, w, h, out, denom);
+}
+
+// ------------------------------------------------------------------ backward
+// For path p, channel u, with gm = dE/dmsg (already / denominator):
+//   T[k]  = sum_ij C x_i y_j           dw      = sum_k gm_k T_k
+//   gw_k  = w gm_k
+//   dx_i += sum_jk C y_j gw_k          dy_j   += sum_ik C x_i gw_k
+template <int L1, int L2, int L3>
+__device__ __forceinline__ float tp_bwd(const float* x, const float* y, float w, const float* gm,
+                                        float* dx, float* dy) {
+  using C = CG<L1, L2, L3>;
+  float dwv = 0.f;
+#pragma unroll
+  for (int q = 0; q < C::n; ++q) {
+    const int i = C::e[q].i, j = C::e[q].j, k = C::e[q].k;
+    const float cg = C::e[q].c * gm[k];
+    dwv += cg * (x[i] * y[j]);
+    dx[i] += (cg * w) * y[j];
+    dy[j] += (cg * w) * x[i];
+  }
+  return dwv;
+}
+
+template <class L, int L1>
+struct BwdPart {
+  static constexpr int MUL = part_mul<L, L1>();
+  static constexpr int D1 = 2 * L1 + 1;
+  static constexpr int XOFF = part_xoff<L, L1>();
+  static constexpr int UPL = MUL == 128 ? 2 : 1;
+  float g[L::NP][UPL][5];
+
+  __device__ __forceinline__ void load(int lane, const float* __restrict__ gc) {
+    if constexpr (MUL > 0) {
+      const int u0 = MUL == 32 ? (lane & 31) : lane;
+      static_for<L::NP>([&](auto pi) {
+        constexpr PathDef p = L::P[pi];
+        if constexpr (p.l1 == L1) {
+          constexpr int D3 = 2 * p.l3 + 1;
+#pragma unroll
+          for (int s = 0; s < UPL; ++s)
+#pragma unroll
+            for (int k = 0; k < D3; ++k) g[pi][s][k] = gc[p.moff + (u0 + 64 * s) * D3 + k];
+        }
+      });
+    }
+  }
+
+  __device__ __forceinline__ void edge(int lane, int64_t e, int j, const float* y,
+                                       const float* __restrict__ w, const float* __restrict__ h,
+                                       float* __restrict__ dw, float* __restrict__ dxc,
+                                       float* dy) {
+    if constexpr (MUL > 0) {
+      if (MUL == 32 && lane >= 32) return;
+      const float* wr = w + e * L::W;
+      float* dwr = dw + e * L::W;
+      const float* hr = h + (int64_t)j * L::DX + XOFF;
+#pragma unroll
+      for (int s = 0; s < UPL; ++s) {
+        const int u = lane + 64 * s;
+        float x[D1], dx[D1];
+#pragma unroll
+        for (int i = 0; i < D1; ++i) {
+          x[i] = hr[u * D1 + i];
+          dx[i] = 0.f;
+        }
+        static_for<L::NP>([&](auto pi) {
+          constexpr PathDef p = L::P[pi];
+          if constexpr (p.l1 == L1) {
+            dwr[p.woff + u] =
+                tp_bwd<p.l1, p.l2, p.l3>(x, y + yoff(p.l2), wr[p.woff + u], g[pi][s], dx,
+                                         dy + yoff(p.l2));
+          }
+        });
+        if (dxc) {
+#pragma unroll
+          for (int i = 0; i < D1; ++i) dxc[e * L::DX + XOFF + u * D1 + i] = dx[i];
+        }
+      }
+    }
+  }
+};
+
+template <class L>
+__global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
+                                                const int* __restrict__ nbr,
+                                                const float* __restrict__ Y,
+                                                const float* __restrict__ w,
+                                                const float* __restrict__ h,
+                                                const float* __restrict__ gagg,
+                                                float* __restrict__ dw, float* __restrict__ dxc,
+                                                float* __restrict__ dYacc, int n_centers) {
+  const int c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (c >= n_centers) return;
+  const int lane = threadIdx.x & 63;
+  const int beg = row_ptr[c], end = row_ptr[c + 1];
+  const float* gc = gagg + (int64_t)c * L::DM;
+  BwdPart<L, 0> pa;
+  BwdPart<L, 1> pb;
+  BwdPart<L, 2> pc;
+  pa.load(lane, gc);
+  pb.load(lane, gc);
+  pc.load(lane, gc);
+  for (int e = beg; e < end; ++e) {
+    const int j = nbr[e];
+    float y[9], dy[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      y[q] = Y[(int64_t)e * 9 + q];
+      dy[q] = 0.f;
+    }
+    pa.edge(lane, e, j, y, w, h, dw, dxc, dy);
+    pb.edge(lane, e, j, y, w, h, dw, dxc, dy);
+    pc.edge(lane, e, j, y, w, h, dw, dxc, dy);
+    float mine = 0.f;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const float s = wave_sum(dy[q]);
+      if (lane == q) mine = s;
+    }
+    if (lane < 9) dYacc[(int64_t)e * 9 + lane] += mine;
+  }
+}
+
+}  // namespace
+
+template <class L>
+static hipError_t tp_fwd_impl(const TpArgs& a, hipStream_t s) {
+  if (a.n_centers <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tp_fwd<L>, dim3((a.n_centers + 3) / 4), dim3(256), 0, s, a.row_ptr, a.nbr,
+                     a.Y, a.w, a.h, a.agg, a.n_centers, a.denom);
+  return hipGetLastError();
+}
+template <class L>
+static hipError_t tp_bwd_impl(const TpArgs& a, hipStream_t s) {
+  if (a.n_centers <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tp_bwd<L>, dim3((a.n_centers + 3) / 4), dim3(256), 0, s, a.row_ptr, a.nbr,
+                     a.Y, a.w, a.h, a.gagg, a.dw, a.dxc, a.dYacc, a.n_centers);
+  return hipGetLastError();
+}
+
+hipError_t launch_tp_fwd(int kind, const TpArgs& a, hipStream_t s) {
+  switch (kind) {
+    case 0: return tp_fwd_impl<LayerFirst>(a, s);
+    case 1: return tp_fwd_impl<LayerMid>(a, s);
+    default: return tp_fwd_impl<LayerLast>(a, s);
+  }
+}
+hipError_t launch_tp_bwd(int kind, const TpArgs& a, hipStream_t s) {
+  switch (kind) {
+    case 0: return tp_bwd_impl<LayerFirst>(a, s);
+    case 1: return tp_bwd_impl<LayerMid>(a, s);
+    default: return tp_bwd_impl<LayerLast>(a, s);
+  }
+}
+
+}  // namespace e3gnn

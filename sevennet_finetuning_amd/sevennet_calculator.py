@@ -1,0 +1,74 @@
+"""ASE calculator on the HIP path -- mirrors SevenNetCalculator
+(sevenn/sevennet_calculator.py:17-157): same constructor arguments, same
+``results`` keys (energy, free_energy, energies, forces, stress) and the same
+ASE stress convention (-sigma in Voigt order xx yy zz yz xz xy, :151-156).
+
+ASE is optional: when importable the class derives from
+``ase.calculators.calculator.Calculator``; otherwise it duck-types the parts
+of that interface the reference uses (``calculate(atoms)`` / ``results``).
+"""
+import numpy as np
+import torch
+
+from . import _keys as KEY
+from .model import E3GNNModel
+from .util import pretrained_name_to_path, unlabeled_atoms_to_graph
+
+try:  # pragma: no cover - ase is not installed in this image
+    from ase.calculators.calculator import Calculator, all_changes
+except ImportError:  # minimal stand-in
+    all_changes = ('positions', 'numbers', 'cell', 'pbc')
+
+    class Calculator:
+        implemented_properties = []
+
+        def __init__(self, **kwargs):
+            self.results = {}
+            self.atoms = None
+
+        def calculate(self, atoms=None, properties=None, system_changes=all_changes):
+            self.atoms = atoms
+
+        def get_property(self, name, atoms=None):
+            self.calculate(atoms)
+            return self.results[name]
+
+
+class SevenNetCalculator(Calculator):
+    def __init__(self, model='SevenNet-0', file_type='checkpoint', device='auto',
+                 sevennet_config=None, **kwargs):
+        super().__init__(**kwargs)
+        file_type = file_type.lower()
+        if file_type not in ('checkpoint', 'torchscript', 'deployed'):
+            raise ValueError('file_type should be checkpoint or torchscript')
+        if isinstance(device, str) and device == 'auto':
+            device = torch.device('cuda', 0)
+        self.device = torch.device(device)
+        import os
+        path = model if os.path.isdir(str(model)) else pretrained_name_to_path(model)
+        self.model = E3GNNModel(path, device=self.device)
+        self.type_map = self.model.type_map()
+        self.cutoff = self.model.cutoff
+        self.sevennet_config = sevennet_config
+        self.implemented_properties = ['free_energy', 'energy', 'forces', 'stress', 'energies']
+
+    def calculate(self, atoms=None, properties=None, system_changes=all_changes):
+        Calculator.calculate(self, atoms, properties, system_changes)
+        if atoms is None:
+            raise ValueError('No atoms to evaluate')
+        data = unlabeled_atoms_to_graph(atoms, self.cutoff)
+        try:
+            data[KEY.NODE_FEATURE] = np.array([self.type_map[int(z)] for z in data[KEY.NODE_FEATURE]])
+        except KeyError as e:
+            raise ValueError(f'atomic number {e} is not a species of this model') from None
+        out = self.model(data)
+        energy = float(out[KEY.PRED_TOTAL_ENERGY].item())
+        self.results = {
+            'free_energy': energy,
+            'energy': energy,
+            'energies': out[KEY.ATOMIC_ENERGY].detach().cpu().reshape(len(atoms)).numpy(),
+            'forces': out[KEY.PRED_FORCE].detach().cpu().numpy(),
+        }
+        if KEY.PRED_STRESS in out:
+            self.results['stress'] = np.array(
+                (-out[KEY.PRED_STRESS]).detach().cpu().numpy()[[0, 1, 2, 4, 5, 3]])

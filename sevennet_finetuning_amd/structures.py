@@ -36,3 +36,63 @@ def si_diamond(cells, a=SI_A, sigma=0.05, seed=0):
 def mixed_symbols(n, seed=1):
     rng = np.random.default_rng(seed)
     return [MIXED_SYMBOLS[i] for i in rng.integers(0, len(MIXED_SYMBOLS), n)]
+
+
+# ASE's chemical_symbols order (index = atomic number), used for the
+# chemical_symbols_to_index type map (sevennet_calculator.py:80-102)
+CHEMICAL_SYMBOLS = (
+    'X H He Li Be B C N O F Ne Na Mg Al Si P S Cl Ar K Ca Sc Ti V Cr Mn Fe Co Ni Cu Zn Ga Ge '
+    'As Se Br Kr Rb Sr Y Zr Nb Mo Tc Ru Rh Pd Ag Cd In Sn Sb Te I Xe Cs Ba La Ce Pr Nd Pm Sm '
+    'Eu Gd Tb Dy Ho Er Tm Yb Lu Hf Ta W Re Os Ir Pt Au Hg Tl Pb Bi Po At Rn Fr Ra Ac Th Pa U '
+    'Np Pu Am Cm Bk Cf Es Fm Md No Lr Rf Db Sg Bh Hs Mt Ds Rg Cn Nh Fl Mc Lv Ts Og').split()
+
+
+def atomic_number(symbol):
+    return CHEMICAL_SYMBOLS.index(symbol)
+
+
+class Atoms:
+    """Minimal ase.Atoms stand-in (ASE is not installed here): the calculator
+    only calls get_positions / get_cell / get_pbc / get_atomic_numbers."""
+
+    def __init__(self, symbols=None, positions=None, cell=None, pbc=True, numbers=None):
+        if numbers is None:
+            numbers = [atomic_number(s) for s in symbols]
+        self.numbers = np.asarray(numbers, dtype=np.int64)
+        self.positions = np.asarray(positions, dtype=np.float64).reshape(-1, 3)
+        self.cell = np.zeros((3, 3)) if cell is None else np.asarray(cell, dtype=np.float64)
+        self.pbc = np.array([pbc] * 3 if np.isscalar(pbc) else pbc, dtype=bool)
+        self.calc = None
+
+    def __len__(self):
+        return len(self.numbers)
+
+    def get_positions(self):
+        return self.positions.copy()
+
+    def get_cell(self):
+        return self.cell.copy()
+
+    def get_pbc(self):
+        return self.pbc.copy()
+
+    def get_atomic_numbers(self):
+        return self.numbers.copy()
+
+    def get_chemical_symbols(self):
+        return [CHEMICAL_SYMBOLS[z] for z in self.numbers]
+
+    def get_volume(self):
+        return abs(np.linalg.det(self.cell))
+
+    def get_potential_energy(self):
+        self.calc.calculate(self)
+        return self.calc.results['energy']
+
+    def get_forces(self):
+        self.calc.calculate(self)
+        return self.calc.results['forces']
+
+    def get_stress(self):
+        self.calc.calculate(self)
+        return self.calc.results['stress']
