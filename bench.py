@@ -35,6 +35,11 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 matrix = vector peak (MI355X_MICROARCH.
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E peak
 
 
+def log(msg):
+    if int(os.environ.get('RANK', '0')) == 0:
+        print(f'[bench] {msg}', file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -106,6 +111,7 @@ def main():
     model = E3GNNModel(device=device)
     box = make_box(args.cells, device)
     n, E = box['n'], box['E']
+    log(f'box: {n} atoms, {E} edges; workspace after first step follows')
 
     def step():
         return model.energy_forces(box['types'], box['center'], box['nbr'], box['vec'])
@@ -114,8 +120,9 @@ def main():
         if world > 1:
             torch.distributed.barrier()
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         step()
+        log(f'warmup {i} done, workspace {model.workspace_bytes() / 1e9:.1f} GB')
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -38,6 +39,21 @@ thread_local std::string g_err;
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
+}
+
+// E3GNN_TRACE_ERRORS=1: report where HIP's thread-local error state got set
+bool trace_errors() {
+  static int on = [] {
+    const char* v = std::getenv("E3GNN_TRACE_ERRORS");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+void trace_point(const char* where) {
+  if (!trace_errors()) return;
+  hipError_t e = hipPeekAtLastError();
+  if (e != hipSuccess) std::fprintf(stderr, "[e3gnn] sticky HIP error %d (%s) at %s\n", (int)e,
+                                    hipGetErrorString(e), where);
 }
 
 #define HIPCHK(expr)                                                                          \
@@ -82,6 +98,18 @@ Irreps merged(const Irreps& ir) {
 struct DBuf {
   void* p = nullptr;
   size_t cap = 0;
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;  // owns device memory: never copied
+  DBuf& operator=(const DBuf&) = delete;
+  DBuf(DBuf&& o) noexcept : p(o.p), cap(o.cap) {
+    o.p = nullptr;
+    o.cap = 0;
+  }
+  DBuf& operator=(DBuf&& o) noexcept {
+    std::swap(p, o.p);
+    std::swap(cap, o.cap);
+    return *this;
+  }
   ~DBuf() {
     if (p) (void)hipFree(p);
   }
@@ -407,10 +435,12 @@ int e3gnn_abi_version(void) { return 1; }
 e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int device) {
   auto m = std::make_unique<e3gnn_model>();
   m->device = device;
+  trace_point("load:entry");
   if (hipSetDevice(device) != hipSuccess) {
     fail(E3GNN_ERR_HIP, "hipSetDevice failed");
     return nullptr;
   }
+  trace_point("load:hipSetDevice");
   minijson::Value man;
   {
     std::ifstream f(manifest_path);
@@ -480,6 +510,7 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
       v[c] = (float)(s / (std::sqrt(128.0) * 8.0));
     }
     if (upload(m->readout_v, v) != hipSuccess) throw std::runtime_error("upload");
+    trace_point("load:readout");
     const float* sc = get("rescale_atomic_energy.scale", m->nsp);
     const float* sh = get("rescale_atomic_energy.shift", m->nsp);
     if (upload(m->scale, std::vector<float>(sc, sc + m->nsp)) != hipSuccess ||
@@ -522,7 +553,9 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
           throw std::runtime_error("linear " + name);
         return L;
       };
+      trace_point("load:layer-begin");
       m->sc.push_back(mk(p + "_self_connection_intro.linear.weight", xin, gin, 1.0));
+      trace_point("load:sc");
       m->si1.push_back(mk(p + "_self_interaction_1.linear.weight", xin, xin, 1.0));
       // backward of si2 feeds dE/dagg_raw = dE/dagg / denominator (convolution.py:117-118)
       m->si2.push_back(mk(p + "_self_interaction_2.linear.weight", mid, gin, 1.0 / den));
@@ -556,11 +589,16 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
           upload(mm.w1t, scaled(w1, 64, 64, s1, true)) != hipSuccess ||
           upload(mm.w2t, scaled(w2, 64, W, s2, true)) != hipSuccess)
         throw std::runtime_error("upload mlp");
+      trace_point("load:mlp");
     }
   } catch (const std::exception& ex) {
     fail(E3GNN_ERR_IO, std::string("model load: ") + ex.what());
     return nullptr;
   }
+  trace_point("load:exit");
+  // every HIP call above was checked; do not leave the host application's
+  // thread-local HIP error state dirty (torch re-reads it after its own calls)
+  (void)hipGetLastError();
   return m.release();
 }
 

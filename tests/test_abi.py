@@ -30,8 +30,11 @@ def test_abi_version_and_errors():
     assert lib.e3gnn_ctx_create(None) is None
 
 
-def test_library_is_gfx950_code_object():
-    out = subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-objdump', '--offloading', _lib.LIB_PATH],
-                         capture_output=True, text=True)
+def test_library_is_gfx950_code_object(tmp_path):
+    import shutil
+    lib = tmp_path / 'lib.so'   # --offloading extracts bundles next to its input
+    shutil.copy(_lib.LIB_PATH, lib)
+    out = subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-objdump', '--offloading', str(lib)],
+                         capture_output=True, text=True, cwd=tmp_path)
     text = out.stdout + out.stderr
     assert 'gfx950' in text

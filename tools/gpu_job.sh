@@ -1,0 +1,29 @@
+#!/bin/bash
+# GPU-box job: each GPU step under its own time limit; stop on any crash-like
+# exit (fault/abort/segfault/timeout), continue only past ordinary test failures.
+set -u
+export PYTHONUNBUFFERED=1
+mkdir -p gpurun_out
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "=== $name: $*"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) step tests 600 python -m pytest tests -m gpu -x -q ;;
+    testsall) step tests 900 python -m pytest tests -m gpu -q ;;
+    layer) step layer 300 python -m pytest tests -m gpu -q -k layerwise ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py --steps 5 --warmup 2 ;;
+    benchq) step bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10 ;;
+    bench10k) step bench10k 300 python bench.py --cells 11 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --profile-only ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
