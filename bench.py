@@ -75,8 +75,11 @@ def cpu_baseline(seconds):
     from oracle.neighbor import neighbor_list
     from oracle.sevennet_ref import SevenNet0Ref
     from sevennet_finetuning_amd.structures import si_diamond
-    threads = len(os.sched_getaffinity(0))
+    # the box's CPU share is OMP_NUM_THREADS (16); sched_getaffinity reports the
+    # whole machine there, and oversubscribing it stalls the run
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get('OMP_NUM_THREADS', '16')))
     torch.set_num_threads(threads)
+    log(f'cpu baseline: {threads} threads, ~{seconds:.0f} s')
     ref = SevenNet0Ref(dtype=torch.float32)
     pos, cell = si_diamond((3, 3, 3), sigma=0.05)
     ei, sh = neighbor_list(pos, cell, 5.0)
@@ -137,6 +140,7 @@ def main():
         dt = float(t)
     ms = dt / args.steps * 1e3
     value = world * n * args.steps / dt
+    log(f'timed: {ms:.3f} ms/step')
     energy = float(out['energy'])
 
     roofline, kernels = None, None
@@ -146,6 +150,7 @@ def main():
         step()
         stats = model.kernel_stats()
         model.set_timing(False)
+        log('stats pass done')
         total = sum(s['ms'] for s in stats.values())
         kernels = {k: {'ms': round(v['ms'], 3), 'launches': v['launches'],
                        'tflops': round(v['flops'] / (v['ms'] * 1e9), 2) if v['ms'] else 0.0,
