@@ -121,6 +121,11 @@ int e3gnn_halo_unpack(const int32_t* idx, int64_t n, int dim, const float* src, 
                       int64_t dst_stride, int accumulate, void* stream);
 
 /* ---- diagnostics ---- */
+/* Kernel implementation of the convolution: 0 = fused radial-MLP + tensor
+ * product (default), 1 = unfused v1 kernels (per-edge weights materialised in
+ * HBM; kept as an independent cross-check).  Env E3GNN_IMPL=v1 sets 1.
+ * Takes effect at the next e3gnn_graph_set / e3gnn_energy_forces. */
+int e3gnn_set_impl(e3gnn_ctx* c, int impl);
 /* enable per-kernel-class HIP-event timing on the context */
 int e3gnn_set_timing(e3gnn_ctx* c, int enable);
 /* Number of kernel classes recorded; fills up to `max` entries: name (static

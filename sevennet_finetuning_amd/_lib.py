@@ -37,6 +37,7 @@ SIGNATURES = {
     'e3gnn_forces': (_c_int, [_vp, _vp, _vp, _vp, _vp]),
     'e3gnn_halo_pack': (_c_int, [_vp, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
     'e3gnn_halo_unpack': (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_i64, _c_int, _vp]),
+    'e3gnn_set_impl': (_c_int, [_vp, _c_int]),
     'e3gnn_set_timing': (_c_int, [_vp, _c_int]),
     'e3gnn_kernel_stats': (_c_int, [_vp, _P(_cp), _P(ctypes.c_double), _P(_c_i64),
                                     _P(ctypes.c_double), _P(ctypes.c_double), _c_int]),

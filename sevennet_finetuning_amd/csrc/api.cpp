@@ -26,6 +26,7 @@
 #include "../../include/e3gnn.h"
 #include "cg_tables.h"
 #include "common.h"
+#include "fused.h"
 #include "minijson.h"
 #include "node.h"
 #include "tp.h"
@@ -178,7 +179,7 @@ struct Pending {
 const char* kClassNames[] = {"graph_build", "edge_embed",  "node_linear", "radial_mlp_fwd",
                              "tp_fwd",      "gate_fwd",    "readout",     "gate_bwd",
                              "tp_bwd",      "radial_mlp_bwd", "gather_src", "edge_force",
-                             "atom_force",  "embed"};
+                             "atom_force",  "embed", "conv_fwd_fused", "conv_bwd_fused"};
 enum Cls {
   C_GRAPH,
   C_EMBED_EDGE,
@@ -194,6 +195,8 @@ enum Cls {
   C_EDGE_FORCE,
   C_ATOM_FORCE,
   C_EMBED_NODE,
+  C_CONV_FWD,
+  C_CONV_BWD,
   C_NCLS
 };
 
@@ -209,7 +212,14 @@ struct e3gnn_ctx {
   int64_t n = 0, nl = 0, E = 0;
   // graph
   DBuf type, center, nbr, vec, row_ptr, src_ptr, src_perm, cnt, err;
-  DBuf Y, emb, dY, demb, fe;
+  DBuf Y, emb, dY, dgu, demb, fe;
+  // 0: fused radial-MLP + TP kernels (fused.hip); 1: the unfused v1 kernels
+  // (materialised per-edge weights; kept as an independent cross-check)
+  int impl = [] {
+    const char* v = std::getenv("E3GNN_IMPL");
+    return (v && std::string(v) == "v1") ? 1 : 0;
+  }();
+  int graph_impl = 0;  // impl in force since the last e3gnn_graph_set (buffers sized for it)
   // per layer
   std::vector<DBuf> x, grad, h, y, w, a1, a2;
   DBuf H1, H2, agg, dw, dxc, dy, dh, eat, part, vpart, scratch6;
@@ -425,6 +435,11 @@ void dense_cg(float* out) {
   for (int q = 0; q < T::n; ++q)
     out[(T::e[q].i * (2 * B + 1) + T::e[q].j) * (2 * C + 1) + T::e[q].k] = T::e[q].c;
 }
+MlpW mlp_ptrs(const e3gnn_model* m, int t) {
+  const auto& mm = m->mlp[t];
+  return MlpW{mm.w0.f(), mm.w1.f(), mm.w2.f(), mm.w2t.f()};
+}
+
 }  // namespace
 
 extern "C" {
@@ -679,8 +694,13 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   HIPCHK(c->dY.ensure(E * 9 * F));
   HIPCHK(c->demb.ensure(E * 8 * F));
   HIPCHK(c->fe.ensure(E * 3 * F));
-  HIPCHK(c->H1.ensure(E * 64 * F));
-  HIPCHK(c->H2.ensure(E * 64 * F));
+  HIPCHK(c->dgu.ensure(E * 3 * F));
+  const bool v1 = c->impl == 1;
+  c->graph_impl = c->impl;
+  if (v1) {
+    HIPCHK(c->H1.ensure(E * 64 * F));
+    HIPCHK(c->H2.ensure(E * 64 * F));
+  }
   int maxW = 0, maxDM = 0;
   for (int t = 0; t < m->nlayer; ++t) {
     const int dx = irreps_dim(m->irreps[t]), dg = irreps_dim(m->gin[t]);
@@ -690,15 +710,17 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
     HIPCHK(c->grad[t].ensure(std::max<int64_t>(n, 1) * dx * F));
     HIPCHK(c->h[t].ensure(n * dx * F));
     HIPCHK(c->y[t].ensure(nl * dg * F));
-    HIPCHK(c->w[t].ensure(E * m->W[t] * F));
-    HIPCHK(c->a1[t].ensure(E * 64 * F));
-    HIPCHK(c->a2[t].ensure(E * 64 * F));
+    if (v1) {
+      HIPCHK(c->w[t].ensure(E * m->W[t] * F));
+      HIPCHK(c->a1[t].ensure(E * 64 * F));
+      HIPCHK(c->a2[t].ensure(E * 64 * F));
+    }
   }
   const int dlast = irreps_dim(m->irreps[m->nlayer]);
   HIPCHK(c->x[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
   HIPCHK(c->grad[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
   HIPCHK(c->agg.ensure(nl * maxDM * F));
-  HIPCHK(c->dw.ensure(E * maxW * F));
+  if (v1) HIPCHK(c->dw.ensure(E * maxW * F));
   HIPCHK(c->dxc.ensure(E * 480 * F));
   HIPCHK(c->dy.ensure(nl * 576 * F));
   HIPCHK(c->dh.ensure(n * 480 * F));
@@ -741,6 +763,7 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   }
   if (E > 0) {
     HIPCHK(hipMemsetAsync(c->dY.p, 0, E * 9 * F, s));
+    HIPCHK(hipMemsetAsync(c->dgu.p, 0, E * 3 * F, s));
     HIPCHK(hipMemsetAsync(c->demb.p, 0, E * 8 * F, s));
   }
   return E3GNN_OK;
@@ -762,6 +785,24 @@ int e3gnn_layer_forward(e3gnn_ctx* c, int t, void* stream) {
     Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], n));
     HIPCHK(launch_gemm(lin_fwd(*m->si1[t], c->x[t].f(), dx, c->h[t].f(), dx, n, 0), s));
   }
+  if (c->graph_impl == 0) {
+    // fused radial MLP + tensor product + segmented sum (fused.hip)
+    Region r(c, s, C_CONV_FWD,
+             tp_flops_per_edge(kind) * E + 2.0 * E * (8 * 64 + 64 * 64 + 64 * W),
+             (double)E * 4 * (8 + 9 + 2 + dx) + nl * 4.0 * dm);
+    FusedArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.row_ptr = c->row_ptr.i();
+    a.nbr = c->nbr.i();
+    a.emb = c->emb.f();
+    a.Y = c->Y.f();
+    a.h = c->h[t].f();
+    a.agg = c->agg.f();
+    a.W = mlp_ptrs(m, t);
+    a.n_centers = (int)nl;
+    a.denom = m->denom[t];
+    HIPCHK(launch_conv_fwd(kind, a, s));
+  } else {
   // radial MLP: emb -> 64 -> 64 -> W  (convolution.py:97-106)
   {
     Region r(c, s, C_MLP_FWD, 2.0 * E * (8 * 64 + 64 * 64 + 64 * W),
@@ -802,6 +843,7 @@ int e3gnn_layer_forward(e3gnn_ctx* c, int t, void* stream) {
     a.n_centers = (int)nl;
     a.denom = m->denom[t];
     HIPCHK(launch_tp_fwd(kind, a, s));
+  }
   }
   // self_interaction_2 + self_connection (intro/outro)
   {
@@ -857,6 +899,25 @@ int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
     Region r(c, s, C_LINEAR, lin_flops(*m->si2[t], nl));
     HIPCHK(launch_gemm(lin_bwd(*m->si2[t], c->dy.f(), dg, c->agg.f(), dm, nl, 0), s));
   }
+  if (c->graph_impl == 0) {
+    Region r(c, s, C_CONV_BWD,
+             3.0 * tp_flops_per_edge(kind) * E + 2.0 * E * (2 * 64 * W + 2 * (8 * 64 + 64 * 64)),
+             (double)E * 4 * (8 + 9 + 2 + 3 + 8 + dx + (t > 0 ? dx : 0)) + nl * 4.0 * dm);
+    FusedArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.row_ptr = c->row_ptr.i();
+    a.nbr = c->nbr.i();
+    a.emb = c->emb.f();
+    a.Y = c->Y.f();
+    a.h = c->h[t].f();
+    a.gagg = c->agg.f();
+    a.dxc = t > 0 ? c->dxc.f() : nullptr;
+    a.dgu = c->dgu.f();
+    a.demb = c->demb.f();
+    a.W = mlp_ptrs(m, t);
+    a.n_centers = (int)nl;
+    HIPCHK(launch_conv_bwd(kind, a, s));
+  } else {
   {
     Region r(c, s, C_TP_BWD, 3.0 * tp_flops_per_edge(kind) * E,
              (double)E * 4 * (2 * W + 2 * 9 + dx + (t > 0 ? dx : 0) + 2) + nl * 4.0 * dm);
@@ -898,6 +959,7 @@ int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
     add_prob(b, p);
     HIPCHK(launch_gemm(b, s));
   }
+  }
   if (t > 0) {
     {
       Region r(c, s, C_GATHER, 0, (double)E * 4 * (dx + 1) + n * 4.0 * dx);
@@ -920,7 +982,7 @@ int e3gnn_forces(e3gnn_ctx* c, float* forces, float* virial6, float* edge_grad, 
   {
     Region r(c, s, C_EDGE_FORCE, 0, (double)E * 4 * (3 + 9 + 8 + 3));
     HIPCHK(launch_edge_force(E, c->vec.f(), m->coeffs.f(), m->cutoff, m->r_on, c->dY.f(),
-                             c->demb.f(), c->fe.f(), c->vpart.f(), s));
+                             c->dgu.f(), c->demb.f(), c->fe.f(), c->vpart.f(), s));
     HIPCHK(launch_final_sum(edge_force_blocks(E), 6, c->vpart.f(),
                             virial6 ? virial6 : c->scratch6.f(), s));
   }
@@ -962,6 +1024,13 @@ int e3gnn_halo_unpack(const int32_t* idx, int64_t n, int dim, const float* src, 
                       int64_t dst_stride, int accumulate, void* stream) {
   if (n < 0 || dim <= 0) return fail(E3GNN_ERR_ARG, "bad halo size");
   HIPCHK(launch_unpack(n, dim, idx, src, dst, dst_stride, accumulate, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_set_impl(e3gnn_ctx* c, int impl) {
+  if (!c) return fail(E3GNN_ERR_ARG, "null context");
+  if (impl != 0 && impl != 1) return fail(E3GNN_ERR_ARG, "impl must be 0 (fused) or 1 (v1)");
+  c->impl = impl;
   return E3GNN_OK;
 }
 
@@ -1009,7 +1078,7 @@ int64_t e3gnn_workspace_bytes(const e3gnn_ctx* c) {
   if (!c) return 0;
   int64_t b = 0;
   const DBuf* fixed[] = {&c->type, &c->center, &c->nbr, &c->vec, &c->row_ptr, &c->src_ptr,
-                         &c->src_perm, &c->cnt, &c->err, &c->Y, &c->emb, &c->dY, &c->demb,
+                         &c->src_perm, &c->cnt, &c->err, &c->Y, &c->emb, &c->dY, &c->dgu, &c->demb,
                          &c->fe, &c->H1, &c->H2, &c->agg, &c->dw, &c->dxc, &c->dy, &c->dh,
                          &c->eat, &c->part, &c->vpart, &c->scratch6};
   for (auto* d : fixed) b += (int64_t)d->cap;

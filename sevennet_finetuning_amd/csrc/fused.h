@@ -1,0 +1,34 @@
+// Launch API of the fused radial-MLP + tensor-product kernels (fused.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace e3gnn {
+
+struct MlpW {
+  const float* w0;   // [8][64]   layer0 / sqrt(8)
+  const float* w1;   // [64][64]  layer1 / 8
+  const float* w2;   // [64][W]   layer2 / 8
+  const float* w2t;  // [W][64]   transpose of w2
+};
+
+struct FusedArgs {
+  const int* row_ptr;
+  const int* nbr;
+  const float* emb;   // [E, 8]
+  const float* Y;     // [E, 9]
+  const float* h;     // [n_nodes, DX]
+  float* agg;         // fwd out [n_centers, DM]
+  const float* gagg;  // bwd in  [n_centers, DM] (dE/dagg / denominator)
+  float* dxc;         // bwd out [E, DX] (nullable)
+  float* dgu;         // bwd in/out [E, 3]  dE/du accumulated over layers
+  float* demb;        // bwd in/out [E, 8]  dE/demb accumulated over layers
+  MlpW W;
+  int n_centers;
+  float denom;
+};
+
+hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s);
+hipError_t launch_conv_bwd(int kind, const FusedArgs& a, hipStream_t s);
+
+}  // namespace e3gnn

@@ -51,8 +51,8 @@ __global__ void k_edge_embed(int64_t E, const float* __restrict__ vec, const flo
 // the same through autograd).  Also writes per-block virial partials.
 __global__ void k_edge_force(int64_t E, const float* __restrict__ vec, const float* __restrict__ coeffs,
                              float rc, float ron, const float* __restrict__ dY,
-                             const float* __restrict__ demb, float* __restrict__ fe,
-                             float* __restrict__ vir_part) {
+                             const float* __restrict__ dgu, const float* __restrict__ demb,
+                             float* __restrict__ fe, float* __restrict__ vir_part) {
   __shared__ float red[6][TPB];
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float v6[6] = {0, 0, 0, 0, 0, 0};
@@ -68,6 +68,11 @@ __global__ void k_edge_force(int64_t E, const float* __restrict__ vec, const flo
     gx += c * (z * g[4] + y * g[5]) - s5 * x * g[6] - c * x * g[8];
     gy += c * (x * g[5] + z * g[7]) + 2.f * s5 * y * g[6];
     gz += c * (x * g[4] + y * g[7]) - s5 * z * g[6] + c * z * g[8];
+    if (dgu) {  // dE/du accumulated directly by the fused kernels
+      gx += dgu[3 * e];
+      gy += dgu[3 * e + 1];
+      gz += dgu[3 * e + 2];
+    }
     const float dot = gx * x + gy * y + gz * z;
     float fx = (gx - dot * x) / r, fy = (gy - dot * y) / r, fz = (gz - dot * z) / r;
     // radial part
@@ -335,13 +340,23 @@ __global__ void k_block_sum(int64_t n, const float* __restrict__ a, float* __res
   }
   if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
-// out[q] = sum_b part[b * k + q], q < k, in block order (one thread per q)
-__global__ void k_final_sum(int nb, int k, const float* __restrict__ part, float* __restrict__ out) {
-  const int q = threadIdx.x;
-  if (q >= k) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(int64_t)b * k + q];
-  out[q] = s;
+// out[q] = sum_b part[b * k + q], q < k: one block of 256, thread t sums the
+// strided subset b = t, t+256, ... in order, then a fixed tree (deterministic)
+__global__ __launch_bounds__(256) void k_final_sum(int nb, int k, const float* __restrict__ part,
+                                                   float* __restrict__ out) {
+  __shared__ float red[TPB];
+  for (int q = 0; q < k; ++q) {
+    float s = 0.f;
+    for (int b = threadIdx.x; b < nb; b += TPB) s += part[(int64_t)b * k + q];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = TPB / 2; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[q] = red[0];
+    __syncthreads();
+  }
 }
 
 // dh[j] = sum_{e: nbr[e] == j} dxc[e]  (transposed CSR, ascending edge order)
@@ -391,9 +406,9 @@ hipError_t launch_edge_embed(int64_t E, const float* vec, const float* coeffs, f
 }
 int edge_force_blocks(int64_t E) { return nblk(E); }
 hipError_t launch_edge_force(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
-                             const float* dY, const float* demb, float* fe, float* vir_part,
-                             hipStream_t s) {
-  LAUNCH(k_edge_force, nblk(E), E, vec, coeffs, rc, ron, dY, demb, fe, vir_part);
+                             const float* dY, const float* dgu, const float* demb, float* fe,
+                             float* vir_part, hipStream_t s) {
+  LAUNCH(k_edge_force, nblk(E), E, vec, coeffs, rc, ron, dY, dgu, demb, fe, vir_part);
   return hipGetLastError();
 }
 hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, const int* src_ptr,
@@ -450,7 +465,7 @@ hipError_t launch_sum(int64_t n, const float* a, float* part, float* out, hipStr
     return hipGetLastError();
   }
   LAUNCH(k_block_sum, nb, n, a, part);
-  hipLaunchKernelGGL(k_final_sum, dim3(1), dim3(64), 0, s, nb, 1, part, out);
+  hipLaunchKernelGGL(k_final_sum, dim3(1), dim3(TPB), 0, s, nb, 1, part, out);
   return hipGetLastError();
 }
 hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStream_t s) {
@@ -458,7 +473,7 @@ hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStr
     (void)hipMemsetAsync(out, 0, sizeof(float) * k, s);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_final_sum, dim3(1), dim3(64), 0, s, nb, k, part, out);
+  hipLaunchKernelGGL(k_final_sum, dim3(1), dim3(TPB), 0, s, nb, k, part, out);
   return hipGetLastError();
 }
 hipError_t launch_gather_rows(int n, int D, const int* ptr, const int* perm, const float* src,

@@ -109,6 +109,10 @@ class E3GNNModel:
             out['edge_grad'] = egrad
         return out
 
+    def set_impl(self, impl):
+        """'fused' (default) or 'v1' (unfused kernels, cross-check)."""
+        _lib.check(self.lib.e3gnn_set_impl(self._ctx, {'fused': 0, 'v1': 1}[impl]))
+
     def set_timing(self, enable=True):
         _lib.check(self.lib.e3gnn_set_timing(self._ctx, int(enable)))
 
