@@ -136,6 +136,10 @@ int e3gnn_reset_stats(e3gnn_ctx* c);
 /* Dense coupling table C_{l1 l2 l3}[m1][m2][m3] * sqrt(2 l3 + 1) used by the
  * kernels (host memory, (2l1+1)(2l2+1)(2l3+1) floats). */
 int e3gnn_cg_table(int l1, int l2, int l3, float* out);
+/* Device pointer + element count of an internal workspace buffer (debug /
+ * layer-wise parity tests): "x","grad" (layer 0..L), "h","y","agg" (0..L-1;
+ * "agg" holds the last layer computed), "Y","emb","dY","dgu","demb","dxc","fe". */
+float* e3gnn_debug_ptr(e3gnn_ctx* c, const char* name, int layer, int64_t* numel);
 /* Bytes of device workspace currently held by the context. */
 int64_t e3gnn_workspace_bytes(const e3gnn_ctx* c);
 

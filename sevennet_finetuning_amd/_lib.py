@@ -44,6 +44,7 @@ SIGNATURES = {
     'e3gnn_reset_stats': (_c_int, [_vp]),
     'e3gnn_cg_table': (_c_int, [_c_int, _c_int, _c_int, _P(_c_f)]),
     'e3gnn_workspace_bytes': (_c_i64, [_vp]),
+    'e3gnn_debug_ptr': (_vp, [_vp, _cp, _c_int, _P(_c_i64)]),
 }
 
 

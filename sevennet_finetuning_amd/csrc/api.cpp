@@ -668,6 +668,10 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   if (n_local < 0 || n_ghost < 0 || n_edges < 0) return fail(E3GNN_ERR_ARG, "negative size");
   if (n_local + n_ghost > (1LL << 30) || n_edges > (1LL << 31) - 1)
     return fail(E3GNN_ERR_ARG, "graph too large for int32 indices");
+  // the fused kernels address node features through 32-bit buffer offsets
+  if ((n_local + n_ghost) * 480LL * 4 > 0x7fffffffLL || n_local * 3136LL * 4 > 0x7fffffffLL)
+    return fail(E3GNN_ERR_ARG,
+                "more than 171k owned atoms (or 1.1M nodes) per device: shard the system");
   if ((n_local + n_ghost > 0 && !type) || (n_edges > 0 && (!edge_center || !edge_nbr || !edge_vec)))
     return fail(E3GNN_ERR_ARG, "null input array");
   e3gnn_model* m = c->m;
@@ -721,7 +725,7 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   HIPCHK(c->grad[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
   HIPCHK(c->agg.ensure(nl * maxDM * F));
   if (v1) HIPCHK(c->dw.ensure(E * maxW * F));
-  HIPCHK(c->dxc.ensure(E * 480 * F));
+  if (v1) HIPCHK(c->dxc.ensure(E * 480 * F));
   HIPCHK(c->dy.ensure(nl * 576 * F));
   HIPCHK(c->dh.ensure(n * 480 * F));
   HIPCHK(c->eat.ensure(std::max<int64_t>(nl, 1) * F));
@@ -800,6 +804,7 @@ int e3gnn_layer_forward(e3gnn_ctx* c, int t, void* stream) {
     a.agg = c->agg.f();
     a.W = mlp_ptrs(m, t);
     a.n_centers = (int)nl;
+    a.n_nodes = (int)n;
     a.denom = m->denom[t];
     HIPCHK(launch_conv_fwd(kind, a, s));
   } else {
@@ -911,11 +916,17 @@ int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
     a.Y = c->Y.f();
     a.h = c->h[t].f();
     a.gagg = c->agg.f();
-    a.dxc = t > 0 ? c->dxc.f() : nullptr;
+    a.center = c->center.i();
+    a.n_edges = (int)E;
+    a.src_ptr = c->src_ptr.i();
+    a.src_perm = c->src_perm.i();
+    a.dh = t > 0 ? c->dh.f() : nullptr;
+    a.scratch_dh = c->dh.f();
     a.dgu = c->dgu.f();
     a.demb = c->demb.f();
     a.W = mlp_ptrs(m, t);
     a.n_centers = (int)nl;
+    a.n_nodes = (int)n;
     HIPCHK(launch_conv_bwd(kind, a, s));
   } else {
   {
@@ -961,7 +972,7 @@ int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
   }
   }
   if (t > 0) {
-    {
+    if (c->graph_impl == 1) {  // fused path writes dh directly (k_conv_bwd_x)
       Region r(c, s, C_GATHER, 0, (double)E * 4 * (dx + 1) + n * 4.0 * dx);
       HIPCHK(launch_gather_rows((int)n, dx, c->src_ptr.i(), c->src_perm.i(), c->dxc.f(),
                                 c->dh.f(), s));
@@ -1072,6 +1083,30 @@ int e3gnn_cg_table(int l1, int l2, int l3, float* out) {
 #undef CGCASE
     default: return fail(E3GNN_ERR_ARG, "no coupling table for this (l1,l2,l3)");
   }
+}
+
+float* e3gnn_debug_ptr(e3gnn_ctx* c, const char* name, int layer, int64_t* numel) {
+  if (!c || !name) return nullptr;
+  const std::string n(name);
+  const e3gnn_model* m = c->m;
+  const int L = m->nlayer;
+  auto ok = [&](int lo, int hi) { return layer >= lo && layer <= hi; };
+  float* p = nullptr;
+  int64_t k = 0;
+  if (n == "x" && ok(0, L)) { p = c->x[layer].f(); k = c->n * irreps_dim(m->irreps[layer]); }
+  else if (n == "grad" && ok(0, L)) { p = c->grad[layer].f(); k = c->n * irreps_dim(m->irreps[layer]); }
+  else if (n == "h" && ok(0, L - 1)) { p = c->h[layer].f(); k = c->n * irreps_dim(m->irreps[layer]); }
+  else if (n == "y" && ok(0, L - 1)) { p = c->y[layer].f(); k = c->nl * irreps_dim(m->gin[layer]); }
+  else if (n == "agg" && ok(0, L - 1)) { p = c->agg.f(); k = c->nl * irreps_dim(m->mid[layer]); }
+  else if (n == "Y") { p = c->Y.f(); k = c->E * 9; }
+  else if (n == "emb") { p = c->emb.f(); k = c->E * 8; }
+  else if (n == "dY") { p = c->dY.f(); k = c->E * 9; }
+  else if (n == "dgu") { p = c->dgu.f(); k = c->E * 3; }
+  else if (n == "demb") { p = c->demb.f(); k = c->E * 8; }
+  else if (n == "dxc") { p = c->dxc.f(); k = c->E * 480; }
+  else if (n == "fe") { p = c->fe.f(); k = c->E * 3; }
+  if (numel) *numel = p ? k : 0;
+  return p;
 }
 
 int64_t e3gnn_workspace_bytes(const e3gnn_ctx* c) {

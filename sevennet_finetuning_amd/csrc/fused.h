@@ -14,17 +14,23 @@ struct MlpW {
 
 struct FusedArgs {
   const int* row_ptr;
+  const int* center;  // [E] edge_index[0] (sorted)
   const int* nbr;
   const float* emb;   // [E, 8]
   const float* Y;     // [E, 9]
   const float* h;     // [n_nodes, DX]
   float* agg;         // fwd out [n_centers, DM]
   const float* gagg;  // bwd in  [n_centers, DM] (dE/dagg / denominator)
-  float* dxc;         // bwd out [E, DX] (nullable)
+  const int* src_ptr;  // [n_nodes + 1] transposed CSR (edges by edge_index[1])
+  const int* src_perm; // [E]
+  float* dh;           // bwd out [n_nodes, DX]: dE/dx of the gathered features (nullable)
+  float* scratch_dh;   // [n_nodes, DX] sink used when dh is null
   float* dgu;         // bwd in/out [E, 3]  dE/du accumulated over layers
   float* demb;        // bwd in/out [E, 8]  dE/demb accumulated over layers
   MlpW W;
   int n_centers;
+  int n_edges;
+  int n_nodes;
   float denom;
 };
 

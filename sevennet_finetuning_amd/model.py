@@ -131,6 +131,24 @@ class E3GNNModel:
     def reset_stats(self):
         _lib.check(self.lib.e3gnn_reset_stats(self._ctx))
 
+    def debug_buffer(self, name, layer=0):
+        """Host copy (numpy fp32) of an internal workspace buffer (after a
+        synchronising call)."""
+        import ctypes
+        import numpy as np
+        n = ctypes.c_int64()
+        ptr = self.lib.e3gnn_debug_ptr(self._ctx, name.encode(), layer, ctypes.byref(n))
+        if not ptr:
+            raise _lib.E3GNNError(f'no debug buffer {name}[{layer}]')
+        out = np.empty(n.value, dtype=np.float32)
+        torch.cuda.synchronize(self.device)
+        hip = ctypes.CDLL('libamdhip64.so.7')  # torch's runtime (same SONAME)
+        rc = hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(ptr),
+                           ctypes.c_size_t(out.nbytes), 2)
+        if rc != 0:
+            raise _lib.E3GNNError(f'hipMemcpy failed ({rc})')
+        return out
+
     def workspace_bytes(self):
         return int(self.lib.e3gnn_workspace_bytes(self._ctx))
 
