@@ -161,6 +161,7 @@ struct e3gnn_model {
   std::vector<std::unique_ptr<Linear>> sc, si1, si2;
   struct Mlp {
     DBuf w0, w1, w2, w0t, w1t, w2t;
+    DBuf w1p, w2p, w2q;  // MFMA-operand orders of the fused kernels (fused.h)
   };
   std::vector<Mlp> mlp;
 };
@@ -437,7 +438,7 @@ void dense_cg(float* out) {
 }
 MlpW mlp_ptrs(const e3gnn_model* m, int t) {
   const auto& mm = m->mlp[t];
-  return MlpW{mm.w0.f(), mm.w1.f(), mm.w2.f(), mm.w2t.f()};
+  return MlpW{mm.w0.f(), mm.w1.f(), mm.w2.f(), mm.w2t.f(), mm.w1p.f(), mm.w2p.f(), mm.w2q.f()};
 }
 
 }  // namespace
@@ -604,6 +605,31 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
           upload(mm.w1t, scaled(w1, 64, 64, s1, true)) != hipSuccess ||
           upload(mm.w2t, scaled(w2, 64, W, s2, true)) != hipSuccess)
         throw std::runtime_error("upload mlp");
+      {
+        // operand orders of fused.hip (see MlpW): per output column n, the 16
+        // k-values lane group g consumes are contiguous (4 x b128 per lane)
+        const auto a1 = scaled(w1, 64, 64, s1, false), a2 = scaled(w2, 64, W, s2, false);
+        auto kperm = [](const std::vector<float>& a, int N) {
+          std::vector<float> o((size_t)N * 64);
+          for (int n = 0; n < N; ++n)
+            for (int g = 0; g < 4; ++g)
+              for (int q = 0; q < 4; ++q)
+                for (int t = 0; t < 4; ++t)
+                  o[(size_t)n * 64 + g * 16 + q * 4 + t] = a[(size_t)(16 * q + 4 * g + t) * N + n];
+          return o;
+        };
+        std::vector<float> q2((size_t)W * 64);
+        for (int cb = 0; cb < W / 16; ++cb)
+          for (int bh = 0; bh < 4; ++bh)
+            for (int g = 0; g < 4; ++g)
+              for (int c = 0; c < 16; ++c)
+                for (int sx = 0; sx < 4; ++sx)
+                  q2[((size_t)(cb * 4 + bh) * 64 + g * 16 + c) * 4 + sx] =
+                      a2[(size_t)(16 * bh + c) * W + 16 * cb + 4 * sx + g];
+        if (W % 16 || upload(mm.w1p, kperm(a1, 64)) != hipSuccess ||
+            upload(mm.w2p, kperm(a2, W)) != hipSuccess || upload(mm.w2q, q2) != hipSuccess)
+          throw std::runtime_error("upload mlp (packed)");
+      }
       trace_point("load:mlp");
     }
   } catch (const std::exception& ex) {

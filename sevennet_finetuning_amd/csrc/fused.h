@@ -10,6 +10,10 @@ struct MlpW {
   const float* w1;   // [64][64]  layer1 / 8
   const float* w2;   // [64][W]   layer2 / 8
   const float* w2t;  // [W][64]   transpose of w2
+  // packed operand orders (16 k-values of one lane group contiguous):
+  const float* w1p;  // [n<64][g][q][t] = w1[16q + 4g + t][n]
+  const float* w2p;  // [n<W][g][q][t]  = w2[16q + 4g + t][n]
+  const float* w2q;  // [n/16][bh][g][c][s] = w2[16bh + c][16(n/16) + 4s + g]
 };
 
 struct FusedArgs {

@@ -57,6 +57,14 @@ __device__ __forceinline__ constexpr int KH(int s) { return 16 * (s >> 2) + (s &
 // otherwise multiplies live registers and halves occupancy.
 __device__ __forceinline__ void phase() { __builtin_amdgcn_sched_barrier(0); }
 
+// materialise a value here: stops the compiler from sinking an accumulation
+// chain past later paths (which keeps every partial product live)
+template <int N>
+__device__ __forceinline__ void pin(float* v) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
 __device__ __forceinline__ f32x4 zero4() {
   f32x4 z;
   z[0] = z[1] = z[2] = z[3] = 0.f;
@@ -72,17 +80,41 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // does not hoist hundreds of 64-bit addresses out of the centre loop (which it
 // did, and spilled).  Offsets outside the descriptor read 0 (padded rows).
 struct WRes {
-  __amdgpu_buffer_rsrc_t w0, w1, w2, w2t;
+  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int nfloats) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
 }
 __device__ __forceinline__ WRes make_wres(const MlpW& W, int width) {
-  return {rsrc(W.w0, 8 * 64), rsrc(W.w1, 64 * 64), rsrc(W.w2, 64 * width), rsrc(W.w2t, 64 * width)};
+  return {rsrc(W.w0, 8 * 64), rsrc(W.w1, 64 * 64), rsrc(W.w2p, 64 * width), rsrc(W.w2q, 64 * width),
+          rsrc(W.w1p, 64 * 64)};
 }
 __device__ __forceinline__ float ldw(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
   // the builtin returns the raw 32 bits (an unsigned int): reinterpret, never convert
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vbytes, sbytes, 0));
+}
+
+__device__ __forceinline__ f32x4 ldw4(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vbytes, sbytes, 0));
+}
+// N contiguous floats from one lane offset (b128/b96/b64 pieces; dword alignment)
+template <int N>
+__device__ __forceinline__ void ldv(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes, float* o) {
+  if constexpr (N >= 4) {
+    const f32x4 v = ldw4(r, vbytes, sbytes);
+    o[0] = v[0], o[1] = v[1], o[2] = v[2], o[3] = v[3];
+    ldv<N - 4>(r, vbytes, sbytes + 16, o + 4);
+  } else if constexpr (N == 3) {
+    typedef float f32x3 __attribute__((ext_vector_type(3)));
+    const f32x3 v = __builtin_bit_cast(f32x3, __builtin_amdgcn_raw_buffer_load_b96(r, vbytes, sbytes, 0));
+    o[0] = v[0], o[1] = v[1], o[2] = v[2];
+  } else if constexpr (N == 2) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 v = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, vbytes, sbytes, 0));
+    o[0] = v[0], o[1] = v[1];
+  } else if constexpr (N == 1) {
+    o[0] = ldw(r, vbytes, sbytes);
+  }
 }
 
 __device__ __forceinline__ void stw(float v, __amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
@@ -112,13 +144,17 @@ __device__ __forceinline__ void mlp_chain(const WRes& R, const float (&b)[2], in
     for (int s = 0; s < 2; ++s) acc = mfma(ldw(R.w0, v0, (4 * s * 64 + 16 * bh) * 4), b[s], acc);
     m.a1[bh] = acc;
   }
-  const int v1 = (4 * g * 64 + c) * 4;  // W1s[KH(s) + 4g][16 bo + c]
+  const int v1 = (c * 64 + g * 16) * 4;  // w1p[16 bo + c][g][s] = W1s[KH(s) + 4g][16 bo + c]
 #pragma unroll
   for (int bo = 0; bo < 4; ++bo) {
     phase();
     float a[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) a[s] = ldw(R.w1, v1, (KH(s) * 64 + 16 * bo) * 4);
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = ldw4(R.w1p, v1, (16 * bo * 64 + 4 * q) * 4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[4 * q + t] = v[t];
+    }
     f32x4 acc = zero4();
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc = mfma(a[s], act_fwd(m.a1[s >> 2][s & 3]), acc);
@@ -141,9 +177,13 @@ __device__ __forceinline__ f32x4 mlp_w_block(const f32x4 (&h2)[4], __amdgpu_buff
                                              int W, int col0, int lane) {
   const int g = lane >> 4, c = lane & 15;
   float b[16];
-  const int v = (4 * g * W + c) * 4;  // W2s[KH(s) + 4g][col0 + c]
+  const int v = (c * 64 + g * 16) * 4;  // w2p[col0 + c][g][s] = W2s[KH(s) + 4g][col0 + c]
 #pragma unroll
-  for (int s = 0; s < 16; ++s) b[s] = ldw(w2, v, (KH(s) * W + col0) * 4);
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 t4 = ldw4(w2, v, (col0 * 64 + 4 * q) * 4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) b[4 * q + t] = t4[t];
+  }
   f32x4 acc = zero4();
 #pragma unroll
   for (int s = 0; s < 16; ++s) acc = mfma(h2[s >> 2][s & 3], b[s], acc);
@@ -151,32 +191,33 @@ __device__ __forceinline__ f32x4 mlp_w_block(const f32x4 (&h2)[4], __amdgpu_buff
 }
 
 // ---------------------------------------------------------------- TP pieces
-template <int L1, int L2, int L3>
-__device__ __forceinline__ void tp_acc(const float* x, const float* y, float w, float* acc) {
-  float t[2 * L3 + 1];
-#pragma unroll
-  for (int k = 0; k < 2 * L3 + 1; ++k) t[k] = 0.f;
-  using C = CG<L1, L2, L3>;
-#pragma unroll
-  for (int q = 0; q < C::n; ++q) t[C::e[q].k] += C::e[q].c * (x[C::e[q].i] * y[C::e[q].j]);
-#pragma unroll
-  for (int k = 0; k < 2 * L3 + 1; ++k) acc[k] += w * t[k];
+// CG entries grouped by (i, j): each pair's partial sum over k is formed and
+// consumed at once (short live ranges, one product per pair)
+template <class C, int I, int J>
+__device__ __forceinline__ constexpr bool cg_pair() {
+  for (int q = 0; q < C::n; ++q)
+    if (C::e[q].i == I && C::e[q].j == J) return true;
+  return false;
 }
 
 template <int L1, int L2, int L3>
-__device__ __forceinline__ float tp_bwd(const float* x, const float* y, float w, const float* gm,
-                                        float* dx, float* dy) {
+__device__ __forceinline__ void tp_acc(const float* x, const float* y, float w, float* acc) {
   using C = CG<L1, L2, L3>;
-  float dwv = 0.f;
+  float t[2 * L3 + 1];
 #pragma unroll
-  for (int q = 0; q < C::n; ++q) {
-    const int i = C::e[q].i, j = C::e[q].j, k = C::e[q].k;
-    const float cg = C::e[q].c * gm[k];
-    dwv += cg * (x[i] * y[j]);
-    dx[i] += (cg * w) * y[j];
-    dy[j] += (cg * w) * x[i];
-  }
-  return dwv;
+  for (int k = 0; k < 2 * L3 + 1; ++k) t[k] = 0.f;
+  sfor<2 * L1 + 1>([&](auto i) {
+    sfor<2 * L2 + 1>([&](auto j) {
+      if constexpr (cg_pair<C, i, j>()) {
+        const float xy = x[i] * y[j];
+        sfor<C::n>([&](auto q) {
+          if constexpr (C::e[q].i == i && C::e[q].j == j) t[C::e[q].k] += C::e[q].c * xy;
+        });
+      }
+    });
+  });
+#pragma unroll
+  for (int k = 0; k < 2 * L3 + 1; ++k) acc[k] += w * t[k];
 }
 
 template <class L, int I>
@@ -254,15 +295,13 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const int* __restrict__ row_pt
           phase();
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int i = 0; i < D1; ++i)
-              x[r][i] = ldw(Rh, (src[r] * L::DX + col * D1) * 4, (XOFF + 16 * j * D1 + i) * 4);
+            ldv<D1>(Rh, (src[r] * L::DX + col * D1) * 4, (XOFF + 16 * j * D1) * 4, x[r]);
           sfor<L::NP>([&](auto pi) {
             constexpr PathDef p = L::P[pi];
             if constexpr (p.l1 == I) {
               constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
               phase();
-              const f32x4 wv = mlp_w_block(h2, R.w2, L::W, p.woff + 16 * j, lane);
+              const f32x4 wv = mlp_w_block(h2, R.w2p, L::W, p.woff + 16 * j, lane);
               float acc[D3];
 #pragma unroll
               for (int k = 0; k < D3; ++k) acc[k] = 0.f;
@@ -309,24 +348,57 @@ template <int L1, int L2, int L3>
 __device__ __forceinline__ void tp_bwd_x(const float* x, const float* y, float w, const float* gm,
                                          float* dx, float* dy) {
   using C = CG<L1, L2, L3>;
+  float gw[2 * L3 + 1];
 #pragma unroll
-  for (int q = 0; q < C::n; ++q) {
-    const int i = C::e[q].i, j = C::e[q].j, k = C::e[q].k;
-    const float cgw = (C::e[q].c * gm[k]) * w;
-    dx[i] += cgw * y[j];
-    dy[j] += cgw * x[i];
-  }
+  for (int k = 0; k < 2 * L3 + 1; ++k) gw[k] = gm[k] * w;
+  sfor<2 * L1 + 1>([&](auto i) {
+    sfor<2 * L2 + 1>([&](auto j) {
+      if constexpr (cg_pair<C, i, j>()) {
+        float t = 0.f;  // sum_k C_ijk g_k w
+        sfor<C::n>([&](auto q) {
+          if constexpr (C::e[q].i == i && C::e[q].j == j) t += C::e[q].c * gw[C::e[q].k];
+        });
+        dx[i] += t * y[j];
+        dy[j] += t * x[i];
+      }
+    });
+  });
 }
 template <int L1, int L2, int L3>
 __device__ __forceinline__ float tp_bwd_w(const float* x, const float* y, const float* gm) {
   using C = CG<L1, L2, L3>;
   float dwv = 0.f;
-#pragma unroll
-  for (int q = 0; q < C::n; ++q)
-    dwv += (C::e[q].c * gm[C::e[q].k]) * (x[C::e[q].i] * y[C::e[q].j]);
+  sfor<2 * L1 + 1>([&](auto i) {
+    sfor<2 * L2 + 1>([&](auto j) {
+      if constexpr (cg_pair<C, i, j>()) {
+        float t = 0.f;
+        sfor<C::n>([&](auto q) {
+          if constexpr (C::e[q].i == i && C::e[q].j == j) t += C::e[q].c * gm[C::e[q].k];
+        });
+        dwv += t * (x[i] * y[j]);
+      }
+    });
+  });
   return dwv;
 }
+// sum over the 16 lanes of a DPP row (fixed order; every lane gets the total)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  return v;
+}
 
+// B1: lane (g, c) = edge slot c of the tile x channels 4g..4g+3 of a 16-channel
+// block (transposed product w^T = W2^T H2^T: D[channel 4g+r][edge c]).  One
+// edge per lane keeps dE/dY in 8 registers; dE/dx[j] is summed over the 16
+// edge lanes of a row (DPP) once per block and accumulated in LDS.
 template <class L>
 __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_ptr,
                                                     const int* __restrict__ src_perm,
@@ -338,48 +410,33 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
                                                     float* __restrict__ dh,
                                                     float* __restrict__ dgu, int n_nodes,
                                                     int n_centers) {
-  // per wave: Y of the tile [16][9] and the dE/dx[j] partials [DX/16][64 lanes]
-  constexpr int NACC = L::DX / 16;
-  __shared__ float lds[4][160 + NACC * 64];
+  __shared__ float lds[4][L::DX];  // dE/dx[j] of the wave's node
   const int wid = threadIdx.x >> 6;
   const int jn = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wid);
   if (jn >= n_nodes) return;
-  float* ybuf = lds[wid];
-  float* dacc = lds[wid] + 160;
+  float* dacc = lds[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
   const int qb = src_ptr[jn], qe = src_ptr[jn + 1];
   const WRes R = make_wres(W, L::W);
-  const float* hj = h + (int64_t)jn * L::DX;
+  const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
   // dE/dagg rows through a descriptor: 32-bit lane offsets (the host checks
   // n_centers * DM * 4 < 2^31), scalar path/channel offsets
   const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
-#pragma unroll
-  for (int q = 0; q < NACC; ++q) dacc[q * 64 + lane] = 0.f;
+  for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
 
   for (int q0 = qb; q0 < qe; q0 += 16) {
     phase();
-    int er[4], vg[4];
+    const int er = (q0 + col < qe) ? src_perm[q0 + col] : -1;  // edge of slot c
+    // padded slots read past the end of the descriptor: 0
+    const int vg = (er >= 0 ? center[er] * L::DM : n_centers * L::DM) * 4;
+    float y[9];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = q0 + 4 * g + r;
-      er[r] = q < qe ? src_perm[q] : -1;
-      // padded slots read past the end of the descriptor: 0
-      vg[r] = (er[r] >= 0 ? center[er[r]] * L::DM : n_centers * L::DM) * 4;
-    }
-#pragma unroll
-    for (int t0 = 0; t0 < 144; t0 += 64) {
-      const int t = t0 + lane;
-      if (t < 144) {
-        const int q = q0 + t / 9;
-        ybuf[t] = q < qe ? Y[(int64_t)src_perm[q] * 9 + t % 9] : 0.f;
-      }
-    }
+    for (int q = 0; q < 9; ++q) y[q] = er >= 0 ? Y[(int64_t)er * 9 + q] : 0.f;
     f32x4 h2[4];
     {
-      const int ec = (q0 + col < qe) ? src_perm[q0 + col] : -1;  // edge of slot `col`
       float b[2];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) b[s] = ec >= 0 ? emb[(int64_t)ec * 8 + 4 * s + g] : 0.f;
+      for (int s = 0; s < 2; ++s) b[s] = er >= 0 ? emb[(int64_t)er * 8 + 4 * s + g] : 0.f;
       MlpT m;
       mlp_chain(R, b, lane, m);
 #pragma unroll
@@ -387,12 +444,9 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
 #pragma unroll
         for (int r = 0; r < 4; ++r) h2[bb][r] = act_fwd(m.a2[bb][r]);
     }
-    // dE/dY (components 1..8; Y_0 is constant) per edge slot, over this lane's channels
-    float dYa[4][8];
+    float dYa[9];  // dE/dY of edge c over this lane's channels (index 0 unused)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) dYa[r][q] = 0.f;
+    for (int q = 0; q < 9; ++q) dYa[q] = 0.f;
 
     sfor<3>([&](auto I) {
       constexpr int MUL = iblock_mul<L, I>();
@@ -400,93 +454,91 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
         constexpr int D1 = 2 * I + 1;
         constexpr int XOFF = iblock_xoff<L, I>();
         for (int jj = 0; jj < MUL / 16; ++jj) {
-          const int u = 16 * jj + col;
-          float x[D1], dx[D1];
+          float x[4 * D1], dx[4 * D1];
           phase();
+          ldv<4 * D1>(Rx, 4 * g * D1 * 4, (XOFF + 16 * jj * D1) * 4, x);
 #pragma unroll
-          for (int i = 0; i < D1; ++i) {
-            x[i] = hj[XOFF + u * D1 + i];
-            dx[i] = 0.f;
-          }
+          for (int i = 0; i < 4 * D1; ++i) dx[i] = 0.f;
           sfor<L::NP>([&](auto pi) {
             constexpr PathDef p = L::P[pi];
             if constexpr (p.l1 == I) {
-              constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
+              constexpr int D3 = 2 * p.l3 + 1;
               phase();
-              const f32x4 wv = mlp_w_block(h2, R.w2, L::W, p.woff + 16 * jj, lane);
+              // w^T block: A = W2s[:, col0 + i]^T (w2p order), B = H2^T
+              f32x4 wv = zero4();
+              {
+                const int col0 = p.woff + 16 * jj;
+                const int v = (col * 64 + g * 16) * 4;
+                float a[16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  const f32x4 t4 = ldw4(R.w2p, v, (col0 * 64 + 4 * q) * 4);
+#pragma unroll
+                  for (int t = 0; t < 4; ++t) a[4 * q + t] = t4[t];
+                }
+#pragma unroll
+                for (int s = 0; s < 16; ++s) wv = mfma(a[s], h2[s >> 2][s & 3], wv);
+              }
+              float gm[4 * D3];
+              ldv<4 * D3>(Rg, vg + 4 * g * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm);
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const float* yr = ybuf + (4 * g + r) * 9;
-                float y[D2], dy[D2], gm[D3];
+                phase();
+                float dy[2 * p.l2 + 1];
 #pragma unroll
-                for (int k = 0; k < D3; ++k)
-                  gm[k] = ldw(Rg, vg[r] + col * D3 * 4, (p.moff + 16 * jj * D3 + k) * 4);
-#pragma unroll
-                for (int q = 0; q < D2; ++q) {
-                  y[q] = yr[yoff(p.l2) + q];
-                  dy[q] = 0.f;
-                }
-                tp_bwd_x<p.l1, p.l2, p.l3>(x, y, wv[r], gm, dx, dy);
+                for (int q = 0; q < 2 * p.l2 + 1; ++q) dy[q] = 0.f;
+                // padded slots: w = 0 and g = 0
+                tp_bwd_x<p.l1, p.l2, p.l3>(x + r * D1, y + yoff(p.l2), wv[r], gm + r * D3,
+                                           dx + r * D1, dy);
                 if constexpr (p.l2 > 0) {
 #pragma unroll
-                  for (int q = 0; q < D2; ++q) dYa[r][yoff(p.l2) - 1 + q] += dy[q];
+                  for (int q = 0; q < 2 * p.l2 + 1; ++q) dYa[yoff(p.l2) + q] += dy[q];
                 }
+                pin<D1>(dx + r * D1);
+                pin<8>(dYa + 1);
               }
+              pin<4 * D1>(dx);
+              pin<8>(dYa + 1);
             }
           });
+          phase();
+          // sum over the tile's 16 edges (row lanes), lane c == 0 accumulates
 #pragma unroll
-          for (int i = 0; i < D1; ++i) dacc[(XOFF / 16 + jj * D1 + i) * 64 + lane] += dx[i];
+          for (int i = 0; i < 4 * D1; ++i) {
+            const float v = row_sum16(dx[i]);
+            if (col == 0) dacc[XOFF + (16 * jj + 4 * g) * D1 + i] += v;
+          }
         }
       }
     });
 
     phase();
-    // dE/dY: sum over the 16 channel lanes of each lane group (fixed tree), then
-    // dE/du through the SH polynomials (serial_code.py:50-70), once per edge
+    // dE/dY of edge c: sum over the 4 lane groups, then dE/du through the SH
+    // polynomials (serial_code.py:50-70)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float v = dYa[r][q];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        dYa[r][q] = v;
-      }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (col == r && er[r] >= 0) {
-        const float* yr = ybuf + (4 * g + r) * 9;
-        const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f, c15 = s3 * s5;
-        const float ux = yr[1] / s3, uy = yr[2] / s3, uz = yr[3] / s3;
-        const float* d = dYa[r];  // d[0..2] = dE/dY_1, d[3..7] = dE/dY_2
-        const float gx = s3 * d[0] + c15 * (uz * d[3] + uy * d[4]) - s5 * ux * d[5] - c15 * ux * d[7];
-        const float gy = s3 * d[1] + c15 * (ux * d[4] + uz * d[6]) + 2.f * s5 * uy * d[5];
-        const float gz = s3 * d[2] + c15 * (ux * d[3] + uy * d[6]) - s5 * uz * d[5] + c15 * uz * d[7];
-        float* o = dgu + (int64_t)er[r] * 3;
-        o[0] += gx;
-        o[1] += gy;
-        o[2] += gz;
-      }
+    for (int q = 1; q < 9; ++q) {
+      float v = dYa[q];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      dYa[q] = v;
+    }
+    if (g == 0 && er >= 0) {
+      const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f, c15 = s3 * s5;
+      const float ux = y[1] / s3, uy = y[2] / s3, uz = y[3] / s3;
+      const float* d = dYa + 1;  // d[0..2] = dE/dY_1, d[3..7] = dE/dY_2
+      const float gx = s3 * d[0] + c15 * (uz * d[3] + uy * d[4]) - s5 * ux * d[5] - c15 * ux * d[7];
+      const float gy = s3 * d[1] + c15 * (ux * d[4] + uz * d[6]) + 2.f * s5 * uy * d[5];
+      const float gz = s3 * d[2] + c15 * (ux * d[3] + uy * d[6]) - s5 * uz * d[5] + c15 * uz * d[7];
+      float* o = dgu + (int64_t)er * 3;
+      o[0] += gx;
+      o[1] += gy;
+      o[2] += gz;
     }
   }
-  // dE/dx[j]: the 4 lane groups hold the same channels for different edges
   phase();
+  __builtin_amdgcn_s_waitcnt(0);
   float* dhj = dh + (int64_t)jn * L::DX;
-  sfor<3>([&](auto I) {
-    constexpr int MUL = iblock_mul<L, I>();
-    if constexpr (MUL > 0) {
-      constexpr int D1 = 2 * I + 1;
-      constexpr int XOFF = iblock_xoff<L, I>();
-      for (int jj = 0; jj < MUL / 16; ++jj)
-#pragma unroll
-        for (int i = 0; i < D1; ++i) {
-          float v = dacc[(XOFF / 16 + jj * D1 + i) * 64 + lane];
-          v += __shfl_xor(v, 16, 64);
-          v += __shfl_xor(v, 32, 64);
-          if (g == 0) dhj[XOFF + (16 * jj + col) * D1 + i] = v;
-        }
-    }
-  });
+  for (int t = lane; t < L::DX; t += 64) dhj[t] = dacc[t];
 }
 
 template <class L>
@@ -533,9 +585,7 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
         phase();
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int i = 0; i < D1; ++i)
-            x[r][i] = ldw(Rh, vh[r] + col * D1 * 4, (XOFF + 16 * jj * D1 + i) * 4);
+          ldv<D1>(Rh, vh[r] + col * D1 * 4, (XOFF + 16 * jj * D1) * 4, x[r]);
         sfor<L::NP>([&](auto pi) {
           constexpr PathDef p = L::P[pi];
           if constexpr (p.l1 == I) {
@@ -546,22 +596,21 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
             for (int r = 0; r < 4; ++r) {
               const float* yr = ybuf + (4 * g + r) * 9;
               float y[D2], gm[D3];
-#pragma unroll
-              for (int k = 0; k < D3; ++k)
-                gm[k] = ldw(Rg, vg[r] + col * D3 * 4, (p.moff + 16 * jj * D3 + k) * 4);
+              ldv<D3>(Rg, vg[r] + col * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm);
 #pragma unroll
               for (int q = 0; q < D2; ++q) y[q] = yr[yoff(p.l2) + q];
               dwbuf[(4 * g + r) * 17 + col] = tp_bwd_w<p.l1, p.l2, p.l3>(x[r], y, gm);
             }
             phase();
             // dH2^T += W2[:, col0:col0+16] dw^T  (B lane = dw[slot c][channel 4s+g])
-            const int va = (g * 64 + col) * 4;  // W2T[col0 + 4s + g][16 bh + c]
+            // w2q[col0/16][bh][g][c][s] = W2s[16 bh + c][col0 + 4s + g]
+            const int va = (g * 16 + col) * 16;
 #pragma unroll
             for (int bh = 0; bh < 4; ++bh) {
+              const f32x4 a4 = ldw4(R.w2q, va, (col0 / 16 * 4 + bh) * 1024);
 #pragma unroll
               for (int s = 0; s < 4; ++s)
-                dh2[bh] = mfma(ldw(R.w2t, va, ((col0 + 4 * s) * 64 + 16 * bh) * 4),
-                               dwbuf[col * 17 + 4 * s + g], dh2[bh]);
+                dh2[bh] = mfma(a4[s], dwbuf[col * 17 + 4 * s + g], dh2[bh]);
             }
           }
         });
@@ -583,9 +632,13 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
 #pragma unroll
   for (int bi = 0; bi < 4; ++bi) {
     phase();
-    float a[16];
+    float a[16];  // W1s[16 bi + c][16q + 4g + t]: 4 contiguous per q
 #pragma unroll
-    for (int s = 0; s < 16; ++s) a[s] = ldw(R.w1, vb, (16 * bi * 64 + KH(s)) * 4);
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = ldw4(R.w1, vb, (16 * bi * 64 + 16 * q) * 4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[4 * q + t] = v[t];
+    }
     f32x4 acc = zero4();
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc = mfma(a[s], da2[s >> 2][s & 3], acc);
@@ -594,8 +647,12 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
   // demb^T = W0 dA1^T (rows n < 8; lanes c >= 8 read 0 outside the descriptor)
   f32x4 de = zero4();
 #pragma unroll
-  for (int s = 0; s < 16; ++s)
-    de = mfma(ldw(R.w0, vb, KH(s) * 4), dh1[s >> 2][s & 3] * act_grad(m.a1[s >> 2][s & 3]), de);
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 a4 = ldw4(R.w0, vb, 16 * q * 4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      de = mfma(a4[t], dh1[q][t] * act_grad(m.a1[q][t]), de);
+  }
   {
     const int e = e0 + col;
     if (g < 2 && e < end) {

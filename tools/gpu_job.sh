@@ -22,11 +22,16 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 5 --warmup 2 ;;
     benchq) step bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10 ;;
+    benchf) step benchf 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    benchn) step benchn 600 env E3GNN_BWD_X=node python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench10k) step bench10k 300 python bench.py --cells 11 --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --profile-only ;;
     prof10k) step prof10k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof10k -o run --output-format csv -- python bench.py --cells 11 --steps 3 --warmup 1 --profile-only ;;
     pmcf) step pmcf 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 1 --warmup 1 --profile-only ;;
     pmcw) step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 1 --warmup 1 --profile-only ;;
+    listc) step listc 120 rocprofv3 -L ;;
+    pmcsq) step pmcsq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES --kernel-trace --output-format csv -d gpurun_out/pmc_sq -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
+    pmcsq2) step pmcsq2 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace --output-format csv -d gpurun_out/pmc_sq2 -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
