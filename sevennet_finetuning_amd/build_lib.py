@@ -21,7 +21,7 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', f'-I{INCLUDE}',
          '-Wall', '-Wno-unused-function']
 # fused.hip: no SLP packing (v_pk_* f32 pairs beside MFMA cost issue slots and
 # double the live registers of the tensor-product loops: 146 -> 123 VGPRs)
-FILE_FLAGS = {'fused.hip': ['-fno-slp-vectorize']}
+FILE_FLAGS = {'fused.hip': os.environ.get('E3GNN_FUSED_FLAGS', '-fno-slp-vectorize').split()}
 
 
 def _deps_mtime():

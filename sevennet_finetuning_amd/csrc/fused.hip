@@ -233,6 +233,51 @@ constexpr int iblock_xoff() {
   return 0;
 }
 
+// ---- block sequence (input irrep I, channel block jj, path) and operand prefetch
+template <class L>
+constexpr int first_path_of(int I) {
+  for (int p = 0; p < L::NP; ++p)
+    if (L::P[p].l1 == I) return p;
+  return -1;
+}
+template <class L>
+constexpr int next_path_same_I(int pi) {
+  for (int p = pi + 1; p < L::NP; ++p)
+    if (L::P[p].l1 == L::P[pi].l1) return p;
+  return -1;
+}
+template <class L>
+constexpr int first_path_after_I(int I) {
+  for (int i = I + 1; i < 3; ++i)
+    if (first_path_of<L>(i) >= 0) return first_path_of<L>(i);
+  return -1;
+}
+// weight column of the block after (I, jj, PI); -1 at the end of the tile
+template <class L, int I, int PI>
+__device__ __forceinline__ int next_block_col(int jj) {
+  constexpr int np = next_path_same_I<L>(PI);
+  if constexpr (np >= 0) {
+    return L::P[np].woff + 16 * jj;
+  } else {
+    constexpr int f = first_path_of<L>(I);
+    constexpr int fn = first_path_after_I<L>(I);
+    if (jj + 1 < L::P[f].mul / 16) return L::P[f].woff + 16 * (jj + 1);
+    return fn >= 0 ? L::P[fn].woff : -1;
+  }
+}
+// 16 k-values of W2[:, col0 + c] for lane group g (w2p order): 4 x b128
+__device__ __forceinline__ void load_w2p(f32x4 (&b)[4], __amdgpu_buffer_rsrc_t w2p, int lane, int col0) {
+  const int v = ((lane & 15) * 64 + (lane >> 4) * 16) * 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) b[q] = ldw4(w2p, v, (col0 * 64 + 4 * q) * 4);
+}
+// w2q blocks of column block col0 (bwd_w dH2 operand): 4 x b128
+__device__ __forceinline__ void load_w2q(f32x4 (&b)[4], __amdgpu_buffer_rsrc_t w2q, int lane, int col0) {
+  const int v = ((lane >> 4) * 16 + (lane & 15)) * 16;
+#pragma unroll
+  for (int bh = 0; bh < 4; ++bh) b[bh] = ldw4(w2q, v, (col0 / 16 * 4 + bh) * 1024);
+}
+
 // per tile: neighbour ids of the lane group's 4 edges, Y of the 16 edges in LDS
 __device__ __forceinline__ void load_tile_edges(const int* __restrict__ nbr,
                                                 const float* __restrict__ Y, int e0, int end,
@@ -274,6 +319,8 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const int* __restrict__ row_pt
   for (int e0 = beg; e0 < end || e0 == beg; e0 += 16) {
     const bool first_tile = e0 == beg;
     int src[4];
+    f32x4 bq[4];
+    load_w2p(bq, R.w2p, lane, L::P[0].woff);
     load_tile_edges(nbr, Y, e0, end, lane, src, ybuf);
     f32x4 h2[4];
     {
@@ -301,7 +348,14 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const int* __restrict__ row_pt
             if constexpr (p.l1 == I) {
               constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
               phase();
-              const f32x4 wv = mlp_w_block(h2, R.w2p, L::W, p.woff + 16 * j, lane);
+              f32x4 wv = zero4();
+#pragma unroll
+              for (int s = 0; s < 16; ++s) wv = mfma(h2[s >> 2][s & 3], bq[s >> 2][s & 3], wv);
+              {  // operands of the next block load under this block's tensor product
+                const int nc = next_block_col<L, I, pi>(j);
+                if (nc >= 0) load_w2p(bq, R.w2p, lane, nc);
+              }
+              phase();
               float acc[D3];
 #pragma unroll
               for (int k = 0; k < D3; ++k) acc[k] = 0.f;
@@ -426,6 +480,8 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
 
   for (int q0 = qb; q0 < qe; q0 += 16) {
     phase();
+    f32x4 bq[4];
+    load_w2p(bq, R.w2p, lane, L::P[0].woff);
     const int er = (q0 + col < qe) ? src_perm[q0 + col] : -1;  // edge of slot c
     // padded slots read past the end of the descriptor: 0
     const int vg = (er >= 0 ? center[er] * L::DM : n_centers * L::DM) * 4;
@@ -466,18 +522,11 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
               phase();
               // w^T block: A = W2s[:, col0 + i]^T (w2p order), B = H2^T
               f32x4 wv = zero4();
+#pragma unroll
+              for (int s = 0; s < 16; ++s) wv = mfma(bq[s >> 2][s & 3], h2[s >> 2][s & 3], wv);
               {
-                const int col0 = p.woff + 16 * jj;
-                const int v = (col * 64 + g * 16) * 4;
-                float a[16];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                  const f32x4 t4 = ldw4(R.w2p, v, (col0 * 64 + 4 * q) * 4);
-#pragma unroll
-                  for (int t = 0; t < 4; ++t) a[4 * q + t] = t4[t];
-                }
-#pragma unroll
-                for (int s = 0; s < 16; ++s) wv = mfma(a[s], h2[s >> 2][s & 3], wv);
+                const int nc = next_block_col<L, I, pi>(jj);
+                if (nc >= 0) load_w2p(bq, R.w2p, lane, nc);
               }
               float gm[4 * D3];
               ldv<4 * D3>(Rg, vg + 4 * g * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm);
@@ -573,6 +622,8 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
 #pragma unroll
   for (int r = 0; r < 4; ++r) vh[r] = src[r] * L::DX * 4;
   f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
+  f32x4 bq[4];
+  load_w2q(bq, R.w2q, lane, L::P[0].woff);
 
   sfor<3>([&](auto I) {
     constexpr int MUL = iblock_mul<L, I>();
@@ -590,7 +641,6 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
           constexpr PathDef p = L::P[pi];
           if constexpr (p.l1 == I) {
             constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
-            const int col0 = p.woff + 16 * jj;
             phase();
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -604,13 +654,15 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
             phase();
             // dH2^T += W2[:, col0:col0+16] dw^T  (B lane = dw[slot c][channel 4s+g])
             // w2q[col0/16][bh][g][c][s] = W2s[16 bh + c][col0 + 4s + g]
-            const int va = (g * 16 + col) * 16;
 #pragma unroll
             for (int bh = 0; bh < 4; ++bh) {
-              const f32x4 a4 = ldw4(R.w2q, va, (col0 / 16 * 4 + bh) * 1024);
 #pragma unroll
               for (int s = 0; s < 4; ++s)
-                dh2[bh] = mfma(a4[s], dwbuf[col * 17 + 4 * s + g], dh2[bh]);
+                dh2[bh] = mfma(bq[bh][s], dwbuf[col * 17 + 4 * s + g], dh2[bh]);
+            }
+            {
+              const int nc = next_block_col<L, I, pi>(jj);
+              if (nc >= 0) load_w2q(bq, R.w2q, lane, nc);
             }
           }
         });
