@@ -348,6 +348,9 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const int* __restrict__ row_pt
             if constexpr (p.l1 == I) {
               constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
               phase();
+              // previous tiles' sum of this block (read early, added at the end)
+              float prev[D3];
+              if (!first_tile) ldv<D3>(Ro, col * D3 * 4, (p.moff + 16 * j * D3) * 4, prev);
               f32x4 wv = zero4();
 #pragma unroll
               for (int s = 0; s < 16; ++s) wv = mfma(h2[s >> 2][s & 3], bq[s >> 2][s & 3], wv);
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const int* __restrict__ row_pt
                 v += __shfl_xor(v, 32, 64);
                 if (g == 0) {
                   const int so = (p.moff + 16 * j * D3 + k) * 4, vo = col * D3 * 4;
-                  stw(first_tile ? v / denom : ldw(Ro, vo, so) + v / denom, Ro, vo, so);
+                  stw(first_tile ? v / denom : prev[k] + v / denom, Ro, vo, so);
                 }
               }
             }
@@ -520,6 +523,9 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
             if constexpr (p.l1 == I) {
               constexpr int D3 = 2 * p.l3 + 1;
               phase();
+              // dE/dagg of the edges' centres: issued before the MFMAs, which hide it
+              float gm[4 * D3];
+              ldv<4 * D3>(Rg, vg + 4 * g * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm);
               // w^T block: A = W2s[:, col0 + i]^T (w2p order), B = H2^T
               f32x4 wv = zero4();
 #pragma unroll
@@ -528,8 +534,6 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
                 const int nc = next_block_col<L, I, pi>(jj);
                 if (nc >= 0) load_w2p(bq, R.w2p, lane, nc);
               }
-              float gm[4 * D3];
-              ldv<4 * D3>(Rg, vg + 4 * g * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm);
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 phase();
@@ -590,6 +594,17 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
   for (int t = lane; t < L::DX; t += 64) dhj[t] = dacc[t];
 }
 
+// dH2^T += W2[:, block] dw^T  (B lane = dw[slot c][channel 4s+g];
+// w2q[col0/16][bh][g][c][s] = W2s[16 bh + c][col0 + 4s + g])
+__device__ __forceinline__ void mfma_dw(f32x4 (&dh2)[4], const f32x4 (&bq)[4], const float* dwb,
+                                        int lane) {
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int bh = 0; bh < 4; ++bh)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) dh2[bh] = mfma(bq[bh][s], dwb[c * 17 + 4 * s + g], dh2[bh]);
+}
+
 template <class L>
 __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ center,
                                                     const int* __restrict__ nbr,
@@ -599,14 +614,15 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
                                                     const float* __restrict__ gagg, MlpW W,
                                                     float* __restrict__ demb, int n_edges,
                                                     int n_nodes, int n_centers) {
-  // per wave: dw transpose tile [16 slots][17] + Y of the tile [16][9]
-  __shared__ float lds[4][16 * 17 + 160];
+  // per wave: two dw transpose tiles [16 slots][17] + Y of the tile [16][9]
+  constexpr int DWB = 16 * 17;
+  __shared__ float lds[4][2 * DWB + 160];
   const int wid = threadIdx.x >> 6;
   const int e0 = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wid) * 16);
   if (e0 >= n_edges) return;
   const int end = n_edges;
   float* dwbuf = lds[wid];
-  float* ybuf = lds[wid] + 16 * 17;
+  float* ybuf = lds[wid] + 2 * DWB;
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
   const WRes R = make_wres(W, L::W);
   int src[4], vg[4];
@@ -624,6 +640,8 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
   f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
   f32x4 bq[4];
   load_w2q(bq, R.w2q, lane, L::P[0].woff);
+  int pend = 0;  // a dE/dw block waits in dwbuf[buf ^ 1] for its MFMAs
+  int buf = 0;
 
   sfor<3>([&](auto I) {
     constexpr int MUL = iblock_mul<L, I>();
@@ -642,34 +660,36 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
           if constexpr (p.l1 == I) {
             constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
             phase();
+            // software pipeline: this block's dE/dagg gathers are issued, then the
+            // previous block's MFMAs run while they are in flight
+            float gm[4][D3];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              ldv<D3>(Rg, vg[r] + col * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm[r]);
+            if (pend) {
+              mfma_dw(dh2, bq, dwbuf + (buf ^ 1) * DWB, lane);
+              load_w2q(bq, R.w2q, lane, p.woff + 16 * jj);
+            }
+            phase();
+            float* dwc = dwbuf + buf * DWB;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float* yr = ybuf + (4 * g + r) * 9;
-              float y[D2], gm[D3];
-              ldv<D3>(Rg, vg[r] + col * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm);
+              float y[D2];
 #pragma unroll
               for (int q = 0; q < D2; ++q) y[q] = yr[yoff(p.l2) + q];
-              dwbuf[(4 * g + r) * 17 + col] = tp_bwd_w<p.l1, p.l2, p.l3>(x[r], y, gm);
+              dwc[(4 * g + r) * 17 + col] = tp_bwd_w<p.l1, p.l2, p.l3>(x[r], y, gm[r]);
             }
-            phase();
-            // dH2^T += W2[:, col0:col0+16] dw^T  (B lane = dw[slot c][channel 4s+g])
-            // w2q[col0/16][bh][g][c][s] = W2s[16 bh + c][col0 + 4s + g]
-#pragma unroll
-            for (int bh = 0; bh < 4; ++bh) {
-#pragma unroll
-              for (int s = 0; s < 4; ++s)
-                dh2[bh] = mfma(bq[bh][s], dwbuf[col * 17 + 4 * s + g], dh2[bh]);
-            }
-            {
-              const int nc = next_block_col<L, I, pi>(jj);
-              if (nc >= 0) load_w2q(bq, R.w2q, lane, nc);
-            }
+            pend = 1;
+            buf ^= 1;
           }
         });
       }
     }
   });
 
+  phase();
+  mfma_dw(dh2, bq, dwbuf + (buf ^ 1) * DWB, lane);  // last block
   // ---- MLP chain backward (pre-activations recomputed)
   phase();
   MlpT m;
