@@ -22,24 +22,26 @@ def _heights(cell):
                      for k in range(3)])
 
 
-def _brute(pos, cell, cutoff, pbc):
+def _brute(pos, cell, cutoff, pbc, centers=None):
     h = _heights(cell)
+    ci = np.arange(len(pos)) if centers is None else np.asarray(centers, dtype=np.int64)
     reps = [int(np.ceil(cutoff / h[k])) if pbc[k] else 0 for k in range(3)]
     ii, jj, ss = [], [], []
     for s in itertools.product(*[range(-r, r + 1) for r in reps]):
         s = np.array(s, dtype=np.float64)
-        d = pos[None, :, :] + (s @ cell)[None, None, :] - pos[:, None, :]
+        d = pos[None, :, :] + (s @ cell)[None, None, :] - pos[ci, None, :]
         mask = np.einsum('ijk,ijk->ij', d, d) < cutoff * cutoff
         if not s.any():
-            np.fill_diagonal(mask, False)
+            mask[np.arange(len(ci)), ci] = False
         i, j = np.nonzero(mask)
+        i = ci[i]
         ii.append(i)
         jj.append(j)
         ss.append(np.broadcast_to(s, (len(i), 3)))
     return np.concatenate(ii), np.concatenate(jj), np.concatenate(ss)
 
 
-def _cell_list(pos, cell, cutoff):
+def _cell_list(pos, cell, cutoff, centers=None):
     inv = np.linalg.inv(cell)
     frac = pos @ inv
     f0 = np.floor(frac)
@@ -58,24 +60,24 @@ def _cell_list(pos, cell, cutoff):
     table[bid[order], slot] = order
     ii, jj, ss = [], [], []
     rc2 = cutoff * cutoff
-    idx = np.arange(len(pos))
+    idx = np.arange(len(pos)) if centers is None else np.asarray(centers, dtype=np.int64)
     for off in itertools.product((-1, 0, 1), repeat=3):
-        nbc = b3 + np.array(off)
+        nbc = b3[idx] + np.array(off)
         sh = np.floor_divide(nbc, nb)
         nbc = nbc - sh * nb
         nbid = (nbc[:, 0] * nb[1] + nbc[:, 1]) * nb[2] + nbc[:, 2]
         cand = table[nbid]                                  # [N, m]
         valid = cand >= 0
         c = np.where(valid, cand, 0)
-        d = posw[c] + (sh.astype(np.float64) @ cell)[:, None, :] - posw[:, None, :]
+        d = posw[c] + (sh.astype(np.float64) @ cell)[:, None, :] - posw[idx, None, :]
         ok = valid & (np.einsum('nmk,nmk->nm', d, d) < rc2)
         zero = ~sh.any(axis=1)
         ok &= ~((c == idx[:, None]) & zero[:, None])
-        i, k = np.nonzero(ok)
-        j = c[i, k]
-        ii.append(i)
+        r, k = np.nonzero(ok)
+        j = c[r, k]
+        ii.append(idx[r])
         jj.append(j)
-        ss.append(sh[i].astype(np.float64))
+        ss.append(sh[r].astype(np.float64))
     i = np.concatenate(ii)
     j = np.concatenate(jj)
     s = np.concatenate(ss)
@@ -83,14 +85,16 @@ def _cell_list(pos, cell, cutoff):
     return i, j, s
 
 
-def neighbor_list(pos, cell, cutoff, pbc=(True, True, True)):
-    """Returns (edge_index int64 [2,E], shift float64 [E,3]) sorted by centre."""
+def neighbor_list(pos, cell, cutoff, pbc=(True, True, True), centers=None):
+    """Returns (edge_index int64 [2,E], shift float64 [E,3]) sorted by centre.
+    ``centers``: optional subset of centre atoms (a rank's owned atoms in the
+    domain decomposition); neighbours are still taken from every atom."""
     pos = np.ascontiguousarray(pos, dtype=np.float64)
     cell = np.ascontiguousarray(cell, dtype=np.float64)
     if all(pbc) and np.all(_heights(cell) >= 3 * cutoff):
-        i, j, s = _cell_list(pos, cell, cutoff)
+        i, j, s = _cell_list(pos, cell, cutoff, centers)
     else:
-        i, j, s = _brute(pos, cell, cutoff, pbc)
+        i, j, s = _brute(pos, cell, cutoff, pbc, centers)
     order = np.lexsort((s[:, 2], s[:, 1], s[:, 0], j, i))
     return (np.stack([i[order], j[order]]).astype(np.int64),
             np.ascontiguousarray(s[order]))

@@ -1,0 +1,49 @@
+"""Spawn targets of the multi-process decomposition tests (gloo, world_size > 1)."""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, HERE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    return dist
+
+
+def worker(rank, world, port, name, engine, out):
+    """Evaluate system `name` decomposed over `world` ranks; rank 0 saves
+    the gathered energy / virial / forces / atomic energies to `out`."""
+    import torch
+    dist = _init(rank, world, port)
+    from _systems import load_manifest_symbols, system
+    from sevennet_finetuning_amd.parallel import (ParallelE3GNN, brick_grid, build_rank_graph,
+                                                  gather_all)
+    pos, cell, types = system(name, load_manifest_symbols())
+    rg = build_rank_graph(pos, cell, types, 5.0, brick_grid(world), rank)
+    if engine == 'cpu':
+        from _segment_cpu import make_engine
+        eng = make_engine(rg)
+    else:
+        from sevennet_finetuning_amd.model import E3GNNModel
+        from sevennet_finetuning_amd.parallel import HipSegmentEngine
+        torch.cuda.set_device(0)
+        eng = HipSegmentEngine(E3GNNModel(device='cuda:0'))
+    drv = ParallelE3GNN(eng)
+    drv.set_graph(rg)
+    res = drv.evaluate()
+    f, ea = gather_all(res, len(pos))
+    if rank == 0:
+        np.savez(out, energy=float(res['energy']), virial=res['virial'].cpu().numpy(),
+                 forces=f.numpy(), atomic=ea.numpy(),
+                 n_ghost=np.array([rg.n_ghost]), n_local=np.array([rg.n_local]))
+    dist.barrier()
+    dist.destroy_process_group()
