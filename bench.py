@@ -73,6 +73,32 @@ def make_box(cells, device):
     }
 
 
+def rocprof_name(cls):
+    """Kernel symbol (as rocprofv3 prints it) of a fused timing class."""
+    kinds = {'first': 'LayerFirst', 'mid': 'LayerMid', 'last': 'LayerLast'}
+    if '.' in cls:
+        k, kind = cls.split('.')
+        return f'k_{k}<e3gnn::{kinds[kind]}>'
+    return cls
+
+
+def pmc_traffic(kernel, cells):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE,
+    separate rocprofv3 --pmc passes of this bench), or None."""
+    path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if d.get('cells') != cells:
+        return None
+    for k, v in d.get('kernels', {}).items():
+        if kernel in k:
+            return v.get('bytes_per_launch')
+    return None
+
+
 def cpu_baseline(seconds):
     """Oracle (plain-PyTorch CPU restatement of the reference) on a bounded
     sample: 216-atom Si box (3x3x3 cells, same recipe), repeated until
@@ -189,6 +215,7 @@ def main():
                    for k, v in stats.items() if v['launches']}
         dom = max(stats, key=lambda k: stats[k]['ms'])
         d = stats[dom]
+        rp_name = rocprof_name(dom)
         if d['flops'] > 0:
             ach = d['flops'] / (d['ms'] * 1e9)
             roofline = {'bound': 'mfma', 'kernel': dom, 'achieved': round(ach, 3),
@@ -204,6 +231,8 @@ def main():
                         'share_of_step': round(d['ms'] / total, 3)}
         tot_flops = sum(v['flops'] for v in stats.values())
         roofline['step_tflops'] = round(tot_flops / (ms * 1e9), 3)
+        roofline['rocprof_kernel'] = rp_name
+        roofline['traffic'] = pmc_traffic(rp_name, args.cells)
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1 and not args.profile_only:

@@ -180,7 +180,11 @@ struct Pending {
 const char* kClassNames[] = {"graph_build", "edge_embed",  "node_linear", "radial_mlp_fwd",
                              "tp_fwd",      "gate_fwd",    "readout",     "gate_bwd",
                              "tp_bwd",      "radial_mlp_bwd", "gather_src", "edge_force",
-                             "atom_force",  "embed", "conv_fwd_fused", "conv_bwd_fused"};
+                             "atom_force",  "embed",
+                             // fused kernels, one class per kernel and block kind
+                             "conv_fwd.first", "conv_fwd.mid", "conv_fwd.last",
+                             "conv_bwd_x.first", "conv_bwd_x.mid", "conv_bwd_x.last",
+                             "conv_bwd_w.first", "conv_bwd_w.mid", "conv_bwd_w.last"};
 enum Cls {
   C_GRAPH,
   C_EMBED_EDGE,
@@ -196,10 +200,12 @@ enum Cls {
   C_EDGE_FORCE,
   C_ATOM_FORCE,
   C_EMBED_NODE,
-  C_CONV_FWD,
-  C_CONV_BWD,
-  C_NCLS
+  C_CONV_FWD,             // + kind (0 first, 1 mid, 2 last)
+  C_CONV_BWD_X = C_CONV_FWD + 3,
+  C_CONV_BWD_W = C_CONV_BWD_X + 3,
+  C_NCLS = C_CONV_BWD_W + 3
 };
+static_assert(sizeof(kClassNames) / sizeof(kClassNames[0]) == C_NCLS, "class names");
 
 // algorithmic per-edge FLOP of one TP forward
 double tp_flops_per_edge(int kind) {
@@ -214,6 +220,14 @@ struct e3gnn_ctx {
   // graph
   DBuf type, center, nbr, vec, row_ptr, src_ptr, src_perm, cnt, err;
   DBuf Y, emb, dY, dgu, demb, fe;
+  // fused dE/dx kernel over CSR edge tiles + per-edge buffer + gather (1,
+  // default) or one wave per neighbour node writing dh directly (0;
+  // E3GNN_BWD_X=node)
+  int bwd_edge = [] {
+    const char* v = std::getenv("E3GNN_BWD_X");
+    return (v && std::string(v) == "node") ? 0 : 1;
+  }();
+  int graph_bwd_edge = 1;
   // 0: fused radial-MLP + TP kernels (fused.hip); 1: the unfused v1 kernels
   // (materialised per-edge weights; kept as an independent cross-check)
   int impl = [] {
@@ -751,7 +765,8 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   HIPCHK(c->grad[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
   HIPCHK(c->agg.ensure(nl * maxDM * F));
   if (v1) HIPCHK(c->dw.ensure(E * maxW * F));
-  if (v1) HIPCHK(c->dxc.ensure(E * 480 * F));
+  c->graph_bwd_edge = c->bwd_edge;
+  if (v1 || c->bwd_edge) HIPCHK(c->dxc.ensure(E * 480 * F));
   HIPCHK(c->dy.ensure(nl * 576 * F));
   HIPCHK(c->dh.ensure(n * 480 * F));
   HIPCHK(c->eat.ensure(std::max<int64_t>(nl, 1) * F));
@@ -817,7 +832,7 @@ int e3gnn_layer_forward(e3gnn_ctx* c, int t, void* stream) {
   }
   if (c->graph_impl == 0) {
     // fused radial MLP + tensor product + segmented sum (fused.hip)
-    Region r(c, s, C_CONV_FWD,
+    Region r(c, s, C_CONV_FWD + kind,
              tp_flops_per_edge(kind) * E + 2.0 * E * (8 * 64 + 64 * 64 + 64 * W),
              (double)E * 4 * (8 + 9 + 2 + dx) + nl * 4.0 * dm);
     FusedArgs a;
@@ -931,9 +946,6 @@ int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
     HIPCHK(launch_gemm(lin_bwd(*m->si2[t], c->dy.f(), dg, c->agg.f(), dm, nl, 0), s));
   }
   if (c->graph_impl == 0) {
-    Region r(c, s, C_CONV_BWD,
-             3.0 * tp_flops_per_edge(kind) * E + 2.0 * E * (2 * 64 * W + 2 * (8 * 64 + 64 * 64)),
-             (double)E * 4 * (8 + 9 + 2 + 3 + 8 + dx + (t > 0 ? dx : 0)) + nl * 4.0 * dm);
     FusedArgs a;
     std::memset(&a, 0, sizeof(a));
     a.row_ptr = c->row_ptr.i();
@@ -947,13 +959,28 @@ int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
     a.src_ptr = c->src_ptr.i();
     a.src_perm = c->src_perm.i();
     a.dh = t > 0 ? c->dh.f() : nullptr;
+    // the last block (224 message channels) is faster per neighbour node
+    a.edge_order = c->graph_bwd_edge && kind != 2;
+    a.dxc = (a.edge_order && t > 0) ? c->dxc.f() : nullptr;
     a.scratch_dh = c->dh.f();
     a.dgu = c->dgu.f();
     a.demb = c->demb.f();
     a.W = mlp_ptrs(m, t);
     a.n_centers = (int)nl;
     a.n_nodes = (int)n;
-    HIPCHK(launch_conv_bwd(kind, a, s));
+    // algorithmic FLOP (the forward radial MLP the dE/dx kernel recomputes is
+    // not counted): dE/dx + dE/dY = 2 x TP; dE/dw = TP, dH2 = dw W2^T, MLP chain
+    {
+      Region r(c, s, C_CONV_BWD_X + kind, 2.0 * tp_flops_per_edge(kind) * E,
+               (double)E * 4 * (8 + 9 + 2 + 3) + nl * 4.0 * dm + n * 4.0 * 2 * dx);
+      HIPCHK(launch_conv_bwd_x(kind, a, s));
+    }
+    {
+      Region r(c, s, C_CONV_BWD_W + kind,
+               tp_flops_per_edge(kind) * E + 2.0 * E * (64 * W + 64 * 64 + 8 * 64),
+               (double)E * 4 * (8 + 9 + 2 + 8 + dx) + nl * 4.0 * dm);
+      HIPCHK(launch_conv_bwd_w(kind, a, s));
+    }
   } else {
   {
     Region r(c, s, C_TP_BWD, 3.0 * tp_flops_per_edge(kind) * E,
@@ -998,7 +1025,9 @@ int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
   }
   }
   if (t > 0) {
-    if (c->graph_impl == 1) {  // fused path writes dh directly (k_conv_bwd_x)
+    // per-edge dE/dx (v1, or the edge-ordered fused kernel) -> dh by the
+    // transposed CSR; the per-neighbour fused kernel wrote dh itself
+    if (c->graph_impl == 1 || (c->graph_bwd_edge && t != m->nlayer - 1)) {
       Region r(c, s, C_GATHER, 0, (double)E * 4 * (dx + 1) + n * 4.0 * dx);
       HIPCHK(launch_gather_rows((int)n, dx, c->src_ptr.i(), c->src_perm.i(), c->dxc.f(),
                                 c->dh.f(), s));

@@ -29,6 +29,8 @@ struct FusedArgs {
   const int* src_perm; // [E]
   float* dh;           // bwd out [n_nodes, DX]: dE/dx of the gathered features (nullable)
   float* scratch_dh;   // [n_nodes, DX] sink used when dh is null
+  float* dxc;          // [E, DX] per-edge dE/dx (edge-ordered dE/dx kernel; nullable)
+  int edge_order;      // dE/dx kernel over CSR edge tiles (writes dxc) vs per neighbour
   float* dgu;         // bwd in/out [E, 3]  dE/du accumulated over layers
   float* demb;        // bwd in/out [E, 8]  dE/demb accumulated over layers
   MlpW W;
@@ -39,6 +41,8 @@ struct FusedArgs {
 };
 
 hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s);
-hipError_t launch_conv_bwd(int kind, const FusedArgs& a, hipStream_t s);
+hipError_t launch_conv_bwd(int kind, const FusedArgs& a, hipStream_t s);  // = _x then _w
+hipError_t launch_conv_bwd_x(int kind, const FusedArgs& a, hipStream_t s);  // dE/dx, dE/du
+hipError_t launch_conv_bwd_w(int kind, const FusedArgs& a, hipStream_t s);  // dE/dw -> dE/demb
 
 }  // namespace e3gnn

@@ -456,7 +456,11 @@ __device__ __forceinline__ float row_sum16(float v) {
 // block (transposed product w^T = W2^T H2^T: D[channel 4g+r][edge c]).  One
 // edge per lane keeps dE/dY in 8 registers; dE/dx[j] is summed over the 16
 // edge lanes of a row (DPP) once per block and accumulated in LDS.
-template <class L>
+// EDGE = true: one wave per fixed tile of 16 consecutive (CSR-order) edges
+// instead of one per neighbour node -- the centres' dE/dagg rows are then read
+// in order (L2-resident) rather than scattered -- and dE/dx is written per
+// edge to dxc (summed per neighbour by the transposed-CSR gather).
+template <class L, bool EDGE>
 __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_ptr,
                                                     const int* __restrict__ src_perm,
                                                     const int* __restrict__ center,
@@ -466,26 +470,33 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
                                                     const float* __restrict__ gagg, MlpW W,
                                                     float* __restrict__ dh,
                                                     float* __restrict__ dgu, int n_nodes,
-                                                    int n_centers) {
-  __shared__ float lds[4][L::DX];  // dE/dx[j] of the wave's node
+                                                    int n_centers, const int* __restrict__ nbr,
+                                                    float* __restrict__ dxc, int n_edges) {
+  __shared__ float lds[4][EDGE ? 1 : L::DX];  // dE/dx[j] of the wave's node
   const int wid = threadIdx.x >> 6;
   const int jn = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wid);
-  if (jn >= n_nodes) return;
+  if (EDGE ? jn * 16 >= n_edges : jn >= n_nodes) return;
   float* dacc = lds[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
-  const int qb = src_ptr[jn], qe = src_ptr[jn + 1];
+  const int qb = EDGE ? jn * 16 : src_ptr[jn];
+  const int qe = EDGE ? min(jn * 16 + 16, n_edges) : src_ptr[jn + 1];
   const WRes R = make_wres(W, L::W);
-  const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
+  const __amdgpu_buffer_rsrc_t Rx =
+      EDGE ? rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4) : rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
   // dE/dagg rows through a descriptor: 32-bit lane offsets (the host checks
   // n_centers * DM * 4 < 2^31), scalar path/channel offsets
   const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
-  for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
+  if constexpr (!EDGE)
+    for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
 
   for (int q0 = qb; q0 < qe; q0 += 16) {
     phase();
     f32x4 bq[4];
     load_w2p(bq, R.w2p, lane, L::P[0].woff);
-    const int er = (q0 + col < qe) ? src_perm[q0 + col] : -1;  // edge of slot c
+    // edge of slot c
+    const int er = (q0 + col < qe) ? (EDGE ? q0 + col : src_perm[q0 + col]) : -1;
+    // EDGE: the slot's gathered row (padded slots: row 0, w = 0 there)
+    const int vx = EDGE ? (er >= 0 ? nbr[er] : 0) * L::DX * 4 : 0;
     // padded slots read past the end of the descriptor: 0
     const int vg = (er >= 0 ? center[er] * L::DM : n_centers * L::DM) * 4;
     float y[9];
@@ -515,7 +526,7 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
         for (int jj = 0; jj < MUL / 16; ++jj) {
           float x[4 * D1], dx[4 * D1];
           phase();
-          ldv<4 * D1>(Rx, 4 * g * D1 * 4, (XOFF + 16 * jj * D1) * 4, x);
+          ldv<4 * D1>(Rx, vx + 4 * g * D1 * 4, (XOFF + 16 * jj * D1) * 4, x);
 #pragma unroll
           for (int i = 0; i < 4 * D1; ++i) dx[i] = 0.f;
           sfor<L::NP>([&](auto pi) {
@@ -555,11 +566,19 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
             }
           });
           phase();
-          // sum over the tile's 16 edges (row lanes), lane c == 0 accumulates
+          if constexpr (EDGE) {  // per-edge dE/dx[nbr] (not needed for the first block)
+            if (dxc && er >= 0) {
+              float* o = dxc + (int64_t)er * L::DX + XOFF + (16 * jj + 4 * g) * D1;
 #pragma unroll
-          for (int i = 0; i < 4 * D1; ++i) {
-            const float v = row_sum16(dx[i]);
-            if (col == 0) dacc[XOFF + (16 * jj + 4 * g) * D1 + i] += v;
+              for (int i = 0; i < 4 * D1; ++i) o[i] = dx[i];
+            }
+          } else {
+            // sum over the tile's 16 edges (row lanes), lane c == 0 accumulates
+#pragma unroll
+            for (int i = 0; i < 4 * D1; ++i) {
+              const float v = row_sum16(dx[i]);
+              if (col == 0) dacc[XOFF + (16 * jj + 4 * g) * D1 + i] += v;
+            }
           }
         }
       }
@@ -588,10 +607,12 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
       o[2] += gz;
     }
   }
-  phase();
-  __builtin_amdgcn_s_waitcnt(0);
-  float* dhj = dh + (int64_t)jn * L::DX;
-  for (int t = lane; t < L::DX; t += 64) dhj[t] = dacc[t];
+  if constexpr (!EDGE) {
+    phase();
+    __builtin_amdgcn_s_waitcnt(0);
+    float* dhj = dh + (int64_t)jn * L::DX;
+    for (int t = lane; t < L::DX; t += 64) dhj[t] = dacc[t];
+  }
 }
 
 // dH2^T += W2[:, block] dw^T  (B lane = dw[slot c][channel 4s+g];
@@ -744,16 +765,25 @@ static hipError_t fwd_impl(const FusedArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 template <class L>
-static hipError_t bwd_impl(const FusedArgs& a, hipStream_t s) {
+static hipError_t bwd_x_impl(const FusedArgs& a, hipStream_t s) {
   if (a.n_nodes <= 0 || a.n_edges <= 0) return hipSuccess;
-  if (a.dh)
-    hipLaunchKernelGGL(k_conv_bwd_x<L>, dim3((a.n_nodes + 3) / 4), dim3(256), 0, s, a.src_ptr,
+  if (a.edge_order) {  // edge-ordered tiles, per-edge dE/dx (caller gathers)
+    const int tiles = (a.n_edges + 15) / 16;
+    hipLaunchKernelGGL((k_conv_bwd_x<L, true>), dim3((tiles + 3) / 4), dim3(256), 0, s, a.src_ptr,
                        a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
-                       a.n_nodes, a.n_centers);
-  else  // first block: dE/dx of the embedding is not needed, only dE/du
-    hipLaunchKernelGGL(k_conv_bwd_x<L>, dim3((a.n_nodes + 3) / 4), dim3(256), 0, s, a.src_ptr,
-                       a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.scratch_dh, a.dgu,
-                       a.n_nodes, a.n_centers);
+                       a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges);
+    return hipGetLastError();
+  }
+  // first block: dE/dx of the embedding is not needed (scratch sink), only dE/du
+  hipLaunchKernelGGL((k_conv_bwd_x<L, false>), dim3((a.n_nodes + 3) / 4), dim3(256), 0, s,
+                     a.src_ptr, a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W,
+                     a.dh ? a.dh : a.scratch_dh, a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc,
+                     a.n_edges);
+  return hipGetLastError();
+}
+template <class L>
+static hipError_t bwd_w_impl(const FusedArgs& a, hipStream_t s) {
+  if (a.n_nodes <= 0 || a.n_edges <= 0) return hipSuccess;
   const int tiles = (a.n_edges + 15) / 16;
   hipLaunchKernelGGL(k_conv_bwd_w<L>, dim3((tiles + 3) / 4), dim3(256), 0, s, a.center, a.nbr,
                      a.emb, a.Y, a.h, a.gagg, a.W, a.demb, a.n_edges, a.n_nodes, a.n_centers);
@@ -767,12 +797,23 @@ hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s) {
     default: return fwd_impl<LayerLast>(a, s);
   }
 }
-hipError_t launch_conv_bwd(int kind, const FusedArgs& a, hipStream_t s) {
+hipError_t launch_conv_bwd_x(int kind, const FusedArgs& a, hipStream_t s) {
   switch (kind) {
-    case 0: return bwd_impl<LayerFirst>(a, s);
-    case 1: return bwd_impl<LayerMid>(a, s);
-    default: return bwd_impl<LayerLast>(a, s);
+    case 0: return bwd_x_impl<LayerFirst>(a, s);
+    case 1: return bwd_x_impl<LayerMid>(a, s);
+    default: return bwd_x_impl<LayerLast>(a, s);
   }
+}
+hipError_t launch_conv_bwd_w(int kind, const FusedArgs& a, hipStream_t s) {
+  switch (kind) {
+    case 0: return bwd_w_impl<LayerFirst>(a, s);
+    case 1: return bwd_w_impl<LayerMid>(a, s);
+    default: return bwd_w_impl<LayerLast>(a, s);
+  }
+}
+hipError_t launch_conv_bwd(int kind, const FusedArgs& a, hipStream_t s) {
+  const hipError_t e = launch_conv_bwd_x(kind, a, s);
+  return e != hipSuccess ? e : launch_conv_bwd_w(kind, a, s);
 }
 
 }  // namespace e3gnn

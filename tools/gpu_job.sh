@@ -24,6 +24,7 @@ for s in "$@"; do
     benchq) step bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10 ;;
     benchf) step benchf 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     benchn) step benchn 600 env E3GNN_BWD_X=node python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    testsn) step testsn 600 env E3GNN_BWD_X=node python -m pytest tests/test_gpu_parity.py -q -x ;;
     bench10k) step bench10k 300 python bench.py --cells 11 --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --profile-only ;;
     prof10k) step prof10k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof10k -o run --output-format csv -- python bench.py --cells 11 --steps 3 --warmup 1 --profile-only ;;
