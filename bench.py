@@ -76,9 +76,9 @@ def make_box(cells, device):
 def rocprof_name(cls):
     """Kernel symbol (as rocprofv3 prints it) of a fused timing class."""
     kinds = {'first': 'LayerFirst', 'mid': 'LayerMid', 'last': 'LayerLast'}
-    if '.' in cls:
+    if '.' in cls:  # template prefix (k_conv_bwd_x has a second, bool argument)
         k, kind = cls.split('.')
-        return f'k_{k}<e3gnn::{kinds[kind]}>'
+        return f'k_{k}<e3gnn::{kinds[kind]}'
     return cls
 
 
