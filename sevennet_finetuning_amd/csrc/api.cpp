@@ -136,6 +136,20 @@ hipError_t upload(DBuf& b, const std::vector<float>& v) {
   return hipMemcpy(b.p, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice);
 }
 
+// bf16 round-to-nearest-even (finite inputs) and its exact widening
+uint16_t bf16_rne(float x) {
+  uint32_t u;
+  std::memcpy(&u, &x, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+float bf16_to_f32(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float x;
+  std::memcpy(&x, &u, 4);
+  return x;
+}
+
 // e3nn o3.Linear on merged irreps: one block per l present in both.
 struct LinBlock {
   int l, K, N, in_off, out_off, w_off, wt_off;
@@ -162,6 +176,7 @@ struct e3gnn_model {
   struct Mlp {
     DBuf w0, w1, w2, w0t, w1t, w2t;
     DBuf w1p, w2p, w2q;  // MFMA-operand orders of the fused kernels (fused.h)
+    DBuf w2b;            // 3-way bf16 split of w2 in 16x16x32 operand order (fused.h)
   };
   std::vector<Mlp> mlp;
 };
@@ -452,7 +467,8 @@ void dense_cg(float* out) {
 }
 MlpW mlp_ptrs(const e3gnn_model* m, int t) {
   const auto& mm = m->mlp[t];
-  return MlpW{mm.w0.f(), mm.w1.f(), mm.w2.f(), mm.w2t.f(), mm.w1p.f(), mm.w2p.f(), mm.w2q.f()};
+  return MlpW{mm.w0.f(),  mm.w1.f(),  mm.w2.f(),  mm.w2t.f(),
+              mm.w1p.f(), mm.w2p.f(), mm.w2q.f(), static_cast<const uint16_t*>(mm.w2b.p)};
 }
 
 }  // namespace
@@ -640,8 +656,26 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
                 for (int sx = 0; sx < 4; ++sx)
                   q2[((size_t)(cb * 4 + bh) * 64 + g * 16 + c) * 4 + sx] =
                       a2[(size_t)(16 * bh + c) * W + 16 * cb + 4 * sx + g];
+        // w2b (MlpW::w2b): w2 = p0 + p1 + p2 exactly (bf16 pieces, round to
+        // nearest even); element t of lane (g, c) in k-half m of column block cb
+        // is w2[16(2m + t/4) + 4g + t%4][16 cb + c]
+        std::vector<float> b2((size_t)W * 64 * 3 / 2);
+        uint16_t* b2h = reinterpret_cast<uint16_t*>(b2.data());
+        for (int cb = 0; cb < W / 16; ++cb)
+          for (int m2 = 0; m2 < 2; ++m2)
+            for (int g = 0; g < 4; ++g)
+              for (int c = 0; c < 16; ++c)
+                for (int t = 0; t < 8; ++t) {
+                  float v = a2[(size_t)(16 * (2 * m2 + t / 4) + 4 * g + t % 4) * W + 16 * cb + c];
+                  for (int pc = 0; pc < 3; ++pc) {
+                    const uint16_t hb = bf16_rne(v);
+                    b2h[((((size_t)cb * 3 + pc) * 2 + m2) * 64 + g * 16 + c) * 8 + t] = hb;
+                    v -= bf16_to_f32(hb);
+                  }
+                }
         if (W % 16 || upload(mm.w1p, kperm(a1, 64)) != hipSuccess ||
-            upload(mm.w2p, kperm(a2, W)) != hipSuccess || upload(mm.w2q, q2) != hipSuccess)
+            upload(mm.w2p, kperm(a2, W)) != hipSuccess || upload(mm.w2q, q2) != hipSuccess ||
+            upload(mm.w2b, b2) != hipSuccess)
           throw std::runtime_error("upload mlp (packed)");
       }
       trace_point("load:mlp");

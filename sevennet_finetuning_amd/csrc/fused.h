@@ -14,6 +14,9 @@ struct MlpW {
   const float* w1p;  // [n<64][g][q][t] = w1[16q + 4g + t][n]
   const float* w2p;  // [n<W][g][q][t]  = w2[16q + 4g + t][n]
   const float* w2q;  // [n/16][bh][g][c][s] = w2[16bh + c][16(n/16) + 4s + g]
+  // w2 as three bf16 pieces (w2 = p0 + p1 + p2, exact) in v_mfma_f32_16x16x32_bf16
+  // operand order: [n/16][piece][m][g][c][t] = piece of w2[16(2m + t/4) + 4g + t%4][n]
+  const uint16_t* w2b;
 };
 
 struct FusedArgs {

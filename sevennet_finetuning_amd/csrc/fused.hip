@@ -80,14 +80,14 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // does not hoist hundreds of 64-bit addresses out of the centre loop (which it
 // did, and spilled).  Offsets outside the descriptor read 0 (padded rows).
 struct WRes {
-  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p;
+  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int nfloats) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
 }
 __device__ __forceinline__ WRes make_wres(const MlpW& W, int width) {
   return {rsrc(W.w0, 8 * 64), rsrc(W.w1, 64 * 64), rsrc(W.w2p, 64 * width), rsrc(W.w2q, 64 * width),
-          rsrc(W.w1p, 64 * 64)};
+          rsrc(W.w1p, 64 * 64), rsrc((const float*)W.w2b, 64 * width * 3 / 2)};
 }
 __device__ __forceinline__ float ldw(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
   // the builtin returns the raw 32 bits (an unsigned int): reinterpret, never convert
@@ -124,6 +124,60 @@ __device__ __forceinline__ void stw(float v, __amdgpu_buffer_rsrc_t r, int vbyte
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_bytes(const void* p, int64_t nbytes) {
   const int n = nbytes > 0x7fffffff ? 0x7fffffff : (int)nbytes;
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, n, 0x00020000);
+}
+
+// ---------------------------------------------------------------- w = H2 W2 on bf16 MFMA
+// The 64 -> W layer of the radial MLP (90 % of its FLOPs) runs on
+// v_mfma_f32_16x16x32_bf16 with both operands split into three bf16 pieces
+// (x = p0 + p1 + p2 exactly, 24 significant bits) and the six piece products
+// with i + j <= 2 accumulated in f32, smallest first: f32-grade accuracy (the
+// dropped terms are below 2^-24 relative) at 12 x 16 = 192 MFMA cycles per
+// 16 x 16 x 64 block instead of 16 x 32 = 512 on v_mfma_f32_16x16x4_f32.
+// k order: element t of lane group g in k-half m is hidden unit
+// 16(2m + t/4) + 4g + t%4, which is exactly register (bh = 2m + t/4, r = t%4)
+// of the H2 accumulators a lane already holds -- no lane movement.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+struct Op3 {
+  bf16x8 v[3][2];  // [piece][k-half]
+};
+// W2 operand of column block col0 (w2b order, 6 x b128 per lane)
+__device__ __forceinline__ void load_w2b(Op3& o, __amdgpu_buffer_rsrc_t w2b, int lane, int col0) {
+#pragma unroll
+  for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      o.v[pc][m] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2b, lane * 16, ((col0 / 16 * 3 + pc) * 2 + m) * 1024, 0));
+}
+// the lane's 16 H2 values (units 16 bh + 4g + r) as three bf16 pieces
+__device__ __forceinline__ void split_h2(const f32x4 (&h2)[4], Op3& o) {
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      float x = h2[2 * m + (t >> 2)][t & 3];
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) {
+        const __bf16 b = (__bf16)x;
+        o.v[pc][m][t] = b;
+        x -= (float)b;
+      }
+    }
+}
+// HA: H2 is the A operand (rows = edges: forward); else W2^T is (rows = channels)
+template <bool HA>
+__device__ __forceinline__ f32x4 w2_block(const Op3& h, const Op3& w) {
+  constexpr int I[6] = {2, 1, 0, 1, 0, 0}, J[6] = {0, 1, 2, 0, 1, 0};
+  f32x4 acc = zero4();
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      acc = HA ? mfma16(h.v[I[q]][m], w.v[J[q]][m], acc) : mfma16(w.v[J[q]][m], h.v[I[q]][m], acc);
+  return acc;
 }
 
 // ---------------------------------------------------------------- radial MLP
@@ -319,17 +373,19 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const int* __restrict__ row_pt
   for (int e0 = beg; e0 < end || e0 == beg; e0 += 16) {
     const bool first_tile = e0 == beg;
     int src[4];
-    f32x4 bq[4];
-    load_w2p(bq, R.w2p, lane, L::P[0].woff);
+    Op3 wq;
+    load_w2b(wq, R.w2b, lane, L::P[0].woff);
     load_tile_edges(nbr, Y, e0, end, lane, src, ybuf);
-    f32x4 h2[4];
+    Op3 hq;
     {
       MlpT m;
       mlp_pre(R, emb, e0, end, lane, m);
+      f32x4 h2[4];
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) h2[b][r] = act_fwd(m.a2[b][r]);
+      split_h2(h2, hq);
     }
     sfor<3>([&](auto I) {
       constexpr int MUL = iblock_mul<L, I>();
@@ -351,12 +407,10 @@ __global__ __launch_bounds__(256) void k_conv_fwd(const int* __restrict__ row_pt
               // previous tiles' sum of this block (read early, added at the end)
               float prev[D3];
               if (!first_tile) ldv<D3>(Ro, col * D3 * 4, (p.moff + 16 * j * D3) * 4, prev);
-              f32x4 wv = zero4();
-#pragma unroll
-              for (int s = 0; s < 16; ++s) wv = mfma(h2[s >> 2][s & 3], bq[s >> 2][s & 3], wv);
+              const f32x4 wv = w2_block<true>(hq, wq);
               {  // operands of the next block load under this block's tensor product
                 const int nc = next_block_col<L, I, pi>(j);
-                if (nc >= 0) load_w2p(bq, R.w2p, lane, nc);
+                if (nc >= 0) load_w2b(wq, R.w2b, lane, nc);
               }
               phase();
               float acc[D3];
@@ -491,8 +545,8 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
 
   for (int q0 = qb; q0 < qe; q0 += 16) {
     phase();
-    f32x4 bq[4];
-    load_w2p(bq, R.w2p, lane, L::P[0].woff);
+    Op3 wq;
+    load_w2b(wq, R.w2b, lane, L::P[0].woff);
     // edge of slot c
     const int er = (q0 + col < qe) ? (EDGE ? q0 + col : src_perm[q0 + col]) : -1;
     // EDGE: the slot's gathered row (padded slots: row 0, w = 0 there)
@@ -502,17 +556,19 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
     float y[9];
 #pragma unroll
     for (int q = 0; q < 9; ++q) y[q] = er >= 0 ? Y[(int64_t)er * 9 + q] : 0.f;
-    f32x4 h2[4];
+    Op3 hq;
     {
       float b[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) b[s] = er >= 0 ? emb[(int64_t)er * 8 + 4 * s + g] : 0.f;
       MlpT m;
       mlp_chain(R, b, lane, m);
+      f32x4 h2[4];
 #pragma unroll
       for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) h2[bb][r] = act_fwd(m.a2[bb][r]);
+      split_h2(h2, hq);
     }
     float dYa[9];  // dE/dY of edge c over this lane's channels (index 0 unused)
 #pragma unroll
@@ -538,12 +594,10 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
               float gm[4 * D3];
               ldv<4 * D3>(Rg, vg + 4 * g * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm);
               // w^T block: A = W2s[:, col0 + i]^T (w2p order), B = H2^T
-              f32x4 wv = zero4();
-#pragma unroll
-              for (int s = 0; s < 16; ++s) wv = mfma(bq[s >> 2][s & 3], h2[s >> 2][s & 3], wv);
+              const f32x4 wv = w2_block<false>(hq, wq);
               {
                 const int nc = next_block_col<L, I, pi>(jj);
-                if (nc >= 0) load_w2p(bq, R.w2p, lane, nc);
+                if (nc >= 0) load_w2b(wq, R.w2b, lane, nc);
               }
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
