@@ -9,7 +9,9 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libe3gnn_hip.so')
+# E3GNN_LIB: an alternative in-tree build of the same library (A/B kernel
+# variants from build_lib --out); never a different implementation
+LIB_PATH = os.environ.get('E3GNN_LIB') or os.path.join(_HERE, 'libe3gnn_hip.so')
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), 'include', 'e3gnn.h')
 
 _c_int, _c_i64, _c_f, _vp = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p

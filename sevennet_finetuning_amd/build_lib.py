@@ -31,14 +31,20 @@ def _deps_mtime():
     return max(os.path.getmtime(f) for f in files)
 
 
-def build(force=False, verbose=False):
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():
-        return LIB
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(force=False, verbose=False, out=None, defines=()):
+    """Compile and link the library (``out``: another path, for A/B variants
+    built with extra ``-D`` ``defines``)."""
+    lib = out or LIB
+    if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _deps_mtime():
+        return lib
+    objdir = OBJDIR if out is None else os.path.join(OBJDIR, os.path.basename(out))
+    os.makedirs(objdir, exist_ok=True)
+    extra = [f'-D{d}' for d in defines]
 
     def compile_one(src):
-        obj = os.path.join(OBJDIR, src + '.o')
-        cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(src, []), '-c', os.path.join(CSRC, src), '-o', obj]
+        obj = os.path.join(objdir, src + '.o')
+        cmd = [HIPCC, *FLAGS, *extra, *FILE_FLAGS.get(src, []), '-c', os.path.join(CSRC, src),
+               '-o', obj]
         if verbose:
             print(' '.join(cmd))
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -48,14 +54,17 @@ def build(force=False, verbose=False):
 
     with ThreadPoolExecutor(max_workers=4) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    tmp = LIB + '.tmp'
+    tmp = lib + '.tmp'
     cmd = [HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f'link failed:\n{r.stdout}\n{r.stderr}')
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == '__main__':
-    print(build(force='--force' in sys.argv, verbose=True))
+    args = sys.argv[1:]
+    out = args[args.index('--out') + 1] if '--out' in args else None
+    defs = [a[2:] for a in args if a.startswith('-D')]
+    print(build(force='--force' in args, verbose=True, out=out, defines=defs))

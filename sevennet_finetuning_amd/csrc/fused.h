@@ -17,6 +17,10 @@ struct MlpW {
   // w2 as three bf16 pieces (w2 = p0 + p1 + p2, exact) in v_mfma_f32_16x16x32_bf16
   // operand order: [n/16][piece][m][g][c][t] = piece of w2[16(2m + t/4) + 4g + t%4][n]
   const uint16_t* w2b;
+  // the same pieces for the dE/dw kernel's K = 32 products over PAIRS of
+  // consecutive visited 16-column blocks: [pair][piece][bh][g][c][t] = piece of
+  // w2[16 bh + c][column of k = 8g + t] (api.cpp bwd_w_block_cols)
+  const uint16_t* w2c;
 };
 
 struct FusedArgs {

@@ -35,6 +35,25 @@
 
 #include <type_traits>
 
+// waves per SIMD the register allocation targets (unified VGPR+AGPR file:
+// 4 waves <= 128 registers, 3 <= 168); without the hint the compiler parks
+// MFMA accumulators in AGPRs and lands just above a boundary
+#ifndef E3GNN_FWD_WAVES
+#define E3GNN_FWD_WAVES 3
+#endif
+// dE/dw kernel's dH2 = dw W2^T product: 0 f32 MFMA per block (operands
+// prefetched a block ahead), 1 bf16x6 per block pair, 2 the same with the
+// pair's operands loaded under its second block
+#ifndef E3GNN_BWDW_MODE
+#define E3GNN_BWDW_MODE 0
+#endif
+#ifndef E3GNN_BWDW_WAVES
+#define E3GNN_BWDW_WAVES 4
+#endif
+#ifndef E3GNN_BWDX_WAVES
+#define E3GNN_BWDX_WAVES 3
+#endif
+
 namespace e3gnn {
 namespace {
 
@@ -80,14 +99,15 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // does not hoist hundreds of 64-bit addresses out of the centre loop (which it
 // did, and spilled).  Offsets outside the descriptor read 0 (padded rows).
 struct WRes {
-  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b;
+  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b, w2c;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int nfloats) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
 }
 __device__ __forceinline__ WRes make_wres(const MlpW& W, int width) {
   return {rsrc(W.w0, 8 * 64), rsrc(W.w1, 64 * 64), rsrc(W.w2p, 64 * width), rsrc(W.w2q, 64 * width),
-          rsrc(W.w1p, 64 * 64), rsrc((const float*)W.w2b, 64 * width * 3 / 2)};
+          rsrc(W.w1p, 64 * 64), rsrc((const float*)W.w2b, 64 * width * 3 / 2),
+          rsrc((const float*)W.w2c, 64 * width * 3 / 2)};
 }
 __device__ __forceinline__ float ldw(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
   // the builtin returns the raw 32 bits (an unsigned int): reinterpret, never convert
@@ -352,7 +372,7 @@ __device__ __forceinline__ void load_tile_edges(const int* __restrict__ nbr,
 // ---------------------------------------------------------------- forward
 // agg[c] = sum_e TP(h[nbr e], Y_e, w_e) / denom; the first tile stores, later ones add.
 template <class L>
-__global__ __launch_bounds__(256) void k_conv_fwd(const int* __restrict__ row_ptr,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_WAVES, E3GNN_FWD_WAVES))) void k_conv_fwd(const int* __restrict__ row_ptr,
                                                   const int* __restrict__ nbr,
                                                   const float* __restrict__ emb,
                                                   const float* __restrict__ Y,
@@ -515,7 +535,7 @@ __device__ __forceinline__ float row_sum16(float v) {
 // in order (L2-resident) rather than scattered -- and dE/dx is written per
 // edge to dxc (summed per neighbour by the transposed-CSR gather).
 template <class L, bool EDGE>
-__global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_ptr,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_WAVES, E3GNN_BWDX_WAVES))) void k_conv_bwd_x(const int* __restrict__ src_ptr,
                                                     const int* __restrict__ src_perm,
                                                     const int* __restrict__ center,
                                                     const float* __restrict__ emb,
@@ -669,7 +689,16 @@ __global__ __launch_bounds__(256) void k_conv_bwd_x(const int* __restrict__ src_
   }
 }
 
-// dH2^T += W2[:, block] dw^T  (B lane = dw[slot c][channel 4s+g];
+// dE/dw of one visited 16-channel block in LDS: [edge slot][DWS]
+constexpr int DWS = 20;       // row stride (16-byte aligned rows for b128 reads)
+constexpr int DWB = 16 * DWS;
+
+// dH2^T += W2[:, pair] dw^T over the block pair P (visited blocks 2P, 2P + 1 in
+// LDS buffers 0 and 1): K = 32 (lane groups 0-1: block 2P, 2-3: block 2P + 1)
+// v_mfma_f32_16x16x32_bf16 with both operands split in three bf16 pieces and the
+// six products with i + j <= 2 (see w2_block): 24 MFMAs x 16 cycles per pair
+// instead of 32 x 32 on v_mfma_f32_16x16x4_f32.
+// dH2^T += W2[:, block] dw^T on v_mfma_f32_16x16x4_f32 (E3GNN_BWDW_MODE 0;
 // w2q[col0/16][bh][g][c][s] = W2s[16 bh + c][col0 + 4s + g])
 __device__ __forceinline__ void mfma_dw(f32x4 (&dh2)[4], const f32x4 (&bq)[4], const float* dwb,
                                         int lane) {
@@ -677,11 +706,47 @@ __device__ __forceinline__ void mfma_dw(f32x4 (&dh2)[4], const f32x4 (&bq)[4], c
 #pragma unroll
   for (int bh = 0; bh < 4; ++bh)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) dh2[bh] = mfma(bq[bh][s], dwb[c * 17 + 4 * s + g], dh2[bh]);
+    for (int s = 0; s < 4; ++s) dh2[bh] = mfma(bq[bh][s], dwb[c * DWS + 4 * s + g], dh2[bh]);
+}
+
+struct PairW {
+  bf16x8 a[4][3];  // [bh][piece]
+};
+__device__ __forceinline__ void load_pair(PairW& w, __amdgpu_buffer_rsrc_t w2c, int P, int lane) {
+#pragma unroll
+  for (int bh = 0; bh < 4; ++bh)
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+      w.a[bh][pc] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2c, lane * 16, ((P * 3 + pc) * 4 + bh) * 1024, 0));
+}
+__device__ __forceinline__ void mfma_pair(f32x4 (&dh2)[4], const PairW& w, const float* dwb, int lane) {
+  const int g = lane >> 4, c = lane & 15;
+  const float* src = dwb + (g >> 1) * DWB + c * DWS + 8 * (g & 1);
+  bf16x8 d[3];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * h);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float x = v[t];
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) {
+        const __bf16 b = (__bf16)x;
+        d[pc][4 * h + t] = b;
+        x -= (float)b;
+      }
+    }
+  }
+  constexpr int I[6] = {2, 1, 0, 1, 0, 0}, J[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+  for (int bh = 0; bh < 4; ++bh)
+#pragma unroll
+    for (int q = 0; q < 6; ++q) dh2[bh] = mfma16(w.a[bh][I[q]], d[J[q]], dh2[bh]);
 }
 
 template <class L>
-__global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ center,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_WAVES, E3GNN_BWDW_WAVES))) void k_conv_bwd_w(const int* __restrict__ center,
                                                     const int* __restrict__ nbr,
                                                     const float* __restrict__ emb,
                                                     const float* __restrict__ Y,
@@ -689,9 +754,8 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
                                                     const float* __restrict__ gagg, MlpW W,
                                                     float* __restrict__ demb, int n_edges,
                                                     int n_nodes, int n_centers) {
-  // per wave: two dw transpose tiles [16 slots][17] + Y of the tile [16][9]
-  constexpr int DWB = 16 * 17;
-  __shared__ float lds[4][2 * DWB + 160];
+  // per wave: two dw transpose tiles [16 slots][DWS] + Y of the tile [16][9]
+  __shared__ __attribute__((aligned(16))) float lds[4][2 * DWB + 160];
   const int wid = threadIdx.x >> 6;
   const int e0 = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wid) * 16);
   if (e0 >= n_edges) return;
@@ -713,10 +777,10 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
 #pragma unroll
   for (int r = 0; r < 4; ++r) vh[r] = src[r] * L::DX * 4;
   f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
-  f32x4 bq[4];
-  load_w2q(bq, R.w2q, lane, L::P[0].woff);
-  int pend = 0;  // a dE/dw block waits in dwbuf[buf ^ 1] for its MFMAs
-  int buf = 0;
+  int nb = 0;  // visited blocks; block b's dE/dw goes to LDS buffer b & 1
+  PairW pw;    // W2 operands of the pair (modes 1, 2)
+  f32x4 bq[4];  // W2 operands of the next block (mode 0)
+  if constexpr (E3GNN_BWDW_MODE == 0) load_w2q(bq, R.w2q, lane, L::P[0].woff);
 
   sfor<3>([&](auto I) {
     constexpr int MUL = iblock_mul<L, I>();
@@ -736,27 +800,36 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
             constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
             phase();
             // software pipeline: this block's dE/dagg gathers are issued, then the
-            // previous block's MFMAs run while they are in flight
+            // MFMAs of the previous (complete) block pair run while they are in flight
             float gm[4][D3];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               ldv<D3>(Rg, vg[r] + col * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm[r]);
-            if (pend) {
-              mfma_dw(dh2, bq, dwbuf + (buf ^ 1) * DWB, lane);
-              load_w2q(bq, R.w2q, lane, p.woff + 16 * jj);
+            if constexpr (E3GNN_BWDW_MODE == 0) {
+              if (nb > 0) {
+                mfma_dw(dh2, bq, dwbuf + ((nb - 1) & 1) * DWB, lane);
+                load_w2q(bq, R.w2q, lane, p.woff + 16 * jj);
+              }
+            } else if constexpr (E3GNN_BWDW_MODE == 1) {
+              if (nb > 0 && (nb & 1) == 0) {
+                load_pair(pw, R.w2c, nb / 2 - 1, lane);
+                mfma_pair(dh2, pw, dwbuf, lane);
+              }
+            } else {
+              if (nb & 1) load_pair(pw, R.w2c, nb / 2, lane);
+              else if (nb > 0) mfma_pair(dh2, pw, dwbuf, lane);
             }
             phase();
-            float* dwc = dwbuf + buf * DWB;
+            float* dwc = dwbuf + (nb & 1) * DWB;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float* yr = ybuf + (4 * g + r) * 9;
               float y[D2];
 #pragma unroll
               for (int q = 0; q < D2; ++q) y[q] = yr[yoff(p.l2) + q];
-              dwc[(4 * g + r) * 17 + col] = tp_bwd_w<p.l1, p.l2, p.l3>(x[r], y, gm[r]);
+              dwc[(4 * g + r) * DWS + col] = tp_bwd_w<p.l1, p.l2, p.l3>(x[r], y, gm[r]);
             }
-            pend = 1;
-            buf ^= 1;
+            ++nb;
           }
         });
       }
@@ -764,7 +837,12 @@ __global__ __launch_bounds__(256) void k_conv_bwd_w(const int* __restrict__ cent
   });
 
   phase();
-  mfma_dw(dh2, bq, dwbuf + (buf ^ 1) * DWB, lane);  // last block
+  if constexpr (E3GNN_BWDW_MODE == 0) {
+    mfma_dw(dh2, bq, dwbuf + ((nb - 1) & 1) * DWB, lane);  // last block
+  } else {
+    if constexpr (E3GNN_BWDW_MODE == 1) load_pair(pw, R.w2c, nb / 2 - 1, lane);
+    mfma_pair(dh2, pw, dwbuf, lane);  // last pair
+  }
   // ---- MLP chain backward (pre-activations recomputed)
   phase();
   MlpT m;

@@ -34,9 +34,13 @@ for s in "$@"; do
     ptest) step ptest 600 python -m pytest tests/test_parallel.py -q ;;
     bench2) step bench2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --cells 11 --same-device --no-cpu-baseline ;;
     report) step report 300 python tools/parity_report.py ;;
+    pmctcp) step pmctcp 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum --kernel-trace --output-format csv -d gpurun_out/pmc_tcp -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
+    pmctcc) step pmctcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum --kernel-trace --output-format csv -d gpurun_out/pmc_tcc -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
     listc) step listc 120 rocprofv3 -L ;;
     pmcsq) step pmcsq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES --kernel-trace --output-format csv -d gpurun_out/pmc_sq -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
     pmcsq2) step pmcsq2 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace --output-format csv -d gpurun_out/pmc_sq2 -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
+    benchv_*) v=${s#benchv_}; step bench_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    testsv_*) v=${s#testsv_}; step tests_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -m pytest tests -m gpu -x -q ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
