@@ -56,6 +56,7 @@ extern "C" {
 
 typedef struct e3gnn_model e3gnn_model;
 typedef struct e3gnn_ctx e3gnn_ctx;
+typedef struct e3gnn_nlist e3gnn_nlist;
 
 const char* e3gnn_last_error(void);
 int e3gnn_abi_version(void);
@@ -119,6 +120,25 @@ int e3gnn_halo_pack(const int32_t* idx, int64_t n, int dim, const float* src, in
 /* dst[idx[r]*dst_stride + k] (+)= src[r*dim + k]; idx entries must be unique */
 int e3gnn_halo_unpack(const int32_t* idx, int64_t n, int dim, const float* src, float* dst,
                       int64_t dst_stride, int accumulate, void* stream);
+
+/* ---- device neighbour list (the graph build in front of the hot path) ----
+ * Replaces ASE primitive_neighbor_list('ijDS', pbc, cell, pos, cutoff,
+ * self_interaction=True) minus the (i, i, S = 0) pair (sevenn/train/
+ * dataload.py:31-68, :113-125) and the host loops of pair_e3gnn.cpp:155-182.
+ * Edges (i, j, S): r_ij = pos[j] + S cell - pos[i], |r_ij| < cutoff, sorted by
+ * (i, j, S) -- the CSR order e3gnn_energy_forces takes.  pos: device f64
+ * [n][3]; cell: HOST f64 [3][3] (rows a, b, c; unused when pbc is all 0);
+ * pbc: HOST int[3], all 1 (periodic) or all 0 (isolated cluster).
+ * e3gnn_nlist_build counts the edges (synchronises `stream`) and keeps the
+ * binning; e3gnn_nlist_fetch then writes edge_center/edge_nbr int32 [E],
+ * shift int32 [E][3] and edge_vec f32 [E][3] (both nullable) -- device memory
+ * the caller sized from *n_edges.  At most 512 neighbours per centre. */
+e3gnn_nlist* e3gnn_nlist_create(int device);
+void e3gnn_nlist_free(e3gnn_nlist* h);
+int e3gnn_nlist_build(e3gnn_nlist* h, int64_t n, const double* pos, const double* cell,
+                      const int* pbc, double cutoff, int64_t* n_edges, void* stream);
+int e3gnn_nlist_fetch(e3gnn_nlist* h, int32_t* edge_center, int32_t* edge_nbr, int32_t* shift,
+                      float* edge_vec, void* stream);
 
 /* ---- diagnostics ---- */
 /* Kernel implementation of the convolution: 0 = fused radial-MLP + tensor

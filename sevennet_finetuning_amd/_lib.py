@@ -39,6 +39,11 @@ SIGNATURES = {
     'e3gnn_forces': (_c_int, [_vp, _vp, _vp, _vp, _vp]),
     'e3gnn_halo_pack': (_c_int, [_vp, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
     'e3gnn_halo_unpack': (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_i64, _c_int, _vp]),
+    'e3gnn_nlist_create': (_vp, [_c_int]),
+    'e3gnn_nlist_free': (None, [_vp]),
+    'e3gnn_nlist_build': (_c_int, [_vp, _c_i64, _vp, _P(ctypes.c_double), _P(_c_int),
+                                   ctypes.c_double, _P(_c_i64), _vp]),
+    'e3gnn_nlist_fetch': (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_set_impl': (_c_int, [_vp, _c_int]),
     'e3gnn_set_timing': (_c_int, [_vp, _c_int]),
     'e3gnn_kernel_stats': (_c_int, [_vp, _P(_cp), _P(ctypes.c_double), _P(_c_i64),

@@ -29,6 +29,7 @@
 #include "fused.h"
 #include "minijson.h"
 #include "node.h"
+#include "neighbor.h"
 #include "tp.h"
 
 using namespace e3gnn;
@@ -1169,6 +1170,160 @@ int e3gnn_halo_unpack(const int32_t* idx, int64_t n, int dim, const float* src, 
                       int64_t dst_stride, int accumulate, void* stream) {
   if (n < 0 || dim <= 0) return fail(E3GNN_ERR_ARG, "bad halo size");
   HIPCHK(launch_unpack(n, dim, idx, src, dst, dst_stride, accumulate, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+// ------------------------------------------------------------ neighbour list
+struct e3gnn_nlist {
+  int device = 0;
+  int64_t n = 0, E = 0;
+  NlGeom G{};
+  const double* pos = nullptr;
+  bool built = false;
+  DBuf f0, bin, bin_count, bin_start, cursor, bin_atoms, deg, row_ptr, err;
+};
+
+e3gnn_nlist* e3gnn_nlist_create(int device) {
+  if (hipSetDevice(device) != hipSuccess) {
+    fail(E3GNN_ERR_HIP, "hipSetDevice failed");
+    return nullptr;
+  }
+  auto* h = new e3gnn_nlist;
+  h->device = device;
+  return h;
+}
+void e3gnn_nlist_free(e3gnn_nlist* h) { delete h; }
+
+namespace {
+// bins of width >= rc per dimension (heights h), at most ~4 per atom
+void nl_bins(NlGeom& G, const double h[3], double rc, int64_t n) {
+  for (int k = 0; k < 3; ++k) G.nb[k] = std::max(1, (int)std::floor(h[k] / rc));
+  while ((int64_t)G.nb[0] * G.nb[1] * G.nb[2] > 4 * n + 64) {
+    int k = 0;
+    for (int q = 1; q < 3; ++q)
+      if (G.nb[q] > G.nb[k]) k = q;
+    G.nb[k] = std::max(1, G.nb[k] / 2);
+  }
+  for (int k = 0; k < 3; ++k) G.R[k] = std::max(1, (int)std::ceil(rc * G.nb[k] / h[k]));
+}
+}  // namespace
+
+int e3gnn_nlist_build(e3gnn_nlist* h, int64_t n, const double* pos, const double* cell,
+                      const int* pbc, double cutoff, int64_t* n_edges, void* stream) {
+  if (!h) return fail(E3GNN_ERR_ARG, "null neighbour-list handle");
+  if (n < 0 || n >= (int64_t)1 << 30) return fail(E3GNN_ERR_ARG, "atom count out of range");
+  if (!(cutoff > 0)) return fail(E3GNN_ERR_ARG, "cutoff must be positive");
+  if (n > 0 && !pos) return fail(E3GNN_ERR_ARG, "null positions");
+  if (!pbc) return fail(E3GNN_ERR_ARG, "null pbc flags");
+  const bool all = pbc[0] && pbc[1] && pbc[2], none = !pbc[0] && !pbc[1] && !pbc[2];
+  if (!all && !none)
+    return fail(E3GNN_ERR_ARG, "device neighbour list: pbc must be all true or all false");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  h->built = false;
+  h->n = n;
+  h->pos = pos;
+  NlGeom& G = h->G;
+  G = NlGeom{};
+  G.rc2 = cutoff * cutoff;
+  G.periodic = all ? 1 : 0;
+  double hgt[3];
+  if (all) {
+    if (!cell) return fail(E3GNN_ERR_ARG, "null cell");
+    for (int k = 0; k < 9; ++k) G.cell[k] = cell[k];
+    const double* a = cell;
+    const double det = a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) +
+                       a[2] * (a[3] * a[7] - a[4] * a[6]);
+    if (!(std::fabs(det) > 1e-12)) return fail(E3GNN_ERR_ARG, "singular cell");
+    // inverse (rows of cell = lattice vectors): frac = pos @ inv
+    G.inv[0] = (a[4] * a[8] - a[5] * a[7]) / det;
+    G.inv[1] = (a[2] * a[7] - a[1] * a[8]) / det;
+    G.inv[2] = (a[1] * a[5] - a[2] * a[4]) / det;
+    G.inv[3] = (a[5] * a[6] - a[3] * a[8]) / det;
+    G.inv[4] = (a[0] * a[8] - a[2] * a[6]) / det;
+    G.inv[5] = (a[2] * a[3] - a[0] * a[5]) / det;
+    G.inv[6] = (a[3] * a[7] - a[4] * a[6]) / det;
+    G.inv[7] = (a[1] * a[6] - a[0] * a[7]) / det;
+    G.inv[8] = (a[0] * a[4] - a[1] * a[3]) / det;
+    for (int k = 0; k < 3; ++k) {  // height along k = |det| / |a_{k+1} x a_{k+2}|
+      const double* u = a + 3 * ((k + 1) % 3);
+      const double* v = a + 3 * ((k + 2) % 3);
+      const double cx = u[1] * v[2] - u[2] * v[1], cy = u[2] * v[0] - u[0] * v[2],
+                   cz = u[0] * v[1] - u[1] * v[0];
+      hgt[k] = std::fabs(det) / std::sqrt(cx * cx + cy * cy + cz * cz);
+    }
+  } else {
+    // isolated cluster: a virtual orthorhombic box 1 A beyond the atoms on
+    // every side, so no image is ever within the cutoff (S = 0 throughout)
+    std::vector<double> hp((size_t)n * 3);
+    if (n) HIPCHK(hipMemcpy(hp.data(), pos, hp.size() * 8, hipMemcpyDefault));
+    double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+    for (int64_t a = 0; a < n; ++a)
+      for (int k = 0; k < 3; ++k) {
+        const double v = hp[3 * a + k];
+        if (!std::isfinite(v)) return fail(E3GNN_ERR_ARG, "non-finite position");
+        lo[k] = a ? std::min(lo[k], v) : v;
+        hi[k] = a ? std::max(hi[k], v) : v;
+      }
+    for (int k = 0; k < 3; ++k) {
+      G.origin[k] = lo[k] - 1.0;
+      hgt[k] = (hi[k] - lo[k]) + 2.0;
+      G.cell[4 * k] = hgt[k];
+      G.inv[4 * k] = 1.0 / hgt[k];
+    }
+  }
+  nl_bins(G, hgt, cutoff, n);
+  const int nbins = G.nb[0] * G.nb[1] * G.nb[2];
+  if (h->f0.ensure((size_t)std::max<int64_t>(n, 1) * 12) != hipSuccess ||
+      h->bin.ensure((size_t)std::max<int64_t>(n, 1) * 4) != hipSuccess ||
+      h->bin_atoms.ensure((size_t)std::max<int64_t>(n, 1) * 4) != hipSuccess ||
+      h->deg.ensure((size_t)std::max<int64_t>(n, 1) * 4) != hipSuccess ||
+      h->row_ptr.ensure((size_t)(n + 1) * 4) != hipSuccess ||
+      h->bin_count.ensure((size_t)nbins * 4) != hipSuccess ||
+      h->bin_start.ensure((size_t)(nbins + 1) * 4) != hipSuccess ||
+      h->cursor.ensure((size_t)nbins * 4) != hipSuccess || h->err.ensure(4) != hipSuccess)
+    return fail(E3GNN_ERR_HIP, "neighbour-list workspace allocation failed");
+  int* err = h->err.i();
+  HIPCHK(hipMemsetAsync(err, 0, 4, s));
+  HIPCHK(hipMemsetAsync(h->bin_count.p, 0, (size_t)nbins * 4, s));
+  HIPCHK(hipMemsetAsync(h->cursor.p, 0, (size_t)nbins * 4, s));
+  HIPCHK(launch_nl_bin((int)n, pos, G, h->f0.i(), h->bin.i(), h->bin_count.i(), err, s));
+  HIPCHK(launch_nl_scan(nbins, h->bin_count.i(), h->bin_start.i(), s));
+  HIPCHK(launch_nl_place((int)n, h->bin.i(), h->bin_start.i(), h->cursor.i(), h->bin_atoms.i(), s));
+  HIPCHK(launch_nl_search(false, (int)n, pos, G, h->f0.i(), h->bin.i(), h->bin_start.i(),
+                          h->bin_atoms.i(), h->deg.i(), nullptr, nullptr, nullptr, nullptr, nullptr,
+                          err, s));
+  if (n > 0) HIPCHK(launch_nl_scan((int)n, h->deg.i(), h->row_ptr.i(), s));
+  int herr = 0, total = 0;
+  HIPCHK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, s));
+  if (n > 0) HIPCHK(hipMemcpyAsync(&total, h->row_ptr.i() + n, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (herr & 1) return fail(E3GNN_ERR_ARG, "non-finite or out-of-box atom position");
+  if (herr & 4)
+    return fail(E3GNN_ERR_GRAPH, "a centre has more than " + std::to_string(NL_MAXD) +
+                                     " neighbours (device neighbour-list limit)");
+  if (total < 0) return fail(E3GNN_ERR_GRAPH, "edge count exceeds int32");
+  h->E = total;
+  h->built = true;
+  if (n_edges) *n_edges = total;
+  return E3GNN_OK;
+}
+
+int e3gnn_nlist_fetch(e3gnn_nlist* h, int32_t* center, int32_t* nbr, int32_t* shift, float* vec,
+                      void* stream) {
+  if (!h || !h->built) return fail(E3GNN_ERR_ARG, "neighbour list not built");
+  if (h->E > 0 && (!center || !nbr)) return fail(E3GNN_ERR_ARG, "null edge output");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  int* err = h->err.i();
+  HIPCHK(hipMemsetAsync(err, 0, 4, s));
+  HIPCHK(launch_nl_search(true, (int)h->n, h->pos, h->G, h->f0.i(), h->bin.i(), h->bin_start.i(),
+                          h->bin_atoms.i(), nullptr, h->row_ptr.i(), center, nbr, shift, vec, err,
+                          s));
+  int herr = 0;
+  HIPCHK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (herr & 2) return fail(E3GNN_ERR_GRAPH, "periodic image shift beyond +-1024 cells");
   return E3GNN_OK;
 }
 

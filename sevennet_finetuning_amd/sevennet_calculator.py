@@ -51,16 +51,49 @@ class SevenNetCalculator(Calculator):
         self.cutoff = self.model.cutoff
         self.sevennet_config = sevennet_config
         self.implemented_properties = ['free_energy', 'energy', 'forces', 'stress', 'energies']
+        self._nlist = None
+
+    def _types(self, atoms):
+        try:
+            return np.array([self.type_map[int(z)] for z in atoms.get_atomic_numbers()])
+        except KeyError as e:
+            raise ValueError(f'atomic number {e} is not a species of this model') from None
+
+    def _calculate_device_graph(self, atoms):
+        """Graph built by the device neighbour list (periodic or isolated
+        systems): positions go to the GPU once, nothing comes back until the
+        results."""
+        from .neighbor import DeviceNeighborList
+        if self._nlist is None:
+            self._nlist = DeviceNeighborList(self.device)
+        pbc = bool(np.all(atoms.get_pbc()))
+        cell = np.array(atoms.get_cell(), dtype=np.float64)
+        center, nbr, _, vec = self._nlist(atoms.get_positions(), cell if pbc else None,
+                                          self.cutoff, (pbc,) * 3)
+        types = torch.as_tensor(self._types(atoms), dtype=torch.int32, device=self.device)
+        res = self.model.energy_forces(types, center, nbr, vec)
+        energy = float(res['energy'].item())
+        self.results = {
+            'free_energy': energy,
+            'energy': energy,
+            'energies': res['atomic_energy'].cpu().numpy(),
+            'forces': res['forces'].cpu().numpy(),
+        }
+        if pbc:
+            sigma = res['virial'].cpu().numpy() / abs(np.linalg.det(cell))
+            self.results['stress'] = -sigma[[0, 1, 2, 4, 5, 3]]
+        return res
 
     def calculate(self, atoms=None, properties=None, system_changes=all_changes):
         Calculator.calculate(self, atoms, properties, system_changes)
         if atoms is None:
             raise ValueError('No atoms to evaluate')
+        pbc = np.asarray(atoms.get_pbc(), dtype=bool).reshape(-1)
+        if pbc.all() or not pbc.any():
+            return self._calculate_device_graph(atoms)
+        # mixed periodicity (slabs): the host list (util.unlabeled_atoms_to_graph)
         data = unlabeled_atoms_to_graph(atoms, self.cutoff)
-        try:
-            data[KEY.NODE_FEATURE] = np.array([self.type_map[int(z)] for z in data[KEY.NODE_FEATURE]])
-        except KeyError as e:
-            raise ValueError(f'atomic number {e} is not a species of this model') from None
+        data[KEY.NODE_FEATURE] = self._types(atoms)
         out = self.model(data)
         energy = float(out[KEY.PRED_TOTAL_ENERGY].item())
         self.results = {
