@@ -11,11 +11,26 @@ namespace e3gnn {
 // table; the constant is frozen in serial_code.py as c5).
 constexpr float SILU_NORM = 1.6791767923989418f;
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_rcp_f32 (1 ulp) instead of an IEEE division (~10 VALU per call)
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ float act_fwd(float x) { return x * sigmoidf_(x) * SILU_NORM; }
 __device__ __forceinline__ float act_grad(float x) {
   const float s = sigmoidf_(x);
   return SILU_NORM * s * (1.0f + x * (1.0f - s));
+}
+
+// sum over the four 16-lane rows of a wave (lanes l, l^16, l^32, l^48), every
+// lane gets the same bits: (r0 + r2) + (r1 + r3) via v_permlane32_swap /
+// v_permlane16_swap (VALU, no LDS round trip).  Inline asm: the builtins'
+// second result (the swapped source register) comes back as a copy of the
+// first with this compiler (tools/microtests/permlane.hip); the s_nop pads the
+// VALU-write -> permlane-read hazard, which hipcc does not insert inside asm.
+__device__ __forceinline__ float sum_rows4(float v) {
+  float a = v, b = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  float s = a + b, t = s;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(s), "+v"(t));
+  return s + t;
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -390,6 +390,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
   const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rh = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
   const __amdgpu_buffer_rsrc_t Ro = rsrc_bytes(out, L::DM * 4);
+  const float rden = 1.0f / denom;
   for (int e0 = beg; e0 < end || e0 == beg; e0 += 16) {
     const bool first_tile = e0 == beg;
     int src[4];
@@ -446,11 +447,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
 #pragma unroll
               for (int k = 0; k < D3; ++k) {
                 float v = acc[k];
-                v += __shfl_xor(v, 16, 64);
-                v += __shfl_xor(v, 32, 64);
+                v = sum_rows4(v) * rden;
                 if (g == 0) {
                   const int so = (p.moff + 16 * j * D3 + k) * 4, vo = col * D3 * 4;
-                  stw(first_tile ? v / denom : prev[k] + v / denom, Ro, vo, so);
+                  stw(first_tile ? v : prev[k] + v, Ro, vo, so);
                 }
               }
             }
@@ -664,13 +664,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
 #pragma unroll
     for (int q = 1; q < 9; ++q) {
       float v = dYa[q];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
+      v = sum_rows4(v);
       dYa[q] = v;
     }
     if (g == 0 && er >= 0) {
       const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f, c15 = s3 * s5;
-      const float ux = y[1] / s3, uy = y[2] / s3, uz = y[3] / s3;
+      const float is3 = 0.57735026918962576f;  // 1 / sqrt(3)
+      const float ux = y[1] * is3, uy = y[2] * is3, uz = y[3] * is3;
       const float* d = dYa + 1;  // d[0..2] = dE/dY_1, d[3..7] = dE/dY_2
       const float gx = s3 * d[0] + c15 * (uz * d[3] + uy * d[4]) - s5 * ux * d[5] - c15 * ux * d[7];
       const float gy = s3 * d[1] + c15 * (ux * d[4] + uz * d[6]) + 2.f * s5 * uy * d[5];
