@@ -29,17 +29,16 @@ __device__ __forceinline__ int find_prob(const GemmBatch& b, int tile) {
   return p;
 }
 
-__global__ __launch_bounds__(256) void k_gemm(GemmBatch batch) {
-  __shared__ float As[BK][BM + PAD];
-  __shared__ float Bs[BK][BN + PAD];
-  const int pi = find_prob(batch, blockIdx.x);
-  const GemmProb& P = batch.p[pi];
-  const int local = blockIdx.x - P.tile_begin;
+// RC: the row group size R as a compile-time constant (1, 3, 5: the irrep
+// blocks' 2l+1; row / R and row % R are then multiplies), 0 = runtime P.R
+template <int RC>
+__device__ __forceinline__ void gemm_tile(const GemmProb& P, int local, float (*As)[BM + PAD],
+                                          float (*Bs)[BN + PAD]) {
   const int tm = local / P.tiles_n, tn = local % P.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int R = P.R;
+  const int R = RC ? RC : P.R;
 
   // staging assignment: A: 4 elements per thread, row = e / BK, k = e % BK
   int a_row[4];
@@ -107,6 +106,20 @@ __global__ __launch_bounds__(256) void k_gemm(GemmBatch batch) {
     }
     if (P.beta) v += P.C[off];
     P.C[off] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gemm(GemmBatch batch) {
+  __shared__ float As[BK][BM + PAD];
+  __shared__ float Bs[BK][BN + PAD];
+  const int pi = find_prob(batch, blockIdx.x);
+  const GemmProb& P = batch.p[pi];
+  const int local = blockIdx.x - P.tile_begin;
+  switch (P.R) {
+    case 1: gemm_tile<1>(P, local, As, Bs); break;
+    case 3: gemm_tile<3>(P, local, As, Bs); break;
+    case 5: gemm_tile<5>(P, local, As, Bs); break;
+    default: gemm_tile<0>(P, local, As, Bs); break;
   }
 }
 }  // namespace
