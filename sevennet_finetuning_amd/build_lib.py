@@ -47,7 +47,8 @@ def build(force=False, verbose=False, out=None, defines=()):
                '-o', obj]
         if verbose:
             print(' '.join(cmd))
-        r = subprocess.run(cmd, capture_output=True, text=True)
+        # a register-allocation pathology once kept clang busy for 30+ minutes
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         if r.returncode != 0:
             raise RuntimeError(f'hipcc failed on {src}:\n{r.stdout}\n{r.stderr}')
         return obj

@@ -50,6 +50,11 @@
 #ifndef E3GNN_BWDW_WAVES
 #define E3GNN_BWDW_WAVES 4
 #endif
+// dE/dx kernel: dE/dagg operands loaded one path block ahead (1; spills 18
+// registers at 3 waves/SIMD: 17.4 -> 20.9 ms per three launches) or at use (0)
+#ifndef E3GNN_BWDX_GMPF
+#define E3GNN_BWDX_GMPF 0
+#endif
 #ifndef E3GNN_BWDX_WAVES
 #define E3GNN_BWDX_WAVES 3
 #endif
@@ -526,6 +531,31 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
+// dE/dagg operands of path PN at channel block jj for the lane's edge (4 * D3
+// floats at the edge centre's row, channels 4g..4g+3)
+template <class L, int PN>
+__device__ __forceinline__ void load_gm(float* gmN, __amdgpu_buffer_rsrc_t Rg, int vg, int g, int jj) {
+  constexpr int D3 = 2 * L::P[PN].l3 + 1;
+  ldv<4 * D3>(Rg, vg + 4 * g * D3 * 4, (L::P[PN].moff + 16 * jj * D3) * 4, gmN);
+}
+// issue the loads of the block after (I, jj, PI) in visiting order (if any)
+template <class L, int I, int PI>
+__device__ __forceinline__ void prefetch_gm(float* gmN, __amdgpu_buffer_rsrc_t Rg, int vg, int g,
+                                            int jj) {
+  constexpr int np = next_path_same_I<L>(PI);
+  if constexpr (np >= 0) {
+    load_gm<L, np>(gmN, Rg, vg, g, jj);
+  } else {
+    constexpr int f = first_path_of<L>(I);
+    constexpr int fn = first_path_after_I<L>(I);
+    if (jj + 1 < L::P[f].mul / 16) {
+      load_gm<L, f>(gmN, Rg, vg, g, jj + 1);
+    } else {
+      if constexpr (fn >= 0) load_gm<L, fn>(gmN, Rg, vg, g, 0);
+    }
+  }
+}
+
 // B1: lane (g, c) = edge slot c of the tile x channels 4g..4g+3 of a 16-channel
 // block (transposed product w^T = W2^T H2^T: D[channel 4g+r][edge c]).  One
 // edge per lane keeps dE/dY in 8 registers; dE/dx[j] is summed over the 16
@@ -593,6 +623,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
     float dYa[9];  // dE/dY of edge c over this lane's channels (index 0 unused)
 #pragma unroll
     for (int q = 0; q < 9; ++q) dYa[q] = 0.f;
+    // dE/dagg operands run one path block ahead of their use (software pipeline)
+    float gmN[20];
+    if constexpr (E3GNN_BWDX_GMPF) load_gm<L, 0>(gmN, Rg, vg, g, 0);
 
     sfor<3>([&](auto I) {
       constexpr int MUL = iblock_mul<L, I>();
@@ -610,9 +643,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
             if constexpr (p.l1 == I) {
               constexpr int D3 = 2 * p.l3 + 1;
               phase();
-              // dE/dagg of the edges' centres: issued before the MFMAs, which hide it
+              // dE/dagg of the edges' centres (loaded during the previous block);
+              // the next block's are issued now
               float gm[4 * D3];
-              ldv<4 * D3>(Rg, vg + 4 * g * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm);
+              if constexpr (E3GNN_BWDX_GMPF) {
+#pragma unroll
+                for (int k = 0; k < 4 * D3; ++k) gm[k] = gmN[k];
+                prefetch_gm<L, I, pi>(gmN, Rg, vg, g, jj);
+              } else {
+                load_gm<L, pi>(gm, Rg, vg, g, jj);
+              }
               // w^T block: A = W2s[:, col0 + i]^T (w2p order), B = H2^T
               const f32x4 wv = w2_block<false>(hq, wq);
               {
