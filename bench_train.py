@@ -1,0 +1,128 @@
+"""Benchmark of the fine-tune step (BASELINE config 5).
+
+``python bench_train.py --gpus N --steps K --warmup W`` (N > 1 under torchrun,
+one process per GPU, RCCL).  A step = one iteration of the reference's
+RehearsalTrainer.run_one_epoch_rehearsal (trainer.py:174-206) with the
+FT_w_reEWC recipe (Huber delta 0.01, force weight 1, stress weight 0.01, EWC
+lambda 1e5, Adam): forward + force/stress (create_graph) + loss backward
+(double backward through the HIP convolution kernels) + gradient all-reduce +
+Adam step on a batch of 8 structures, then the same on a memory batch of 8.
+Structures: 54-atom primitive diamond cells (3x3x3), species drawn from
+{Li, P, S, Cl}, N(0, 0.05 A) displacements, rc = 5 A; synthetic labels
+(energy -4 eV/atom + noise, forces/stress noise; default_rng(2)); synthetic
+Fisher (the reference's fisher_sevenn.pt does not travel to the GPU box).
+Every rank draws its own batches (weak scaling: 16 structures per rank per
+step).  value = structures processed by all ranks / max-over-ranks time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def log(msg):
+    if int(os.environ.get('RANK', '0')) == 0:
+        print(f'[bench_train] {msg}', file=sys.stderr, flush=True)
+
+
+def make_batches(rank, n_batches, batch_size, symbols):
+    from sevennet_finetuning_amd import train
+    from sevennet_finetuning_amd.structures import diamond_primitive, mixed_symbols
+    rng = np.random.default_rng(2)
+    graphs = []
+    for k in range(n_batches * batch_size):
+        seed = 10_000 * rank + k
+        pos, cell = diamond_primitive((3, 3, 3), sigma=0.05, seed=seed)
+        types = [symbols.index(s) for s in mixed_symbols(len(pos), seed=seed + 1)]
+        graphs.append(train.labeled_graph(
+            pos, cell, types, 5.0, energy=-4.0 * len(pos) + rng.normal(0, 0.5),
+            force=rng.normal(0, 0.3, (len(pos), 3)), stress=rng.normal(0, 2e-3, 6)))
+    return [graphs[i * batch_size:(i + 1) * batch_size] for i in range(n_batches)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=8)
+    args = ap.parse_args()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    device = torch.device('cuda', local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=device)
+
+    from sevennet_finetuning_amd import train
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    model = SevenNetTrainable(device=device)
+    fisher = {n: torch.full_like(p, 1e-3) for n, p in model.named_parameters()}
+    opt = {n: p.detach().clone() for n, p in model.named_parameters()}
+    cfg = {'loss': 'huber', 'loss_param': {'delta': 0.01}, 'force_loss_weight': 1.0,
+           'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
+           'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
+           'scheduler_param': {'gamma': 0.99}, 'is_ddp': world > 1, 'device': device,
+           'continue': {'fisher_information': fisher, 'opt_params': opt, 'ewc_lambda': 1e5}}
+    tr = train.Trainer(model, cfg)
+    n_b = 4
+    batches = make_batches(rank, 2 * n_b, args.batch, model.chemical_symbols)
+    dev_batches = [train.collate(b, device=device, dtype=torch.float32) for b in batches]
+    atoms_per_step = sum(int(b['num_atoms'].sum()) for b in dev_batches[:2])
+    edges = int(dev_batches[0]['edge_index'].shape[1])
+    log(f'{args.batch} x 54-atom structures per batch, {edges} edges; rank {rank}/{world}')
+    model.train(True)
+
+    def step(i):
+        b, m = dev_batches[(2 * i) % (2 * n_b)], dev_batches[(2 * i + 1) % (2 * n_b)]
+        return tr.rehearsal_step(b, m)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    for i in range(args.warmup):
+        step(i)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss, mloss = step(i)
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t)
+    ms = dt / args.steps * 1e3
+    structs = 2 * args.batch * world * args.steps
+    if rank == 0:
+        print(json.dumps({
+            'metric': 'structures/sec fine-tune step (rehearsal + EWC), SevenNet-0',
+            'value': round(structs / dt, 2), 'unit': 'structures/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+            'data': 'synthetic 54-atom mixed-species diamond cells, synthetic labels/Fisher',
+            'config': {'workload': f'rehearsal step: 2 x {args.batch} structures per rank '
+                                   f'({atoms_per_step} atoms), force+stress+energy Huber + EWC, '
+                                   'Adam, grad all-reduce',
+                       'atoms_per_rank_step': atoms_per_step, 'edges_per_batch': edges,
+                       'parallelism': f'dp{world}'},
+            'atoms_per_s': round(atoms_per_step * world * args.steps / dt, 1),
+            'loss': float(loss), 'mem_loss': float(mloss)}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -121,6 +121,39 @@ int e3gnn_halo_pack(const int32_t* idx, int64_t n, int dim, const float* src, in
 int e3gnn_halo_unpack(const int32_t* idx, int64_t n, int dim, const float* src, float* dst,
                       int64_t dst_stride, int accumulate, void* stream);
 
+/* ---- training ops (fine-tune step) ----
+ * Stateless convolution primitives on caller-owned device tensors, for the
+ * differentiable model of sevennet_finetuning_amd/nn.py, which replaces the
+ * reference's e3nn TensorProduct + message_gather inside
+ * IrrepsConvolution.forward (sevenn/nn/convolution.py:104-123) when the
+ * trainer takes parameter gradients of a force loss (create_graph=True,
+ * force_output.py:158-215; trainer.py:155-222).  The product
+ *   agg[i] = sum_{e: edge_center[e] = i} TP(h[edge_nbr[e]], Y[e], w[e])
+ * is trilinear in (h, Y, w), so every derivative of every order is one of the
+ * two launches below with permuted operands.  `kind` selects the SevenNet-0
+ * path table: 0 = first block (h 128, w 384, agg 1152), 1 = middle blocks
+ * (480, 960, 3136), 2 = last block (480, 224, 224); e3gnn_conv_dims reports
+ * them.  Sums are raw (no 1/denominator; the caller divides). */
+int e3gnn_conv_dims(int kind, int* h_dim, int* w_dim, int* agg_dim);
+/* CSR of the edges (edge_center sorted non-decreasing): row_ptr[n+1],
+ * transposed CSR src_ptr[n+1] / src_perm[E] (edges per neighbour, ascending
+ * edge id), scratch[n+1] int32.  Validates the graph (synchronises `stream`;
+ * E3GNN_ERR_GRAPH if unsorted or out of range). */
+int e3gnn_conv_graph(int64_t n_nodes, int64_t n_edges, const int32_t* edge_center,
+                     const int32_t* edge_nbr, int32_t* row_ptr, int32_t* src_ptr,
+                     int32_t* src_perm, int32_t* scratch, void* stream);
+/* agg[n_nodes x agg_dim] = segmented sum of TP(h[nbr], Y, w); Y [E x 9],
+ * w [E x w_dim], h [n_nodes x h_dim]. */
+int e3gnn_conv_forward(int kind, int64_t n_nodes, const int32_t* row_ptr, const int32_t* edge_nbr,
+                       const float* h, const float* Y, const float* w, float* agg, void* stream);
+/* Gradients of <gagg, agg(h, Y, w)>: dY [E x 9] and dw [E x w_dim]
+ * (overwritten), dh [n_nodes x h_dim] (nullable; needs dxc [E x h_dim] scratch
+ * and the transposed CSR; summed per neighbour in ascending edge order). */
+int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_t* row_ptr,
+                        const int32_t* edge_nbr, const int32_t* src_ptr, const int32_t* src_perm,
+                        const float* h, const float* Y, const float* w, const float* gagg,
+                        float* dh, float* dY, float* dw, float* dxc, void* stream);
+
 /* ---- device neighbour list (the graph build in front of the hot path) ----
  * Replaces ASE primitive_neighbor_list('ijDS', pbc, cell, pos, cutoff,
  * self_interaction=True) minus the (i, i, S = 0) pair (sevenn/train/

@@ -39,6 +39,11 @@ SIGNATURES = {
     'e3gnn_forces': (_c_int, [_vp, _vp, _vp, _vp, _vp]),
     'e3gnn_halo_pack': (_c_int, [_vp, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
     'e3gnn_halo_unpack': (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_i64, _c_int, _vp]),
+    'e3gnn_conv_dims': (_c_int, [_c_int, _P(_c_int), _P(_c_int), _P(_c_int)]),
+    'e3gnn_conv_graph': (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'e3gnn_conv_forward': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'e3gnn_conv_backward': (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                     _vp, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_nlist_create': (_vp, [_c_int]),
     'e3gnn_nlist_free': (None, [_vp]),
     'e3gnn_nlist_build': (_c_int, [_vp, _c_i64, _vp, _P(ctypes.c_double), _P(_c_int),

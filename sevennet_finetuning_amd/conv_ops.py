@@ -1,0 +1,176 @@
+"""Differentiable (to second order) convolution op on the HIP kernels.
+
+The reference computes, inside ``IrrepsConvolution.forward``
+(sevenn/nn/convolution.py:104-123),
+
+    msg[e] = TP(x[edge_index[1][e]], Y[e], w[e])       e3nn uvu TensorProduct
+    agg[i] = sum_{e: edge_index[0][e] = i} msg[e]       message_gather :19-32
+
+and the fine-tune step differentiates it twice: once for the forces
+(``autograd.grad(..., create_graph=self.training)``, force_output.py:158-215)
+and once more for the parameter gradients of the force/stress loss
+(trainer.py:155-222).  ``agg(h, Y, w)`` is trilinear, so with
+``s = <g, agg(h, Y, w)>`` every derivative is one of two launches of
+libe3gnn_hip.so with permuted operands:
+
+    forward   F(h, Y, w)        = agg                         e3gnn_conv_forward
+    backward  B(h, Y, w, g)     = (ds/dh, ds/dY, ds/dw)       e3gnn_conv_backward
+
+and the derivative of B against cotangents (a_h, a_Y, a_w) is
+
+    d/dg = F(a_h, Y, w) + F(h, a_Y, w) + F(h, Y, a_w)
+    d/dh = B(h, a_Y, w, g).dh + B(h, Y, a_w, g).dh
+    d/dY = B(a_h, Y, w, g).dY + B(h, Y, a_w, g).dY
+    d/dw = B(a_h, Y, w, g).dw + B(h, a_Y, w, g).dw
+
+(each B call supplies two of the six terms).  There is no CPU fallback: the
+default backend is the library, and a missing library raises ``E3GNNError``.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+class ConvGraph:
+    """Edge CSR of one (batched) graph on the device: ``edge_center`` sorted
+    non-decreasing (the aggregation target, edge_index[0]), ``edge_nbr`` the
+    gathered source (edge_index[1]), plus the transposed CSR the dE/dh sum
+    uses.  Built once per batch and shared by the five interaction blocks."""
+
+    def __init__(self, n_nodes, edge_center, edge_nbr, backend):
+        self.n_nodes = int(n_nodes)
+        self.n_edges = int(edge_center.shape[0])
+        self.edge_center = edge_center
+        self.edge_nbr = edge_nbr
+        self.backend = backend
+        self.aux = backend.build(self)
+
+
+class HipConvBackend:
+    """The kernels of libe3gnn_hip.so (include/e3gnn.h, training ops)."""
+
+    def __init__(self):
+        self.lib = _lib.load()
+        self.dims = {}
+        for kind in (0, 1, 2):
+            a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            _lib.check(self.lib.e3gnn_conv_dims(kind, a, b, c))
+            self.dims[kind] = (a.value, b.value, c.value)
+
+    @staticmethod
+    def _stream(t):
+        return torch.cuda.current_stream(t.device).cuda_stream
+
+    def build(self, g):
+        dev = g.edge_center.device
+        if dev.type != 'cuda':
+            raise _lib.E3GNNError(f'the HIP conv op needs device tensors, got {dev}')
+        n, E = g.n_nodes, g.n_edges
+        ce = g.edge_center.to(torch.int32).contiguous()
+        nb = g.edge_nbr.to(torch.int32).contiguous()
+        aux = {'center': ce, 'nbr': nb,
+               'row_ptr': torch.empty(n + 1, dtype=torch.int32, device=dev),
+               'src_ptr': torch.empty(n + 1, dtype=torch.int32, device=dev),
+               'src_perm': torch.empty(max(E, 1), dtype=torch.int32, device=dev)}
+        scratch = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        _lib.check(self.lib.e3gnn_conv_graph(
+            n, E, ce.data_ptr(), nb.data_ptr(), aux['row_ptr'].data_ptr(),
+            aux['src_ptr'].data_ptr(), aux['src_perm'].data_ptr(), scratch.data_ptr(),
+            self._stream(ce)))
+        return aux
+
+    def _check(self, kind, g, h, Y, w):
+        dx, dw, _ = self.dims[kind]
+        for name, t, shape in (('h', h, (g.n_nodes, dx)), ('Y', Y, (g.n_edges, 9)),
+                               ('w', w, (g.n_edges, dw))):
+            if tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_cuda:
+                raise _lib.E3GNNError(f'conv kind {kind}: {name} must be float32 {shape} on '
+                                      f'the GPU, got {t.dtype} {tuple(t.shape)} on {t.device}')
+
+    def forward(self, kind, g, h, Y, w):
+        self._check(kind, g, h, Y, w)
+        h, Y, w = h.contiguous(), Y.contiguous(), w.contiguous()
+        agg = torch.empty(g.n_nodes, self.dims[kind][2], device=h.device)
+        a = g.aux
+        _lib.check(self.lib.e3gnn_conv_forward(
+            kind, g.n_nodes, a['row_ptr'].data_ptr(), a['nbr'].data_ptr(), h.data_ptr(),
+            Y.data_ptr(), w.data_ptr(), agg.data_ptr(), self._stream(h)))
+        return agg
+
+    def backward(self, kind, g, h, Y, w, gagg, need_h=True):
+        self._check(kind, g, h, Y, w)
+        dx, dwd, dm = self.dims[kind]
+        h, Y, w = h.contiguous(), Y.contiguous(), w.contiguous()
+        gagg = gagg.to(torch.float32).contiguous()
+        if tuple(gagg.shape) != (g.n_nodes, dm):
+            raise _lib.E3GNNError(f'conv kind {kind}: gagg must be {(g.n_nodes, dm)}')
+        dev = h.device
+        E = g.n_edges
+        dY = torch.empty(E, 9, device=dev)
+        dw = torch.empty(E, dwd, device=dev)
+        dh = torch.empty(g.n_nodes, dx, device=dev) if need_h else None
+        dxc = torch.empty(E, dx, device=dev) if need_h and E else None
+        a = g.aux
+        _lib.check(self.lib.e3gnn_conv_backward(
+            kind, g.n_nodes, E, a['row_ptr'].data_ptr(), a['nbr'].data_ptr(),
+            a['src_ptr'].data_ptr(), a['src_perm'].data_ptr(), h.data_ptr(), Y.data_ptr(),
+            w.data_ptr(), gagg.data_ptr(), dh.data_ptr() if dh is not None else None,
+            dY.data_ptr(), dw.data_ptr(), dxc.data_ptr() if dxc is not None else None,
+            self._stream(h)))
+        return dh, dY, dw
+
+
+def _add(acc, t):
+    if t is None:
+        return acc
+    return t if acc is None else acc + t
+
+
+class _ConvForward(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, Y, w, kind, graph):
+        ctx.save_for_backward(h, Y, w)
+        ctx.kind, ctx.graph = kind, graph
+        return graph.backend.forward(kind, graph, h, Y, w)
+
+    @staticmethod
+    def backward(ctx, g):
+        h, Y, w = ctx.saved_tensors
+        dh, dY, dw = _ConvBackward.apply(h, Y, w, g, ctx.kind, ctx.graph)
+        return dh, dY, dw, None, None
+
+
+class _ConvBackward(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, Y, w, g, kind, graph):
+        ctx.save_for_backward(h, Y, w, g)
+        ctx.kind, ctx.graph = kind, graph
+        return graph.backend.backward(kind, graph, h, Y, w, g)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, ah, aY, aw):
+        h, Y, w, g = ctx.saved_tensors
+        k, gr = ctx.kind, ctx.graph
+        be = gr.backend
+        gg = gh = gY = gw = None
+        if ah is not None:
+            gg = _add(gg, be.forward(k, gr, ah, Y, w))
+            _, t_Y, t_w = be.backward(k, gr, ah, Y, w, g, need_h=False)
+            gY, gw = _add(gY, t_Y), _add(gw, t_w)
+        if aY is not None:
+            gg = _add(gg, be.forward(k, gr, h, aY, w))
+            t_h, _, t_w = be.backward(k, gr, h, aY, w, g)
+            gh, gw = _add(gh, t_h), _add(gw, t_w)
+        if aw is not None:
+            gg = _add(gg, be.forward(k, gr, h, Y, aw))
+            t_h, t_Y, _ = be.backward(k, gr, h, Y, aw, g)
+            gh, gY = _add(gh, t_h), _add(gY, t_Y)
+        return gh, gY, gw, gg, None, None
+
+
+def conv(h, Y, w, kind, graph):
+    """Raw (un-normalised) aggregated messages of one interaction block."""
+    return _ConvForward.apply(h, Y, w, kind, graph)

@@ -1173,6 +1173,109 @@ int e3gnn_halo_unpack(const int32_t* idx, int64_t n, int dim, const float* src, 
   return E3GNN_OK;
 }
 
+// ------------------------------------------------------------ training ops
+// Stateless convolution primitives over caller-owned device tensors, the
+// kernel side of the fine-tune step (sevenn/train/trainer.py:155-222): the
+// uvu tensor product + segmented sum (convolution.py:104-123) and its
+// gradients w.r.t. all three operands.  The product is trilinear in
+// (h, Y, w), so every derivative of any order is one of these two launches
+// with permuted operands (sevennet_finetuning_amd/conv_ops.py).
+namespace {
+bool conv_kind_dims(int kind, int* dx, int* w, int* dm) {
+  switch (kind) {
+    case 0: *dx = LayerFirst::DX; *w = LayerFirst::W; *dm = LayerFirst::DM; return true;
+    case 1: *dx = LayerMid::DX; *w = LayerMid::W; *dm = LayerMid::DM; return true;
+    case 2: *dx = LayerLast::DX; *w = LayerLast::W; *dm = LayerLast::DM; return true;
+    default: return false;
+  }
+}
+}  // namespace
+
+int e3gnn_conv_dims(int kind, int* dx, int* w, int* dm) {
+  int a, b, d;
+  if (!conv_kind_dims(kind, &a, &b, &d)) return fail(E3GNN_ERR_ARG, "conv kind must be 0, 1 or 2");
+  if (dx) *dx = a;
+  if (w) *w = b;
+  if (dm) *dm = d;
+  return E3GNN_OK;
+}
+
+int e3gnn_conv_graph(int64_t n_nodes, int64_t n_edges, const int32_t* edge_center,
+                     const int32_t* edge_nbr, int32_t* row_ptr, int32_t* src_ptr,
+                     int32_t* src_perm, int32_t* scratch, void* stream) {
+  if (n_nodes < 0 || n_edges < 0 || n_nodes >= (int64_t)1 << 31 || n_edges >= (int64_t)1 << 31)
+    return fail(E3GNN_ERR_ARG, "conv graph size out of int32 range");
+  if (!row_ptr || !src_ptr || !scratch || (n_edges > 0 && (!edge_center || !edge_nbr || !src_perm)))
+    return fail(E3GNN_ERR_ARG, "null conv graph buffer");
+  hipStream_t s = (hipStream_t)stream;
+  int* err_d = scratch + n_nodes;
+  HIPCHK(hipMemsetAsync(err_d, 0, 4, s));
+  HIPCHK(launch_build_graph(n_edges, (int)n_nodes, (int)n_nodes, edge_center, edge_nbr, row_ptr,
+                            src_ptr, src_perm, scratch, err_d, s));
+  int err = 0;
+  HIPCHK(hipMemcpyAsync(&err, err_d, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (err) {
+    std::string msg = "invalid graph:";
+    if (err & 1) msg += " edge_center not sorted non-decreasing;";
+    if (err & 2) msg += " edge_center out of [0, n_nodes);";
+    if (err & 4) msg += " edge_nbr out of [0, n_nodes);";
+    return fail(E3GNN_ERR_GRAPH, msg);
+  }
+  return E3GNN_OK;
+}
+
+int e3gnn_conv_forward(int kind, int64_t n_nodes, const int32_t* row_ptr, const int32_t* edge_nbr,
+                       const float* h, const float* Y, const float* w, float* agg,
+                       void* stream) {
+  int dx, W, dm;
+  if (!conv_kind_dims(kind, &dx, &W, &dm)) return fail(E3GNN_ERR_ARG, "conv kind must be 0, 1 or 2");
+  if (n_nodes <= 0) return E3GNN_OK;
+  if (!row_ptr || !h || !Y || !w || !agg) return fail(E3GNN_ERR_ARG, "null conv operand");
+  TpArgs a{};
+  a.row_ptr = row_ptr;
+  a.nbr = edge_nbr;
+  a.Y = Y;
+  a.w = w;
+  a.h = h;
+  a.agg = agg;
+  a.n_centers = (int)n_nodes;
+  a.denom = 1.0f;
+  HIPCHK(launch_tp_fwd(kind, a, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_t* row_ptr,
+                        const int32_t* edge_nbr, const int32_t* src_ptr, const int32_t* src_perm,
+                        const float* h, const float* Y, const float* w, const float* gagg,
+                        float* dh, float* dY, float* dw, float* dxc, void* stream) {
+  int dx, W, dm;
+  if (!conv_kind_dims(kind, &dx, &W, &dm)) return fail(E3GNN_ERR_ARG, "conv kind must be 0, 1 or 2");
+  hipStream_t s = (hipStream_t)stream;
+  if (dh && n_nodes > 0) HIPCHK(hipMemsetAsync(dh, 0, n_nodes * dx * 4, s));
+  if (n_edges <= 0 || n_nodes <= 0) return E3GNN_OK;
+  if (!row_ptr || !edge_nbr || !h || !Y || !w || !gagg || !dY || !dw)
+    return fail(E3GNN_ERR_ARG, "null conv operand");
+  if (dh && (!dxc || !src_ptr || !src_perm))
+    return fail(E3GNN_ERR_ARG, "dh needs dxc scratch and the transposed CSR");
+  HIPCHK(hipMemsetAsync(dY, 0, n_edges * 9 * 4, s));
+  TpArgs a{};
+  a.row_ptr = row_ptr;
+  a.nbr = edge_nbr;
+  a.Y = Y;
+  a.w = w;
+  a.h = h;
+  a.gagg = gagg;
+  a.dw = dw;
+  a.dxc = dh ? dxc : nullptr;
+  a.dYacc = dY;
+  a.n_centers = (int)n_nodes;
+  a.denom = 1.0f;
+  HIPCHK(launch_tp_bwd(kind, a, s));
+  if (dh) HIPCHK(launch_gather_rows((int)n_nodes, dx, src_ptr, src_perm, dxc, dh, s));
+  return E3GNN_OK;
+}
+
 // ------------------------------------------------------------ neighbour list
 struct e3gnn_nlist {
   int device = 0;

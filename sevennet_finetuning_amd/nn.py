@@ -1,0 +1,335 @@
+"""Trainable SevenNet-0 on the HIP convolution op -- the model the fine-tune
+step differentiates (BASELINE config 5).
+
+Mirrors the reference's training-mode ``AtomGraphSequential``
+(sevenn/model_build.py:186-445 with ``set_is_batch_data(True)``,
+trainer.py:18-27):
+
+  EdgeEmbedding        edge_embedding.py:220-230  (BesselBasis :85-116 with
+                       trainable coeffs, XPLORCutoff :163-173, SphericalEncoding
+                       :177-198)  -- on a precomputed, grad-requiring edge_vec
+                       (dataset.py:177-185, collate.py:49)
+  OnehotEmbedding      node_embedding.py:39-48, linear.py:37-44
+  5 x interaction      interaction_blocks.py:22-86: SelfConnectionLinearIntro,
+                       IrrepsLinear si1, IrrepsConvolution (radial MLP + uvu TP +
+                       neighbour sum / denominator, convolution.py:104-123),
+                       IrrepsLinear si2, SelfConnectionOutro, EquivariantGate
+  readout              model_build.py:374-408, SpeciesWiseRescale scale.py:67-73,
+                       AtomReduce linear.py:76-90 (per graph)
+  ForceStressOutputFromEdge  force_output.py:158-215 (create_graph while training)
+
+The tensor product + neighbour sum runs in libe3gnn_hip.so through
+``conv_ops.conv`` (double-backward capable); the dense e3nn linears and the
+radial MLP are plain GEMMs (hipBLASLt through torch) and the element-wise
+pieces are torch plumbing.  Parameter names, shapes and order are the
+reference's ``named_parameters()`` (so the reference's ``state_dict``,
+``fisher_sevenn.pt`` and ``opt_params_sevenn.pt`` load by name), and every
+parameter is a view of ONE contiguous fp32 buffer whose gradients also live in
+one buffer: the data-parallel gradient all-reduce is a single collective with
+no packing copy (``flat_grad``).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import torch
+
+from . import _keys as KEY
+from . import conv_ops
+
+ASSETS = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'assets')
+
+
+def parse_irreps(s):
+    out = []
+    for term in s.split('+'):
+        mul, ir = term.strip().split('x')
+        if ir[-1] != 'e':
+            raise ValueError(f'{s}: the SevenNet-0 path is even parity only')
+        out.append((int(mul), int(ir[:-1])))
+    return out
+
+
+def _offsets(irreps):
+    return np.cumsum([0] + [m * (2 * l + 1) for m, l in irreps]).tolist()
+
+
+class _Linear:
+    """e3nn o3.Linear without bias (sevenn/nn/linear.py:46-49): one block per
+    (i_in, i_out) pair of equal l, i_in-major, each (mul_in, mul_out)
+    row-major in the flat weight, path weight 1/sqrt(fan-in of i_out)."""
+
+    def __init__(self, irreps_in, irreps_out):
+        self.irreps_in, self.irreps_out = irreps_in, irreps_out
+        self.ins = [(i, j) for i, (_, li) in enumerate(irreps_in)
+                    for j, (_, lo) in enumerate(irreps_out) if li == lo]
+        fan = {j: sum(irreps_in[i][0] for i, jj in self.ins if jj == j) for _, j in self.ins}
+        self.alpha = {j: 1.0 / math.sqrt(f) for j, f in fan.items()}
+        self.in_off, self.out_off = _offsets(irreps_in), _offsets(irreps_out)
+        self.numel = sum(irreps_in[i][0] * irreps_out[j][0] for i, j in self.ins)
+
+    def __call__(self, x, w_flat):
+        n = x.shape[0]
+        outs = [None] * len(self.irreps_out)
+        woff = 0
+        for i, j in self.ins:
+            mi, l = self.irreps_in[i]
+            mo = self.irreps_out[j][0]
+            w = w_flat[woff:woff + mi * mo].view(mi, mo)
+            woff += mi * mo
+            d = 2 * l + 1
+            xi = x[:, self.in_off[i]:self.in_off[i + 1]].reshape(n, mi, d)
+            y = torch.matmul(xi.transpose(1, 2), w).transpose(1, 2) * self.alpha[j]
+            outs[j] = y if outs[j] is None else outs[j] + y
+        parts = []
+        for j, (mo, l) in enumerate(self.irreps_out):
+            if outs[j] is None:
+                outs[j] = x.new_zeros(n, mo, 2 * l + 1)
+            parts.append(outs[j].reshape(n, -1))
+        return torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
+
+
+def _gate_irreps(irreps_out):
+    """e3nn Gate.irreps_in for EquivariantGate (equivariant_gate.py:48-55)."""
+    scal = [(m, l) for m, l in irreps_out if l == 0]
+    gated = [(m, l) for m, l in irreps_out if l > 0]
+    full = scal + [(m, 0) for m, _ in gated] + gated
+    simp = []
+    for m, l in sorted(full, key=lambda t: t[1]):
+        if simp and simp[-1][1] == l:
+            simp[-1] = (simp[-1][0] + m, l)
+        else:
+            simp.append((m, l))
+    return simp, scal, gated
+
+
+def _conv_mid(irreps_x, lmax_out):
+    """Sorted mid irreps of IrrepsConvolution (convolution.py:72-95)."""
+    ins = [(mul, l3) for mul, l1 in irreps_x for l2 in range(3)
+           for l3 in range(abs(l1 - l2), l1 + l2 + 1) if l3 <= lmax_out]
+    return [ins[k] for k in sorted(range(len(ins)), key=lambda k: (ins[k][1], k))]
+
+
+def spherical_harmonics(vec):
+    """e3nn SphericalHarmonics(0e+1e+2e, normalize=True, 'component')
+    (edge_embedding.py:177-198)."""
+    r = torch.linalg.norm(vec, dim=-1, keepdim=True)
+    u = vec / r
+    x, y, z = u[:, 0], u[:, 1], u[:, 2]
+    s3, s5, s15 = math.sqrt(3.0), math.sqrt(5.0), math.sqrt(15.0)
+    return torch.stack([
+        torch.ones_like(x), s3 * x, s3 * y, s3 * z,
+        s15 * x * z, s15 * x * y, s5 * (y * y - 0.5 * (x * x + z * z)), s15 * y * z,
+        0.5 * s15 * (z * z - x * x)], dim=-1)
+
+
+class SevenNetTrainable(torch.nn.Module):
+    """Training-mode SevenNet-0 (batched graphs) with reference parameter names.
+
+    ``train_shift_scale`` / ``train_denominator`` / ``train_radial_coeffs``
+    set ``requires_grad`` as the reference's config keys do
+    (scale.py:58-61, convolution.py:60, edge_embedding.py:107-110).
+    ``conv_backend`` defaults to the HIP kernels; tests may pass another
+    object with the same three methods to check host logic on the CPU."""
+
+    def __init__(self, model_dir=os.path.join(ASSETS, 'sevennet0'), device='cuda',
+                 train_shift_scale=False, train_denominator=False, train_radial_coeffs=True,
+                 conv_backend=None, dtype=torch.float32):
+        super().__init__()
+        self.dtype = dtype
+        with open(os.path.join(model_dir, 'manifest.json')) as f:
+            man = json.load(f)
+        self.manifest = man
+        self.chemical_symbols = list(man['chemical_symbols'])
+        self.nsp = int(man['num_species'])
+        self.cutoff = float(man['cutoff'])
+        self.r_on = float(man['cutoff_function']['cutoff_on'])
+        self.silu_norm = float(man['silu_norm'])
+        self.irreps = [parse_irreps(s) for s in man['irreps_manual']]
+        self.nlayer = int(man['num_convolution_layer'])
+        self.conv_backend = conv_backend if conv_backend is not None \
+            else conv_ops.HipConvBackend()
+        flat_host = np.fromfile(os.path.join(model_dir, 'weights.bin'), dtype='<f4')
+        total = sum(t['numel'] for t in man['tensors'])
+        self.flat = torch.empty(total, dtype=dtype, device=device)
+        self.flat_grad = torch.zeros(total, dtype=dtype, device=device)
+        self.slices = {}
+        off = 0
+        for t in man['tensors']:
+            name, n = t['name'], int(t['numel'])
+            self.flat[off:off + n].copy_(
+                torch.from_numpy(flat_host[t['offset']:t['offset'] + n].copy()))
+            p = torch.nn.Parameter(self.flat[off:off + n].view(t['shape']))
+            self._register_nested(name, p)
+            self.slices[name] = (off, n, tuple(t['shape']))
+            off += n
+        self._build_layers()
+        for name, p in self.named_parameters():
+            if name.startswith('rescale_atomic_energy.'):
+                p.requires_grad_(train_shift_scale)
+            elif name.endswith('.denominator'):
+                p.requires_grad_(train_denominator)
+            elif name == 'edge_embedding.basis_function.coeffs':
+                p.requires_grad_(train_radial_coeffs)
+        self.attach_flat_grad()
+        self.is_batch_data = True
+
+    # ------------------------------------------------------------ parameters
+    def _register_nested(self, name, p):
+        parts = name.split('.')
+        mod = self
+        for part in parts[:-1]:
+            if part not in mod._modules:
+                mod.add_module(part, torch.nn.Module())
+            mod = mod._modules[part]
+        mod.register_parameter(parts[-1], p)
+
+    def param(self, name):
+        mod = self
+        for part in name.split('.'):
+            mod = getattr(mod, part)
+        return mod
+
+    def attach_flat_grad(self):
+        """Point every parameter's .grad at its slice of ``flat_grad`` so that
+        backward accumulates in place into one contiguous buffer."""
+        for name, p in self.named_parameters():
+            off, n, shape = self.slices[name]
+            p.grad = self.flat_grad[off:off + n].view(shape)
+
+    def zero_grad(self, set_to_none=False):
+        self.flat_grad.zero_()
+        self.attach_flat_grad()
+
+    def grads_in_flat_buffer(self):
+        base = self.flat_grad.data_ptr()
+        end = base + self.flat_grad.numel() * self.flat_grad.element_size()
+        return all(p.grad is not None and base <= p.grad.data_ptr() < end
+                   for p in self.parameters())
+
+    def set_is_batch_data(self, flag: bool):
+        self.is_batch_data = bool(flag)
+
+    # ------------------------------------------------------------ structure
+    def _build_layers(self):
+        irr = self.irreps
+        self.blocks = []
+        for t in range(self.nlayer):
+            x_ir, out_ir = irr[t], irr[t + 1]
+            last = t == self.nlayer - 1
+            gin, scal, gated = _gate_irreps(out_ir)
+            mid = _conv_mid(x_ir, 0 if last else 2)
+            kind = 0 if t == 0 else (2 if last else 1)
+            dx, dw, dm = self.conv_backend.dims[kind]
+            xdim = _offsets(x_ir)[-1]
+            wdim = sum(m for m, l1 in x_ir for l2 in range(3)
+                       for l3 in range(abs(l1 - l2), l1 + l2 + 1) if l3 <= (0 if last else 2))
+            if (dx, dw, dm) != (xdim, wdim, _offsets(mid)[-1]):
+                raise ValueError(f'block {t}: irreps {x_ir} -> {out_ir} have no kernel path '
+                                 f'table (kind {kind} is {dx}/{dw}/{dm})')
+            self.blocks.append({
+                'kind': kind, 'gate': (gin, scal, gated),
+                'sc': _Linear(x_ir, gin), 'si1': _Linear(x_ir, x_ir), 'si2': _Linear(mid, gin)})
+        self.readout1 = _Linear(irr[-1], [(irr[-1][0][0] // 2, 0)])
+        self.readout2 = _Linear([(irr[-1][0][0] // 2, 0)], [(1, 0)])
+
+    def act(self, x):
+        return torch.nn.functional.silu(x) * self.silu_norm
+
+    def gate(self, x, gate_irreps):
+        # e3nn nn.Gate (equivariant_gate.py:59-61)
+        _, scal, gated = gate_irreps
+        n = x.shape[0]
+        ns = sum(m for m, _ in scal)
+        ng = sum(m for m, _ in gated)
+        s = self.act(x[:, :ns])
+        if ng == 0:
+            return s
+        g = self.act(x[:, ns:ns + ng])
+        outs, off, goff = [s], ns + ng, 0
+        for m, l in gated:
+            d = 2 * l + 1
+            blk = x[:, off:off + m * d].reshape(n, m, d)
+            outs.append((g[:, goff:goff + m].unsqueeze(-1) * blk).reshape(n, -1))
+            off += m * d
+            goff += m
+        return torch.cat(outs, dim=1)
+
+    def _edge_basis(self, r):
+        # BesselBasis (edge_embedding.py:114-116) * XPLORCutoff (:163-173)
+        rc, ron = self.cutoff, self.r_on
+        coeffs = self.param('edge_embedding.basis_function.coeffs')
+        ur = r.unsqueeze(-1)
+        bessel = (2.0 / rc) * torch.sin(coeffs * ur) / ur
+        r2 = r * r
+        env = torch.where(r < ron, torch.ones_like(r),
+                          (rc * rc - r2) ** 2 * (rc * rc + 2 * r2 - 3 * ron * ron)
+                          / (rc * rc - ron * ron) ** 3)
+        return bessel * env.unsqueeze(-1)
+
+    # ------------------------------------------------------------ forward
+    def forward(self, data):
+        """AtomGraphSequential.forward on a batched AtomGraphData dict:
+        ``x`` (type index), ``edge_index``, ``edge_vec``, ``batch``,
+        ``num_atoms``, ``cell_volume`` -> adds ``atomic_energy``,
+        ``inferred_total_energy`` [B], ``inferred_force`` [N,3],
+        ``inferred_stress`` [B,6] (eV/A^3, order xx,yy,zz,xy,yz,zx)."""
+        dev = self.flat.device
+        types = data[KEY.NODE_FEATURE].to(dev).long()
+        n = int(types.shape[0])
+        ei = data[KEY.EDGE_IDX].to(dev).long()
+        vec = data[KEY.EDGE_VEC].to(dev, self.dtype)
+        if not vec.requires_grad:
+            vec = vec.detach().requires_grad_(True)
+        batch = data[KEY.BATCH].to(dev).long() if KEY.BATCH in data else \
+            torch.zeros(n, dtype=torch.long, device=dev)
+        center, nbr = ei[0], ei[1]
+        vec_k = vec
+        if center.numel() > 1 and bool((center[1:] < center[:-1]).any()):
+            perm = torch.argsort(center, stable=True)
+            center, nbr, vec_k = center[perm], nbr[perm], vec[perm]
+        graph = conv_ops.ConvGraph(n, center, nbr, self.conv_backend)
+
+        r = torch.linalg.norm(vec_k, dim=-1)
+        emb = self._edge_basis(r)
+        Y = spherical_harmonics(vec_k)
+        P = self.param
+        x = P('onehot_to_feature_x.linear.weight').view(self.nsp, -1)[types] / math.sqrt(self.nsp)
+        for t, blk in enumerate(self.blocks):
+            sc = blk['sc'](x, P(f'{t}_self_connection_intro.linear.weight'))
+            h = blk['si1'](x, P(f'{t}_self_interaction_1.linear.weight'))
+            pre = f'{t}_convolution'
+            hid = self.act(emb @ (P(f'{pre}.weight_nn.layer0.weight') / math.sqrt(8.0)))
+            hid = self.act(hid @ (P(f'{pre}.weight_nn.layer1.weight') / 8.0))
+            w = hid @ (P(f'{pre}.weight_nn.layer2.weight') / 8.0)
+            agg = conv_ops.conv(h, Y, w, blk['kind'], graph) / P(f'{pre}.denominator')
+            y = blk['si2'](agg, P(f'{t}_self_interaction_2.linear.weight')) + sc
+            x = self.gate(y, blk['gate'])
+        hidden = self.readout1(x, P('reduce_input_to_hidden.linear.weight'))
+        e_s = self.readout2(hidden, P('reduce_hidden_to_energy.linear.weight'))[:, 0]
+        atomic = e_s * P('rescale_atomic_energy.scale')[types] + \
+            P('rescale_atomic_energy.shift')[types]
+        nb = int(data[KEY.NUM_ATOMS].numel()) if KEY.NUM_ATOMS in data else 1
+        energy = torch.zeros(nb, device=dev, dtype=atomic.dtype).index_add(0, batch, atomic)
+
+        out = dict(data)
+        out[KEY.EDGE_VEC] = vec
+        out[KEY.ATOMIC_ENERGY] = atomic.unsqueeze(-1)
+        out[KEY.PRED_TOTAL_ENERGY] = energy
+        # ForceStressOutputFromEdge (force_output.py:158-215)
+        fij, = torch.autograd.grad([energy.sum()], [vec], create_graph=self.training,
+                                   allow_unused=False)
+        src, dst = ei[0], ei[1]
+        force = torch.zeros(n, 3, device=dev, dtype=fij.dtype).index_add(0, src, fij) \
+            - torch.zeros(n, 3, device=dev, dtype=fij.dtype).index_add(0, dst, fij)
+        out[KEY.PRED_FORCE] = force
+        voigt = torch.cat([vec * fij, (vec[:, 0] * fij[:, 1]).unsqueeze(-1),
+                           (vec[:, 1] * fij[:, 2]).unsqueeze(-1),
+                           (vec[:, 2] * fij[:, 0]).unsqueeze(-1)], dim=-1)
+        s_atom = torch.zeros(n, 6, device=dev, dtype=fij.dtype).index_add(0, dst, voigt)
+        s_graph = torch.zeros(nb, 6, device=dev, dtype=fij.dtype).index_add(0, batch, s_atom)
+        if KEY.CELL_VOLUME in data:
+            vol = data[KEY.CELL_VOLUME].to(dev, self.dtype).view(-1)
+            out[KEY.PRED_STRESS] = torch.neg(s_graph) / vol.unsqueeze(-1)
+        return out

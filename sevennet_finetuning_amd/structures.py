@@ -33,6 +33,26 @@ def si_diamond(cells, a=SI_A, sigma=0.05, seed=0):
     return pos, cell
 
 
+def diamond_primitive(cells, a=SI_A, sigma=0.05, seed=0):
+    """Fine-tune cells of SURVEY.md 8d config 5: the 2-atom fcc primitive
+    diamond cell (vectors a/2 (0,1,1), (1,0,1), (1,1,0); basis 0 and
+    (1/4,1/4,1/4) in fractional coordinates) replicated n1 x n2 x n3,
+    N(0, sigma) displacements from ``default_rng(seed)``, wrapped back into
+    the (triclinic) cell.  Returns (pos [N,3] float64, cell [3,3])."""
+    cells = tuple(int(c) for c in cells)
+    prim = 0.5 * a * np.array([[0.0, 1.0, 1.0], [1.0, 0.0, 1.0], [1.0, 1.0, 0.0]])
+    frac = np.array([(np.array(ijk) + b) / np.array(cells)
+                     for ijk in itertools.product(*[range(c) for c in cells])
+                     for b in ([0.0, 0.0, 0.0], [0.25, 0.25, 0.25])])
+    cell = prim * np.array(cells, dtype=np.float64)[:, None]
+    pos = frac @ cell
+    if sigma:
+        pos = pos + np.random.default_rng(seed).normal(0.0, sigma, pos.shape)
+        f = np.mod(pos @ np.linalg.inv(cell), 1.0)
+        pos = f @ cell
+    return pos, cell
+
+
 def mixed_symbols(n, seed=1):
     rng = np.random.default_rng(seed)
     return [MIXED_SYMBOLS[i] for i in rng.integers(0, len(MIXED_SYMBOLS), n)]

@@ -1,0 +1,491 @@
+"""Fine-tune step (rehearsal + EWC, data parallel) over the trainable HIP
+model -- SURVEY.md §8f row 1, BASELINE config 5.
+
+Mirrors, by name and behaviour:
+  LossDefinition / PerAtomEnergyLoss / ForceLoss / StressLoss / EWCLoss,
+  get_loss_functions_from_config          sevenn/train/loss.py:8-309
+  optim_dict / scheduler_dict / loss_dict sevenn/train/optim.py
+  Trainer.run_one_epoch, compute_fisher_matrix,
+  RehearsalTrainer.run_one_epoch_rehearsal  sevenn/train/trainer.py:15-222
+  PyG Collater of AtomGraphData           sevenn/train/collate.py, torch_geometric
+                                          (edge_index offset by the running atom
+                                          count, ``batch`` vector, per-graph rows)
+
+Data parallelism: one process per GPU (torch.distributed, backend "nccl" =
+RCCL over xGMI; "gloo" in the CPU tests).  Where the reference wraps the model
+in DDP (trainer.py:18-23), this build keeps every parameter gradient in ONE
+contiguous buffer (``SevenNetTrainable.flat_grad``) and averages it with a
+single all-reduce after each backward -- the same arithmetic as DDP's
+bucketed averaging (earlier, already-synchronised accumulation + the mean of
+the new contributions), one collective of 3.4 MB per backward.
+"""
+import math
+import os
+
+import numpy as np
+import torch
+
+from . import _keys as KEY
+
+# config keys (sevenn/_keys.py:100-233)
+LOSS, LOSS_PARAM = 'loss', 'loss_param'
+OPTIMIZER, OPTIM_PARAM = 'optimizer', 'optim_param'
+SCHEDULER, SCHEDULER_PARAM = 'scheduler', 'scheduler_param'
+FORCE_WEIGHT, STRESS_WEIGHT = 'force_loss_weight', 'stress_loss_weight'
+IS_TRAIN_STRESS, DEVICE = 'is_train_stress', 'device'
+CONTINUE, FISHER, OPT_PARAMS, EWC_LAMBDA = 'continue', 'fisher_information', 'opt_params', \
+    'ewc_lambda'
+LOAD_DATASET_WITH_WEIGHTS, DATA_WEIGHT = 'load_dataset_with_weights', 'data_weight'
+PER_ATOM_ENERGY = 'per_atom_energy'
+IS_DDP, LOCAL_RANK = 'is_ddp', 'local_rank'
+
+
+# ------------------------------------------------------------------ losses
+class LossDefinition:
+    """loss.py:8-94: criterion on flattened (pred, ref), NaN labels dropped."""
+
+    def __init__(self, name, unit=None, criterion=None, ref_key=None, pred_key=None,
+                 vdim=None, use_weight=False, weight_key=None, delete_unlabled=True):
+        if criterion is not None and hasattr(criterion, 'reduction'):
+            if use_weight:
+                assert criterion.reduction == 'none'
+                assert weight_key is not None
+            else:
+                assert criterion.reduction != 'none'
+        assert isinstance(vdim, int)
+        self.name, self.unit, self.vdim = name, unit, vdim
+        self.criterion = criterion
+        self.ref_key, self.pred_key = ref_key, pred_key
+        self.use_weight, self.weight_key = use_weight, weight_key
+        self.delete_unlabeled = delete_unlabled
+
+    def assign_criteria(self, criterion):
+        if self.criterion is not None:
+            raise ValueError('Loss uses its own criterion.')
+        self.criterion = criterion
+
+    def _preprocess(self, batch_data, model=None):
+        if self.pred_key is None or self.ref_key is None:
+            raise NotImplementedError('LossDefinition is not implemented.')
+        return (torch.reshape(batch_data[self.pred_key], (-1,)),
+                torch.reshape(batch_data[self.ref_key], (-1,)))
+
+    def _get_data_weight(self, batch_data):
+        return torch.repeat_interleave(batch_data[DATA_WEIGHT][self.weight_key], self.vdim)
+
+    def get_loss(self, batch_data, model=None):
+        if self.criterion is None:
+            raise NotImplementedError('LossDefinition has no criterion.')
+        pred, ref = self._preprocess(batch_data, model)
+        weights = self._get_data_weight(batch_data) if self.use_weight else None
+        if self.delete_unlabeled:
+            keep = ~torch.isnan(ref)
+            pred, ref = pred[keep], ref[keep]
+            if len(pred) == 0:
+                return torch.zeros(1, device=pred.device)
+            if self.use_weight:
+                weights = weights[keep]
+        if self.use_weight:
+            return torch.mean(self.criterion(pred, ref) * weights)
+        return self.criterion(pred, ref)
+
+
+class PerAtomEnergyLoss(LossDefinition):
+    """loss.py:97-130: (E_pred / N, E_ref / N) per graph."""
+
+    def __init__(self, name='Energy', unit='eV/atom', criterion=None, ref_key=KEY.ENERGY,
+                 pred_key=KEY.PRED_TOTAL_ENERGY, weight_key=PER_ATOM_ENERGY, **kwargs):
+        super().__init__(name=name, unit=unit, criterion=criterion, ref_key=ref_key,
+                         pred_key=pred_key, weight_key=weight_key, vdim=1, **kwargs)
+
+    def _preprocess(self, batch_data, model=None):
+        n = batch_data[KEY.NUM_ATOMS]
+        return batch_data[self.pred_key] / n, batch_data[self.ref_key] / n
+
+
+class ForceLoss(LossDefinition):
+    """loss.py:133-171."""
+
+    def __init__(self, name='Force', unit='eV/A', criterion=None, ref_key=KEY.FORCE,
+                 pred_key=KEY.PRED_FORCE, weight_key=KEY.FORCE, **kwargs):
+        super().__init__(name=name, unit=unit, criterion=criterion, ref_key=ref_key,
+                         pred_key=pred_key, vdim=3, weight_key=weight_key, **kwargs)
+
+    def _get_data_weight(self, batch_data):
+        w = batch_data[DATA_WEIGHT][self.weight_key][batch_data[KEY.BATCH]]
+        return torch.repeat_interleave(w, self.vdim)
+
+
+class StressLoss(LossDefinition):
+    """loss.py:174-206: both sides in kbar."""
+
+    TO_KB = 1602.1766208  # eV/A^3 to kbar
+
+    def __init__(self, name='Stress', unit='kbar', criterion=None, ref_key=KEY.STRESS,
+                 pred_key=KEY.PRED_STRESS, weight_key=KEY.STRESS, **kwargs):
+        super().__init__(name=name, unit=unit, criterion=criterion, ref_key=ref_key,
+                         pred_key=pred_key, vdim=6, weight_key=weight_key, **kwargs)
+
+    def _preprocess(self, batch_data, model=None):
+        return (torch.reshape(batch_data[self.pred_key] * self.TO_KB, (-1,)),
+                torch.reshape(batch_data[self.ref_key] * self.TO_KB, (-1,)))
+
+
+class EWCLoss(LossDefinition):
+    """loss.py:209-252: sum over named parameters of F * (theta - theta*)^2."""
+
+    def __init__(self, fisher_dict, opt_params_dict, name='EWC', device=None, **kwargs):
+        super().__init__(criterion=None, name=name, ref_key=None, pred_key=None,
+                         weight_key=None, use_weight=False, vdim=0, **kwargs)
+        self.fisher_dict, self.opt_params_dict = fisher_dict, opt_params_dict
+        self.device = device
+        if device is not None:
+            self.to(device)
+
+    def to(self, device):
+        for d in (self.fisher_dict, self.opt_params_dict):
+            for k in d:
+                d[k] = d[k].to(device)
+        self.device = device
+
+    def get_loss(self, batch_data, model=None):
+        if model is None:
+            raise ValueError('EWC requires model to compute loss')
+        ewc = torch.zeros(1, device=self.device)
+        for name, p in model.named_parameters():
+            if name not in self.fisher_dict or name not in self.opt_params_dict:
+                continue
+            ewc = ewc + torch.sum(self.fisher_dict[name] * (p - self.opt_params_dict[name]) ** 2)
+        return ewc
+
+
+loss_dict = {'mse': torch.nn.MSELoss, 'huber': torch.nn.HuberLoss, 'custom': 'custom'}
+
+
+def get_loss_functions_from_config(config):
+    """loss.py:255-297 -> list of (LossDefinition, weight)."""
+    loss = loss_dict[config[LOSS].lower()]
+    loss_param = config.get(LOSS_PARAM, {}) or {}
+    if loss == 'custom':
+        raise NotImplementedError('custom loss callbacks are not part of this build')
+    reduction, use_weight = 'mean', False
+    if LOAD_DATASET_WITH_WEIGHTS in config:
+        reduction, use_weight = 'none', True
+    common = {'criterion': loss(reduction=reduction, **loss_param), 'use_weight': use_weight}
+    fns = [(PerAtomEnergyLoss(**common), 1.0), (ForceLoss(**common), config[FORCE_WEIGHT])]
+    if config[IS_TRAIN_STRESS]:
+        fns.append((StressLoss(**common), config[STRESS_WEIGHT]))
+    cont = config.get(CONTINUE, {}) or {}
+    fpath, opath = cont.get(FISHER, False), cont.get(OPT_PARAMS, False)
+    if fpath is not False and opath is not False:
+        fisher = fpath if isinstance(fpath, dict) else torch.load(fpath, weights_only=True)
+        opt = opath if isinstance(opath, dict) else torch.load(opath, weights_only=True)
+        lam = float(cont[EWC_LAMBDA])
+        fns.append((EWCLoss(dict(fisher), dict(opt), device=config.get(DEVICE)), lam / 2.0))
+    return fns
+
+
+# ------------------------------------------------------------------ schedulers
+class CosineAnnealingWarmupRestarts(torch.optim.lr_scheduler.LRScheduler):
+    """Restatement of the ``cosine_annealing_warmup`` package's scheduler
+    (katsura-jp/pytorch-cosine-annealing-with-warmup, unpinned VCS dependency,
+    pyproject.toml:29; used via optim.py:22): linear warmup from min_lr to
+    max_lr over ``warmup_steps``, cosine decay to min_lr over the rest of the
+    cycle, cycles growing by ``cycle_mult``, max_lr decaying by ``gamma`` per
+    cycle.  Pinned by the learning-rate column of the reference's fine-tuning
+    log (example_inputs/fine_tuning/FT_w_reEWC/log.sevenn:284-374)."""
+
+    def __init__(self, optimizer, first_cycle_steps, cycle_mult=1.0, max_lr=0.1, min_lr=0.001,
+                 warmup_steps=0, gamma=1.0, last_epoch=-1):
+        assert warmup_steps < first_cycle_steps
+        self.first_cycle_steps = first_cycle_steps
+        self.cycle_mult = cycle_mult
+        self.base_max_lr = self.max_lr = max_lr
+        self.min_lr = min_lr
+        self.warmup_steps = warmup_steps
+        self.gamma = gamma
+        self.cur_cycle_steps = first_cycle_steps
+        self.cycle = 0
+        self.step_in_cycle = last_epoch
+        super().__init__(optimizer, last_epoch)
+        self.base_lrs = []
+        for g in self.optimizer.param_groups:
+            g['lr'] = self.min_lr
+            self.base_lrs.append(self.min_lr)
+
+    def get_lr(self):
+        if self.step_in_cycle == -1:
+            return self.base_lrs
+        if self.step_in_cycle < self.warmup_steps:
+            return [(self.max_lr - b) * self.step_in_cycle / self.warmup_steps + b
+                    for b in self.base_lrs]
+        span = self.cur_cycle_steps - self.warmup_steps
+        return [b + (self.max_lr - b) * (1 + math.cos(
+            math.pi * (self.step_in_cycle - self.warmup_steps) / span)) / 2
+            for b in self.base_lrs]
+
+    def step(self, epoch=None):
+        if epoch is None:
+            epoch = self.last_epoch + 1
+            self.step_in_cycle += 1
+            if self.step_in_cycle >= self.cur_cycle_steps:
+                self.cycle += 1
+                self.step_in_cycle -= self.cur_cycle_steps
+                self.cur_cycle_steps = int((self.cur_cycle_steps - self.warmup_steps)
+                                           * self.cycle_mult) + self.warmup_steps
+        else:
+            if epoch >= self.first_cycle_steps:
+                if self.cycle_mult == 1.0:
+                    self.step_in_cycle = epoch % self.first_cycle_steps
+                    self.cycle = epoch // self.first_cycle_steps
+                else:
+                    n = int(math.log(epoch / self.first_cycle_steps * (self.cycle_mult - 1) + 1,
+                                     self.cycle_mult))
+                    self.cycle = n
+                    self.step_in_cycle = epoch - int(self.first_cycle_steps
+                                                     * (self.cycle_mult ** n - 1)
+                                                     / (self.cycle_mult - 1))
+                    self.cur_cycle_steps = self.first_cycle_steps * self.cycle_mult ** n
+            else:
+                self.cur_cycle_steps = self.first_cycle_steps
+                self.step_in_cycle = epoch
+        self.max_lr = self.base_max_lr * (self.gamma ** self.cycle)
+        self.last_epoch = math.floor(epoch)
+        for g, lr in zip(self.optimizer.param_groups, self.get_lr()):
+            g['lr'] = lr
+
+
+_S = torch.optim.lr_scheduler
+optim_dict = {'sgd': torch.optim.SGD, 'adagrad': torch.optim.Adagrad, 'adam': torch.optim.Adam,
+              'adamw': torch.optim.AdamW, 'radam': torch.optim.RAdam}
+scheduler_dict = {'steplr': _S.StepLR, 'multisteplr': _S.MultiStepLR,
+                  'exponentiallr': _S.ExponentialLR, 'cosineannealinglr': _S.CosineAnnealingLR,
+                  'reducelronplateau': _S.ReduceLROnPlateau, 'linearlr': _S.LinearLR,
+                  'cosineannealingwarmuplr': CosineAnnealingWarmupRestarts}
+
+
+# ------------------------------------------------------------------ batching
+def _float(a):
+    """float tensor, keeping float64 inputs float64 (the model casts to its own dtype)"""
+    t = torch.as_tensor(a)
+    return t if t.is_floating_point() else t.to(torch.float32)
+
+
+_PER_GRAPH = (KEY.ENERGY, KEY.STRESS, KEY.CELL_VOLUME, KEY.NUM_ATOMS)
+
+
+def labeled_graph(pos, cell, types, cutoff, energy=None, force=None, stress=None):
+    """AtomGraphData dict of one labelled structure, as
+    sevenn/train/dataload.py:71-140 builds it: reference edge convention
+    (util.unlabeled_atoms_to_graph), ``x`` = type index, labels ``total_energy``
+    (eV), ``force_of_atoms`` [N,3] and ``stress`` [1,6] in the model's output
+    convention (xx,yy,zz,xy,yz,zx, i.e. -ASE stress reordered, dataload.py:104-105);
+    a missing label is NaN, which the losses drop (loss.py:70-80)."""
+    from .neighbor import neighbor_list
+    pos = np.asarray(pos, dtype=np.float64)
+    cell = np.asarray(cell, dtype=np.float64).reshape(3, 3)
+    ei, sh = neighbor_list(pos, cell, cutoff)
+    vec = pos[ei[1]] + sh @ cell - pos[ei[0]]
+    n = len(pos)
+    return {
+        KEY.NODE_FEATURE: torch.as_tensor(np.asarray(types), dtype=torch.long),
+        KEY.POS: torch.as_tensor(pos),
+        KEY.EDGE_IDX: torch.as_tensor(ei, dtype=torch.long),
+        KEY.EDGE_VEC: torch.as_tensor(vec),
+        KEY.CELL_SHIFT: torch.as_tensor(sh),
+        KEY.CELL_VOLUME: torch.tensor(abs(float(np.linalg.det(cell)))),
+        KEY.NUM_ATOMS: torch.tensor(n),
+        KEY.ENERGY: torch.tensor(float('nan') if energy is None else float(energy)),
+        KEY.FORCE: torch.as_tensor(np.full((n, 3), np.nan) if force is None
+                                   else np.asarray(force, dtype=np.float64)),
+        KEY.STRESS: torch.as_tensor(np.full((1, 6), np.nan) if stress is None
+                                    else np.asarray(stress, dtype=np.float64).reshape(1, 6)),
+    }
+
+
+def collate(graphs, device=None, dtype=None):
+    """PyG ``Collater`` over AtomGraphData dicts: node rows concatenated,
+    ``edge_index`` offset by the running atom count, a ``batch`` vector,
+    per-graph scalars/rows stacked (``num_atoms`` [B], ``cell_volume`` [B],
+    ``total_energy`` [B], ``stress`` [B,6]); floating tensors cast to
+    ``dtype`` when given (the model's)."""
+    nodes, edges, pg = {}, {}, {k: [] for k in _PER_GRAPH}
+    batch, off = [], 0
+    for b, g in enumerate(graphs):
+        n = int(torch.as_tensor(g[KEY.NODE_FEATURE]).shape[0])
+        for k in (KEY.NODE_FEATURE, KEY.FORCE, KEY.POS):
+            if k in g:
+                nodes.setdefault(k, []).append(torch.as_tensor(g[k]))
+        edges.setdefault(KEY.EDGE_IDX, []).append(torch.as_tensor(g[KEY.EDGE_IDX]).long() + off)
+        for k in (KEY.EDGE_VEC, KEY.CELL_SHIFT):
+            if k in g:
+                edges.setdefault(k, []).append(_float(g[k]))
+        for k in _PER_GRAPH:
+            if k in g:
+                pg[k].append(_float(g[k]).reshape(1, -1))
+        batch.append(torch.full((n,), b, dtype=torch.long))
+        off += n
+    out = {k: torch.cat(v, 0) for k, v in nodes.items()}
+    out[KEY.NODE_FEATURE] = out[KEY.NODE_FEATURE].long()
+    if KEY.FORCE in out:
+        out[KEY.FORCE] = _float(out[KEY.FORCE])
+    out[KEY.EDGE_IDX] = torch.cat(edges[KEY.EDGE_IDX], 1)
+    for k in (KEY.EDGE_VEC, KEY.CELL_SHIFT):
+        if k in edges:
+            out[k] = torch.cat(edges[k], 0)
+    for k, v in pg.items():
+        if v:
+            t = torch.cat(v, 0)
+            out[k] = t if k == KEY.STRESS else t.view(-1)
+    out[KEY.NUM_ATOMS] = out[KEY.NUM_ATOMS].long()
+    out[KEY.BATCH] = torch.cat(batch)
+    if dtype is not None:
+        out = {k: v.to(dtype) if v.is_floating_point() else v for k, v in out.items()}
+    if device is not None:
+        out = {k: v.to(device, non_blocking=True) for k, v in out.items()}
+    return out
+
+
+# ------------------------------------------------------------------ trainer
+class Trainer:
+    """trainer.py:15-152 over a SevenNetTrainable (flat parameter/grad
+    buffers).  ``config`` uses the reference's keys."""
+
+    def __init__(self, model, config):
+        self.distributed = bool(config.get(IS_DDP, False))
+        self.model = model
+        self.model.set_is_batch_data(True)
+        self.device = model.flat.device
+        if self.distributed:
+            import torch.distributed as dist
+            self.world = dist.get_world_size()
+            dist.barrier()
+            # every rank starts from rank 0's parameters (DDP's broadcast)
+            dist.broadcast(self.model.flat, 0)
+        else:
+            self.world = 1
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        opt = optim_dict[config[OPTIMIZER].lower()]
+        self.optimizer = opt(params, **config.get(OPTIM_PARAM, {}))
+        sch = scheduler_dict[config[SCHEDULER].lower()]
+        self.scheduler = sch(self.optimizer, **config.get(SCHEDULER_PARAM, {}))
+        self.loss_functions = get_loss_functions_from_config(config)
+        for loss_def, _ in self.loss_functions:
+            if isinstance(loss_def, EWCLoss) and loss_def.device is None:
+                loss_def.to(self.device)
+
+    # ---- the pieces of one step
+    def zero_grad(self):
+        self.model.zero_grad()
+
+    def total_loss(self, output):
+        total = torch.zeros(1, device=self.device)
+        for loss_def, w in self.loss_functions:
+            total = total + loss_def.get_loss(output, self.model) * w
+        return total
+
+    def backward(self, loss):
+        loss.backward()
+        if self.distributed:
+            import torch.distributed as dist
+            g = self.model.flat_grad
+            dist.all_reduce(g)
+            g.div_(self.world)
+
+    def train_step(self, batch):
+        """One optimizer step of Trainer.run_one_epoch (trainer.py:55-68)."""
+        self.zero_grad()
+        output = self.model(batch)
+        loss = self.total_loss(output)
+        self.backward(loss)
+        self.optimizer.step()
+        return loss.detach(), output
+
+    def rehearsal_step(self, batch, batch_mem):
+        """One iteration of RehearsalTrainer.run_one_epoch_rehearsal
+        (trainer.py:174-206): zero_grad once, backward+step on the new batch,
+        then backward (accumulating) + step on the memory batch."""
+        self.zero_grad()
+        output = self.model(batch)
+        loss = self.total_loss(output)
+        self.backward(loss)
+        self.optimizer.step()
+        memout = self.model(batch_mem)
+        mem_loss = self.total_loss(memout)
+        self.backward(mem_loss)
+        self.optimizer.step()
+        return loss.detach(), mem_loss.detach()
+
+    def run_one_epoch(self, loader, is_train=False):
+        self.model.train(is_train)
+        losses = []
+        for batch in loader:
+            batch = {k: v.to(self.device, non_blocking=True) for k, v in batch.items()}
+            if is_train:
+                losses.append(self.train_step(batch)[0])
+            else:
+                losses.append(self.total_loss(self.model(batch)).detach())
+        return losses
+
+    def run_one_epoch_rehearsal(self, loader, memloader, is_train=False):
+        self.model.train(is_train)
+        mem_iter = iter(memloader)
+        out = []
+        for batch in loader:
+            try:
+                batch_mem = next(mem_iter)
+            except StopIteration:
+                mem_iter = iter(memloader)
+                batch_mem = next(mem_iter)
+            batch = {k: v.to(self.device) for k, v in batch.items()}
+            batch_mem = {k: v.to(self.device) for k, v in batch_mem.items()}
+            if is_train:
+                out.append(self.rehearsal_step(batch, batch_mem))
+            else:
+                out.append((self.total_loss(self.model(batch)).detach(),
+                            self.total_loss(self.model(batch_mem)).detach()))
+        return out
+
+    def scheduler_step(self, metric=None):
+        if self.scheduler is None:
+            return
+        if isinstance(self.scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
+            self.scheduler.step(metric)
+        else:
+            self.scheduler.step()
+
+    def get_lr(self):
+        return self.optimizer.param_groups[0]['lr']
+
+    def compute_fisher_matrix(self, loader, loss_thr):
+        """trainer.py:124-152: mean over batches (below loss_thr, if >= 0) of
+        squared loss gradients, and the current parameters."""
+        fisher = {n: torch.zeros_like(p) for n, p in self.model.named_parameters()}
+        self.model.train()
+        cnt = 0
+        for batch in loader:
+            self.zero_grad()
+            batch = {k: v.to(self.device) for k, v in batch.items()}
+            total = self.total_loss(self.model(batch))
+            if loss_thr < 0 or total < loss_thr:
+                self.backward(total)
+                for n, p in self.model.named_parameters():
+                    if p.grad is not None and p.requires_grad:
+                        fisher[n] += p.grad.detach().clone() ** 2
+                cnt += 1
+        for n in fisher:
+            fisher[n] /= cnt
+        opt = {n: p.data.detach().clone() for n, p in self.model.named_parameters()}
+        return fisher, opt, cnt
+
+
+def setup_distributed(backend=None):
+    """One process per GPU from torchrun's env (RANK/LOCAL_RANK/WORLD_SIZE/
+    MASTER_*); backend "nccl" (RCCL) on GPUs, "gloo" otherwise."""
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        if backend is None:
+            backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+        dist.init_process_group(backend)
+    local = int(os.environ.get('LOCAL_RANK', 0))
+    return dist.get_rank(), dist.get_world_size(), local

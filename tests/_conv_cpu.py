@@ -1,0 +1,62 @@
+"""CPU test double of conv_ops.HipConvBackend (TEST INFRASTRUCTURE).
+
+Implements the same three methods (build / forward / backward) with the
+oracle's uvu tensor product (oracle/sevennet_ref.py, convolution.py:104-123)
+and torch autograd for the operand gradients, in any dtype.  Used to check the
+host logic of the trainable model and trainer on the CPU, and -- in float64 --
+as the reference the HIP training path is compared with on the GPU.
+"""
+import numpy as np
+import torch
+
+from oracle.cg import tp_cg
+from oracle.sevennet_ref import conv_instructions
+
+X_FIRST = [(128, 0)]
+X_MID = [(128, 0), (64, 1), (32, 2)]
+KINDS = {0: (X_FIRST, 2), 1: (X_MID, 2), 2: (X_MID, 0)}
+
+
+class CpuConvBackend:
+    def __init__(self):
+        self.dims = {}
+        self.tables = {}
+        for kind, (irr, lmax) in KINDS.items():
+            ins, mid, perm = conv_instructions(irr, lmax)
+            dx = sum(m * (2 * l + 1) for m, l in irr)
+            self.dims[kind] = (dx, sum(i[3] for i in ins), sum(m * (2 * l + 1) for m, l in mid))
+            self.tables[kind] = (irr, ins, perm)
+
+    def build(self, g):
+        return {}
+
+    def forward(self, kind, g, h, Y, w):
+        irr, ins, perm = self.tables[kind]
+        xs = h[g.edge_nbr.long()]
+        e = xs.shape[0]
+        x_off = np.cumsum([0] + [m * (2 * l + 1) for m, l in irr])
+        sh_off = [0, 1, 4, 9]
+        outs = [None] * len(ins)
+        woff = 0
+        for k, (i, l2, l3, mul) in enumerate(ins):
+            l1 = irr[i][1]
+            xi = xs[:, x_off[i]:x_off[i + 1]].reshape(e, mul, 2 * l1 + 1)
+            y = Y[:, sh_off[l2]:sh_off[l2 + 1]]
+            c = torch.as_tensor(tp_cg(l1, l2, l3), dtype=h.dtype)
+            m = torch.einsum('eui,ej,ijk->euk', xi, y, c) * w[:, woff:woff + mul].unsqueeze(-1)
+            woff += mul
+            outs[perm[k]] = m.reshape(e, -1)
+        msg = torch.cat(outs, dim=1)
+        return torch.zeros(g.n_nodes, msg.shape[1], dtype=h.dtype).index_add(
+            0, g.edge_center.long(), msg)
+
+    def backward(self, kind, g, h, Y, w, gagg, need_h=True):
+        with torch.enable_grad():
+            hh, YY, ww = (t.detach().requires_grad_(True) for t in (h, Y, w))
+            s = (self.forward(kind, g, hh, YY, ww) * gagg.detach()).sum()
+            dh, dY, dw = torch.autograd.grad(s, [hh, YY, ww], allow_unused=True)
+        zero = torch.zeros_like
+        dh = dh if dh is not None else zero(h)
+        dY = dY if dY is not None else zero(Y)
+        dw = dw if dw is not None else zero(w)
+        return (dh if need_h else None), dY, dw

@@ -1,0 +1,196 @@
+"""Fine-tune step on the HIP kernels (conv_ops -> libe3gnn_hip.so training
+ops) against the float64 CPU double of the same op (_conv_cpu.py, the
+oracle's uvu tensor product).  Needs an MI355X: ``pytest -m gpu``.
+
+Tolerances (fp32 kernels vs float64): convolution outputs and their first and
+second derivatives 2e-5 relative to the output's max magnitude; model forces
+1e-4 eV/A (north_star), energies 2e-6 relative; parameter gradients of the
+force loss (double backward, create_graph=True) 1e-4 relative in norm.
+"""
+import numpy as np
+import pytest
+import torch
+
+from _conv_cpu import CpuConvBackend
+from _systems import load_manifest_symbols
+from sevennet_finetuning_amd import _keys as KEY
+from sevennet_finetuning_amd import conv_ops, train
+from sevennet_finetuning_amd.structures import diamond_primitive, mixed_symbols
+
+pytestmark = pytest.mark.gpu
+SYMS = load_manifest_symbols()
+DEV = 'cuda:0'
+
+
+def ft_structure(seed, cells=(3, 3, 3)):
+    pos, cell = diamond_primitive(cells, sigma=0.05, seed=seed)
+    types = np.array([SYMS.index(s) for s in mixed_symbols(len(pos), seed=seed + 1)])
+    return pos, cell, types
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.fixture(scope='module')
+def hip_backend():
+    assert torch.cuda.is_available(), 'GPU tests need a HIP device'
+    return conv_ops.HipConvBackend()
+
+
+def _problem(kind, dims, n=61, seed=0):
+    """Ragged random graph: some nodes without edges, some with many,
+    sorted centres, random neighbours (repeats allowed)."""
+    rng = np.random.default_rng(seed)
+    deg = rng.integers(0, 12, n)
+    deg[::7] = 0
+    deg[3] = 40
+    center = np.repeat(np.arange(n), deg)
+    e = len(center)
+    nbr = rng.integers(0, n, e)
+    dx, dw, dm = dims[kind]
+    h = rng.normal(size=(n, dx))
+    Y = rng.normal(size=(e, 9))
+    w = rng.normal(size=(e, dw))
+    g = rng.normal(size=(n, dm))
+    probe = [rng.normal(size=(n, dx)), rng.normal(size=(e, 9)), rng.normal(size=(e, dw))]
+    return center, nbr, (h, Y, w), g, probe
+
+
+def _derivs(conv, graph, ops, g, probe, dtype, device):
+    t = [torch.tensor(a, dtype=dtype, device=device, requires_grad=True) for a in ops]
+    gt = torch.tensor(g, dtype=dtype, device=device)
+    pt = [torch.tensor(a, dtype=dtype, device=device) for a in probe]
+    agg = conv(*t, graph)
+    d1 = torch.autograd.grad((agg * gt).sum(), t, create_graph=True)
+    s = sum((di * pi).sum() for di, pi in zip(d1, pt))
+    d2 = torch.autograd.grad(s, t)
+    return agg, d1, d2
+
+
+@pytest.mark.parametrize('kind', [0, 1, 2])
+def test_conv_op_first_and_second_derivatives(hip_backend, kind):
+    center, nbr, ops, g, probe = _problem(kind, hip_backend.dims, seed=kind)
+    cpu = CpuConvBackend()
+    gc = conv_ops.ConvGraph(len(g), torch.tensor(center), torch.tensor(nbr), cpu)
+    gh = conv_ops.ConvGraph(len(g), torch.tensor(center, device=DEV),
+                            torch.tensor(nbr, device=DEV), hip_backend)
+    fwd = lambda h, Y, w, gr: conv_ops.conv(h, Y, w, kind, gr)  # noqa: E731
+    ref = _derivs(fwd, gc, ops, g, probe, torch.float64, 'cpu')
+    got = _derivs(fwd, gh, ops, g, probe, torch.float32, DEV)
+    assert _rel(got[0], ref[0]) < 2e-5
+    for a, b in zip(got[1], ref[1]):
+        assert _rel(a, b) < 2e-5
+    for a, b in zip(got[2], ref[2]):
+        assert _rel(a, b) < 2e-5
+
+
+def test_conv_graph_rejects_unsorted(hip_backend):
+    from sevennet_finetuning_amd._lib import E3GNNError
+    with pytest.raises(E3GNNError, match='not sorted'):
+        conv_ops.ConvGraph(4, torch.tensor([0, 2, 1], device=DEV),
+                           torch.tensor([1, 1, 1], device=DEV), hip_backend)
+    with pytest.raises(E3GNNError, match='out of'):
+        conv_ops.ConvGraph(4, torch.tensor([0, 1, 2], device=DEV),
+                           torch.tensor([1, 9, 1], device=DEV), hip_backend)
+
+
+@pytest.fixture(scope='module')
+def models(hip_backend):
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    m32 = SevenNetTrainable(device=DEV)
+    m64 = SevenNetTrainable(device='cpu', conv_backend=CpuConvBackend(), dtype=torch.float64)
+    return m32, m64
+
+
+def _batch(seeds, cells=(3, 3, 3), labels=True):
+    gs = []
+    for s in seeds:
+        pos, cell, types = ft_structure(s, cells)
+        rng = np.random.default_rng(1000 + s)
+        lab = dict(energy=-4.0 * len(pos), force=rng.normal(0, 0.3, (len(pos), 3)),
+                   stress=rng.normal(0, 2e-3, 6)) if labels else {}
+        gs.append(train.labeled_graph(pos, cell, types, 5.0, **lab))
+    return gs
+
+
+def test_trainable_energy_force_stress_vs_fp64(models):
+    m32, m64 = models
+    gs = _batch([0, 1, 2])
+    m32.train(False)
+    m64.train(False)
+    a = m32(train.collate(gs, device=DEV, dtype=torch.float32))
+    b = m64(train.collate(gs, dtype=torch.float64))
+    e32, e64 = a[KEY.PRED_TOTAL_ENERGY].detach().cpu().double(), b[KEY.PRED_TOTAL_ENERGY].detach()
+    assert float(((e32 - e64).abs() / e64.abs()).max()) < 2e-6
+    assert float((a[KEY.PRED_FORCE].detach().cpu().double() - b[KEY.PRED_FORCE]).abs().max()) \
+        < 1e-4
+    assert float((a[KEY.PRED_STRESS].detach().cpu().double() - b[KEY.PRED_STRESS]).abs().max()) \
+        < 2e-6
+
+
+def test_force_loss_parameter_gradients_vs_fp64(models):
+    """The double-backward gradient every fine-tune step takes (force loss,
+    create_graph=True) through the HIP kernels, against float64."""
+    m32, m64 = models
+    cfg = {'loss': 'mse', 'force_loss_weight': 1.0, 'stress_loss_weight': 1e-2,
+           'is_train_stress': True, 'continue': {'fisher_information': False,
+                                                 'opt_params': False}}
+    fns = train.get_loss_functions_from_config(cfg)
+    gs = _batch([3, 4])
+    grads = []
+    for m, kw in ((m32, dict(device=DEV, dtype=torch.float32)), (m64, dict(dtype=torch.float64))):
+        m.train(True)
+        m.zero_grad()
+        out = m(train.collate(gs, **kw))
+        loss = sum(f.get_loss(out, m) * w for f, w in fns)
+        loss.backward()
+        grads.append(m.flat_grad.detach().cpu().double().clone())
+        m.train(False)
+    g32, g64 = grads
+    assert float(g64.abs().max()) > 0
+    assert float((g32 - g64).norm() / g64.norm()) < 1e-4
+    # per tensor, relative to each tensor's own scale
+    for name, (off, n, _) in m64.slices.items():
+        ref = g64[off:off + n]
+        if float(ref.abs().max()) == 0.0:
+            assert float(g32[off:off + n].abs().max()) == 0.0, name
+            continue
+        assert float((g32[off:off + n] - ref).norm() / ref.norm()) < 1e-3, name
+
+
+def test_rehearsal_ewc_steps_reduce_loss(models):
+    """A few rehearsal+EWC Adam steps (the reference's FT_w_reEWC recipe,
+    Huber delta 0.01) on fixed batches lower the data loss of both batches,
+    and the EWC term grows from exactly zero at the optimum."""
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    m = SevenNetTrainable(device=DEV)
+    fisher = {n: torch.full_like(p, 1e-3) for n, p in m.named_parameters()}
+    opt = {n: p.detach().clone() for n, p in m.named_parameters()}
+    cfg = {'loss': 'huber', 'loss_param': {'delta': 0.01}, 'force_loss_weight': 1.0,
+           'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
+           'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
+           'scheduler_param': {'gamma': 0.99},
+           'continue': {'fisher_information': fisher, 'opt_params': opt, 'ewc_lambda': 1e2},
+           'device': DEV}
+    tr = train.Trainer(m, cfg)
+    data_fns = [(f, w) for f, w in tr.loss_functions if not isinstance(f, train.EWCLoss)]
+    ewc = [f for f, _ in tr.loss_functions if isinstance(f, train.EWCLoss)][0]
+    b = train.collate(_batch([5, 6]), device=DEV, dtype=torch.float32)
+    mem = train.collate(_batch([7]), device=DEV, dtype=torch.float32)
+
+    def data_loss():
+        m.train(True)
+        return sum(float(sum(f.get_loss(m(x), m) * w for f, w in data_fns).detach())
+                   for x in (b, mem))
+
+    before = data_loss()
+    assert float(ewc.get_loss({}, m)) == 0.0
+    for _ in range(5):
+        loss, mloss = tr.rehearsal_step(b, mem)
+        assert torch.isfinite(loss).all() and torch.isfinite(mloss).all()
+    after = data_loss()
+    m.train(False)
+    assert after < before
+    assert float(ewc.get_loss({}, m)) > 0.0
