@@ -47,12 +47,46 @@ def make_batches(rank, n_batches, batch_size, symbols):
     return [graphs[i * batch_size:(i + 1) * batch_size] for i in range(n_batches)]
 
 
+def cpu_baseline(batches, cfg, seconds):
+    """The same rehearsal step on the host CPU: the trainable model with the
+    oracle's uvu tensor product (tests/_conv_cpu.py, plain PyTorch, fp32) in
+    place of the HIP kernels, all host threads of this process's share."""
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    from _conv_cpu import CpuConvBackend
+    from sevennet_finetuning_amd import train
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get('OMP_NUM_THREADS', '16')))
+    torch.set_num_threads(threads)
+    model = SevenNetTrainable(device='cpu', conv_backend=CpuConvBackend())
+    c = dict(cfg, device='cpu', is_ddp=False)
+    c['continue'] = dict(cfg['continue'],
+                         fisher_information={k: v.cpu() for k, v in
+                                             cfg['continue']['fisher_information'].items()},
+                         opt_params={k: v.cpu() for k, v in
+                                     cfg['continue']['opt_params'].items()})
+    tr = train.Trainer(model, c)
+    model.train(True)
+    b = [train.collate(x, dtype=torch.float32) for x in batches[:2]]
+    t0, n = time.perf_counter(), 0   # ~17 s per step on 8 cores: no separate warm step
+    while time.perf_counter() - t0 < seconds:
+        tr.rehearsal_step(b[0], b[1])
+        n += 1
+    dt = time.perf_counter() - t0
+    structs = n * sum(len(x) for x in batches[:2])
+    return {'value': round(structs / dt, 3), 'unit': 'structures/s', 'cores': threads,
+            'kind': 'port',
+            'sample': f'{n} rehearsal steps (2 x {len(batches[0])} structures) in {dt:.1f} s, '
+                      'trainable model + oracle uvu TP (tests/_conv_cpu.py), torch CPU fp32'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=8)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-seconds', type=float, default=10.0)
     args = ap.parse_args()
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -106,6 +140,10 @@ def main():
         dt = float(t)
     ms = dt / args.steps * 1e3
     structs = 2 * args.batch * world * args.steps
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log('cpu baseline ...')
+        cpu = cpu_baseline(batches, cfg, args.cpu_seconds)
     if rank == 0:
         print(json.dumps({
             'metric': 'structures/sec fine-tune step (rehearsal + EWC), SevenNet-0',
@@ -119,7 +157,7 @@ def main():
                        'atoms_per_rank_step': atoms_per_step, 'edges_per_batch': edges,
                        'parallelism': f'dp{world}'},
             'atoms_per_s': round(atoms_per_step * world * args.steps / dt, 1),
-            'loss': float(loss), 'mem_loss': float(mloss)}), flush=True)
+            'loss': float(loss), 'mem_loss': float(mloss), 'cpu_baseline': cpu}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -58,7 +58,14 @@ def _offsets(irreps):
 class _Linear:
     """e3nn o3.Linear without bias (sevenn/nn/linear.py:46-49): one block per
     (i_in, i_out) pair of equal l, i_in-major, each (mul_in, mul_out)
-    row-major in the flat weight, path weight 1/sqrt(fan-in of i_out)."""
+    row-major in the flat weight, path weight 1/sqrt(fan-in of i_out).
+
+    Launch-lean form (the fine-tune step is launch-bound at its batch sizes):
+    inputs of one l that are adjacent in x (the sorted mid irreps are) form one
+    (n, sum mul, 2l+1) block and their weight blocks one stacked matrix, so each
+    output irrep is ONE GEMM, W^T x_l, written straight into the mul-major
+    layout; x and the weight are split (backward: one cat) rather than sliced
+    (backward: zero-fill + copy per slice)."""
 
     def __init__(self, irreps_in, irreps_out):
         self.irreps_in, self.irreps_out = irreps_in, irreps_out
@@ -68,26 +75,58 @@ class _Linear:
         self.alpha = {j: 1.0 / math.sqrt(f) for j, f in fan.items()}
         self.in_off, self.out_off = _offsets(irreps_in), _offsets(irreps_out)
         self.numel = sum(irreps_in[i][0] * irreps_out[j][0] for i, j in self.ins)
+        self.w_sizes = [irreps_in[i][0] * irreps_out[j][0] for i, j in self.ins]
+        # per output j: runs of consecutive input irreps feeding it
+        self.groups = {}
+        for k, (i, j) in enumerate(self.ins):
+            runs = self.groups.setdefault(j, [])
+            if runs and runs[-1][-1][0] == i - 1:
+                runs[-1].append((i, k))
+            else:
+                runs.append([(i, k)])
+        # x split points: every input irrep boundary
+        self.x_sizes = [m * (2 * l + 1) for m, l in irreps_in]
 
     def __call__(self, x, w_flat):
         n = x.shape[0]
-        outs = [None] * len(self.irreps_out)
-        woff = 0
-        for i, j in self.ins:
-            mi, l = self.irreps_in[i]
-            mo = self.irreps_out[j][0]
-            w = w_flat[woff:woff + mi * mo].view(mi, mo)
-            woff += mi * mo
-            d = 2 * l + 1
-            xi = x[:, self.in_off[i]:self.in_off[i + 1]].reshape(n, mi, d)
-            y = torch.matmul(xi.transpose(1, 2), w).transpose(1, 2) * self.alpha[j]
-            outs[j] = y if outs[j] is None else outs[j] + y
+        xs = x.split(self.x_sizes, dim=1) if len(self.x_sizes) > 1 else (x,)
+        ws = w_flat.split(self.w_sizes) if len(self.w_sizes) > 1 else (w_flat,)
         parts = []
         for j, (mo, l) in enumerate(self.irreps_out):
-            if outs[j] is None:
-                outs[j] = x.new_zeros(n, mo, 2 * l + 1)
-            parts.append(outs[j].reshape(n, -1))
-        return torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
+            d = 2 * l + 1
+            acc = None
+            for run in self.groups.get(j, []):
+                mul = sum(self.irreps_in[i][0] for i, _ in run)
+                xr = xs[run[0][0]] if len(run) == 1 else torch.cat([xs[i] for i, _ in run], 1)
+                wr = ws[run[0][1]].view(-1, mo) if len(run) == 1 else \
+                    torch.cat([ws[k].view(-1, mo) for _, k in run], 0)
+                if d == 1:
+                    y = torch.mm(xr, wr)
+                else:
+                    y = torch.matmul(wr.t(), xr.view(n, mul, d)).reshape(n, mo * d)
+                acc = y if acc is None else acc + y
+            if acc is None:
+                acc = x.new_zeros(n, mo * d)
+            parts.append(acc)
+        out = torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
+        return out * self.alpha[0] if self._uniform_alpha() else self._scale(out)
+
+    def _uniform_alpha(self):
+        if not hasattr(self, '_ua'):
+            vals = {self.alpha.get(j) for j in range(len(self.irreps_out))}
+            self._ua = len(vals) == 1 and None not in vals
+        return self._ua
+
+    def _scale(self, out):
+        if not hasattr(self, '_alpha_cols'):
+            cols = []
+            for j, (mo, l) in enumerate(self.irreps_out):
+                cols += [self.alpha.get(j, 0.0)] * (mo * (2 * l + 1))
+            self._alpha64 = torch.tensor(cols, dtype=torch.float64)
+            self._alpha_cols = self._alpha64
+        if self._alpha_cols.device != out.device or self._alpha_cols.dtype != out.dtype:
+            self._alpha_cols = self._alpha64.to(out.device, out.dtype)
+        return out * self._alpha_cols
 
 
 def _gate_irreps(irreps_out):
@@ -238,22 +277,21 @@ class SevenNetTrainable(torch.nn.Module):
         return torch.nn.functional.silu(x) * self.silu_norm
 
     def gate(self, x, gate_irreps):
-        # e3nn nn.Gate (equivariant_gate.py:59-61)
+        # e3nn nn.Gate (equivariant_gate.py:59-61); split, not sliced (one cat
+        # in the backward instead of a zero-fill + copy per slice)
         _, scal, gated = gate_irreps
         n = x.shape[0]
         ns = sum(m for m, _ in scal)
         ng = sum(m for m, _ in gated)
-        s = self.act(x[:, :ns])
         if ng == 0:
-            return s
-        g = self.act(x[:, ns:ns + ng])
-        outs, off, goff = [s], ns + ng, 0
-        for m, l in gated:
-            d = 2 * l + 1
-            blk = x[:, off:off + m * d].reshape(n, m, d)
-            outs.append((g[:, goff:goff + m].unsqueeze(-1) * blk).reshape(n, -1))
-            off += m * d
-            goff += m
+            return self.act(x[:, :ns] if x.shape[1] != ns else x)
+        sizes = [ns, ng] + [m * (2 * l + 1) for m, l in gated]
+        pieces = x.split(sizes, dim=1)
+        outs = [self.act(pieces[0])]
+        gs = self.act(pieces[1]).split([m for m, _ in gated], dim=1)
+        for k, (m, l) in enumerate(gated):
+            blk = pieces[2 + k].view(n, m, 2 * l + 1)
+            outs.append((gs[k].unsqueeze(-1) * blk).reshape(n, -1))
         return torch.cat(outs, dim=1)
 
     def _edge_basis(self, r):

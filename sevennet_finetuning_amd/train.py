@@ -148,15 +148,57 @@ class EWCLoss(LossDefinition):
                 d[k] = d[k].to(device)
         self.device = device
 
+    def _flat_terms(self, model):
+        """(fisher, theta*) laid out like ``model.flat`` (zero Fisher where a
+        parameter is absent from either dict), built once per model."""
+        params = dict(model.named_parameters())
+        key = (id(model), model.flat.data_ptr(), tuple(p.requires_grad for p in params.values()))
+        if getattr(self, '_flat_key', None) != key:
+            f = torch.zeros_like(model.flat)
+            o = torch.zeros_like(model.flat)
+            trainable = torch.zeros_like(model.flat)
+            for name, (off, n, _) in model.slices.items():
+                if name in self.fisher_dict and name in self.opt_params_dict:
+                    f[off:off + n] = self.fisher_dict[name].reshape(-1).to(f)
+                    o[off:off + n] = self.opt_params_dict[name].reshape(-1).to(o)
+                trainable[off:off + n] = float(params[name].requires_grad)
+            self._flat, self._flat_key = (f, o, f * trainable), key
+        return self._flat
+
     def get_loss(self, batch_data, model=None):
         if model is None:
             raise ValueError('EWC requires model to compute loss')
+        if hasattr(model, 'flat') and hasattr(model, 'flat_grad') and model.grads_in_flat_buffer():
+            # SevenNetTrainable: every parameter is a view of model.flat and
+            # every .grad a view of model.flat_grad -> one fused term
+            f, o, f_train = self._flat_terms(model)
+            return _FlatEWC.apply(model, f, o, f_train, *model.parameters()).view(1)
         ewc = torch.zeros(1, device=self.device)
         for name, p in model.named_parameters():
             if name not in self.fisher_dict or name not in self.opt_params_dict:
                 continue
             ewc = ewc + torch.sum(self.fisher_dict[name] * (p - self.opt_params_dict[name]) ** 2)
         return ewc
+
+
+class _FlatEWC(torch.autograd.Function):
+    """sum F (theta - theta*)^2 over the model's flat parameter buffer in one
+    pass; the backward adds 2 F (theta - theta*) straight into the flat
+    gradient buffer (trainable slots only) instead of one accumulation per
+    parameter tensor -- the same .grad values the per-tensor loop produces."""
+
+    @staticmethod
+    def forward(ctx, model, f, o, f_train, *params):
+        d = model.flat.detach() - o
+        ctx.model, ctx.f_train = model, f_train
+        ctx.save_for_backward(d)
+        return torch.sum(f * d * d)
+
+    @staticmethod
+    def backward(ctx, g):
+        d, = ctx.saved_tensors
+        ctx.model.flat_grad.add_(2.0 * g * ctx.f_train * d)
+        return (None,) * (4 + len(ctx.model.slices))
 
 
 loss_dict = {'mse': torch.nn.MSELoss, 'huber': torch.nn.HuberLoss, 'custom': 'custom'}

@@ -368,3 +368,32 @@ def test_data_parallel_rehearsal_step_gloo(tmp_path):
     with torch.no_grad():
         want = theta - lr * g1 * mask - lr * (g1 + g2) * mask
     assert torch.allclose(got, want, rtol=1e-12, atol=1e-14)
+
+
+def test_flat_ewc_equals_per_tensor_loop(model64):
+    """The fused flat-buffer EWC (one pass over model.flat, gradient straight
+    into flat_grad) gives the per-parameter loop's value and gradients,
+    skipping parameters missing from the dicts and frozen ones."""
+    torch.manual_seed(3)
+    names = [n for n, _ in model64.named_parameters()]
+    fisher = {n: torch.rand_like(p, dtype=torch.float64) for n, p in model64.named_parameters()
+              if n != names[2]}
+    opt = {n: (p.detach() + 1e-2 * torch.randn_like(p)) for n, p in model64.named_parameters()}
+    ewc = train.EWCLoss(fisher, opt)
+    model64.zero_grad()
+    fused = ewc.get_loss({}, model64)
+    fused.backward()
+    g_fused = model64.flat_grad.clone()
+    model64.zero_grad()
+    want = torch.zeros(1, dtype=torch.float64)
+    for n, p in model64.named_parameters():
+        if n in fisher:
+            want = want + torch.sum(fisher[n] * (p - opt[n]) ** 2)
+    want.backward()
+    g_loop = model64.flat_grad.clone()
+    model64.zero_grad()
+    assert fused.shape == (1,)
+    assert torch.allclose(fused, want, rtol=1e-13)
+    assert torch.allclose(g_fused, g_loop, rtol=1e-12, atol=1e-15)
+    frozen = model64.slices['rescale_atomic_energy.scale']
+    assert float(g_loop[frozen[0]:frozen[0] + frozen[1]].abs().max()) == 0.0

@@ -27,6 +27,9 @@ for s in "$@"; do
     testsn) step testsn 600 env E3GNN_BWD_X=node python -m pytest tests/test_gpu_parity.py -q -x ;;
     bench10k) step bench10k 300 python bench.py --cells 11 --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --profile-only ;;
+    proftrain) step proftrain 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_train -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 && mkdir -p gpurun_out/prof_train && cp /tmp/prof_train/*/*stats* /tmp/prof_train/*stats* gpurun_out/prof_train/ 2>/dev/null; ls gpurun_out/prof_train ;;
+    traintests) step traintests 400 python -m pytest tests/test_gpu_train.py -x -q --timeout 200 --timeout-method thread ;;
+    benchtrain) step benchtrain 300 python bench_train.py --steps 10 --warmup 3 ;;
     prof10k) step prof10k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof10k -o run --output-format csv -- python bench.py --cells 11 --steps 3 --warmup 1 --profile-only ;;
     pmcf) step pmcf 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 1 --warmup 1 --profile-only ;;
     pmcw) step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 1 --warmup 1 --profile-only ;;
