@@ -173,6 +173,31 @@ int e3gnn_nlist_build(e3gnn_nlist* h, int64_t n, const double* pos, const double
 int e3gnn_nlist_fetch(e3gnn_nlist* h, int32_t* edge_center, int32_t* edge_nbr, int32_t* shift,
                       float* edge_vec, void* stream);
 
+/* ---- DFT-D3 dispersion ----
+ * Replaces the reference's LAMMPS pair style d3 (sevenn/pair_e3gnn/pair_d3.cu):
+ * e3gnn_d3_create = PairD3::settings + coeff (:265-307, :656-767),
+ * e3gnn_d3_compute = PairD3::compute + update (:2030-2056, :2003-2024).
+ * damping: 1 zero ("damp_zero"), 2 Becke-Johnson ("damp_bj"), 4 "damp_bjm"
+ * (the BJ kernel, as in the reference); 3 "damp_zerom" is refused (the
+ * reference leaves it unimplemented, :1550-1553).  func = {s6, s8, a1, a2,
+ * alp6, alp8} (setfuncpar :422-653: a1 = rs6, a2 = rs18, s8 = s18, alp8 =
+ * alp6 + 2); rthr / cn_thr: squared cutoffs in bohr^2 (pair_style d3 args).
+ * Per-type tables (host, copied): rcov [nt] (bohr), r2r4 [nt], r0ab [nt][nt]
+ * (bohr), mxc [nt], c6ab [nt][nt][5][5][3] = (C6, CN_ref_i, CN_ref_j).
+ * e3gnn_d3_compute takes HOST arrays as LAMMPS holds them: pos f64 [n][3] (A),
+ * cell f64 [3][3] (rows a, b, c, A), pbc int[3], type int32 [n] in
+ * [0, ntypes); returns energy (eV), forces f64 [n][3] (eV/A) and virial6 (eV,
+ * LAMMPS order xx, yy, zz, xy, xz, yz) on the host; synchronises `stream`.
+ * Deterministic (no atomics). */
+typedef struct e3gnn_d3 e3gnn_d3;
+e3gnn_d3* e3gnn_d3_create(int device, int damping, const float* func, float rthr, float cn_thr,
+                          int ntypes, const float* rcov, const float* r2r4, const float* r0ab,
+                          const int32_t* mxc, const float* c6ab);
+void e3gnn_d3_free(e3gnn_d3* h);
+int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* cell,
+                     const int32_t* pbc, const int32_t* type, double* energy, double* forces,
+                     double* virial6, void* stream);
+
 /* ---- diagnostics ---- */
 /* Kernel implementation of the convolution: 0 = fused radial-MLP + tensor
  * product (default), 1 = unfused v1 kernels (per-edge weights materialised in

@@ -25,6 +25,7 @@
 
 #include "../../include/e3gnn.h"
 #include "cg_tables.h"
+#include "d3.h"
 #include "common.h"
 #include "fused.h"
 #include "minijson.h"
@@ -1515,3 +1516,170 @@ int64_t e3gnn_workspace_bytes(const e3gnn_ctx* c) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ DFT-D3
+// PairD3 (sevenn/pair_e3gnn/pair_d3.cu) over host arrays, as LAMMPS hands
+// them to PairD3::compute: settings/coeff -> e3gnn_d3_create, compute ->
+// e3gnn_d3_compute (wrap into the cell :1182-1224, image lists :1026-1045 and
+// :1230-1266, the four kernels of d3.hip, update :2003-2024).
+struct e3gnn_d3 {
+  int device = 0;
+  D3Params p{};
+  DBuf rcov, r2r4, r0ab, mxc, c6ab, x, type, tau_v, tau_c, cn, rows, forces, totals;
+};
+
+e3gnn_d3* e3gnn_d3_create(int device, int damping, const float* func, float rthr, float cn_thr,
+                          int ntypes, const float* rcov, const float* r2r4, const float* r0ab,
+                          const int32_t* mxc, const float* c6ab) {
+  if (damping != 1 && damping != 2 && damping != 4) {
+    fail(E3GNN_ERR_ARG, damping == 3 ? "damp_zerom is not implemented (nor by the reference, "
+                                       "pair_d3.cu:1550-1553)"
+                                     : "damping must be 1 (zero), 2 (bj) or 4 (bjm)");
+    return nullptr;
+  }
+  if (ntypes <= 0 || !func || !rcov || !r2r4 || !r0ab || !mxc || !c6ab || !(rthr > 0) ||
+      !(cn_thr > 0)) {
+    fail(E3GNN_ERR_ARG, "d3: bad parameters");
+    return nullptr;
+  }
+  for (int t = 0; t < ntypes; ++t)
+    if (mxc[t] < 0 || mxc[t] > 5) {
+      fail(E3GNN_ERR_ARG, "d3: mxc out of [0, 5]");
+      return nullptr;
+    }
+  if (hipSetDevice(device) != hipSuccess) {
+    fail(E3GNN_ERR_HIP, "hipSetDevice failed");
+    return nullptr;
+  }
+  auto* h = new e3gnn_d3;
+  h->device = device;
+  const size_t nt = (size_t)ntypes;
+  auto up = [](DBuf& b, const void* src, size_t bytes) {
+    if (b.ensure(bytes) != hipSuccess) return false;
+    return hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!up(h->rcov, rcov, nt * 4) || !up(h->r2r4, r2r4, nt * 4) || !up(h->r0ab, r0ab, nt * nt * 4) ||
+      !up(h->mxc, mxc, nt * 4) || !up(h->c6ab, c6ab, nt * nt * 75 * 4)) {
+    delete h;
+    fail(E3GNN_ERR_HIP, "d3: table upload failed");
+    return nullptr;
+  }
+  D3Params& p = h->p;
+  p.damping = damping == 1 ? 1 : 2;
+  p.ntypes = ntypes;
+  p.s6 = func[0];
+  p.s8 = func[1];
+  p.a1 = func[2];
+  p.a2 = func[3];
+  p.alp6 = func[4];
+  p.alp8 = func[5];
+  p.rthr = rthr;
+  p.cn_thr = cn_thr;
+  p.rcov = h->rcov.f();
+  p.r2r4 = h->r2r4.f();
+  p.r0ab = h->r0ab.f();
+  p.mxc = h->mxc.i();
+  p.c6ab = h->c6ab.f();
+  return h;
+}
+
+void e3gnn_d3_free(e3gnn_d3* h) { delete h; }
+
+namespace {
+// rep = int(|sqrt(thr) / height|) + 1 per periodic axis (:1026-1045); the
+// translations i a + j b + k c with k fastest (:1230-1266)
+void d3_images(const double lat[3][3], float thr, const int* pbc, std::vector<float>& tau,
+               int& t0) {
+  const double rc = std::sqrt((double)thr);
+  int rep[3];
+  for (int k = 0; k < 3; ++k) {
+    const double* u = lat[(k + 1) % 3];
+    const double* v = lat[(k + 2) % 3];
+    const double c[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2],
+                         u[0] * v[1] - u[1] * v[0]};
+    const double len = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    const double h = (c[0] * lat[k][0] + c[1] * lat[k][1] + c[2] * lat[k][2]) / len;
+    rep[k] = pbc[k] ? (int)std::fabs(rc / h) + 1 : 0;
+  }
+  tau.clear();
+  for (int a = -rep[0]; a <= rep[0]; ++a)
+    for (int b = -rep[1]; b <= rep[1]; ++b)
+      for (int c = -rep[2]; c <= rep[2]; ++c)
+        for (int d = 0; d < 3; ++d)
+          tau.push_back((float)(lat[0][d] * a + lat[1][d] * b + lat[2][d] * c));
+  t0 = (rep[0] * (2 * rep[1] + 1) + rep[1]) * (2 * rep[2] + 1) + rep[2];
+}
+}  // namespace
+
+int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* cell,
+                     const int32_t* pbc, const int32_t* type, double* energy, double* forces,
+                     double* virial6, void* stream) {
+  if (!h) return fail(E3GNN_ERR_ARG, "null d3 handle");
+  if (n < 0 || n >= (int64_t)1 << 31) return fail(E3GNN_ERR_ARG, "d3: atom count out of range");
+  if (n > 0 && (!pos || !type || !forces)) return fail(E3GNN_ERR_ARG, "d3: null input");
+  if (!cell || !pbc || !energy || !virial6) return fail(E3GNN_ERR_ARG, "d3: null input");
+  for (int64_t i = 0; i < n; ++i)
+    if (type[i] < 0 || type[i] >= h->p.ntypes) return fail(E3GNN_ERR_ARG, "d3: type out of range");
+  // lattice in bohr, rows a, b, c
+  double lat[3][3];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) lat[r][c] = cell[3 * r + c] / D3_AU_TO_ANG;
+  const double det = lat[0][0] * (lat[1][1] * lat[2][2] - lat[1][2] * lat[2][1]) -
+                     lat[0][1] * (lat[1][0] * lat[2][2] - lat[1][2] * lat[2][0]) +
+                     lat[0][2] * (lat[1][0] * lat[2][1] - lat[1][1] * lat[2][0]);
+  if (!(std::fabs(det) > 1e-12)) return fail(E3GNN_ERR_ARG, "d3: singular cell");
+  // inverse (columns of inv = reciprocal rows / det); frac = pos . inv
+  double inv[3][3];
+  inv[0][0] = (lat[1][1] * lat[2][2] - lat[1][2] * lat[2][1]) / det;
+  inv[0][1] = (lat[0][2] * lat[2][1] - lat[0][1] * lat[2][2]) / det;
+  inv[0][2] = (lat[0][1] * lat[1][2] - lat[0][2] * lat[1][1]) / det;
+  inv[1][0] = (lat[1][2] * lat[2][0] - lat[1][0] * lat[2][2]) / det;
+  inv[1][1] = (lat[0][0] * lat[2][2] - lat[0][2] * lat[2][0]) / det;
+  inv[1][2] = (lat[0][2] * lat[1][0] - lat[0][0] * lat[1][2]) / det;
+  inv[2][0] = (lat[1][0] * lat[2][1] - lat[1][1] * lat[2][0]) / det;
+  inv[2][1] = (lat[0][1] * lat[2][0] - lat[0][0] * lat[2][1]) / det;
+  inv[2][2] = (lat[0][0] * lat[1][1] - lat[0][1] * lat[1][0]) / det;
+  std::vector<float> xw((size_t)n * 3);
+  for (int64_t i = 0; i < n; ++i) {
+    double p[3], a[3];
+    for (int d = 0; d < 3; ++d) p[d] = pos[3 * i + d] / D3_AU_TO_ANG;
+    for (int k = 0; k < 3; ++k) {
+      // row vector p = a . lat  ->  a = p . inv
+      a[k] = p[0] * inv[0][k] + p[1] * inv[1][k] + p[2] * inv[2][k];
+      if (pbc[k]) a[k] -= std::floor(a[k]);
+    }
+    for (int d = 0; d < 3; ++d)
+      xw[3 * i + d] = (float)(a[0] * lat[0][d] + a[1] * lat[1][d] + a[2] * lat[2][d]);
+  }
+  std::vector<float> tv, tc;
+  int t0v, t0c;
+  d3_images(lat, h->p.rthr, pbc, tv, t0v);
+  d3_images(lat, h->p.cn_thr, pbc, tc, t0c);
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  HIPCHK(h->x.ensure(nn * 12));
+  HIPCHK(h->type.ensure(nn * 4));
+  HIPCHK(h->tau_v.ensure(tv.size() * 4));
+  HIPCHK(h->tau_c.ensure(tc.size() * 4));
+  HIPCHK(h->cn.ensure(nn * 8));
+  HIPCHK(h->rows.ensure(nn * 64));
+  HIPCHK(h->forces.ensure(nn * 24));
+  HIPCHK(h->totals.ensure(7 * 8));
+  if (n > 0) {
+    HIPCHK(hipMemcpyAsync(h->x.p, xw.data(), n * 12, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->type.p, type, n * 4, hipMemcpyHostToDevice, s));
+  }
+  HIPCHK(hipMemcpyAsync(h->tau_v.p, tv.data(), tv.size() * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(h->tau_c.p, tc.data(), tc.size() * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(launch_d3(h->p, (int)n, h->x.f(), h->type.i(), h->tau_v.f(), (int)(tv.size() / 3), t0v,
+                   h->tau_c.f(), (int)(tc.size() / 3), t0c, (double*)h->cn.p, (double*)h->rows.p,
+                   (double*)h->forces.p, (double*)h->totals.p, s));
+  double tot[7];
+  HIPCHK(hipMemcpyAsync(tot, h->totals.p, 7 * 8, hipMemcpyDeviceToHost, s));
+  if (n > 0) HIPCHK(hipMemcpyAsync(forces, h->forces.p, n * 24, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *energy = tot[0];
+  for (int k = 0; k < 6; ++k) virial6[k] = tot[1 + k];
+  return E3GNN_OK;
+}

@@ -1,0 +1,333 @@
+// DFT-D3 dispersion (zero and Becke-Johnson damping) with the C6(CN) chain,
+// energy + forces + virial -- SURVEY.md §8f row 4, the reference's LAMMPS
+// pair style d3 (sevenn/pair_e3gnn/pair_d3.cu:808-2056).
+//
+// Same arithmetic as the reference (fp32 per pair-image term, C6 interpolation
+// in fp64, units bohr / hartree), different decomposition.  The reference
+// walks unordered pairs (i >= j) and scatters into both atoms with
+// float/double atomics; here one workgroup owns one atom i and walks every
+// (j, image) item of its row, so every per-atom output (CN_i, dE/dCN_i, F_i)
+// is written by exactly one workgroup -- no atomics, bitwise deterministic --
+// at twice the pair evaluations.  Per-row energy/virial partials are reduced
+// in a fixed order by a one-block kernel.
+//
+//   k_d3_cn      CN_i = sum_{j,T} 1/(1+exp(-K1((rcov_i+rcov_j)/r - 1)))   (:1051-1104)
+//   k_d3_disp    C6_ij, dC6/dCN_i for a chunk of j into LDS (:808-887), then
+//                E, F_i (direct), virial, dE/dCN_i over the chunk's images
+//                (:1273-1505 zero, :1558-1768 BJ)
+//   k_d3_chain   F_i += (dE/dCN_i + dE/dCN_j) dCN/dr r_hat, virial   (:1812-1976)
+//   k_d3_reduce  energy and virial over rows, fixed order
+//
+// Items are (j, image) with the image index fastest, so a wavefront reads 64
+// consecutive translation vectors (coalesced) for one j (broadcast).
+#include "d3.h"
+
+namespace e3gnn {
+
+
+
+namespace {
+
+constexpr float K1 = 16.0f;
+constexpr float K3 = -4.0f;
+constexpr int MAXC = 5;
+constexpr int BLK = 256;
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int k = 0; k < BLK / 64; ++k) s += red[k];   // fixed order
+  return s;
+}
+
+__device__ __forceinline__ float load_tau(const float* tau, int t, int c) { return tau[3 * t + c]; }
+
+// CN_i, one workgroup per atom
+__global__ __launch_bounds__(BLK) void k_d3_cn(D3Params p, int n, const float* __restrict__ x,
+                                                const int* __restrict__ type,
+                                                const float* __restrict__ tau, int nt, int t0,
+                                                double* __restrict__ cn) {
+  __shared__ double red[BLK / 64];
+  const int i = blockIdx.x;
+  const float xi0 = x[3 * i], xi1 = x[3 * i + 1], xi2 = x[3 * i + 2];
+  const float rci = p.rcov[type[i]];
+  float acc = 0.f;
+  const int64_t items = (int64_t)n * nt;
+  for (int64_t k = threadIdx.x; k < items; k += BLK) {
+    const int j = (int)(k / nt), t = (int)(k - (int64_t)j * nt);
+    if (j == i && t == t0) continue;
+    const float rx = x[3 * j] - xi0 + load_tau(tau, t, 0);
+    const float ry = x[3 * j + 1] - xi1 + load_tau(tau, t, 1);
+    const float rz = x[3 * j + 2] - xi2 + load_tau(tau, t, 2);
+    const float r2 = rx * rx + ry * ry + rz * rz;
+    if (r2 <= p.cn_thr) {
+      const float rcs = rci + p.rcov[type[j]];
+      acc += 1.0f / (1.0f + expf(-K1 * (rcs * rsqrtf(r2) - 1.0f)));
+    }
+  }
+  const double s = block_sum((double)acc, red);
+  if (threadIdx.x == 0) cn[i] = s;
+}
+
+// C6(CN_i, CN_j) and its CN derivatives (kernel_get_dC6_dCNij, :808-887)
+__device__ void c6_pair(const D3Params& p, int ti, int tj, double cni, double cnj, float& c6,
+                        float& dci, float& dcj) {
+  const float* tab = p.c6ab + ((size_t)ti * p.ntypes + tj) * (MAXC * MAXC * 3);
+  const int ma = p.mxc[ti], mb = p.mxc[tj];
+  float c6mem = -1e30f, rsave = 9999.0f;
+  double num = 0.0, den = 0.0, dni = 0.0, ddi = 0.0, dnj = 0.0, ddj = 0.0;
+  const float fcni = (float)cni, fcnj = (float)cnj;
+  for (int a = 0; a < ma; ++a)
+    for (int b = 0; b < mb; ++b) {
+      const float* e = tab + (a * MAXC + b) * 3;
+      const float ref = e[0];
+      if (ref > 0.0f) {
+        const float ca = e[1], cb = e[2];
+        const float r = (ca - fcni) * (ca - fcni) + (cb - fcnj) * (cb - fcnj);
+        if (r < rsave) {
+          rsave = r;
+          c6mem = ref;
+        }
+        double ex = exp((double)K3 * (double)r);
+        num += ref * ex;
+        den += ex;
+        ex *= 2.0 * K3;
+        double tm = ex * (fcni - ca);
+        dni += ref * tm;
+        ddi += tm;
+        tm = ex * (fcnj - cb);
+        dnj += ref * tm;
+        ddj += tm;
+      }
+    }
+  if (den > 1e-99) {
+    const double rd = 1.0 / den, u = num * rd;
+    c6 = (float)u;
+    dci = (float)(rd * fma(u, -ddi, dni));
+    dcj = (float)(rd * fma(u, -ddj, dnj));
+  } else {
+    c6 = c6mem;
+    dci = 0.f;
+    dcj = 0.f;
+  }
+}
+
+// row outputs: [0] energy, [1..6] virial (xx,yy,zz,xy,xz,yz), [7] dE/dCN
+constexpr int ROW = 8;
+
+template <int DAMP>
+__global__ __launch_bounds__(BLK) void k_d3_disp(D3Params p, int n, const float* __restrict__ x,
+                                                  const int* __restrict__ type,
+                                                  const float* __restrict__ tau, int nt, int t0,
+                                                  const double* __restrict__ cn,
+                                                  double* __restrict__ rows,
+                                                  double* __restrict__ forces) {
+  __shared__ float s_c6[BLK], s_dc[BLK];
+  __shared__ double red[BLK / 64];
+  const int i = blockIdx.x;
+  const int ti = type[i];
+  const float xi0 = x[3 * i], xi1 = x[3 * i + 1], xi2 = x[3 * i + 2];
+  const double cni = cn[i];
+  float e = 0.f, fx = 0.f, fy = 0.f, fz = 0.f, dcn = 0.f;
+  float v00 = 0.f, v11 = 0.f, v22 = 0.f, v01 = 0.f, v02 = 0.f, v12 = 0.f;
+  for (int j0 = 0; j0 < n; j0 += BLK) {
+    const int jn = min(BLK, n - j0);
+    __syncthreads();
+    if ((int)threadIdx.x < jn) {
+      const int j = j0 + threadIdx.x;
+      float c6, dci, dcj;
+      c6_pair(p, ti, type[j], cni, cn[j], c6, dci, dcj);
+      s_c6[threadIdx.x] = c6;
+      s_dc[threadIdx.x] = dci;
+    }
+    __syncthreads();
+    const int64_t items = (int64_t)jn * nt;
+    for (int64_t k = threadIdx.x; k < items; k += BLK) {
+      const int jj = (int)(k / nt), t = (int)(k - (int64_t)jj * nt);
+      const int j = j0 + jj;
+      if (j == i && t == t0) continue;
+      const float rx = x[3 * j] - xi0 + load_tau(tau, t, 0);
+      const float ry = x[3 * j + 1] - xi1 + load_tau(tau, t, 1);
+      const float rz = x[3 * j + 2] - xi2 + load_tau(tau, t, 2);
+      const float r2 = rx * rx + ry * ry + rz * rz;
+      if (r2 > p.rthr) continue;
+      const int tj = type[j];
+      const float c6 = s_c6[jj];
+      float erest, x1;  // x1: -(dE/dr)/r per unit C6... (reference's x1 convention)
+      if constexpr (DAMP == 1) {
+        // zero damping, alp6 = 14 / alp8 = 16 as fixed powers (:1338-1356)
+        const float r0 = p.r0ab[ti * p.ntypes + tj];
+        const float s8r42 = p.s8 * p.r2r4[ti] * p.r2r4[tj];
+        const float rrc = rsqrtf(r2);
+        float u1 = p.a1 * r0 * rrc;
+        float t6 = u1 * u1;
+        t6 *= u1;
+        t6 *= t6;
+        t6 *= u1;
+        t6 *= t6;
+        const float d6 = 1.0f / fmaf(t6, 6.0f, 1.0f);
+        float u2 = p.a2 * r0 * rrc;
+        float t8 = u2 * u2;
+        t8 *= t8;
+        t8 *= t8;
+        t8 *= t8;
+        const float d8 = 1.0f / fmaf(t8, 6.0f, 1.0f);
+        const float r2rc = rrc * rrc, r6rc = r2rc * r2rc * r2rc, r8rc = r6rc * r2rc;
+        erest = r6rc * fmaf(3.0f * r2rc, s8r42 * d8, p.s6 * d6);
+        // vec = x1 * rij  (x1 already carries 1/r)
+        x1 = 6.0f * c6 * r8rc *
+             fmaf(r2rc, s8r42 * d8 * fmaf(3.0f * p.alp8 * t8, d8, -4.0f),
+                  p.s6 * d6 * fmaf(p.alp6 * t6, d6, -1.0f));
+      } else {
+        const float r42x3 = p.r2r4[ti] * p.r2r4[tj] * 3.0f;
+        const float R0 = fmaf(p.a1, sqrtf(r42x3), p.a2);
+        const float R02 = R0 * R0, R06 = R02 * R02 * R02, R08 = R06 * R02;
+        const float s8r = p.s8 * r42x3;
+        const float r = sqrtf(r2), r5 = r2 * r2 * r, r7 = r5 * r2;
+        const float t6 = 1.0f / fmaf(r5, r, R06);
+        const float t8 = 1.0f / fmaf(r7, r, R08);
+        erest = fmaf(s8r, t8, p.s6 * t6);
+        x1 = -c6 * fmaf(8.0f * s8r * r7, t8 * t8, 6.0f * p.s6 * r5 * t6 * t6) / r;
+      }
+      // row weights: every unordered pair appears in two rows, the self
+      // images of i once -> energy / virial carry 1/2; F_i and dE/dCN_i the
+      // full derivative of this row's own atom
+      e -= 0.5f * erest * c6;
+      dcn -= erest * s_dc[jj];
+      const float vx = x1 * rx, vy = x1 * ry, vz = x1 * rz;  // = -(dE/dr) r_hat
+      if (j != i) {
+        fx -= vx;
+        fy -= vy;
+        fz -= vz;
+      }
+      v00 += 0.5f * vx * rx;
+      v11 += 0.5f * vy * ry;
+      v22 += 0.5f * vz * rz;
+      v01 += 0.5f * vx * ry;
+      v02 += 0.5f * vx * rz;
+      v12 += 0.5f * vy * rz;
+    }
+  }
+  double* row = rows + (size_t)i * ROW;
+  const double se = block_sum(e, red);
+  const double sfx = block_sum(fx, red), sfy = block_sum(fy, red), sfz = block_sum(fz, red);
+  const double s00 = block_sum(v00, red), s11 = block_sum(v11, red), s22 = block_sum(v22, red);
+  const double s01 = block_sum(v01, red), s02 = block_sum(v02, red), s12 = block_sum(v12, red);
+  const double sdc = block_sum(dcn, red);
+  if (threadIdx.x == 0) {
+    row[0] = se;
+    row[1] = s00;
+    row[2] = s11;
+    row[3] = s22;
+    row[4] = s01;
+    row[5] = s02;
+    row[6] = s12;
+    row[7] = sdc;
+    forces[3 * i] = sfx;
+    forces[3 * i + 1] = sfy;
+    forces[3 * i + 2] = sfz;
+  }
+}
+
+// F_i += sum_j,T (dE/dCN_i + dE/dCN_j) dCN/dr r_hat ; virial (:1812-1976)
+__global__ __launch_bounds__(BLK) void k_d3_chain(D3Params p, int n, const float* __restrict__ x,
+                                                   const int* __restrict__ type,
+                                                   const float* __restrict__ tau, int nt, int t0,
+                                                   double* __restrict__ rows,
+                                                   double* __restrict__ forces) {
+  __shared__ double red[BLK / 64];
+  const int i = blockIdx.x;
+  const float xi0 = x[3 * i], xi1 = x[3 * i + 1], xi2 = x[3 * i + 2];
+  const float rci = p.rcov[type[i]];
+  const float dci = (float)rows[(size_t)i * ROW + 7];
+  float fx = 0.f, fy = 0.f, fz = 0.f;
+  float v00 = 0.f, v11 = 0.f, v22 = 0.f, v01 = 0.f, v02 = 0.f, v12 = 0.f;
+  const int64_t items = (int64_t)n * nt;
+  for (int64_t k = threadIdx.x; k < items; k += BLK) {
+    const int j = (int)(k / nt), t = (int)(k - (int64_t)j * nt);
+    if (j == i && t == t0) continue;
+    const float rx = x[3 * j] - xi0 + load_tau(tau, t, 0);
+    const float ry = x[3 * j + 1] - xi1 + load_tau(tau, t, 1);
+    const float rz = x[3 * j + 2] - xi2 + load_tau(tau, t, 2);
+    const float r2 = rx * rx + ry * ry + rz * rz;
+    if (r2 >= p.cn_thr) continue;
+    const float rcs = rci + p.rcov[type[j]];
+    const float rrc = rsqrtf(r2);
+    const float ex = expf(-K1 * (rcs * rrc - 1.0f));
+    const float dcnn = -K1 * rcs * ex / (r2 * (ex + 1.0f) * (ex + 1.0f));
+    // self images: weight dE/dCN_i once; pairs: (i, j) and (j, i) rows each 1/2
+    const float w = j == i ? dci : 0.5f * (dci + (float)rows[(size_t)j * ROW + 7]);
+    const float x1 = dcnn * w * rrc;
+    const float vx = x1 * rx, vy = x1 * ry, vz = x1 * rz;   // (dE/dr) r_hat, this row's share
+    if (j != i) {
+      fx += 2.0f * vx;
+      fy += 2.0f * vy;
+      fz += 2.0f * vz;
+    }
+    v00 -= vx * rx;
+    v11 -= vy * ry;
+    v22 -= vz * rz;
+    v01 -= vx * ry;
+    v02 -= vx * rz;
+    v12 -= vy * rz;
+  }
+  const double sfx = block_sum(fx, red), sfy = block_sum(fy, red), sfz = block_sum(fz, red);
+  const double s00 = block_sum(v00, red), s11 = block_sum(v11, red), s22 = block_sum(v22, red);
+  const double s01 = block_sum(v01, red), s02 = block_sum(v02, red), s12 = block_sum(v12, red);
+  if (threadIdx.x == 0) {
+    double* row = rows + (size_t)i * ROW;
+    row[1] += s00;
+    row[2] += s11;
+    row[3] += s22;
+    row[4] += s01;
+    row[5] += s02;
+    row[6] += s12;
+    forces[3 * i] += sfx;
+    forces[3 * i + 1] += sfy;
+    forces[3 * i + 2] += sfz;
+  }
+}
+
+// totals[0] = energy (eV), totals[1..6] = virial (eV); fixed-order sums over
+// rows; forces to eV/A (update, :2003-2024)
+__global__ __launch_bounds__(BLK) void k_d3_reduce(int n, const double* __restrict__ rows,
+                                                    double* __restrict__ forces,
+                                                    double* __restrict__ totals) {
+  __shared__ double red[BLK / 64];
+  for (int c = 0; c < 7; ++c) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += BLK) s += rows[(size_t)i * ROW + c];
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) totals[c] = s * D3_AU_TO_EV;
+  }
+  for (int k = threadIdx.x; k < 3 * n; k += BLK) forces[k] *= D3_AU_TO_EV / D3_AU_TO_ANG;
+}
+
+}  // namespace
+
+hipError_t launch_d3(const D3Params& p, int n, const float* x, const int* type,
+                     const float* tau_vdw, int nt_vdw, int t0_vdw, const float* tau_cn, int nt_cn,
+                     int t0_cn, double* cn, double* rows, double* forces, double* totals,
+                     hipStream_t s) {
+  if (n <= 0) {
+    hipMemsetAsync(totals, 0, 7 * sizeof(double), s);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_d3_cn, dim3(n), dim3(BLK), 0, s, p, n, x, type, tau_cn, nt_cn, t0_cn, cn);
+  if (p.damping == 1)
+    hipLaunchKernelGGL(k_d3_disp<1>, dim3(n), dim3(BLK), 0, s, p, n, x, type, tau_vdw, nt_vdw,
+                       t0_vdw, cn, rows, forces);
+  else
+    hipLaunchKernelGGL(k_d3_disp<2>, dim3(n), dim3(BLK), 0, s, p, n, x, type, tau_vdw, nt_vdw,
+                       t0_vdw, cn, rows, forces);
+  hipLaunchKernelGGL(k_d3_chain, dim3(n), dim3(BLK), 0, s, p, n, x, type, tau_cn, nt_cn, t0_cn,
+                     rows, forces);
+  hipLaunchKernelGGL(k_d3_reduce, dim3(1), dim3(BLK), 0, s, n, rows, forces, totals);
+  return hipGetLastError();
+}
+
+}  // namespace e3gnn
