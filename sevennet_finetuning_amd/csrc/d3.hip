@@ -44,6 +44,27 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return s;
 }
 
+// (j, image) items of a row, image fastest, thread k takes items k, k + BLK, ...:
+// one 32-bit division at the start, then an add-and-carry per step (no 64-bit
+// division in the loop)
+struct ItemIter {
+  int j, t, nt, qj, qt;
+  __device__ explicit ItemIter(int nt_) : nt(nt_) {
+    j = threadIdx.x / nt;
+    t = threadIdx.x - j * nt;
+    qj = BLK / nt;
+    qt = BLK - qj * nt;
+  }
+  __device__ __forceinline__ void next() {
+    j += qj;
+    t += qt;
+    if (t >= nt) {
+      t -= nt;
+      ++j;
+    }
+  }
+};
+
 __device__ __forceinline__ float load_tau(const float* tau, int t, int c) { return tau[3 * t + c]; }
 
 // CN_i, one workgroup per atom
@@ -56,9 +77,8 @@ __global__ __launch_bounds__(BLK) void k_d3_cn(D3Params p, int n, const float* _
   const float xi0 = x[3 * i], xi1 = x[3 * i + 1], xi2 = x[3 * i + 2];
   const float rci = p.rcov[type[i]];
   float acc = 0.f;
-  const int64_t items = (int64_t)n * nt;
-  for (int64_t k = threadIdx.x; k < items; k += BLK) {
-    const int j = (int)(k / nt), t = (int)(k - (int64_t)j * nt);
+  for (ItemIter it(nt); it.j < n; it.next()) {
+    const int j = it.j, t = it.t;
     if (j == i && t == t0) continue;
     const float rx = x[3 * j] - xi0 + load_tau(tau, t, 0);
     const float ry = x[3 * j + 1] - xi1 + load_tau(tau, t, 1);
@@ -145,9 +165,8 @@ __global__ __launch_bounds__(BLK) void k_d3_disp(D3Params p, int n, const float*
       s_dc[threadIdx.x] = dci;
     }
     __syncthreads();
-    const int64_t items = (int64_t)jn * nt;
-    for (int64_t k = threadIdx.x; k < items; k += BLK) {
-      const int jj = (int)(k / nt), t = (int)(k - (int64_t)jj * nt);
+    for (ItemIter it(nt); it.j < jn; it.next()) {
+      const int jj = it.j, t = it.t;
       const int j = j0 + jj;
       if (j == i && t == t0) continue;
       const float rx = x[3 * j] - xi0 + load_tau(tau, t, 0);
@@ -246,9 +265,8 @@ __global__ __launch_bounds__(BLK) void k_d3_chain(D3Params p, int n, const float
   const float dci = (float)rows[(size_t)i * ROW + 7];
   float fx = 0.f, fy = 0.f, fz = 0.f;
   float v00 = 0.f, v11 = 0.f, v22 = 0.f, v01 = 0.f, v02 = 0.f, v12 = 0.f;
-  const int64_t items = (int64_t)n * nt;
-  for (int64_t k = threadIdx.x; k < items; k += BLK) {
-    const int j = (int)(k / nt), t = (int)(k - (int64_t)j * nt);
+  for (ItemIter it(nt); it.j < n; it.next()) {
+    const int j = it.j, t = it.t;
     if (j == i && t == t0) continue;
     const float rx = x[3 * j] - xi0 + load_tau(tau, t, 0);
     const float ry = x[3 * j + 1] - xi1 + load_tau(tau, t, 1);
