@@ -1525,7 +1525,8 @@ int64_t e3gnn_workspace_bytes(const e3gnn_ctx* c) {
 struct e3gnn_d3 {
   int device = 0;
   D3Params p{};
-  DBuf rcov, r2r4, r0ab, mxc, c6ab, x, type, tau_v, tau_c, cn, rows, forces, totals;
+  DBuf rcov, r2r4, r0ab, mxc, c6ab, x, type, bin_of, bin_start, off_v, off_c, cn, c6tab, rows,
+      forces, totals;
 };
 
 e3gnn_d3* e3gnn_d3_create(int device, int damping, const float* func, float rthr, float cn_thr,
@@ -1586,28 +1587,24 @@ e3gnn_d3* e3gnn_d3_create(int device, int damping, const float* func, float rthr
 void e3gnn_d3_free(e3gnn_d3* h) { delete h; }
 
 namespace {
-// rep = int(|sqrt(thr) / height|) + 1 per periodic axis (:1026-1045); the
-// translations i a + j b + k c with k fastest (:1230-1266)
-void d3_images(const double lat[3][3], float thr, const int* pbc, std::vector<float>& tau,
-               int& t0) {
+constexpr double D3_BIN_BOHR = 20.0;     // target bin edge (~60 atoms per bin at solid density)
+constexpr int64_t D3_C6TAB_MAX = 32768;  // n^2 C6 table up to 8.6 GB; beyond: C6 per item
+
+// stencil of bin offsets covering a sphere of radius sqrt(thr): R = floor(rc /
+// bin height) + 1 bins along each periodic axis (every (bin, image) pair once)
+std::vector<int> d3_stencil(float thr, const double binh[3], const int* pbc) {
   const double rc = std::sqrt((double)thr);
-  int rep[3];
-  for (int k = 0; k < 3; ++k) {
-    const double* u = lat[(k + 1) % 3];
-    const double* v = lat[(k + 2) % 3];
-    const double c[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2],
-                         u[0] * v[1] - u[1] * v[0]};
-    const double len = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
-    const double h = (c[0] * lat[k][0] + c[1] * lat[k][1] + c[2] * lat[k][2]) / len;
-    rep[k] = pbc[k] ? (int)std::fabs(rc / h) + 1 : 0;
-  }
-  tau.clear();
-  for (int a = -rep[0]; a <= rep[0]; ++a)
-    for (int b = -rep[1]; b <= rep[1]; ++b)
-      for (int c = -rep[2]; c <= rep[2]; ++c)
-        for (int d = 0; d < 3; ++d)
-          tau.push_back((float)(lat[0][d] * a + lat[1][d] * b + lat[2][d] * c));
-  t0 = (rep[0] * (2 * rep[1] + 1) + rep[1]) * (2 * rep[2] + 1) + rep[2];
+  int R[3];
+  for (int k = 0; k < 3; ++k) R[k] = pbc[k] ? (int)std::floor(rc / binh[k]) + 1 : 0;
+  std::vector<int> off;
+  for (int a = -R[0]; a <= R[0]; ++a)
+    for (int b = -R[1]; b <= R[1]; ++b)
+      for (int c = -R[2]; c <= R[2]; ++c) {
+        off.push_back(a);
+        off.push_back(b);
+        off.push_back(c);
+      }
+  return off;
 }
 }  // namespace
 
@@ -1639,46 +1636,113 @@ int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* ce
   inv[2][0] = (lat[1][0] * lat[2][1] - lat[1][1] * lat[2][0]) / det;
   inv[2][1] = (lat[0][1] * lat[2][0] - lat[0][0] * lat[2][1]) / det;
   inv[2][2] = (lat[0][0] * lat[1][1] - lat[0][1] * lat[1][0]) / det;
+  // wrap (load_atom_info :1182-1224) and bin along the lattice vectors
+  double hgt[3], binh[3];
+  int nb[3];
+  bool all_pbc = true;
+  for (int k = 0; k < 3; ++k) {
+    const double* u = lat[(k + 1) % 3];
+    const double* v = lat[(k + 2) % 3];
+    const double c[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2],
+                         u[0] * v[1] - u[1] * v[0]};
+    hgt[k] = std::fabs(c[0] * lat[k][0] + c[1] * lat[k][1] + c[2] * lat[k][2]) /
+           std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    nb[k] = pbc[k] ? std::max(1, (int)(hgt[k] / D3_BIN_BOHR)) : 1;
+    binh[k] = hgt[k] / nb[k];
+    all_pbc = all_pbc && pbc[k];
+  }
+  const int nbins = nb[0] * nb[1] * nb[2];
   std::vector<float> xw((size_t)n * 3);
+  std::vector<int> bin((size_t)n), cnt(nbins + 1, 0);
   for (int64_t i = 0; i < n; ++i) {
     double p[3], a[3];
+    int b[3];
     for (int d = 0; d < 3; ++d) p[d] = pos[3 * i + d] / D3_AU_TO_ANG;
     for (int k = 0; k < 3; ++k) {
       // row vector p = a . lat  ->  a = p . inv
       a[k] = p[0] * inv[0][k] + p[1] * inv[1][k] + p[2] * inv[2][k];
       if (pbc[k]) a[k] -= std::floor(a[k]);
+      b[k] = pbc[k] ? std::min(nb[k] - 1, std::max(0, (int)(a[k] * nb[k]))) : 0;
     }
     for (int d = 0; d < 3; ++d)
       xw[3 * i + d] = (float)(a[0] * lat[0][d] + a[1] * lat[1][d] + a[2] * lat[2][d]);
+    bin[i] = (b[0] * nb[1] + b[1]) * nb[2] + b[2];
+    ++cnt[bin[i] + 1];
   }
-  std::vector<float> tv, tc;
-  int t0v, t0c;
-  d3_images(lat, h->p.rthr, pbc, tv, t0v);
-  d3_images(lat, h->p.cn_thr, pbc, tc, t0c);
+  for (int b = 0; b < nbins; ++b) cnt[b + 1] += cnt[b];
+  // counting sort by bin (stable: ascending atom id inside a bin)
+  std::vector<int> perm((size_t)n), fill(cnt.begin(), cnt.end() - 1);
+  for (int64_t i = 0; i < n; ++i) perm[fill[bin[i]]++] = (int)i;
+  std::vector<float> xs((size_t)n * 4);
+  std::vector<int> ts((size_t)n), bs((size_t)n);
+  for (int64_t s2 = 0; s2 < n; ++s2) {
+    const int i = perm[s2];
+    for (int d = 0; d < 3; ++d) xs[4 * s2 + d] = xw[3 * i + d];
+    std::memcpy(&xs[4 * s2 + 3], &type[i], 4);   // type bits in .w
+    ts[s2] = type[i];
+    bs[s2] = bin[i];
+  }
+  const std::vector<int> ov = d3_stencil(h->p.rthr, binh, pbc);
+  const std::vector<int> oc = d3_stencil(h->p.cn_thr, binh, pbc);
+  // half of the longest bin diagonal
+  double hd = 0.0;
+  for (int sa = -1; sa <= 1; sa += 2)
+    for (int sb = -1; sb <= 1; sb += 2) {
+      double d[3];
+      for (int c = 0; c < 3; ++c)
+        d[c] = lat[0][c] / nb[0] + sa * lat[1][c] / nb[1] + sb * lat[2][c] / nb[2];
+      hd = std::max(hd, 0.5 * std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]));
+    }
   HIPCHK(hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
   const size_t nn = (size_t)std::max<int64_t>(n, 1);
-  HIPCHK(h->x.ensure(nn * 12));
+  const bool use_tab = n <= D3_C6TAB_MAX;
+  HIPCHK(h->x.ensure(nn * 16));
   HIPCHK(h->type.ensure(nn * 4));
-  HIPCHK(h->tau_v.ensure(tv.size() * 4));
-  HIPCHK(h->tau_c.ensure(tc.size() * 4));
+  HIPCHK(h->bin_of.ensure(nn * 4));
+  HIPCHK(h->bin_start.ensure((nbins + 1) * 4));
+  HIPCHK(h->off_v.ensure(ov.size() * 4));
+  HIPCHK(h->off_c.ensure(oc.size() * 4));
   HIPCHK(h->cn.ensure(nn * 8));
+  if (use_tab) HIPCHK(h->c6tab.ensure(nn * nn * 8));
   HIPCHK(h->rows.ensure(nn * 64));
   HIPCHK(h->forces.ensure(nn * 24));
   HIPCHK(h->totals.ensure(7 * 8));
   if (n > 0) {
-    HIPCHK(hipMemcpyAsync(h->x.p, xw.data(), n * 12, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(h->type.p, type, n * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->x.p, xs.data(), n * 16, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->type.p, ts.data(), n * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->bin_of.p, bs.data(), n * 4, hipMemcpyHostToDevice, s));
   }
-  HIPCHK(hipMemcpyAsync(h->tau_v.p, tv.data(), tv.size() * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(h->tau_c.p, tc.data(), tc.size() * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(launch_d3(h->p, (int)n, h->x.f(), h->type.i(), h->tau_v.f(), (int)(tv.size() / 3), t0v,
-                   h->tau_c.f(), (int)(tc.size() / 3), t0c, (double*)h->cn.p, (double*)h->rows.p,
+  HIPCHK(hipMemcpyAsync(h->bin_start.p, cnt.data(), (nbins + 1) * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(h->off_v.p, ov.data(), ov.size() * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(h->off_c.p, oc.data(), oc.size() * 4, hipMemcpyHostToDevice, s));
+  D3Grid g{};
+  for (int k = 0; k < 3; ++k) {
+    g.nb[k] = nb[k];
+    g.inv_nb[k] = (float)(1.0 / nb[k]);
+  }
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) g.lat[3 * r + c] = (float)lat[r][c];
+  g.cull = all_pbc ? 1 : 0;
+  const double rv = std::sqrt((double)h->p.rthr) + hd, rcn = std::sqrt((double)h->p.cn_thr) + hd;
+  g.cull2_vdw = (float)(rv * rv * (1.0 + 1e-5));
+  g.cull2_cn = (float)(rcn * rcn * (1.0 + 1e-5));
+  g.bin_of = h->bin_of.i();
+  g.bin_start = h->bin_start.i();
+  g.off_vdw = h->off_v.i();
+  g.off_cn = h->off_c.i();
+  g.n_off_vdw = (int)(ov.size() / 3);
+  g.n_off_cn = (int)(oc.size() / 3);
+  HIPCHK(launch_d3(h->p, g, (int)n, (const float4*)h->x.p, h->type.i(), (double*)h->cn.p,
+                   use_tab ? (float2*)h->c6tab.p : nullptr, (double*)h->rows.p,
                    (double*)h->forces.p, (double*)h->totals.p, s));
   double tot[7];
+  std::vector<double> fs((size_t)n * 3);
   HIPCHK(hipMemcpyAsync(tot, h->totals.p, 7 * 8, hipMemcpyDeviceToHost, s));
-  if (n > 0) HIPCHK(hipMemcpyAsync(forces, h->forces.p, n * 24, hipMemcpyDeviceToHost, s));
+  if (n > 0) HIPCHK(hipMemcpyAsync(fs.data(), h->forces.p, n * 24, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  for (int64_t s2 = 0; s2 < n; ++s2)
+    for (int d = 0; d < 3; ++d) forces[3 * perm[s2] + d] = fs[3 * s2 + d];
   *energy = tot[0];
   for (int k = 0; k < 6; ++k) virial6[k] = tot[1 + k];
   return E3GNN_OK;

@@ -20,12 +20,27 @@ struct D3Params {
   const float* c6ab;    // [nt, nt, 5, 5, 3] (C6, CN_ref_i, CN_ref_j)
 };
 
-// cn [n], rows [n x 8] scratch; forces [n x 3] (eV/A) and totals [7]
-// (energy eV, virial xx,yy,zz,xy,xz,yz eV) out.  x [n x 3] bohr wrapped into
-// the cell, tau_* [nt x 3] bohr translations, t0_* the index of the zero one.
-hipError_t launch_d3(const D3Params& p, int n, const float* x, const int* type,
-                     const float* tau_vdw, int nt_vdw, int t0_vdw, const float* tau_cn, int nt_cn,
-                     int t0_cn, double* cn, double* rows, double* forces, double* totals,
+// Atoms binned along the lattice vectors (host-sorted by bin) and the
+// stencils of bin offsets that cover each cutoff sphere.
+struct D3Grid {
+  int nb[3];               // bins per lattice vector (1 on a non-periodic axis)
+  float inv_nb[3];
+  float lat[9];            // lattice rows a, b, c (bohr)
+  int cull;                // skip cells whose centre is beyond rc + half diagonal
+  float cull2_vdw, cull2_cn;
+  const int* bin_of;       // [n] bin of each (sorted) atom
+  const int* bin_start;    // [nbins + 1]
+  const int* off_vdw;      // [n_off_vdw][3] bin offsets
+  const int* off_cn;
+  int n_off_vdw, n_off_cn;
+};
+
+// x [n] (x, y, z bohr wrapped, type as int bits; bin-sorted), type [n]; cn [n], rows [n x 8],
+// c6tab [n x n] (nullable: C6 per pair-image instead) scratch; forces
+// [n x 3] (eV/A, sorted order) and totals [7] (energy eV, virial
+// xx,yy,zz,xy,xz,yz eV) out.
+hipError_t launch_d3(const D3Params& p, const D3Grid& g, int n, const float4* x, const int* type,
+                     double* cn, float2* c6tab, double* rows, double* forces, double* totals,
                      hipStream_t s);
 
 }  // namespace e3gnn
