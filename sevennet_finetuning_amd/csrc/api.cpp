@@ -1696,7 +1696,9 @@ int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* ce
   HIPCHK(hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
   const size_t nn = (size_t)std::max<int64_t>(n, 1);
-  const bool use_tab = n <= D3_C6TAB_MAX;
+  // E3GNN_D3_NO_C6TAB=1: the per-item C6 path of large systems (tests)
+  const char* no_tab = std::getenv("E3GNN_D3_NO_C6TAB");
+  const bool use_tab = n <= D3_C6TAB_MAX && !(no_tab && no_tab[0] == '1');
   HIPCHK(h->x.ensure(nn * 16));
   HIPCHK(h->type.ensure(nn * 4));
   HIPCHK(h->bin_of.ensure(nn * 4));

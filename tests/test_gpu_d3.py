@@ -120,3 +120,15 @@ def test_d3_calculator_stress_convention():
     v = ref['virial']
     want = -np.array([v[0], v[1], v[2], v[5], v[4], v[3]]) / abs(np.linalg.det(cell))
     assert np.allclose(res['stress'], want, atol=1e-5 * np.abs(want).max())
+
+
+def test_per_item_c6_path_matches_table_path(monkeypatch):
+    """Systems above 32,768 atoms evaluate C6 per pair-image instead of from
+    the n x n table; both paths give the same result."""
+    d = np.load(f'{GOLD}/hfo2_resdat.npz')
+    z = np.array([CHEMICAL_SYMBOLS.index(str(s)) for s in d['symbols']])
+    a, pair, types = _hip(d['pos'], d['cell'], z, 'damp_zero', 'pbe', rthr=3000.0)
+    monkeypatch.setenv('E3GNN_D3_NO_C6TAB', '1')
+    b = pair.compute(d['pos'], d['cell'], types)
+    assert abs(a['energy'] - b['energy']) <= 1e-6 * abs(a['energy'])
+    assert np.abs(a['forces'] - b['forces']).max() <= 1e-6 * np.abs(a['forces']).max() + 1e-9
