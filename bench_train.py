@@ -58,7 +58,7 @@ def cpu_baseline(batches, cfg, seconds):
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get('OMP_NUM_THREADS', '16')))
     torch.set_num_threads(threads)
     model = SevenNetTrainable(device='cpu', conv_backend=CpuConvBackend())
-    c = dict(cfg, device='cpu', is_ddp=False)
+    c = dict(cfg, device='cpu', is_ddp=False, hip_graph=False)
     c['continue'] = dict(cfg['continue'],
                          fisher_information={k: v.cpu() for k, v in
                                              cfg['continue']['fisher_information'].items()},
@@ -86,6 +86,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--eager', action='store_true',
+                    help='no HIP-graph capture of the step (always eager for N > 1)')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     args = ap.parse_args()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -106,6 +108,7 @@ def main():
            'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
            'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
            'scheduler_param': {'gamma': 0.99}, 'is_ddp': world > 1, 'device': device,
+           'hip_graph': world == 1 and not args.eager,
            'continue': {'fisher_information': fisher, 'opt_params': opt, 'ewc_lambda': 1e5}}
     tr = train.Trainer(model, cfg)
     n_b = 4
@@ -155,7 +158,8 @@ def main():
                                    f'({atoms_per_step} atoms), force+stress+energy Huber + EWC, '
                                    'Adam, grad all-reduce',
                        'atoms_per_rank_step': atoms_per_step, 'edges_per_batch': edges,
-                       'parallelism': f'dp{world}'},
+                       'parallelism': f'dp{world}',
+                       'hip_graph': bool(tr.hip_graph)},
             'atoms_per_s': round(atoms_per_step * world * args.steps / dt, 1),
             'loss': float(loss), 'mem_loss': float(mloss), 'cpu_baseline': cpu}), flush=True)
     if world > 1:

@@ -47,6 +47,14 @@ class ConvGraph:
         self.backend = backend
         self.aux = backend.build(self)
 
+    def rebuild(self, edge_center, edge_nbr):
+        """Same sizes, new edges, into the SAME device buffers (a captured HIP
+        graph keeps reading them): the per-step update of a graphed step."""
+        if int(edge_center.shape[0]) != self.n_edges:
+            raise ValueError('rebuild needs the same edge count')
+        self.edge_center, self.edge_nbr = edge_center, edge_nbr
+        self.backend.build(self, into=self.aux)
+
 
 class HipConvBackend:
     """The kernels of libe3gnn_hip.so (include/e3gnn.h, training ops)."""
@@ -63,22 +71,26 @@ class HipConvBackend:
     def _stream(t):
         return torch.cuda.current_stream(t.device).cuda_stream
 
-    def build(self, g):
+    def build(self, g, into=None):
         dev = g.edge_center.device
         if dev.type != 'cuda':
             raise _lib.E3GNNError(f'the HIP conv op needs device tensors, got {dev}')
         n, E = g.n_nodes, g.n_edges
-        ce = g.edge_center.to(torch.int32).contiguous()
-        nb = g.edge_nbr.to(torch.int32).contiguous()
-        aux = {'center': ce, 'nbr': nb,
-               'row_ptr': torch.empty(n + 1, dtype=torch.int32, device=dev),
-               'src_ptr': torch.empty(n + 1, dtype=torch.int32, device=dev),
-               'src_perm': torch.empty(max(E, 1), dtype=torch.int32, device=dev)}
-        scratch = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        if into is None:
+            aux = {'center': g.edge_center.to(torch.int32).contiguous(),
+                   'nbr': g.edge_nbr.to(torch.int32).contiguous(),
+                   'row_ptr': torch.empty(n + 1, dtype=torch.int32, device=dev),
+                   'src_ptr': torch.empty(n + 1, dtype=torch.int32, device=dev),
+                   'src_perm': torch.empty(max(E, 1), dtype=torch.int32, device=dev),
+                   'scratch': torch.empty(n + 1, dtype=torch.int32, device=dev)}
+        else:
+            aux = into
+            aux['center'].copy_(g.edge_center)
+            aux['nbr'].copy_(g.edge_nbr)
         _lib.check(self.lib.e3gnn_conv_graph(
-            n, E, ce.data_ptr(), nb.data_ptr(), aux['row_ptr'].data_ptr(),
-            aux['src_ptr'].data_ptr(), aux['src_perm'].data_ptr(), scratch.data_ptr(),
-            self._stream(ce)))
+            n, E, aux['center'].data_ptr(), aux['nbr'].data_ptr(), aux['row_ptr'].data_ptr(),
+            aux['src_ptr'].data_ptr(), aux['src_perm'].data_ptr(), aux['scratch'].data_ptr(),
+            self._stream(aux['center'])))
         return aux
 
     def _check(self, kind, g, h, Y, w):

@@ -307,7 +307,7 @@ class SevenNetTrainable(torch.nn.Module):
         return bessel * env.unsqueeze(-1)
 
     # ------------------------------------------------------------ forward
-    def forward(self, data):
+    def forward(self, data, graph=None):
         """AtomGraphSequential.forward on a batched AtomGraphData dict:
         ``x`` (type index), ``edge_index``, ``edge_vec``, ``batch``,
         ``num_atoms``, ``cell_volume`` -> adds ``atomic_energy``,
@@ -324,10 +324,11 @@ class SevenNetTrainable(torch.nn.Module):
             torch.zeros(n, dtype=torch.long, device=dev)
         center, nbr = ei[0], ei[1]
         vec_k = vec
-        if center.numel() > 1 and bool((center[1:] < center[:-1]).any()):
-            perm = torch.argsort(center, stable=True)
-            center, nbr, vec_k = center[perm], nbr[perm], vec[perm]
-        graph = conv_ops.ConvGraph(n, center, nbr, self.conv_backend)
+        if graph is None:
+            if center.numel() > 1 and bool((center[1:] < center[:-1]).any()):
+                perm = torch.argsort(center, stable=True)
+                center, nbr, vec_k = center[perm], nbr[perm], vec[perm]
+            graph = conv_ops.ConvGraph(n, center, nbr, self.conv_backend)
 
         r = torch.linalg.norm(vec_k, dim=-1)
         emb = self._edge_basis(r)

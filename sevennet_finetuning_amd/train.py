@@ -38,6 +38,7 @@ CONTINUE, FISHER, OPT_PARAMS, EWC_LAMBDA = 'continue', 'fisher_information', 'op
 LOAD_DATASET_WITH_WEIGHTS, DATA_WEIGHT = 'load_dataset_with_weights', 'data_weight'
 PER_ATOM_ENERGY = 'per_atom_energy'
 IS_DDP, LOCAL_RANK = 'is_ddp', 'local_rank'
+HIP_GRAPH = 'hip_graph'
 
 
 # ------------------------------------------------------------------ losses
@@ -73,11 +74,24 @@ class LossDefinition:
     def _get_data_weight(self, batch_data):
         return torch.repeat_interleave(batch_data[DATA_WEIGHT][self.weight_key], self.vdim)
 
+    # static = True: no data-dependent shapes (the HIP-graph-captured step):
+    # unlabeled entries get ref := pred (zero loss, zero gradient) and the mean
+    # is rescaled from all entries to the labelled ones -- the same value as
+    # dropping them, without a host round trip
+    static = False
+
     def get_loss(self, batch_data, model=None):
         if self.criterion is None:
             raise NotImplementedError('LossDefinition has no criterion.')
         pred, ref = self._preprocess(batch_data, model)
         weights = self._get_data_weight(batch_data) if self.use_weight else None
+        if self.delete_unlabeled and self.static:
+            keep = ~torch.isnan(ref)
+            ref = torch.where(keep, ref, pred.detach())
+            scale = ref.numel() / keep.sum().clamp_min(1).to(pred.dtype)
+            if self.use_weight:
+                return torch.mean(self.criterion(pred, ref) * weights) * scale
+            return self.criterion(pred, ref) * scale
         if self.delete_unlabeled:
             keep = ~torch.isnan(ref)
             pred, ref = pred[keep], ref[keep]
@@ -228,6 +242,14 @@ def get_loss_functions_from_config(config):
 
 
 # ------------------------------------------------------------------ schedulers
+def _set_lr(group, lr):
+    """in place for a tensor lr (a captured optimizer step reads its memory)"""
+    if torch.is_tensor(group['lr']):
+        group['lr'].fill_(float(lr))
+    else:
+        group['lr'] = lr
+
+
 class CosineAnnealingWarmupRestarts(torch.optim.lr_scheduler.LRScheduler):
     """Restatement of the ``cosine_annealing_warmup`` package's scheduler
     (katsura-jp/pytorch-cosine-annealing-with-warmup, unpinned VCS dependency,
@@ -252,7 +274,7 @@ class CosineAnnealingWarmupRestarts(torch.optim.lr_scheduler.LRScheduler):
         super().__init__(optimizer, last_epoch)
         self.base_lrs = []
         for g in self.optimizer.param_groups:
-            g['lr'] = self.min_lr
+            _set_lr(g, self.min_lr)
             self.base_lrs.append(self.min_lr)
 
     def get_lr(self):
@@ -294,7 +316,7 @@ class CosineAnnealingWarmupRestarts(torch.optim.lr_scheduler.LRScheduler):
         self.max_lr = self.base_max_lr * (self.gamma ** self.cycle)
         self.last_epoch = math.floor(epoch)
         for g, lr in zip(self.optimizer.param_groups, self.get_lr()):
-            g['lr'] = lr
+            _set_lr(g, lr)
 
 
 _S = torch.optim.lr_scheduler
@@ -408,13 +430,26 @@ class Trainer:
             self.world = 1
         params = [p for p in self.model.parameters() if p.requires_grad]
         opt = optim_dict[config[OPTIMIZER].lower()]
-        self.optimizer = opt(params, **config.get(OPTIM_PARAM, {}))
+        optim_param = dict(config.get(OPTIM_PARAM, {}))
+        # HIP_GRAPH (this build): replay the rehearsal step as one captured HIP
+        # graph per batch-shape signature (single process); the optimizer then
+        # keeps its step count and lr on the device
+        self.hip_graph = bool(config.get(HIP_GRAPH, False)) and not self.distributed
+        if self.hip_graph:
+            if config[OPTIMIZER].lower() not in ('adam', 'adamw'):
+                raise ValueError('hip_graph supports the adam/adamw optimizers')
+            optim_param['capturable'] = True
+            optim_param['lr'] = torch.tensor(float(optim_param.get('lr', 1e-3)),
+                                             device=self.device)
+        self.optimizer = opt(params, **optim_param)
         sch = scheduler_dict[config[SCHEDULER].lower()]
         self.scheduler = sch(self.optimizer, **config.get(SCHEDULER_PARAM, {}))
         self.loss_functions = get_loss_functions_from_config(config)
         for loss_def, _ in self.loss_functions:
             if isinstance(loss_def, EWCLoss) and loss_def.device is None:
                 loss_def.to(self.device)
+            loss_def.static = self.hip_graph
+        self._graphed = GraphedRehearsalStep(self) if self.hip_graph else None
 
     # ---- the pieces of one step
     def zero_grad(self):
@@ -447,12 +482,17 @@ class Trainer:
         """One iteration of RehearsalTrainer.run_one_epoch_rehearsal
         (trainer.py:174-206): zero_grad once, backward+step on the new batch,
         then backward (accumulating) + step on the memory batch."""
+        if self._graphed is not None:
+            return self._graphed(batch, batch_mem)
+        return self._rehearsal_body(batch, batch_mem)
+
+    def _rehearsal_body(self, batch, batch_mem, graphs=(None, None)):
         self.zero_grad()
-        output = self.model(batch)
+        output = self.model(batch, graph=graphs[0])
         loss = self.total_loss(output)
         self.backward(loss)
         self.optimizer.step()
-        memout = self.model(batch_mem)
+        memout = self.model(batch_mem, graph=graphs[1])
         mem_loss = self.total_loss(memout)
         self.backward(mem_loss)
         self.optimizer.step()
@@ -519,6 +559,91 @@ class Trainer:
             fisher[n] /= cnt
         opt = {n: p.data.detach().clone() for n, p in self.model.named_parameters()}
         return fisher, opt, cnt
+
+
+class GraphedRehearsalStep:
+    """The rehearsal step as ONE captured HIP graph per batch-shape signature
+    (launch-bound at the reference's batch sizes: ~8k kernels per step).
+
+    Per call: the batch tensors are copied into the graph's static inputs, the
+    two edge CSRs are rebuilt in place (e3gnn_conv_graph, which also validates
+    the graph), and the graph is replayed.  A new signature is captured after
+    two eager warm-up steps on a side stream; the warm-ups' parameter and
+    optimizer updates are rolled back, so the trajectory equals the eager
+    step's.  Everything inside is device-side: the model takes the prebuilt
+    ConvGraphs, the losses run in static mode, the optimizer is capturable."""
+
+    def __init__(self, trainer):
+        self.tr = trainer
+        self.cache = {}
+
+    @staticmethod
+    def _sig(b):
+        return tuple((k, tuple(v.shape), str(v.dtype)) for k, v in sorted(b.items())
+                     if torch.is_tensor(v))
+
+    def _graph_of(self, b):
+        from . import conv_ops
+        ei = b[KEY.EDGE_IDX]
+        n = int(b[KEY.NODE_FEATURE].shape[0])
+        return conv_ops.ConvGraph(n, ei[0], ei[1], self.tr.model.conv_backend)
+
+    def _state(self):
+        opt = self.tr.optimizer
+        st = {id(p): {k: (v.clone() if torch.is_tensor(v) else v) for k, v in s.items()}
+              for p, s in opt.state.items()}
+        return self.tr.model.flat.detach().clone(), st
+
+    def _restore(self, snap):
+        flat, st = snap
+        with torch.no_grad():
+            self.tr.model.flat.copy_(flat)
+        for p, s in self.tr.optimizer.state.items():
+            for k, v in st.get(id(p), {}).items():
+                if torch.is_tensor(s.get(k)):
+                    s[k].copy_(v)
+
+    def _capture(self, batch, mem):
+        tr = self.tr
+        sb = {k: v.clone() for k, v in batch.items()}
+        sm = {k: v.clone() for k, v in mem.items()}
+        graphs = (self._graph_of(sb), self._graph_of(sm))
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            first = not tr.optimizer.state
+            if first:   # create the optimizer state, then undo the update
+                snap0 = tr.model.flat.detach().clone()
+                tr._rehearsal_body(sb, sm, graphs)
+                with torch.no_grad():
+                    tr.model.flat.copy_(snap0)
+                for s in tr.optimizer.state.values():
+                    for v in s.values():
+                        if torch.is_tensor(v):
+                            v.zero_()
+            snap = self._state()
+            for _ in range(2):
+                tr._rehearsal_body(sb, sm, graphs)
+            self._restore(snap)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss, mloss = tr._rehearsal_body(sb, sm, graphs)
+        return {'g': g, 'b': sb, 'm': sm, 'graphs': graphs, 'out': (loss, mloss)}
+
+    def __call__(self, batch, mem):
+        key = (self._sig(batch), self._sig(mem))
+        ent = self.cache.get(key)
+        if ent is None:
+            ent = self.cache[key] = self._capture(batch, mem)
+        for dst, src in ((ent['b'], batch), (ent['m'], mem)):
+            for k, v in src.items():
+                if torch.is_tensor(v):
+                    dst[k].copy_(v, non_blocking=True)
+        for gr, b in zip(ent['graphs'], (ent['b'], ent['m'])):
+            gr.rebuild(b[KEY.EDGE_IDX][0], b[KEY.EDGE_IDX][1])
+        ent['g'].replay()
+        return ent['out'][0].detach().clone(), ent['out'][1].detach().clone()
 
 
 def setup_distributed(backend=None):

@@ -27,8 +27,8 @@ class CpuConvBackend:
             self.dims[kind] = (dx, sum(i[3] for i in ins), sum(m * (2 * l + 1) for m, l in mid))
             self.tables[kind] = (irr, ins, perm)
 
-    def build(self, g):
-        return {}
+    def build(self, g, into=None):
+        return {} if into is None else into
 
     def forward(self, kind, g, h, Y, w):
         irr, ins, perm = self.tables[kind]

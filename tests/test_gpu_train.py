@@ -194,3 +194,38 @@ def test_rehearsal_ewc_steps_reduce_loss(models):
     m.train(False)
     assert after < before
     assert float(ewc.get_loss({}, m)) > 0.0
+
+
+def test_graphed_rehearsal_step_equals_eager():
+    """The HIP-graph-captured rehearsal step (train.GraphedRehearsalStep)
+    reproduces the eager step: same parameters after three steps on changing
+    batches of one shape, and a new shape is captured separately."""
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+
+    def run(graph, batches):
+        m = SevenNetTrainable(device=DEV)
+        fisher = {n: torch.full_like(p, 1e-3) for n, p in m.named_parameters()}
+        opt = {n: p.detach().clone() for n, p in m.named_parameters()}
+        cfg = {'loss': 'huber', 'loss_param': {'delta': 0.01}, 'force_loss_weight': 1.0,
+               'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
+               'optim_param': {'lr': 1e-4}, 'scheduler': 'exponentiallr',
+               'scheduler_param': {'gamma': 0.99}, 'device': DEV, 'hip_graph': graph,
+               'continue': {'fisher_information': fisher, 'opt_params': opt,
+                            'ewc_lambda': 1e2}}
+        tr = train.Trainer(m, cfg)
+        m.train(True)
+        losses = [tuple(float(x) for x in tr.rehearsal_step(b, mm)) for b, mm in batches]
+        return m.flat.detach().double().cpu(), losses, tr
+
+    def coll(seeds, cells=(3, 3, 3)):
+        return train.collate(_batch(seeds, cells), device=DEV, dtype=torch.float32)
+    batches = [(coll([1, 2]), coll([3])), (coll([4, 5]), coll([6])), (coll([7, 8]), coll([9])),
+               (coll([10], (2, 2, 2)), coll([11]))]
+    # one label NaN: the static (masked) loss drops it like the eager one
+    batches[1][0][KEY.FORCE][3, 1] = float('nan')
+    fe, le, _ = run(False, batches)
+    fg, lg, tr = run(True, batches)
+    assert len(tr._graphed.cache) == 2
+    for a, b in zip(le, lg):
+        assert abs(a[0] - b[0]) <= 1e-5 * abs(a[0]) and abs(a[1] - b[1]) <= 1e-5 * abs(a[1])
+    assert float((fe - fg).abs().max()) <= 1e-6 * float(fe.abs().max())
