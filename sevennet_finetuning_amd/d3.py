@@ -157,9 +157,9 @@ class PairD3:
 
 
 class D3Calculator:
-    """ASE-style calculator over PairD3 (results: energy, free_energy,
-    energies is not available (D3 is not atom-decomposed here), forces,
-    stress = -virial / V in ASE order xx, yy, zz, yz, xz, xy)."""
+    """ASE-style calculator over PairD3.  Results: energy, free_energy,
+    forces and stress = -virial / V in ASE order (xx, yy, zz, yz, xz, xy);
+    no per-atom energies (the reference's pair style reports none either)."""
 
     implemented_properties = ['free_energy', 'energy', 'forces', 'stress']
 
