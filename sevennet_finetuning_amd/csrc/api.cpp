@@ -1587,7 +1587,7 @@ e3gnn_d3* e3gnn_d3_create(int device, int damping, const float* func, float rthr
 void e3gnn_d3_free(e3gnn_d3* h) { delete h; }
 
 namespace {
-constexpr double D3_BIN_BOHR = 20.0;     // target bin edge (~60 atoms per bin at solid density)
+constexpr double D3_BIN_BOHR = 30.0;     // bin edge: swept 12-40 bohr on 8k-atom Si, 30 best
 constexpr int64_t D3_C6TAB_MAX = 32768;  // n^2 C6 table up to 8.6 GB; beyond: C6 per item
 
 // stencil of bin offsets covering a sphere of radius sqrt(thr): R = floor(rc /
@@ -1637,6 +1637,9 @@ int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* ce
   inv[2][1] = (lat[0][1] * lat[2][0] - lat[0][0] * lat[2][1]) / det;
   inv[2][2] = (lat[0][0] * lat[1][1] - lat[0][1] * lat[1][0]) / det;
   // wrap (load_atom_info :1182-1224) and bin along the lattice vectors
+  // (E3GNN_D3_BIN: bin edge in bohr, for tuning)
+  const char* bin_env = std::getenv("E3GNN_D3_BIN");
+  const double bin_w = bin_env ? std::max(2.0, std::atof(bin_env)) : D3_BIN_BOHR;
   double hgt[3], binh[3];
   int nb[3];
   bool all_pbc = true;
@@ -1647,7 +1650,7 @@ int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* ce
                          u[0] * v[1] - u[1] * v[0]};
     hgt[k] = std::fabs(c[0] * lat[k][0] + c[1] * lat[k][1] + c[2] * lat[k][2]) /
            std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
-    nb[k] = pbc[k] ? std::max(1, (int)(hgt[k] / D3_BIN_BOHR)) : 1;
+    nb[k] = pbc[k] ? std::max(1, (int)(hgt[k] / bin_w)) : 1;
     binh[k] = hgt[k] / nb[k];
     all_pbc = all_pbc && pbc[k];
   }
