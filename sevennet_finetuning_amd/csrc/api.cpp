@@ -1525,8 +1525,8 @@ int64_t e3gnn_workspace_bytes(const e3gnn_ctx* c) {
 struct e3gnn_d3 {
   int device = 0;
   D3Params p{};
-  DBuf rcov, r2r4, r0ab, mxc, c6ab, x, type, bin_of, bin_start, off_v, off_c, cn, c6tab, rows,
-      forces, totals;
+  DBuf rcov, r2r4, r0ab, mxc, c6ab, cnref, x, type, bin_of, bin_start, off_v, off_c, cn, gw,
+      c6tab, rows, forces, totals;
 };
 
 e3gnn_d3* e3gnn_d3_create(int device, int damping, const float* func, float rthr, float cn_thr,
@@ -1581,6 +1581,33 @@ e3gnn_d3* e3gnn_d3_create(int device, int damping, const float* func, float rthr
   p.r0ab = h->r0ab.f();
   p.mxc = h->mxc.i();
   p.c6ab = h->c6ab.f();
+  // reference CN per (type, grid index), if the table is separable that way
+  // (Grimme's data is: a reference CN belongs to an element's reference)
+  std::vector<float> cr((size_t)ntypes * 5, 0.0f);
+  std::vector<int> seen((size_t)ntypes * 5, 0);
+  bool separable = true;
+  for (int a = 0; a < ntypes; ++a)
+    for (int b = 0; b < ntypes; ++b)
+      for (int ia = 0; ia < 5; ++ia)
+        for (int ib = 0; ib < 5; ++ib) {
+          const float* e = c6ab + ((((size_t)a * ntypes + b) * 5 + ia) * 5 + ib) * 3;
+          if (!(e[0] > 0.0f)) continue;
+          const int ka = a * 5 + ia, kb = b * 5 + ib;
+          if (seen[ka] && cr[ka] != e[1]) separable = false;
+          if (seen[kb] && cr[kb] != e[2]) separable = false;
+          cr[ka] = e[1];
+          cr[kb] = e[2];
+          seen[ka] = seen[kb] = 1;
+        }
+  p.cnref = nullptr;
+  if (separable) {
+    if (!up(h->cnref, cr.data(), cr.size() * 4)) {
+      delete h;
+      fail(E3GNN_ERR_HIP, "d3: table upload failed");
+      return nullptr;
+    }
+    p.cnref = h->cnref.f();
+  }
   return h;
 }
 
@@ -1710,6 +1737,7 @@ int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* ce
   HIPCHK(h->off_c.ensure(oc.size() * 4));
   HIPCHK(h->cn.ensure(nn * 8));
   if (use_tab) HIPCHK(h->c6tab.ensure(nn * nn * 8));
+  HIPCHK(h->gw.ensure(nn * 80));
   HIPCHK(h->rows.ensure(nn * 64));
   HIPCHK(h->forces.ensure(nn * 24));
   HIPCHK(h->totals.ensure(7 * 8));
@@ -1739,7 +1767,7 @@ int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* ce
   g.n_off_vdw = (int)(ov.size() / 3);
   g.n_off_cn = (int)(oc.size() / 3);
   HIPCHK(launch_d3(h->p, g, (int)n, (const float4*)h->x.p, h->type.i(), (double*)h->cn.p,
-                   use_tab ? (float2*)h->c6tab.p : nullptr, (double*)h->rows.p,
+                   (double*)h->gw.p, use_tab ? (float2*)h->c6tab.p : nullptr, (double*)h->rows.p,
                    (double*)h->forces.p, (double*)h->totals.p, s));
   double tot[7];
   std::vector<double> fs((size_t)n * 3);

@@ -18,6 +18,9 @@ struct D3Params {
   const float* r0ab;    // [nt, nt] bohr
   const int* mxc;       // [nt]
   const float* c6ab;    // [nt, nt, 5, 5, 3] (C6, CN_ref_i, CN_ref_j)
+  const float* cnref;   // [nt, 5] reference CN of (type, grid index), or null when the
+                        // table's reference CNs are not per (element, index) (never for
+                        // Grimme's data; checked at create)
 };
 
 // Atoms binned along the lattice vectors (host-sorted by bin) and the
@@ -39,8 +42,9 @@ struct D3Grid {
 // c6tab [n x n] (nullable: C6 per pair-image instead) scratch; forces
 // [n x 3] (eV/A, sorted order) and totals [7] (energy eV, virial
 // xx,yy,zz,xy,xz,yz eV) out.
+// gw [n x 10] scratch (Gaussian factors, separable path)
 hipError_t launch_d3(const D3Params& p, const D3Grid& g, int n, const float4* x, const int* type,
-                     double* cn, float2* c6tab, double* rows, double* forces, double* totals,
-                     hipStream_t s);
+                     double* cn, double* gw, float2* c6tab, double* rows, double* forces,
+                     double* totals, hipStream_t s);
 
 }  // namespace e3gnn

@@ -150,10 +150,35 @@ __device__ void c6_pair(const D3Params& p, int ti, int tj, float cni, float cnj,
   }
 }
 
+// The Gaussian weight of reference (a, b) is separable:
+//   exp(K3 ((CNref_a - CN_i)^2 + (CNref_b - CN_j)^2)) = g_ia g_jb,
+// because a reference CN belongs to (element, grid index) in the D3 data.  So
+// each atom's factors g_ia and dg_ia/dCN_i are computed once (5 fp64 exps per
+// atom) and a pair costs 25 fp64 multiply-adds instead of 25 fp64 exps.
+__global__ __launch_bounds__(BLK) void k_d3_gauss(D3Params p, int n, const int* __restrict__ type,
+                                                   const double* __restrict__ cn,
+                                                   double* __restrict__ gw) {
+  const int i = blockIdx.x * BLK + threadIdx.x;
+  if (i >= n) return;
+  const int ti = type[i];
+  const float cni = (float)cn[i];
+  for (int a = 0; a < MAXC; ++a) {
+    double g = 0.0, dg = 0.0;
+    if (a < p.mxc[ti]) {
+      const float d = p.cnref[ti * MAXC + a] - cni;
+      g = exp((double)K3 * (double)(d * d));
+      dg = g * (2.0 * K3) * (double)(-d);
+    }
+    gw[(size_t)i * 10 + a] = g;
+    gw[(size_t)i * 10 + 5 + a] = dg;
+  }
+}
+
 // (C6_ij, dC6_ij/dCN_i) for every ordered pair from one evaluation per
 // unordered pair (i >= j, the reference's linear triangle index, :71-74)
 __global__ __launch_bounds__(BLK) void k_d3_c6tab(D3Params p, int n, const int* __restrict__ type,
                                                    const double* __restrict__ cn,
+                                                   const double* __restrict__ gw,
                                                    float2* __restrict__ tab) {
   const int64_t npair = (int64_t)n * (n + 1) / 2;
   const int64_t k = (int64_t)blockIdx.x * BLK + threadIdx.x;
@@ -162,10 +187,108 @@ __global__ __launch_bounds__(BLK) void k_d3_c6tab(D3Params p, int n, const int* 
   while ((int64_t)i * (i + 1) / 2 > k) --i;
   while ((int64_t)(i + 1) * (i + 2) / 2 <= k) ++i;
   const int j = (int)(k - (int64_t)i * (i + 1) / 2);
+  const int ti = type[i], tj = type[j];
   float c6, dci, dcj;
-  c6_pair(p, type[i], type[j], (float)cn[i], (float)cn[j], c6, dci, dcj);
+  if (gw) {
+    const double* gi = gw + (size_t)i * 10;
+    const double* gj = gw + (size_t)j * 10;
+    const float* t = p.c6ab + ((size_t)ti * p.ntypes + tj) * (MAXC * MAXC * 3);
+    const int ma = p.mxc[ti], mb = p.mxc[tj];
+    double num = 0.0, den = 0.0, dni = 0.0, ddi = 0.0, dnj = 0.0, ddj = 0.0;
+    for (int a = 0; a < ma; ++a) {
+      double rn = 0.0, rd = 0.0, rnj = 0.0, rdj = 0.0;   // sums over b
+      for (int b = 0; b < mb; ++b) {
+        const float ref = t[(a * MAXC + b) * 3];
+        if (ref > 0.0f) {
+          rn = fma((double)ref, gj[b], rn);
+          rd += gj[b];
+          rnj = fma((double)ref, gj[5 + b], rnj);
+          rdj += gj[5 + b];
+        }
+      }
+      num = fma(gi[a], rn, num);
+      den = fma(gi[a], rd, den);
+      dni = fma(gi[5 + a], rn, dni);
+      ddi = fma(gi[5 + a], rd, ddi);
+      dnj = fma(gi[a], rnj, dnj);
+      ddj = fma(gi[a], rdj, ddj);
+    }
+    if (den > 1e-99) {
+      const double r = 1.0 / den, u = num * r;
+      c6 = (float)u;
+      dci = (float)(r * fma(u, -ddi, dni));
+      dcj = (float)(r * fma(u, -ddj, dnj));
+    } else {   // all weights underflow: the reference's nearest-reference value
+      c6_pair(p, ti, tj, (float)cn[i], (float)cn[j], c6, dci, dcj);
+    }
+  } else {
+    c6_pair(p, ti, tj, (float)cn[i], (float)cn[j], c6, dci, dcj);
+  }
   tab[(size_t)i * n + j] = make_float2(c6, dci);
   tab[(size_t)j * n + i] = make_float2(c6, dcj);
+}
+
+// Separable path: row i = one workgroup, coalesced row writes, ordered pairs
+// (25 fp64 multiply-adds each; only dC6/dCN_i is needed per ordered pair)
+__global__ __launch_bounds__(BLK) void k_d3_c6rows(D3Params p, int n, const int* __restrict__ type,
+                                                    const double* __restrict__ cn,
+                                                    const double* __restrict__ gw,
+                                                    float2* __restrict__ tab) {
+  // this row's reference C6 grids against every partner type, in LDS
+  constexpr int MAXT_LDS = 64;
+  __shared__ float s_ref[MAXT_LDS * MAXC * MAXC];
+  const int i = blockIdx.x;
+  const int ti = type[i], ma = p.mxc[ti];
+  const bool lds = p.ntypes <= MAXT_LDS;
+  if (lds)
+    for (int k = threadIdx.x; k < p.ntypes * MAXC * MAXC; k += BLK) {
+      const int tj = k / (MAXC * MAXC), ab = k - tj * (MAXC * MAXC);
+      s_ref[k] = p.c6ab[(((size_t)ti * p.ntypes + tj) * (MAXC * MAXC) + ab) * 3];
+    }
+  __syncthreads();
+  double gi[MAXC], dgi[MAXC];
+#pragma unroll
+  for (int a = 0; a < MAXC; ++a) {
+    gi[a] = gw[(size_t)i * 10 + a];
+    dgi[a] = gw[(size_t)i * 10 + 5 + a];
+  }
+  for (int j = threadIdx.x; j < n; j += BLK) {
+    const int tj = type[j], mb = p.mxc[tj];
+    double gj[MAXC];
+#pragma unroll
+    for (int b = 0; b < MAXC; ++b) gj[b] = gw[(size_t)j * 10 + b];
+    double num = 0.0, den = 0.0, dni = 0.0, ddi = 0.0;
+#pragma unroll
+    for (int a = 0; a < MAXC; ++a) {
+      if (a < ma) {
+        double rn = 0.0, rd = 0.0;
+#pragma unroll
+        for (int b = 0; b < MAXC; ++b) {
+          const float ref = lds ? s_ref[(tj * MAXC + a) * MAXC + b]
+                                : p.c6ab[(((size_t)ti * p.ntypes + tj) * (MAXC * MAXC) +
+                                          a * MAXC + b) * 3];
+          if (b < mb && ref > 0.0f) {
+            rn = fma((double)ref, gj[b], rn);
+            rd += gj[b];
+          }
+        }
+        num = fma(gi[a], rn, num);
+        den = fma(gi[a], rd, den);
+        dni = fma(dgi[a], rn, dni);
+        ddi = fma(dgi[a], rd, ddi);
+      }
+    }
+    float c6, dci;
+    if (den > 1e-99) {
+      const double r = 1.0 / den, u = num * r;
+      c6 = (float)u;
+      dci = (float)(r * fma(u, -ddi, dni));
+    } else {   // all weights underflow: the reference's nearest-reference value
+      float dcj;
+      c6_pair(p, ti, tj, (float)cn[i], (float)cn[j], c6, dci, dcj);
+    }
+    tab[(size_t)i * n + j] = make_float2(c6, dci);
+  }
 }
 
 // row outputs: [0] energy, [1..6] virial (xx,yy,zz,xy,xz,yz), [7] dE/dCN
@@ -339,17 +462,24 @@ __global__ __launch_bounds__(BLK) void k_d3_reduce(int n, const double* __restri
 }  // namespace
 
 hipError_t launch_d3(const D3Params& p, const D3Grid& g, int n, const float4* x, const int* type,
-                     double* cn, float2* c6tab, double* rows, double* forces, double* totals,
-                     hipStream_t s) {
+                     double* cn, double* gw, float2* c6tab, double* rows, double* forces,
+                     double* totals, hipStream_t s) {
   if (n <= 0) {
     hipMemsetAsync(totals, 0, 7 * sizeof(double), s);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_d3_cn, dim3(n), dim3(BLK), 0, s, p, g, x, type, cn);
   if (c6tab) {
-    const int64_t npair = (int64_t)n * (n + 1) / 2;
-    hipLaunchKernelGGL(k_d3_c6tab, dim3((unsigned)((npair + BLK - 1) / BLK)), dim3(BLK), 0, s, p,
-                       n, type, cn, c6tab);
+    if (p.cnref)
+      hipLaunchKernelGGL(k_d3_gauss, dim3((n + BLK - 1) / BLK), dim3(BLK), 0, s, p, n, type, cn,
+                         gw);
+    if (p.cnref) {
+      hipLaunchKernelGGL(k_d3_c6rows, dim3(n), dim3(BLK), 0, s, p, n, type, cn, gw, c6tab);
+    } else {
+      const int64_t npair = (int64_t)n * (n + 1) / 2;
+      hipLaunchKernelGGL(k_d3_c6tab, dim3((unsigned)((npair + BLK - 1) / BLK)), dim3(BLK), 0, s,
+                         p, n, type, cn, nullptr, c6tab);
+    }
   }
   if (p.damping == 1) {
     if (c6tab)
