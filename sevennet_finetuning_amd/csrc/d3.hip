@@ -303,10 +303,35 @@ __global__ __launch_bounds__(BLK) void k_d3_disp(D3Params p, D3Grid g, int n,
                                                   double* __restrict__ rows,
                                                   double* __restrict__ forces) {
   __shared__ double red[NW];
+  // per partner type: BJ (R0^6, R0^8, s8 * 3 r2r4_i r2r4_j), zero (a1 R0ab,
+  // a2 R0ab, s8 r2r4_i r2r4_j) -- one LDS read per item instead of the
+  // table loads, products and a sqrt
+  constexpr int MAXT_LDS = 64;
+  __shared__ float s_tp[MAXT_LDS][3];
   const int i = blockIdx.x;
   const int ti = type[i];
   const float cni = (float)cn[i];
   const float2* trow = TAB ? c6tab + (size_t)i * n : nullptr;
+  const bool lds = p.ntypes <= MAXT_LDS;
+  auto pair_consts = [&](int tj, float& c0, float& c1, float& c2) {
+    if constexpr (DAMP == 1) {
+      const float r0 = p.r0ab[ti * p.ntypes + tj];
+      c0 = p.a1 * r0;
+      c1 = p.a2 * r0;
+      c2 = p.s8 * p.r2r4[ti] * p.r2r4[tj];
+    } else {
+      const float r42x3 = p.r2r4[ti] * p.r2r4[tj] * 3.0f;
+      const float R0 = fmaf(p.a1, sqrtf(r42x3), p.a2);
+      const float R02 = R0 * R0;
+      c0 = R02 * R02 * R02;
+      c1 = c0 * R02;
+      c2 = p.s8 * r42x3;
+    }
+  };
+  if (lds)
+    for (int tj = threadIdx.x; tj < p.ntypes; tj += BLK)
+      pair_consts(tj, s_tp[tj][0], s_tp[tj][1], s_tp[tj][2]);
+  __syncthreads();
   float e = 0.f, fx = 0.f, fy = 0.f, fz = 0.f, dcn = 0.f;
   float v00 = 0.f, v11 = 0.f, v22 = 0.f, v01 = 0.f, v02 = 0.f, v12 = 0.f;
   for_pairs<false>(g, g.off_vdw, g.n_off_vdw, g.cull2_vdw, p.rthr, x, i,
@@ -321,19 +346,26 @@ __global__ __launch_bounds__(BLK) void k_d3_disp(D3Params p, D3Grid g, int n,
       c6_pair(p, ti, tj, cni, (float)cn[j], c6, dc, dcj_unused);
     }
     float erest, x1;  // vec = x1 * r_ij = -(dE/dr) r_hat (the reference's x1 convention)
+    float k0, k1, k2;
+    if (lds) {
+      k0 = s_tp[tj][0];
+      k1 = s_tp[tj][1];
+      k2 = s_tp[tj][2];
+    } else {
+      pair_consts(tj, k0, k1, k2);
+    }
     if constexpr (DAMP == 1) {
       // zero damping, alp6 = 14 / alp8 = 16 as fixed powers (:1338-1356)
-      const float r0 = p.r0ab[ti * p.ntypes + tj];
-      const float s8r42 = p.s8 * p.r2r4[ti] * p.r2r4[tj];
+      const float s8r42 = k2;
       const float rrc = rsqrtf(r2);
-      const float u1 = p.a1 * r0 * rrc;
+      const float u1 = k0 * rrc;
       float t6 = u1 * u1;
       t6 *= u1;
       t6 *= t6;
       t6 *= u1;
       t6 *= t6;
       const float d6 = __builtin_amdgcn_rcpf(fmaf(t6, 6.0f, 1.0f));
-      const float u2 = p.a2 * r0 * rrc;
+      const float u2 = k1 * rrc;
       float t8 = u2 * u2;
       t8 *= t8;
       t8 *= t8;
@@ -345,10 +377,7 @@ __global__ __launch_bounds__(BLK) void k_d3_disp(D3Params p, D3Grid g, int n,
            fmaf(r2rc, s8r42 * d8 * fmaf(3.0f * p.alp8 * t8, d8, -4.0f),
                 p.s6 * d6 * fmaf(p.alp6 * t6, d6, -1.0f));
     } else {
-      const float r42x3 = p.r2r4[ti] * p.r2r4[tj] * 3.0f;
-      const float R0 = fmaf(p.a1, sqrtf(r42x3), p.a2);
-      const float R02 = R0 * R0, R06 = R02 * R02 * R02, R08 = R06 * R02;
-      const float s8r = p.s8 * r42x3;
+      const float R06 = k0, R08 = k1, s8r = k2;
       const float rrc = rsqrtf(r2), r = r2 * rrc, r5 = r2 * r2 * r, r7 = r5 * r2;
       const float t6 = __builtin_amdgcn_rcpf(fmaf(r5, r, R06));   // 1 ulp
       const float t8 = __builtin_amdgcn_rcpf(fmaf(r7, r, R08));
@@ -358,20 +387,21 @@ __global__ __launch_bounds__(BLK) void k_d3_disp(D3Params p, D3Grid g, int n,
     // row weights: every unordered pair appears in two rows, the self images
     // of i once -> energy / virial carry 1/2; F_i and dE/dCN_i the full
     // derivative for this row's own atom (self images: no force)
-    e -= 0.5f * erest * c6;
-    dcn -= erest * dc;
+    // (the 1/2 of energy and virial is applied once per row, below)
+    e = fmaf(-erest, c6, e);
+    dcn = fmaf(-erest, dc, dcn);
     const float vx = x1 * rx, vy = x1 * ry, vz = x1 * rz;
     if (j != i) {
       fx -= vx;
       fy -= vy;
       fz -= vz;
     }
-    v00 += 0.5f * vx * rx;
-    v11 += 0.5f * vy * ry;
-    v22 += 0.5f * vz * rz;
-    v01 += 0.5f * vx * ry;
-    v02 += 0.5f * vx * rz;
-    v12 += 0.5f * vy * rz;
+    v00 = fmaf(vx, rx, v00);
+    v11 = fmaf(vy, ry, v11);
+    v22 = fmaf(vz, rz, v22);
+    v01 = fmaf(vx, ry, v01);
+    v02 = fmaf(vx, rz, v02);
+    v12 = fmaf(vy, rz, v12);
   });
   double* row = rows + (size_t)i * ROW;
   const double se = block_sum(e, red);
@@ -380,13 +410,13 @@ __global__ __launch_bounds__(BLK) void k_d3_disp(D3Params p, D3Grid g, int n,
   const double s01 = block_sum(v01, red), s02 = block_sum(v02, red), s12 = block_sum(v12, red);
   const double sdc = block_sum(dcn, red);
   if (threadIdx.x == 0) {
-    row[0] = se;
-    row[1] = s00;
-    row[2] = s11;
-    row[3] = s22;
-    row[4] = s01;
-    row[5] = s02;
-    row[6] = s12;
+    row[0] = 0.5 * se;
+    row[1] = 0.5 * s00;
+    row[2] = 0.5 * s11;
+    row[3] = 0.5 * s22;
+    row[4] = 0.5 * s01;
+    row[5] = 0.5 * s02;
+    row[6] = 0.5 * s12;
     row[7] = sdc;
     forces[3 * i] = sfx;
     forces[3 * i + 1] = sfy;
