@@ -132,3 +132,22 @@ def test_per_item_c6_path_matches_table_path(monkeypatch):
     b = pair.compute(d['pos'], d['cell'], types)
     assert abs(a['energy'] - b['energy']) <= 1e-6 * abs(a['energy'])
     assert np.abs(a['forces'] - b['forces']).max() <= 1e-6 * np.abs(a['forces']).max() + 1e-9
+
+
+@pytest.mark.parametrize('bin_bohr', ['5', '8', '13'])
+def test_multi_bin_traversal_matches_oracle(monkeypatch, bin_bohr):
+    """Small bins (E3GNN_D3_BIN) put several bins along every axis of these
+    small cells, so the stencil walk, the image arithmetic of out-of-cell bins
+    and the centre-distance culling are all exercised against the oracle
+    (the default 30-bohr bins give one bin per axis below ~16 A)."""
+    monkeypatch.setenv('E3GNN_D3_BIN', bin_bohr)
+    d = np.load(f'{GOLD}/hfo2_resdat.npz')
+    z = np.array([CHEMICAL_SYMBOLS.index(str(s)) for s in d['symbols']])
+    kw = dict(rthr=3000.0)
+    got, _, _ = _hip(d['pos'], d['cell'], z, 'damp_bj', 'pbe', **kw)
+    _compare(got, _oracle(d['pos'], d['cell'], z, 'damp_bj', 'pbe', **kw))
+    pos, cell = si_diamond((2, 2, 2), sigma=0.08, seed=3)
+    zz = np.array([CHEMICAL_SYMBOLS.index(s) for s in mixed_symbols(len(pos))])
+    kw = dict(rthr=2000.0, cn_thr=900.0)
+    got, _, _ = _hip(pos, cell, zz, 'damp_zero', 'pbe0', **kw)
+    _compare(got, _oracle(pos, cell, zz, 'damp_zero', 'pbe0', **kw))
