@@ -20,6 +20,8 @@
 #include "cg_tables.h"
 #include "tp.h"
 
+#include <algorithm>
+
 #include <type_traits>
 #include <utility>
 
@@ -127,21 +129,25 @@ __device__ __forceinline__ void fwd_part(int lane, int beg, int end, const int* 
 }
 
 template <class L>
-__global__ __launch_bounds__(256) void k_tp_fwd(const int* __restrict__ row_ptr,
+__global__ __launch_bounds__(192) void k_tp_fwd(const int* __restrict__ row_ptr,
                                                 const int* __restrict__ nbr,
                                                 const float* __restrict__ Y,
                                                 const float* __restrict__ w,
                                                 const float* __restrict__ h,
                                                 float* __restrict__ agg, int n_centers,
                                                 float denom) {
-  const int c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  // one workgroup per centre, one wave per input irrep (its paths write
+  // disjoint message slots): 3x the waves of a wave-per-centre mapping, which
+  // matters for the small batched graphs of the fine-tune step
+  const int c = blockIdx.x;
   if (c >= n_centers) return;
+  const int part = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int beg = row_ptr[c], end = row_ptr[c + 1];
   float* out = agg + (int64_t)c * L::DM;
-  fwd_part<L, 0>(lane, beg, end, nbr, Y, w, h, out, denom);
-  fwd_part<L, 1>(lane, beg, end, nbr, Y, w, h, out, denom);
-  fwd_part<L, 2>(lane, beg, end, nbr, Y, w, h, out, denom);
+  if (part == 0) fwd_part<L, 0>(lane, beg, end, nbr, Y, w, h, out, denom);
+  else if (part == 1) fwd_part<L, 1>(lane, beg, end, nbr, Y, w, h, out, denom);
+  else fwd_part<L, 2>(lane, beg, end, nbr, Y, w, h, out, denom);
 }
 
 // ------------------------------------------------------------------ backward
@@ -232,8 +238,13 @@ __global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
                                                 const float* __restrict__ h,
                                                 const float* __restrict__ gagg,
                                                 float* __restrict__ dw, float* __restrict__ dxc,
-                                                float* __restrict__ dYacc, int n_centers) {
-  const int c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+                                                float* __restrict__ dYacc, int n_centers,
+                                                int split) {
+  // `split` waves per centre, wave k taking the centre's edges k, k + split, ...
+  // (every per-edge output has one writer); split > 1 only when there are few
+  // centres (the fine-tune step's batches)
+  const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int c = wg / split, k0 = wg - c * split;
   if (c >= n_centers) return;
   const int lane = threadIdx.x & 63;
   const int beg = row_ptr[c], end = row_ptr[c + 1];
@@ -244,7 +255,7 @@ __global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
   pa.load(lane, gc);
   pb.load(lane, gc);
   pc.load(lane, gc);
-  for (int e = beg; e < end; ++e) {
+  for (int e = beg + k0; e < end; e += split) {
     const int j = nbr[e];
     float y[9], dy[9];
 #pragma unroll
@@ -270,15 +281,17 @@ __global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
 template <class L>
 static hipError_t tp_fwd_impl(const TpArgs& a, hipStream_t s) {
   if (a.n_centers <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_tp_fwd<L>, dim3((a.n_centers + 3) / 4), dim3(256), 0, s, a.row_ptr, a.nbr,
-                     a.Y, a.w, a.h, a.agg, a.n_centers, a.denom);
+  hipLaunchKernelGGL(k_tp_fwd<L>, dim3(a.n_centers), dim3(192), 0, s, a.row_ptr, a.nbr, a.Y, a.w,
+                     a.h, a.agg, a.n_centers, a.denom);
   return hipGetLastError();
 }
 template <class L>
 static hipError_t tp_bwd_impl(const TpArgs& a, hipStream_t s) {
   if (a.n_centers <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_tp_bwd<L>, dim3((a.n_centers + 3) / 4), dim3(256), 0, s, a.row_ptr, a.nbr,
-                     a.Y, a.w, a.h, a.gagg, a.dw, a.dxc, a.dYacc, a.n_centers);
+  const int split = std::max(1, std::min(8, 16384 / a.n_centers));
+  const int64_t waves = (int64_t)a.n_centers * split;
+  hipLaunchKernelGGL(k_tp_bwd<L>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a.row_ptr,
+                     a.nbr, a.Y, a.w, a.h, a.gagg, a.dw, a.dxc, a.dYacc, a.n_centers, split);
   return hipGetLastError();
 }
 
