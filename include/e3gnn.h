@@ -154,6 +154,14 @@ int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_
                         const float* h, const float* Y, const float* w, const float* gagg,
                         float* dh, float* dY, float* dw, float* dxc, void* stream);
 
+/* Scaled SiLU of the trainable model (y = scale * silu(x); e3nn normalize2mom,
+ * SevenNet's act_radial / act_scalar / act_gate, silu_norm 1.6792), element-
+ * wise over n floats: op 0 out0 = y(x); op 1 out0 = g * y'(x); op 2 (the
+ * derivative of op 1 against the cotangent gg) out0 = gg * g * y''(x),
+ * out1 = gg * y'(x) (either nullable). */
+int e3gnn_act(int op, int64_t n, const float* x, const float* g, const float* gg, float* out0,
+              float* out1, float scale, void* stream);
+
 /* ---- device neighbour list (the graph build in front of the hot path) ----
  * Replaces ASE primitive_neighbor_list('ijDS', pbc, cell, pos, cutoff,
  * self_interaction=True) minus the (i, i, S = 0) pair (sevenn/train/

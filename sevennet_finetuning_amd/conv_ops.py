@@ -186,3 +186,57 @@ class _ConvBackward(torch.autograd.Function):
 def conv(h, Y, w, kind, graph):
     """Raw (un-normalised) aggregated messages of one interaction block."""
     return _ConvForward.apply(h, Y, w, kind, graph)
+
+
+# ------------------------------------------------------------------ scaled SiLU
+def _act_call(lib, op, x, g=None, gg=None, out0=None, out1=None, scale=1.0):
+    p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    _lib.check(lib.e3gnn_act(op, x.numel(), p(x), p(g), p(gg), p(out0), p(out1),
+                             ctypes.c_float(scale), torch.cuda.current_stream(x.device).cuda_stream))
+
+
+class _Act(torch.autograd.Function):
+    # the INPUT tensors are saved (not their contiguous copies): the double
+    # backward must reach the original x through them
+    @staticmethod
+    def forward(ctx, x, scale, lib):
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        _act_call(lib, 0, xc, out0=y, scale=scale)
+        ctx.save_for_backward(x)
+        ctx.scale, ctx.lib = scale, lib
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, = ctx.saved_tensors
+        return _ActBackward.apply(x, g, ctx.scale, ctx.lib), None, None
+
+
+class _ActBackward(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, scale, lib):
+        xc, gc = x.contiguous(), g.contiguous()
+        dx = torch.empty_like(xc)
+        _act_call(lib, 1, xc, g=gc, out0=dx, scale=scale)
+        ctx.save_for_backward(x, g)
+        ctx.scale, ctx.lib = scale, lib
+        return dx
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gg):
+        x, g = ctx.saved_tensors
+        xc, gc, ggc = x.contiguous(), g.contiguous(), gg.contiguous()
+        need_x, need_g = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = torch.empty_like(xc) if need_x else None
+        dg = torch.empty_like(xc) if need_g else None
+        if need_x or need_g:
+            _act_call(ctx.lib, 2, xc, g=gc, gg=ggc, out0=dx, out1=dg, scale=ctx.scale)
+        return dx, dg, None, None
+
+
+def scaled_silu(x, scale, lib):
+    """scale * silu(x) on the HIP kernels of libe3gnn_hip.so (e3gnn_act),
+    differentiable twice (the fine-tune step's force loss)."""
+    return _Act.apply(x, float(scale), lib)

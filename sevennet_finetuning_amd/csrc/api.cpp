@@ -26,6 +26,7 @@
 #include "../../include/e3gnn.h"
 #include "cg_tables.h"
 #include "d3.h"
+#include "train_ops.h"
 #include "common.h"
 #include "fused.h"
 #include "minijson.h"
@@ -1274,6 +1275,17 @@ int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_
   a.denom = 1.0f;
   HIPCHK(launch_tp_bwd(kind, a, s));
   if (dh) HIPCHK(launch_gather_rows((int)n_nodes, dx, src_ptr, src_perm, dxc, dh, s));
+  return E3GNN_OK;
+}
+
+int e3gnn_act(int op, int64_t n, const float* x, const float* g, const float* gg, float* out0,
+              float* out1, float scale, void* stream) {
+  if (op < 0 || op > 2) return fail(E3GNN_ERR_ARG, "act op must be 0, 1 or 2");
+  if (n < 0) return fail(E3GNN_ERR_ARG, "negative size");
+  if (n > 0 && (!x || (op == 0 && !out0) || (op == 1 && (!g || !out0)) ||
+                (op == 2 && (!g || !gg || (!out0 && !out1)))))
+    return fail(E3GNN_ERR_ARG, "null act operand");
+  HIPCHK(launch_act(op, n, x, g, gg, out0, out1, scale, (hipStream_t)stream));
   return E3GNN_OK;
 }
 

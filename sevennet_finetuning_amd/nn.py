@@ -274,7 +274,17 @@ class SevenNetTrainable(torch.nn.Module):
         self.readout2 = _Linear([(irr[-1][0][0] // 2, 0)], [(1, 0)])
 
     def act(self, x):
+        # HIP kernels on the GPU (one launch per derivative order); the CPU
+        # runs of this model are the tests' float64 double
+        if x.is_cuda and x.dtype == torch.float32:
+            return conv_ops.scaled_silu(x, self.silu_norm, self._act_lib())
         return torch.nn.functional.silu(x) * self.silu_norm
+
+    def _act_lib(self):
+        if getattr(self, '_lib_handle', None) is None:
+            from . import _lib
+            self._lib_handle = _lib.load()
+        return self._lib_handle
 
     def gate(self, x, gate_irreps):
         # e3nn nn.Gate (equivariant_gate.py:59-61); split, not sliced (one cat
