@@ -39,6 +39,7 @@ LOAD_DATASET_WITH_WEIGHTS, DATA_WEIGHT = 'load_dataset_with_weights', 'data_weig
 PER_ATOM_ENERGY = 'per_atom_energy'
 IS_DDP, LOCAL_RANK = 'is_ddp', 'local_rank'
 HIP_GRAPH = 'hip_graph'
+BLAS = 'blas'
 
 
 # ------------------------------------------------------------------ losses
@@ -428,6 +429,14 @@ class Trainer:
             dist.broadcast(self.model.flat, 0)
         else:
             self.world = 1
+        # BLAS (this build): the radial-MLP GEMMs of the step (12k x 64 x 960
+        # and transposes) run 1.4x faster per step on rocBLAS than on torch's
+        # default hipBLASLt on MI355X (bench_train: 29.1 -> 21.1 ms); fp32 either
+        # way.  Process-wide torch setting, applied when the model is on a GPU.
+        blas = str(config.get(BLAS, 'rocblas')).lower()
+        if self.device.type == 'cuda' and blas in ('rocblas', 'hipblaslt'):
+            torch.backends.cuda.preferred_blas_library('cublas' if blas == 'rocblas'
+                                                       else 'cublaslt')
         params = [p for p in self.model.parameters() if p.requires_grad]
         opt = optim_dict[config[OPTIMIZER].lower()]
         optim_param = dict(config.get(OPTIM_PARAM, {}))
