@@ -105,3 +105,34 @@ class SevenNetCalculator(Calculator):
         if KEY.PRED_STRESS in out:
             self.results['stress'] = np.array(
                 (-out[KEY.PRED_STRESS]).detach().cpu().numpy()[[0, 1, 2, 4, 5, 3]])
+
+
+class SevenNetD3Calculator(Calculator):
+    """SevenNet-0 + DFT-D3 in one calculator: what LAMMPS runs as
+    ``pair_style hybrid/overlay e3gnn d3 <rthr> <cn_thr> <damping> <functional>``
+    (the reference's pair_e3gnn.cpp + pair_d3.cu), i.e. energies, forces and
+    stresses of the two terms summed.  Per-atom energies are the SevenNet
+    ones (the D3 term is not atom-decomposed, as in pair_d3.cu)."""
+
+    def __init__(self, model='SevenNet-0', file_type='checkpoint', device='auto',
+                 damping_type='damp_bj', functional_name='pbe', vdw_cutoff=9000.0,
+                 cn_cutoff=1600.0, **kwargs):
+        super().__init__(**kwargs)
+        from .d3 import D3Calculator
+        self.sevennet = SevenNetCalculator(model, file_type, device)
+        dev = self.sevennet.device
+        self.d3 = D3Calculator(damping_type, functional_name, vdw_cutoff, cn_cutoff,
+                               device=dev.index or 0)
+        self.implemented_properties = ['free_energy', 'energy', 'forces', 'stress', 'energies']
+
+    def calculate(self, atoms=None, properties=None, system_changes=all_changes):
+        a = self.sevennet
+        a.calculate(atoms, properties, system_changes)
+        b = self.d3.calculate(atoms)
+        r = dict(a.results)
+        r['energy'] = r['free_energy'] = a.results['energy'] + b['energy']
+        r['forces'] = a.results['forces'] + b['forces']
+        r['stress'] = a.results['stress'] + b['stress']
+        self.results = r
+        self.atoms = atoms
+        return r

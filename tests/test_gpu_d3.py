@@ -151,3 +151,23 @@ def test_multi_bin_traversal_matches_oracle(monkeypatch, bin_bohr):
     kw = dict(rthr=2000.0, cn_thr=900.0)
     got, _, _ = _hip(pos, cell, zz, 'damp_zero', 'pbe0', **kw)
     _compare(got, _oracle(pos, cell, zz, 'damp_zero', 'pbe0', **kw))
+
+
+def test_sevennet_d3_calculator_is_the_sum():
+    """SevenNetD3Calculator (pair_style hybrid/overlay e3gnn d3) = SevenNet-0 +
+    D3 term by term."""
+    from sevennet_finetuning_amd.d3 import D3Calculator
+    from sevennet_finetuning_amd.sevennet_calculator import (SevenNetCalculator,
+                                                             SevenNetD3Calculator)
+    from sevennet_finetuning_amd.structures import Atoms
+    pos, cell, z = si8()
+    at = Atoms(numbers=z, positions=pos, cell=cell, pbc=True)
+    both = SevenNetD3Calculator(device='cuda:0')
+    both.calculate(at)
+    a = SevenNetCalculator(device='cuda:0')
+    a.calculate(at)
+    b = D3Calculator().calculate(at)
+    assert abs(both.results['energy'] - (a.results['energy'] + b['energy'])) < 1e-6
+    assert np.allclose(both.results['forces'], a.results['forces'] + b['forces'], atol=1e-6)
+    assert np.allclose(both.results['stress'], a.results['stress'] + b['stress'], atol=1e-9)
+    assert both.results['energy'] < a.results['energy']   # dispersion binds
