@@ -21,6 +21,12 @@
  *     pair_e3gnn_parallel.cpp:474-519
  *   pack/unpack_{forward,reverse}_comm_gnn                          e3gnn_halo_pack/_unpack
  *     pair_e3gnn_parallel.cpp:803-933
+ *   ASE primitive_neighbor_list / pair_e3gnn.cpp:144-182            e3gnn_nlist_*
+ *   e3nn TensorProduct + message_gather under double backward       e3gnn_conv_graph /
+ *     (training: convolution.py:104-123, trainer.py:155-222)         _forward / _backward
+ *   e3nn normalize2mom(silu) and its derivatives (training)          e3gnn_act
+ *   LAMMPS pair_style d3 settings/coeff, compute/update             e3gnn_d3_create /
+ *     (pair_d3.cu:265-767, :2003-2056)                               e3gnn_d3_compute
  *   error->all(FLERR, msg)                                           return code +
  *                                                                    e3gnn_last_error()
  *
