@@ -168,6 +168,15 @@ int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_
 int e3gnn_act(int op, int64_t n, const float* x, const float* g, const float* gg, float* out0,
               float* out1, float scale, void* stream);
 
+/* e3nn Gate of the trainable model (EquivariantGate, equivariant_gate.py:13-61)
+ * on n rows: y = [scalars | gates | gated blocks], o = [act(scalars) |
+ * act(gate_k) * block_k] with act = scale * silu.  op 0: out0 = o; op 1: out0 =
+ * dy for the output cotangent go; op 2 (cotangent q of that dy): out0 = d/dgo,
+ * out1 = d/dy (either nullable).  dims[13]: n_scalars, n_gates, row_in, row_out,
+ * n_groups (<= 2), then per group: offset_in, offset_out, mul, 2l+1. */
+int e3gnn_gate(int op, int64_t n, const int32_t* dims, const float* y, const float* go,
+               const float* q, float* out0, float* out1, float scale, void* stream);
+
 /* ---- device neighbour list (the graph build in front of the hot path) ----
  * Replaces ASE primitive_neighbor_list('ijDS', pbc, cell, pos, cutoff,
  * self_interaction=True) minus the (i, i, S = 0) pair (sevenn/train/

@@ -240,3 +240,76 @@ def scaled_silu(x, scale, lib):
     """scale * silu(x) on the HIP kernels of libe3gnn_hip.so (e3gnn_act),
     differentiable twice (the fine-tune step's force loss)."""
     return _Act.apply(x, float(scale), lib)
+
+
+# ------------------------------------------------------------------ gate
+def _gate_call(lib, op, dims, y, go=None, q=None, out0=None, out1=None, scale=1.0):
+    p = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    _lib.check(lib.e3gnn_gate(op, y.shape[0], dims.ctypes.data, p(y), p(go), p(q), p(out0),
+                              p(out1), ctypes.c_float(scale),
+                              torch.cuda.current_stream(y.device).cuda_stream))
+
+
+class _Gate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, dims, scale, lib):
+        yc = y.contiguous()
+        o = torch.empty(y.shape[0], int(dims[3]), device=y.device, dtype=y.dtype)
+        _gate_call(lib, 0, dims, yc, out0=o, scale=scale)
+        ctx.save_for_backward(y)
+        ctx.dims, ctx.scale, ctx.lib = dims, scale, lib
+        return o
+
+    @staticmethod
+    def backward(ctx, go):
+        y, = ctx.saved_tensors
+        return _GateBackward.apply(y, go, ctx.dims, ctx.scale, ctx.lib), None, None, None
+
+
+class _GateBackward(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, go, dims, scale, lib):
+        yc, gc = y.contiguous(), go.contiguous()
+        dy = torch.empty_like(yc)
+        _gate_call(lib, 1, dims, yc, go=gc, out0=dy, scale=scale)
+        ctx.save_for_backward(y, go)
+        ctx.dims, ctx.scale, ctx.lib = dims, scale, lib
+        return dy
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, q):
+        y, go = ctx.saved_tensors
+        yc, gc, qc = y.contiguous(), go.contiguous(), q.contiguous()
+        need_y, need_go = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dgo = torch.empty_like(gc) if need_go else None
+        dyy = torch.empty_like(yc) if need_y else None
+        if need_y or need_go:
+            _gate_call(ctx.lib, 2, ctx.dims, yc, go=gc, q=qc, out0=dgo, out1=dyy,
+                       scale=ctx.scale)
+        return dyy, dgo, None, None, None
+
+
+def gate_dims(scal, gated):
+    """dims vector of e3gnn_gate for Gate irreps (scalars, gated (mul, l))."""
+    import numpy as np
+    ns = sum(m for m, _ in scal)
+    ng = sum(m for m, _ in gated)
+    if len(gated) > 2:
+        raise ValueError('the fused gate takes at most two gated irreps')
+    din = ns + ng + sum(m * (2 * l + 1) for m, l in gated)
+    dout = ns + sum(m * (2 * l + 1) for m, l in gated)
+    d = [ns, ng, din, dout, len(gated)]
+    off_in, off_out = ns + ng, ns
+    for m, l in gated:
+        d += [off_in, off_out, m, 2 * l + 1]
+        off_in += m * (2 * l + 1)
+        off_out += m * (2 * l + 1)
+    d += [0] * (13 - len(d))
+    return np.asarray(d, dtype=np.int32)
+
+
+def gate(y, dims, scale, lib):
+    """e3nn Gate (scale * silu on scalars and gates) on the HIP kernels,
+    differentiable twice."""
+    return _Gate.apply(y, dims, float(scale), lib)

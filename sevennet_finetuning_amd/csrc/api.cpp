@@ -1289,6 +1289,17 @@ int e3gnn_act(int op, int64_t n, const float* x, const float* g, const float* gg
   return E3GNN_OK;
 }
 
+int e3gnn_gate(int op, int64_t n, const int32_t* dims, const float* y, const float* go,
+               const float* q, float* out0, float* out1, float scale, void* stream) {
+  if (op < 0 || op > 2) return fail(E3GNN_ERR_ARG, "gate op must be 0, 1 or 2");
+  if (n < 0 || !dims) return fail(E3GNN_ERR_ARG, "bad gate arguments");
+  if (dims[4] < 0 || dims[4] > 2) return fail(E3GNN_ERR_ARG, "at most two gated irreps");
+  if (n > 0 && (!y || (op >= 1 && !go) || (op == 2 && !q) || (op < 2 && !out0)))
+    return fail(E3GNN_ERR_ARG, "null gate operand");
+  HIPCHK(launch_gate(op, n, dims, y, go, q, out0, out1, scale, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
 // ------------------------------------------------------------ neighbour list
 struct e3gnn_nlist {
   int device = 0;

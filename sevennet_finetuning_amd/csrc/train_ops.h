@@ -8,4 +8,9 @@ namespace e3gnn {
 // out1 = gg c silu'(x) (either nullable)
 hipError_t launch_act(int op, int64_t n, const float* x, const float* g, const float* gg,
                       float* out0, float* out1, float c, hipStream_t s);
+// e3nn Gate rows (nn.py gate): op 0 out0 = o(y); 1 out0 = dy(y, go);
+// 2 (cotangent q of dy) out0 = d/dgo, out1 = d/dy (either nullable).
+// dims: ns, ng, din, dout, ngroups, then per group (<= 2): off_in, off_out, mul, 2l+1
+hipError_t launch_gate(int op, int64_t n, const int* dims, const float* y, const float* go,
+                       const float* q, float* out0, float* out1, float c, hipStream_t s);
 }  // namespace e3gnn

@@ -54,3 +54,148 @@ hipError_t launch_act(int op, int64_t n, const float* x, const float* g, const f
 }
 
 }  // namespace e3gnn
+
+// ------------------------------------------------------------------ gate
+// e3nn Gate of the trainable model (equivariant_gate.py:13-61): input row
+// y = [s (NS) | g (NG) | gated blocks (mul_k x (2l_k+1))], output row
+// o = [act(s) | act(g_k) * block_k].  One thread per (row, scalar-or-gate
+// channel); a gate thread owns its block's 2l+1 components.  Gated blocks are
+// described by per-gate (offset, width): blocks follow the gates in order.
+namespace e3gnn {
+namespace {
+
+struct GateDims {
+  int ns, ng, din, dout;   // scalars, gates, input row, output row
+  int goff_in[2], goff_out[2], gmul[2], gdim[2], ngrp;   // up to 2 gated irreps
+};
+
+__device__ __forceinline__ void act3(float x, float c, float& y, float& d1, float& d2) {
+  const float s = 1.0f / (1.0f + __expf(-x));
+  y = c * x * s;
+  d1 = c * s * (1.0f + x * (1.0f - s));
+  d2 = c * s * (1.0f - s) * (2.0f + x * (1.0f - 2.0f * s));
+}
+
+// gate thread t in [0, ng) -> group, index within group
+__device__ __forceinline__ void gate_of(const GateDims& D, int t, int& grp, int& k) {
+  grp = t < D.gmul[0] ? 0 : 1;
+  k = grp == 0 ? t : t - D.gmul[0];
+}
+
+__global__ void k_gate_fwd(int64_t n, GateDims D, const float* __restrict__ y,
+                           float* __restrict__ o, float c) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = D.ns + D.ng;
+  if (tid >= n * per) return;
+  const int64_t r = tid / per;
+  const int t = (int)(tid - r * per);
+  const float* yr = y + r * D.din;
+  float* orow = o + r * D.dout;
+  float a, d1, d2;
+  if (t < D.ns) {
+    act3(yr[t], c, a, d1, d2);
+    orow[t] = a;
+    return;
+  }
+  int grp, k;
+  gate_of(D, t - D.ns, grp, k);
+  act3(yr[D.ns + t - D.ns], c, a, d1, d2);
+  const int w = D.gdim[grp];
+  for (int m = 0; m < w; ++m)
+    orow[D.goff_out[grp] + k * w + m] = a * yr[D.goff_in[grp] + k * w + m];
+}
+
+// dy from go
+__global__ void k_gate_bwd(int64_t n, GateDims D, const float* __restrict__ y,
+                           const float* __restrict__ go, float* __restrict__ dy, float c) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = D.ns + D.ng;
+  if (tid >= n * per) return;
+  const int64_t r = tid / per;
+  const int t = (int)(tid - r * per);
+  const float* yr = y + r * D.din;
+  const float* gr = go + r * D.dout;
+  float* dr = dy + r * D.din;
+  float a, d1, d2;
+  if (t < D.ns) {
+    act3(yr[t], c, a, d1, d2);
+    dr[t] = gr[t] * d1;
+    return;
+  }
+  int grp, k;
+  gate_of(D, t - D.ns, grp, k);
+  act3(yr[t], c, a, d1, d2);
+  const int w = D.gdim[grp];
+  float sg = 0.f;
+  for (int m = 0; m < w; ++m) {
+    const int ii = D.goff_in[grp] + k * w + m, oo = D.goff_out[grp] + k * w + m;
+    sg = fmaf(gr[oo], yr[ii], sg);
+    dr[ii] = gr[oo] * a;
+  }
+  dr[t] = sg * d1;
+}
+
+// cotangent q of dy: dgo (nullable) and dyy (nullable)
+__global__ void k_gate_bwd2(int64_t n, GateDims D, const float* __restrict__ y,
+                            const float* __restrict__ go, const float* __restrict__ q,
+                            float* __restrict__ dgo, float* __restrict__ dyy, float c) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = D.ns + D.ng;
+  if (tid >= n * per) return;
+  const int64_t r = tid / per;
+  const int t = (int)(tid - r * per);
+  const float* yr = y + r * D.din;
+  const float* gr = go + r * D.dout;
+  const float* qr = q + r * D.din;
+  float a, d1, d2;
+  if (t < D.ns) {
+    act3(yr[t], c, a, d1, d2);
+    if (dgo) dgo[r * D.dout + t] = qr[t] * d1;
+    if (dyy) dyy[r * D.din + t] = qr[t] * gr[t] * d2;
+    return;
+  }
+  int grp, k;
+  gate_of(D, t - D.ns, grp, k);
+  act3(yr[t], c, a, d1, d2);
+  const int w = D.gdim[grp];
+  const float qg = qr[t];
+  float sgb = 0.f, sqb = 0.f;   // sum_m go*blk, sum_m q_blk*go
+  for (int m = 0; m < w; ++m) {
+    const int ii = D.goff_in[grp] + k * w + m, oo = D.goff_out[grp] + k * w + m;
+    const float b = yr[ii], g = gr[oo], qb = qr[ii];
+    if (dgo) dgo[r * D.dout + oo] = qg * b * d1 + qb * a;
+    if (dyy) dyy[r * D.din + ii] = qg * g * d1;
+    sgb = fmaf(g, b, sgb);
+    sqb = fmaf(qb, g, sqb);
+  }
+  if (dyy) dyy[r * D.din + t] = qg * sgb * d2 + sqb * d1;
+}
+
+}  // namespace
+
+hipError_t launch_gate(int op, int64_t n, const int* dims, const float* y, const float* go,
+                       const float* q, float* out0, float* out1, float c, hipStream_t s) {
+  GateDims D{};
+  D.ns = dims[0];
+  D.ng = dims[1];
+  D.din = dims[2];
+  D.dout = dims[3];
+  D.ngrp = dims[4];
+  for (int g = 0; g < 2; ++g) {
+    D.goff_in[g] = dims[5 + 4 * g];
+    D.goff_out[g] = dims[6 + 4 * g];
+    D.gmul[g] = dims[7 + 4 * g];
+    D.gdim[g] = dims[8 + 4 * g];
+  }
+  const int64_t total = n * (D.ns + D.ng);
+  if (total <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  switch (op) {
+    case 0: hipLaunchKernelGGL(k_gate_fwd, grid, block, 0, s, n, D, y, out0, c); break;
+    case 1: hipLaunchKernelGGL(k_gate_bwd, grid, block, 0, s, n, D, y, go, out0, c); break;
+    default: hipLaunchKernelGGL(k_gate_bwd2, grid, block, 0, s, n, D, y, go, q, out0, out1, c); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace e3gnn

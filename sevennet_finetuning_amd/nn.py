@@ -213,6 +213,7 @@ class SevenNetTrainable(torch.nn.Module):
                 p.requires_grad_(train_radial_coeffs)
         self.attach_flat_grad()
         self.is_batch_data = True
+        self._gate_dims = {}
 
     # ------------------------------------------------------------ parameters
     def _register_nested(self, name, p):
@@ -293,6 +294,11 @@ class SevenNetTrainable(torch.nn.Module):
         n = x.shape[0]
         ns = sum(m for m, _ in scal)
         ng = sum(m for m, _ in gated)
+        if ng > 0 and x.is_cuda and x.dtype == torch.float32 and len(gated) <= 2:
+            key = id(gate_irreps)
+            if key not in self._gate_dims:
+                self._gate_dims[key] = conv_ops.gate_dims(scal, gated)
+            return conv_ops.gate(x, self._gate_dims[key], self.silu_norm, self._act_lib())
         if ng == 0:
             return self.act(x[:, :ns] if x.shape[1] != ns else x)
         sizes = [ns, ng] + [m * (2 * l + 1) for m, l in gated]

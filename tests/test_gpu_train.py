@@ -280,3 +280,38 @@ def test_scaled_silu_op_noncontiguous_input_second_order():
     ref = run(lambda x: torch.nn.functional.silu(x) * c, torch.float64, 'cpu')
     for a, b in zip(got, ref):
         assert _rel(a, b) < 2e-6
+
+
+def test_fused_gate_op_derivatives():
+    """e3gnn_gate (fused e3nn Gate of the trainable model) against the torch
+    composite in float64: value, first and second derivatives, through a
+    column slice of a wider tensor (the gate input is a view in the model)."""
+    from sevennet_finetuning_amd import _lib
+    lib = _lib.load()
+    scal, gated = [(128, 0)], [(64, 1), (32, 2)]
+    dims = conv_ops.gate_dims(scal, gated)
+    c = 1.679177
+    rng = np.random.default_rng(5)
+    din, dout = int(dims[2]), int(dims[3])
+    base_v = rng.normal(0, 1.5, (37, din + 7))
+    gv, pv = rng.normal(size=(37, dout)), rng.normal(size=(37, din + 7))
+
+    def composite(x):
+        act = lambda t: torch.nn.functional.silu(t) * c  # noqa: E731
+        s, g = act(x[:, :128]), act(x[:, 128:224])
+        b1 = x[:, 224:416].reshape(-1, 64, 3) * g[:, :64].unsqueeze(-1)
+        b2 = x[:, 416:576].reshape(-1, 32, 5) * g[:, 64:96].unsqueeze(-1)
+        return torch.cat([s, b1.reshape(len(x), -1), b2.reshape(len(x), -1)], 1)
+
+    def run(fn, dtype, dev):
+        base = torch.tensor(base_v, dtype=dtype, device=dev, requires_grad=True)
+        x = base[:, 3:3 + din]
+        y = fn(x)
+        d1, = torch.autograd.grad((y * torch.tensor(gv, dtype=dtype, device=dev)).sum(), [base],
+                                  create_graph=True)
+        d2, = torch.autograd.grad((d1 * torch.tensor(pv, dtype=dtype, device=dev)).sum(), [base])
+        return y, d1, d2
+    got = run(lambda x: conv_ops.gate(x, dims, c, lib), torch.float32, DEV)
+    ref = run(composite, torch.float64, 'cpu')
+    for a, b in zip(got, ref):
+        assert _rel(a, b) < 2e-6
