@@ -25,6 +25,7 @@
  *   e3nn TensorProduct + message_gather under double backward       e3gnn_conv_graph /
  *     (training: convolution.py:104-123, trainer.py:155-222)         _forward / _backward
  *   e3nn normalize2mom(silu) and its derivatives (training)          e3gnn_act
+ *   EquivariantGate / e3nn Gate and its derivatives (training)       e3gnn_gate
  *   LAMMPS pair_style d3 settings/coeff, compute/update             e3gnn_d3_create /
  *     (pair_d3.cu:265-767, :2003-2056)                               e3gnn_d3_compute
  *   error->all(FLERR, msg)                                           return code +
