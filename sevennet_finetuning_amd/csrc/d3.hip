@@ -228,6 +228,42 @@ __global__ __launch_bounds__(BLK) void k_d3_c6tab(D3Params p, int n, const int* 
   tab[(size_t)j * n + i] = make_float2(c6, dcj);
 }
 
+// C6_ij and dC6_ij/dCN_i from the per-atom Gaussian factors (separable path)
+__device__ __forceinline__ void c6_sep(const D3Params& p, int ti, int tj,
+                                       const double* __restrict__ gi,
+                                       const double* __restrict__ gj, float cni, float cnj,
+                                       float& c6, float& dci) {
+  const float* t = p.c6ab + ((size_t)ti * p.ntypes + tj) * (MAXC * MAXC * 3);
+  const int ma = p.mxc[ti], mb = p.mxc[tj];
+  double gjv[MAXC];
+#pragma unroll
+  for (int b = 0; b < MAXC; ++b) gjv[b] = b < mb ? gj[b] : 0.0;
+  double num = 0.0, den = 0.0, dni = 0.0, ddi = 0.0;
+  for (int a = 0; a < ma; ++a) {
+    double rn = 0.0, rd = 0.0;
+#pragma unroll
+    for (int b = 0; b < MAXC; ++b) {
+      const float ref = b < mb ? t[(a * MAXC + b) * 3] : 0.0f;
+      if (ref > 0.0f) {
+        rn = fma((double)ref, gjv[b], rn);
+        rd += gjv[b];
+      }
+    }
+    num = fma(gi[a], rn, num);
+    den = fma(gi[a], rd, den);
+    dni = fma(gi[5 + a], rn, dni);
+    ddi = fma(gi[5 + a], rd, ddi);
+  }
+  if (den > 1e-99) {
+    const double r = 1.0 / den, u = num * r;
+    c6 = (float)u;
+    dci = (float)(r * fma(u, -ddi, dni));
+  } else {
+    float dcj;
+    c6_pair(p, ti, tj, cni, cnj, c6, dci, dcj);
+  }
+}
+
 // Separable path: row i = one workgroup, coalesced row writes, ordered pairs
 // (25 fp64 multiply-adds each; only dC6/dCN_i is needed per ordered pair)
 __global__ __launch_bounds__(BLK) void k_d3_c6rows(D3Params p, int n, const int* __restrict__ type,
@@ -300,6 +336,7 @@ __global__ __launch_bounds__(BLK) void k_d3_disp(D3Params p, D3Grid g, int n,
                                                   const int* __restrict__ type,
                                                   const double* __restrict__ cn,
                                                   const float2* __restrict__ c6tab,
+                                                  const double* __restrict__ gw,
                                                   double* __restrict__ rows,
                                                   double* __restrict__ forces) {
   __shared__ double red[NW];
@@ -341,6 +378,8 @@ __global__ __launch_bounds__(BLK) void k_d3_disp(D3Params p, D3Grid g, int n,
       const float2 t = trow[j];
       c6 = t.x;
       dc = t.y;
+    } else if (gw) {   // > 32k atoms: separable weights per item (25 fp64 FMAs)
+      c6_sep(p, ti, tj, gw + (size_t)i * 10, gw + (size_t)j * 10, cni, (float)cn[j], c6, dc);
     } else {
       float dcj_unused;
       c6_pair(p, ti, tj, cni, (float)cn[j], c6, dc, dcj_unused);
@@ -499,10 +538,9 @@ hipError_t launch_d3(const D3Params& p, const D3Grid& g, int n, const float4* x,
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_d3_cn, dim3(n), dim3(BLK), 0, s, p, g, x, type, cn);
+  if (p.cnref)
+    hipLaunchKernelGGL(k_d3_gauss, dim3((n + BLK - 1) / BLK), dim3(BLK), 0, s, p, n, type, cn, gw);
   if (c6tab) {
-    if (p.cnref)
-      hipLaunchKernelGGL(k_d3_gauss, dim3((n + BLK - 1) / BLK), dim3(BLK), 0, s, p, n, type, cn,
-                         gw);
     if (p.cnref) {
       hipLaunchKernelGGL(k_d3_c6rows, dim3(n), dim3(BLK), 0, s, p, n, type, cn, gw, c6tab);
     } else {
@@ -514,17 +552,17 @@ hipError_t launch_d3(const D3Params& p, const D3Grid& g, int n, const float4* x,
   if (p.damping == 1) {
     if (c6tab)
       hipLaunchKernelGGL((k_d3_disp<1, true>), dim3(n), dim3(BLK), 0, s, p, g, n, x, type, cn,
-                         c6tab, rows, forces);
+                         c6tab, p.cnref ? gw : nullptr, rows, forces);
     else
       hipLaunchKernelGGL((k_d3_disp<1, false>), dim3(n), dim3(BLK), 0, s, p, g, n, x, type, cn,
-                         c6tab, rows, forces);
+                         c6tab, p.cnref ? gw : nullptr, rows, forces);
   } else {
     if (c6tab)
       hipLaunchKernelGGL((k_d3_disp<2, true>), dim3(n), dim3(BLK), 0, s, p, g, n, x, type, cn,
-                         c6tab, rows, forces);
+                         c6tab, p.cnref ? gw : nullptr, rows, forces);
     else
       hipLaunchKernelGGL((k_d3_disp<2, false>), dim3(n), dim3(BLK), 0, s, p, g, n, x, type, cn,
-                         c6tab, rows, forces);
+                         c6tab, p.cnref ? gw : nullptr, rows, forces);
   }
   hipLaunchKernelGGL(k_d3_chain, dim3(n), dim3(BLK), 0, s, p, g, x, type, rows, forces);
   hipLaunchKernelGGL(k_d3_reduce, dim3(1), dim3(BLK), 0, s, n, rows, forces, totals);
