@@ -1642,7 +1642,8 @@ constexpr int64_t D3_C6TAB_MAX = 32768;  // n^2 C6 table up to 8.6 GB; beyond: C
 
 // stencil of bin offsets covering a sphere of radius sqrt(thr): R = floor(rc /
 // bin height) + 1 bins along each periodic axis (every (bin, image) pair once)
-std::vector<int> d3_stencil(float thr, const double binh[3], const int* pbc) {
+std::vector<int> d3_stencil(float thr, const double binh[3], const int* pbc,
+                            const double lat[3][3], const int nb[3], double hd, bool prune) {
   const double rc = std::sqrt((double)thr);
   int R[3];
   for (int k = 0; k < 3; ++k) R[k] = pbc[k] ? (int)std::floor(rc / binh[k]) + 1 : 0;
@@ -1650,6 +1651,14 @@ std::vector<int> d3_stencil(float thr, const double binh[3], const int* pbc) {
   for (int a = -R[0]; a <= R[0]; ++a)
     for (int b = -R[1]; b <= R[1]; ++b)
       for (int c = -R[2]; c <= R[2]; ++c) {
+        if (prune) {
+          // a cell whose centre is farther than rc + one full bin diagonal from
+          // the home cell's centre cannot hold a partner of any atom of it
+          double d[3];
+          for (int k = 0; k < 3; ++k)
+            d[k] = a * lat[0][k] / nb[0] + b * lat[1][k] / nb[1] + c * lat[2][k] / nb[2];
+          if (std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]) > rc + 2.0 * hd + 1e-9) continue;
+        }
         off.push_back(a);
         off.push_back(b);
         off.push_back(c);
@@ -1735,8 +1744,6 @@ int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* ce
     ts[s2] = type[i];
     bs[s2] = bin[i];
   }
-  const std::vector<int> ov = d3_stencil(h->p.rthr, binh, pbc);
-  const std::vector<int> oc = d3_stencil(h->p.cn_thr, binh, pbc);
   // half of the longest bin diagonal
   double hd = 0.0;
   for (int sa = -1; sa <= 1; sa += 2)
@@ -1746,6 +1753,8 @@ int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* ce
         d[c] = lat[0][c] / nb[0] + sa * lat[1][c] / nb[1] + sb * lat[2][c] / nb[2];
       hd = std::max(hd, 0.5 * std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]));
     }
+  const std::vector<int> ov = d3_stencil(h->p.rthr, binh, pbc, lat, nb, hd, all_pbc);
+  const std::vector<int> oc = d3_stencil(h->p.cn_thr, binh, pbc, lat, nb, hd, all_pbc);
   HIPCHK(hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
   const size_t nn = (size_t)std::max<int64_t>(n, 1);
