@@ -458,7 +458,8 @@ class Trainer:
             if isinstance(loss_def, EWCLoss) and loss_def.device is None:
                 loss_def.to(self.device)
             loss_def.static = self.hip_graph
-        self._graphed = GraphedRehearsalStep(self) if self.hip_graph else None
+        self._graphed = GraphedRehearsalStep(self, config.get('hip_graph_max', 16)) \
+            if self.hip_graph else None
 
     # ---- the pieces of one step
     def zero_grad(self):
@@ -582,9 +583,12 @@ class GraphedRehearsalStep:
     step's.  Everything inside is device-side: the model takes the prebuilt
     ConvGraphs, the losses run in static mode, the optimizer is capturable."""
 
-    def __init__(self, trainer):
+    def __init__(self, trainer, max_graphs=16):
         self.tr = trainer
         self.cache = {}
+        # each captured shape keeps its own memory pool: beyond max_graphs
+        # distinct shapes (variable-size datasets) new shapes run eagerly
+        self.max_graphs = int(max_graphs)
 
     @staticmethod
     def _sig(b):
@@ -644,6 +648,8 @@ class GraphedRehearsalStep:
         key = (self._sig(batch), self._sig(mem))
         ent = self.cache.get(key)
         if ent is None:
+            if len(self.cache) >= self.max_graphs:
+                return self.tr._rehearsal_body(batch, mem)
             ent = self.cache[key] = self._capture(batch, mem)
         for dst, src in ((ent['b'], batch), (ent['m'], mem)):
             for k, v in src.items():

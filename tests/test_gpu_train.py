@@ -227,6 +227,10 @@ def test_graphed_rehearsal_step_equals_eager():
     fe, le, _ = run(False, batches)
     fg, lg, tr = run(True, batches)
     assert len(tr._graphed.cache) == 2
+    tr._graphed.max_graphs = 2      # a third shape now runs eagerly
+    third = (coll([12], (2, 2, 1)), coll([13], (2, 2, 1)))
+    assert all(torch.isfinite(t).all() for t in tr.rehearsal_step(*third))
+    assert len(tr._graphed.cache) == 2
     for a, b in zip(le, lg):
         assert abs(a[0] - b[0]) <= 1e-5 * abs(a[0]) and abs(a[1] - b[1]) <= 1e-5 * abs(a[1])
     # Adam normalises every component: where a gradient is ~0, fp32 rounding
