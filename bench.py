@@ -14,9 +14,16 @@ N > 1: one process per GPU (torchrun), spatial domain decomposition
 (23^3 cells per rank in a px x py x pz brick grid, e.g. 46^3 cells = 778,688
 atoms on 8 GPUs) -- weak scaling -- and every step does the per-layer ghost
 feature exchange, the reverse gradient and ghost-force exchanges (RCCL
-all_to_all) and the energy/virial all_reduce.  The timed region is bracketed
-by barrier + synchronize; the max over ranks is reported and value = total
-atoms / that time.
+all_to_all) and the energy/virial all_reduce.  ``--strong``: one 46^3-cell
+box (778,688 atoms, north_star's 800k config) split over the N ranks, N = 1
+included (one device holds it).  The timed region is bracketed by barrier +
+synchronize; the max over ranks is reported and value = total atoms / that
+time.  The rank graph is uploaded once (a step moves no host data, like the
+single-device step).
+
+Before timing, a full-size property check runs at the same size (a displaced
+8-atom cell tiled to the box: E = k^3 E_cell, per-image forces equal; through
+the halo exchanges when N > 1) and the run fails if it does not hold.
 
 Also reported: ``roofline`` for the dominant kernel class (HIP-event timed
 inside the library, on the stream the kernels run on) and ``cpu_baseline``
@@ -48,7 +55,15 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--cells', type=int, default=23, help='n for an n^3 conventional-cell box')
+    ap.add_argument('--cells', type=int, default=None,
+                    help='n for an n^3 conventional-cell box: per rank (weak scaling, default '
+                         '23) or in total (--strong, default 46)')
+    ap.add_argument('--strong', action='store_true',
+                    help='strong scaling: one --cells^3 box (default 46^3 = 778,688 atoms, '
+                         'north_star config 4) split over the N ranks')
+    ap.add_argument('--no-parity-check', action='store_true')
+    ap.add_argument('--cpu-cells', type=int, default=6,
+                    help='cpu_baseline sample: n^3 cells (6 -> 1,728 atoms)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--same-device', action='store_true',
@@ -123,10 +138,12 @@ def pmc_traffic(kernel, cells):
     return None
 
 
-def cpu_baseline(seconds):
+def cpu_baseline(seconds, cells):
     """Oracle (plain-PyTorch CPU restatement of the reference) on a bounded
-    sample: 216-atom Si box (3x3x3 cells, same recipe), repeated until
-    ~`seconds` of CPU work, all host threads."""
+    sample of the same workload: a cells^3 Si box (default 6^3 = 1,728 atoms,
+    where the reference CPU path is already at its flat large-box throughput,
+    SURVEY.md 6), the same recipe as the bench box, timed for >= 1 evaluation
+    and ~`seconds` of CPU work on the host's thread share."""
     from oracle.neighbor import neighbor_list
     from oracle.sevennet_ref import SevenNet0Ref
     from sevennet_finetuning_amd.structures import si_diamond
@@ -134,23 +151,79 @@ def cpu_baseline(seconds):
     # whole machine there, and oversubscribing it stalls the run
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get('OMP_NUM_THREADS', '16')))
     torch.set_num_threads(threads)
-    log(f'cpu baseline: {threads} threads, ~{seconds:.0f} s')
+    log(f'cpu baseline: {threads} threads, {cells}^3 cells, ~{seconds:.0f} s')
     ref = SevenNet0Ref(dtype=torch.float32)
-    pos, cell = si_diamond((3, 3, 3), sigma=0.05)
+    pos, cell = si_diamond((cells,) * 3, sigma=0.05)
     ei, sh = neighbor_list(pos, cell, 5.0)
     args = (torch.tensor(pos, dtype=torch.float32), torch.full((len(pos),), 69),
             torch.tensor(ei), torch.tensor(sh, dtype=torch.float32),
             torch.tensor(cell, dtype=torch.float32))
-    ref(*args)  # warm
     t0, n = time.perf_counter(), 0
-    while time.perf_counter() - t0 < seconds:
+    while n == 0 or time.perf_counter() - t0 < seconds:
         ref(*args)
         n += 1
     dt = time.perf_counter() - t0
     return {'value': round(n * len(pos) / dt, 2), 'unit': 'atoms/s', 'cores': threads,
             'kind': 'port',
-            'sample': f'{n} energy+force+stress evals of a 216-atom Si box (3x3x3 cells, '
-                      f'6048 edges) in {dt:.1f} s, oracle/sevennet_ref.py fp32, torch CPU'}
+            'sample': f'{n} energy+force+stress evals of a {len(pos)}-atom Si box ({cells}^3 '
+                      f'cells, {ei.shape[1]} edges) in {dt:.1f} s, oracle/sevennet_ref.py fp32, '
+                      f'torch CPU, first call included',
+            'reference_context': 'the reference frozen TorchScript CPU path measured in the '
+                                 'survey container: 272 atoms/s at 10,648 atoms, 8 threads '
+                                 '(SURVEY.md 8d); not re-run here (a shipped program), not '
+                                 'part of vs_baseline'}
+
+
+def parity_check_serial(model, cells, device):
+    """Full-size property check outside the timed region: a displaced 8-atom
+    cell tiled cells^3 times (same size as the bench box) has E = cells^3
+    E_cell and per-image forces equal to the cell's (tests/test_gpu_fullsize.py)."""
+    from sevennet_finetuning_amd.neighbor import DeviceNeighborList, neighbor_list
+    from sevennet_finetuning_amd.structures import si_diamond, tile
+    pos1, cell1 = si_diamond((1, 1, 1), sigma=0.05)
+    ei, sh = neighbor_list(pos1, cell1, 5.0)
+    vec1 = pos1[ei[1]] + sh @ cell1 - pos1[ei[0]]
+    t = lambda a, dt=torch.int32: torch.as_tensor(a, dtype=dt, device=device)
+    one = model.energy_forces(t(np.full(8, 69)), t(ei[0]), t(ei[1]), t(vec1, torch.float32))
+    e1, f1 = float(one['energy']), one['forces'].cpu().numpy()
+    posk, cellk = tile(pos1, cell1, (cells,) * 3)
+    c, nb, _, vec = DeviceNeighborList(device)(posk, cellk, 5.0)
+    big = model.energy_forces(t(np.full(len(posk), 69)), c, nb, vec)
+    k3 = cells ** 3
+    de = abs(float(big['energy']) - k3 * e1) / abs(k3 * e1)
+    df = float(np.abs(big['forces'].cpu().numpy().reshape(k3, 8, 3) - f1[None]).max())
+    return {'property': f'tiled displaced 8-atom cell, {len(posk)} atoms: E = k^3 E_cell, '
+                        'per-image forces equal', 'energy_rel_err': de, 'max_force_err': df,
+            'ok': bool(de <= 2e-6 and df <= 1e-4)}
+
+
+def parity_check_parallel(model, cells_total, grid, rank, device):
+    """Same property through the decomposed path (halo exchanges over the
+    process group): tiled 8-atom cell over the whole box."""
+    from sevennet_finetuning_amd.neighbor import neighbor_list
+    from sevennet_finetuning_amd.parallel import HipSegmentEngine, ParallelE3GNN, build_rank_graph
+    from sevennet_finetuning_amd.structures import si_diamond, tile
+    pos1, cell1 = si_diamond((1, 1, 1), sigma=0.05)
+    ei, sh = neighbor_list(pos1, cell1, 5.0)
+    vec1 = pos1[ei[1]] + sh @ cell1 - pos1[ei[0]]
+    t = lambda a, dt=torch.int32: torch.as_tensor(a, dtype=dt, device=device)
+    one = model.energy_forces(t(np.full(8, 69)), t(ei[0]), t(ei[1]), t(vec1, torch.float32))
+    e1, f1 = float(one['energy']), one['forces'].cpu().numpy()
+    posk, cellk = tile(pos1, cell1, cells_total)
+    rg = build_rank_graph(posk, cellk, np.full(len(posk), 69), 5.0, grid, rank)
+    drv = ParallelE3GNN(HipSegmentEngine(model))
+    drv.set_graph(rg)
+    out = drv.evaluate()
+    k3 = int(np.prod(cells_total))
+    de = abs(float(out['energy']) - k3 * e1) / abs(k3 * e1)
+    f = out['forces'].cpu().numpy()
+    df = float(np.abs(f - f1[np.asarray(out['owned']) % 8]).max()) if len(f) else 0.0
+    t = torch.tensor([df], dtype=torch.float64, device=device)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    df = float(t)
+    return {'property': f'tiled displaced 8-atom cell, {len(posk)} atoms over the ranks: '
+                        'E = k^3 E_cell, per-image forces equal', 'energy_rel_err': de,
+            'max_force_err': df, 'ok': bool(de <= 2e-6 and df <= 1e-4)}
 
 
 def main():
@@ -172,24 +245,35 @@ def main():
 
     from sevennet_finetuning_amd.model import E3GNNModel
     model = E3GNNModel(device=device)
+    cells = args.cells or (46 if args.strong else 23)
+    scaling = 'strong' if args.strong else 'weak'
+    parity = None
     if world == 1:
-        box = make_box(args.cells, device)
+        box = make_box(cells, device)
         n, E = box['n'], box['E']
         n_rank, parallelism = n, 'single'
         log(f'box: {n} atoms, {E} edges; workspace after first step follows')
+        if not args.no_parity_check:
+            parity = parity_check_serial(model, cells, device)
+            log(f'parity check: {parity}')
 
         def step():
             return model.energy_forces(box['types'], box['center'], box['nbr'], box['vec'])
     else:
-        # spatial decomposition (parallel.py): an (args.cells * grid) box, one
-        # brick of args.cells^3 cells per rank, halo exchange per layer over RCCL
+        # spatial decomposition (parallel.py): weak -- an (cells * grid) box, one
+        # brick of cells^3 per rank; strong -- one cells^3 box split over the
+        # ranks; halo exchange per layer over RCCL
         from sevennet_finetuning_amd.parallel import (HipSegmentEngine, ParallelE3GNN,
                                                       brick_grid, build_rank_graph)
         from sevennet_finetuning_amd.structures import si_diamond
         grid = brick_grid(world)
-        pos, cell = si_diamond(tuple(args.cells * g for g in grid), sigma=0.05)
+        total = (cells,) * 3 if args.strong else tuple(cells * g for g in grid)
+        pos, cell = si_diamond(total, sigma=0.05)
         n = len(pos)
         rg = build_rank_graph(pos, cell, np.full(n, 69), 5.0, grid, rank)
+        if not args.no_parity_check:
+            parity = parity_check_parallel(model, total, grid, rank, device)
+            log(f'parity check: {parity}')
         drv = ParallelE3GNN(HipSegmentEngine(model))
         drv.set_graph(rg)
         E, n_rank = len(rg.center), rg.n_local
@@ -199,6 +283,9 @@ def main():
 
         def step():
             return drv.evaluate()
+
+    if parity is not None and not parity['ok']:
+        raise RuntimeError(f'full-size parity check failed: {parity}')
 
     def barrier():
         if world > 1:
@@ -256,7 +343,7 @@ def main():
         tot_flops = sum(v['flops'] for v in stats.values())
         roofline['step_tflops'] = round(tot_flops / (ms * 1e9), 3)
         roofline['rocprof_kernel'] = rp_name
-        roofline['traffic'] = pmc_traffic(rp_name, args.cells)
+        roofline['traffic'] = pmc_traffic(rp_name, cells)
 
     nl = None
     if world == 1 and not args.profile_only:
@@ -264,21 +351,23 @@ def main():
         log(f'neighbour list: device {nl["device_ms"]} ms, host {nl["host_ms"]} ms')
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1 and not args.profile_only:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu = cpu_baseline(args.cpu_seconds, args.cpu_cells)
 
     if rank == 0:
         line = {
             'metric': 'atoms/sec energy+force, SevenNet-0 lmax=2, 100k-atom box',
             'value': round(value, 2), 'unit': 'atoms/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+            'higher_is_better': True, 'scaling': scaling, 'vs_baseline': None, 'dtype': 'f32',
             'data': 'synthetic Si diamond box, default_rng(0) 0.05 A displacements; '
                     'SevenNet-0 weights (reference opt_params_sevenn.pt)',
             'config': {'workload': f'SevenNet-0 energy+force+virial, {n}-atom periodic Si box '
-                                   f'({args.cells}^3 cells per rank), {E} edges on rank 0',
+                                   f'({cells}^3 cells{"" if args.strong else " per rank"}), '
+                                   f'{E} edges on rank 0',
                        'atoms_per_rank': n_rank, 'edges_per_rank': E,
                        'parallelism': parallelism},
             'energy': energy,
+            'parity_check': parity,
             'roofline': roofline,
             'cpu_baseline': cpu,
             'neighbor_list': nl,

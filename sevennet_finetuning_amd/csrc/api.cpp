@@ -790,10 +790,13 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   if (n_local < 0 || n_ghost < 0 || n_edges < 0) return fail(E3GNN_ERR_ARG, "negative size");
   if (n_local + n_ghost > (1LL << 30) || n_edges > (1LL << 31) - 1)
     return fail(E3GNN_ERR_ARG, "graph too large for int32 indices");
-  // the fused kernels address node features through 32-bit buffer offsets
-  if ((n_local + n_ghost) * 480LL * 4 > 0x7fffffffLL || n_local * 3136LL * 4 > 0x7fffffffLL)
-    return fail(E3GNN_ERR_ARG,
-                "more than 171k owned atoms (or 1.1M nodes) per device: shard the system");
+  // the fused kernels gather node-feature rows through one 32-bit buffer
+  // descriptor (n x 480 fp32 < 2 GiB); dE/dagg rows are addressed per edge tile
+  // (any size), except on the per-neighbour dE/dx variant (E3GNN_BWD_X=node)
+  if ((n_local + n_ghost) * 480LL * 4 > 0x7fffffffLL)
+    return fail(E3GNN_ERR_ARG, "more than 1.1M atoms (owned + ghost) per device: shard the system");
+  if (!c->bwd_edge && n_local * 3136LL * 4 > 0x7fffffffLL)
+    return fail(E3GNN_ERR_ARG, "E3GNN_BWD_X=node supports at most 171k owned atoms per device");
   if ((n_local + n_ghost > 0 && !type) || (n_edges > 0 && (!edge_center || !edge_nbr || !edge_vec)))
     return fail(E3GNN_ERR_ARG, "null input array");
   e3gnn_model* m = c->m;

@@ -587,9 +587,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
   const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rx =
       EDGE ? rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4) : rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
-  // dE/dagg rows through a descriptor: 32-bit lane offsets (the host checks
-  // n_centers * DM * 4 < 2^31), scalar path/channel offsets
-  const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
+  // dE/dagg rows through a descriptor (32-bit lane offsets, scalar
+  // path/channel offsets).  EDGE: based at the tile's first centre -- 16
+  // consecutive CSR edges span at most 16 centres, so the offsets stay small
+  // at any system size; per neighbour node (last block, DM = 224): whole array
+  // (the host checks n_centers * 224 * 4 < 2^31)
+  const __amdgpu_buffer_rsrc_t RgAll = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
   if constexpr (!EDGE)
     for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
 
@@ -601,8 +604,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
     const int er = (q0 + col < qe) ? (EDGE ? q0 + col : src_perm[q0 + col]) : -1;
     // EDGE: the slot's gathered row (padded slots: row 0, w = 0 there)
     const int vx = EDGE ? (er >= 0 ? nbr[er] : 0) * L::DX * 4 : 0;
+    int cb = 0, nc = n_centers;  // centre rows [cb, cb + nc) under the descriptor
+    if constexpr (EDGE) {
+      cb = __builtin_amdgcn_readfirstlane(center[q0]);
+      nc = __builtin_amdgcn_readfirstlane(center[qe - 1]) - cb + 1;
+    }
+    const __amdgpu_buffer_rsrc_t Rg =
+        EDGE ? rsrc_bytes(gagg + (int64_t)cb * L::DM, (int64_t)nc * L::DM * 4) : RgAll;
     // padded slots read past the end of the descriptor: 0
-    const int vg = (er >= 0 ? center[er] * L::DM : n_centers * L::DM) * 4;
+    const int vg = (er >= 0 ? (center[er] - cb) * L::DM : nc * L::DM) * 4;
     float y[9];
 #pragma unroll
     for (int q = 0; q < 9; ++q) y[q] = er >= 0 ? Y[(int64_t)er * 9 + q] : 0.f;
@@ -806,13 +816,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_
   const WRes R = make_wres(W, L::W);
   int src[4], vg[4];
   load_tile_edges(nbr, Y, e0, end, lane, src, ybuf);
+  // dE/dagg rows of the tile's centres [cb, cb + nc): descriptor based at the
+  // first one (16 consecutive CSR edges: small offsets at any system size)
+  const int cb = __builtin_amdgcn_readfirstlane(center[e0]);
+  const int nc = __builtin_amdgcn_readfirstlane(center[min(e0 + 16, end) - 1]) - cb + 1;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int e = e0 + 4 * g + r;
-    vg[r] = (e < end ? center[e] * L::DM : n_centers * L::DM) * 4;  // padded: reads 0
+    vg[r] = (e < end ? (center[e] - cb) * L::DM : nc * L::DM) * 4;  // padded: reads 0
   }
   const __amdgpu_buffer_rsrc_t Rh = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
-  const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
+  const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg + (int64_t)cb * L::DM, (int64_t)nc * L::DM * 4);
   int vh[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) vh[r] = src[r] * L::DX * 4;

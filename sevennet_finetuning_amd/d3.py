@@ -175,10 +175,21 @@ class D3Calculator:
             self.pair.coeff(elems)
         types = np.searchsorted(np.asarray(elems), z)
         cell = np.asarray(atoms.get_cell(), dtype=np.float64).reshape(3, 3)
-        out = self.pair.compute(atoms.get_positions(), cell, types, atoms.get_pbc())
+        pbc = np.asarray(atoms.get_pbc(), dtype=bool).reshape(-1)
+        pos = np.asarray(atoms.get_positions(), dtype=np.float64)
         vol = abs(np.linalg.det(cell))
+        molecule = not pbc.any()
+        if molecule and not vol > 1e-12:
+            # isolated molecule without a cell: any box works when no axis is
+            # periodic (one bin per axis, no images); no stress
+            ext = (pos.max(0) - pos.min(0)) if len(pos) else np.zeros(3)
+            cell = np.diag(np.maximum(ext, 1.0) + 1.0)
+        elif not vol > 1e-12:
+            raise ValueError('D3: periodic axes need a non-singular cell')
+        out = self.pair.compute(pos, cell, types, pbc)
         v = out['virial']
         self.results = {'energy': out['energy'], 'free_energy': out['energy'],
-                        'forces': out['forces'],
-                        'stress': -np.array([v[0], v[1], v[2], v[5], v[4], v[3]]) / vol}
+                        'forces': out['forces']}
+        if not molecule:
+            self.results['stress'] = -np.array([v[0], v[1], v[2], v[5], v[4], v[3]]) / vol
         return self.results

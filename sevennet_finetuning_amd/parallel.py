@@ -25,7 +25,8 @@ Here, one process per GPU:
   xGMI with backend "nccl"; host-staged with "gloo"), packing and unpacking
   with the library's halo kernels.  Reverse exchanges accumulate per peer
   block in rank order (deterministic; no atomics).
-* ``ParallelE3GNN`` runs one evaluation: graph_set, 5 x (halo forward, layer
+* ``ParallelE3GNN.set_graph`` uploads a rank graph once per neighbour list;
+  ``evaluate`` runs one evaluation: graph_set, 5 x (halo forward, layer
   forward), readout, 5 x (layer backward, halo reverse), forces, reverse of
   the ghost forces, one all_reduce of (energy, virial).
 
@@ -215,15 +216,24 @@ class HipSegmentEngine:
     def _s(self):
         return self.m.stream_handle()
 
-    def graph_set(self, rg):
+    def upload(self, rg):
+        """Rank graph -> resident device tensors, once per neighbour-list build
+        (the reference rebuilds its graph tensors per LAMMPS neighbour list,
+        pair_e3gnn_parallel.cpp:258-314), so a step moves no host data."""
         dev = self.device
         t32 = lambda a: torch.as_tensor(np.asarray(a, dtype=np.int32), device=dev)
         self.n = rg.n_local + rg.n_ghost
         self.nl = rg.n_local
+        self.n_ghost = rg.n_ghost
         self._in = (t32(rg.types), t32(rg.center), t32(rg.nbr),
-                    torch.as_tensor(rg.vec, dtype=torch.float32, device=dev))
+                    torch.as_tensor(np.asarray(rg.vec, dtype=np.float32), device=dev))
+
+    def graph_set(self):
+        """Per evaluation: CSR indices, transposed CSR, edge embedding and
+        layer-0 features from the resident tensors (same work as the
+        single-device e3gnn_energy_forces)."""
         ty, c, nb, v = self._in
-        _lib.check(self.lib.e3gnn_graph_set(self.ctx, rg.n_local, rg.n_ghost, len(rg.center),
+        _lib.check(self.lib.e3gnn_graph_set(self.ctx, self.nl, self.n_ghost, int(c.numel()),
                                             ty.data_ptr(), c.data_ptr(), nb.data_ptr(),
                                             v.data_ptr(), self._s()))
 
@@ -288,10 +298,13 @@ class ParallelE3GNN:
         self.halo = None
 
     def set_graph(self, rg):
+        """New neighbour list: handshake, halo index lists and the one-time
+        upload of the rank graph; ``evaluate`` then moves no host data."""
         if rg.send_rows is None:
             handshake(rg, self.group, self._comm_device())
         self.rg = rg
         self.halo = Halo(rg, self.eng, self.group)
+        self.eng.upload(rg)
 
     def _comm_device(self):
         if dist.is_initialized() and dist.get_backend(self.group) == 'nccl':
@@ -300,7 +313,7 @@ class ParallelE3GNN:
 
     def evaluate(self):
         eng, halo, L = self.eng, self.halo, self.eng.num_layers
-        eng.graph_set(self.rg)
+        eng.graph_set()
         for t in range(L):
             if t > 0:
                 halo.forward('x', t)          # forward_comm of the layer-t features

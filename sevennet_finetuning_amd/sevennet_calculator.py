@@ -132,7 +132,11 @@ class SevenNetD3Calculator(Calculator):
         r = dict(a.results)
         r['energy'] = r['free_energy'] = a.results['energy'] + b['energy']
         r['forces'] = a.results['forces'] + b['forces']
-        r['stress'] = a.results['stress'] + b['stress']
+        # stress only where both terms define one (periodic cells)
+        if 'stress' in a.results and 'stress' in b:
+            r['stress'] = a.results['stress'] + b['stress']
+        else:
+            r.pop('stress', None)
         self.results = r
         self.atoms = atoms
         return r

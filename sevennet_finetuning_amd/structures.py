@@ -53,6 +53,19 @@ def diamond_primitive(cells, a=SI_A, sigma=0.05, seed=0):
     return pos, cell
 
 
+def tile(pos, cell, reps):
+    """Periodic supercell of (pos, cell): reps = (k1, k2, k3) copies along the
+    lattice vectors, image-major (atom a of image m is row m * len(pos) + a).
+    Every image has the same environment, so E(supercell) = k1 k2 k3 E(cell)
+    and the forces repeat per image (the full-size parity property)."""
+    reps = tuple(int(k) for k in reps)
+    pos = np.asarray(pos, dtype=np.float64)
+    cell = np.asarray(cell, dtype=np.float64)
+    shifts = np.array(list(itertools.product(*[range(k) for k in reps])), dtype=np.float64)
+    big = (shifts @ cell)[:, None, :] + pos[None]
+    return big.reshape(-1, 3), cell * np.array(reps, dtype=np.float64)[:, None]
+
+
 def mixed_symbols(n, seed=1):
     rng = np.random.default_rng(seed)
     return [MIXED_SYMBOLS[i] for i in rng.integers(0, len(MIXED_SYMBOLS), n)]

@@ -644,7 +644,24 @@ class GraphedRehearsalStep:
             loss, mloss = tr._rehearsal_body(sb, sm, graphs)
         return {'g': g, 'b': sb, 'm': sm, 'graphs': graphs, 'out': (loss, mloss)}
 
+    @staticmethod
+    def _centre_sorted(b):
+        """The captured model takes a prebuilt ConvGraph, i.e. edges CSR-sorted
+        by centre (the eager model sorts them itself): stable device argsort
+        of the per-edge entries, no host sync."""
+        ei = b.get(KEY.EDGE_IDX)
+        if ei is None or ei.shape[1] < 2:
+            return b
+        perm = torch.argsort(ei[0], stable=True)
+        out = dict(b)
+        out[KEY.EDGE_IDX] = ei[:, perm]
+        for k in (KEY.EDGE_VEC, KEY.CELL_SHIFT):
+            if k in b and torch.is_tensor(b[k]):
+                out[k] = b[k][perm]
+        return out
+
     def __call__(self, batch, mem):
+        batch, mem = self._centre_sorted(batch), self._centre_sorted(mem)
         key = (self._sig(batch), self._sig(mem))
         ent = self.cache.get(key)
         if ent is None:

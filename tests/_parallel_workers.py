@@ -39,11 +39,19 @@ def worker(rank, world, port, name, engine, out):
         eng = HipSegmentEngine(E3GNNModel(device='cuda:0'))
     drv = ParallelE3GNN(eng)
     drv.set_graph(rg)
+    # several evaluations of one neighbour list: the rank graph is uploaded
+    # once (set_graph), every evaluation gives the same result
     res = drv.evaluate()
+    first = (float(res['energy']), res['forces'].detach().cpu().clone())
+    for _ in range(2):
+        res = drv.evaluate()
+    same = first[0] == float(res['energy']) and torch.equal(first[1], res['forces'].detach().cpu())
+    uploads = getattr(eng, 'uploads', -1)
     f, ea = gather_all(res, len(pos))
     if rank == 0:
         np.savez(out, energy=float(res['energy']), virial=res['virial'].cpu().numpy(),
-                 forces=f.numpy(), atomic=ea.numpy(),
+                 forces=f.numpy(), atomic=ea.numpy(), repeat_same=np.array([same]),
+                 uploads=np.array([uploads]),
                  n_ghost=np.array([rg.n_ghost]), n_local=np.array([rg.n_local]))
     dist.barrier()
     dist.destroy_process_group()

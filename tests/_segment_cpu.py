@@ -31,17 +31,23 @@ class CpuSegmentEngine:
         self.num_layers = self.ref.nlayer
 
     # -- graph
-    def graph_set(self, rg):
-        r = self.ref
+    uploads = 0
+
+    def upload(self, rg):
+        self.uploads += 1
         self.nl, self.n = rg.n_local, rg.n_local + rg.n_ghost
         self.center = torch.as_tensor(rg.center, dtype=torch.int64)
         self.nbr = torch.as_tensor(rg.nbr, dtype=torch.int64)
-        self.vec = torch.as_tensor(rg.vec, dtype=self.dtype).clone().requires_grad_(True)
+        self._vec = torch.as_tensor(rg.vec, dtype=self.dtype).clone()
+        self._types = torch.as_tensor(rg.types, dtype=torch.int64)
+
+    def graph_set(self):
+        r = self.ref
+        self.vec = self._vec.clone().requires_grad_(True)
         self.emb = r.edge_embedding(self.vec.norm(dim=-1))
         self.sh = spherical_harmonics_l2(self.vec)
         nsp = len(r.symbols)
-        onehot = torch.nn.functional.one_hot(torch.as_tensor(rg.types, dtype=torch.int64),
-                                             nsp).to(self.dtype)
+        onehot = torch.nn.functional.one_hot(self._types, nsp).to(self.dtype)
         x0 = (onehot @ r.t('onehot_to_feature_x.linear.weight').reshape(nsp, -1)) / math.sqrt(nsp)
         self.x = {0: x0.detach()}
         self.out = {}

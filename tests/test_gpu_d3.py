@@ -171,3 +171,32 @@ def test_sevennet_d3_calculator_is_the_sum():
     assert np.allclose(both.results['forces'], a.results['forces'] + b['forces'], atol=1e-6)
     assert np.allclose(both.results['stress'], a.results['stress'] + b['stress'], atol=1e-9)
     assert both.results['energy'] < a.results['energy']   # dispersion binds
+
+
+def test_sevennet_d3_calculator_molecule():
+    """A molecule without cell or pbc: energies and forces summed, no stress
+    (neither term defines one), no division by the zero cell volume."""
+    from sevennet_finetuning_amd.d3 import D3Calculator
+    from sevennet_finetuning_amd.sevennet_calculator import (SevenNetCalculator,
+                                                             SevenNetD3Calculator)
+    from sevennet_finetuning_amd.structures import Atoms
+    rng = np.random.default_rng(11)
+    pos = rng.uniform(0, 5.0, (10, 3))
+    keep = [0]
+    for i in range(1, len(pos)):
+        if np.min(np.linalg.norm(pos[keep] - pos[i], axis=1)) > 1.2:
+            keep.append(i)
+    pos = pos[keep]
+    z = np.array([6, 8, 1, 7, 6, 1, 8, 6, 1, 1])[:len(pos)]
+    at = Atoms(numbers=z, positions=pos, cell=None, pbc=False)
+    both = SevenNetD3Calculator(device='cuda:0')
+    both.calculate(at)
+    assert 'stress' not in both.results
+    a = SevenNetCalculator(device='cuda:0')
+    a.calculate(at)
+    b = D3Calculator().calculate(at)
+    assert 'stress' not in b
+    ref = _oracle(pos, np.eye(3) * 30.0, z, 'damp_bj', 'pbe', pbc=(False, False, False))
+    assert abs(b['energy'] - ref['energy']) <= 1e-5 * abs(ref['energy'])
+    assert abs(both.results['energy'] - (a.results['energy'] + b['energy'])) < 1e-6
+    assert np.allclose(both.results['forces'], a.results['forces'] + b['forces'], atol=1e-6)

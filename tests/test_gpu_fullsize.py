@@ -1,0 +1,125 @@
+"""Correctness at the sizes the headline numbers are quoted on (BASELINE.json
+configs 3 and 4): the 97,336-atom box (23^3 conventional Si cells, 2.7M
+edges) and the 778,688-atom box (46^3 cells, 21.8M edges) on one device.
+
+The oracle cannot evaluate these sizes in test time, so parity is carried by
+size-independent properties (force_output.py:74-130 defines
+the quantities):
+* supercell property: a displaced 8-atom cell tiled k^3 times has
+  E = k^3 E_cell, per-image forces equal to the cell's and the same stress;
+  the 8-atom cell itself is checked against the fp64 oracle here, so the
+  property ties the full-size result to the oracle;
+* the fused kernels against the independent unfused v1 kernels on the bench
+  box (random per-atom displacements, every atom's environment distinct);
+* bitwise run-to-run determinism on the bench box.
+"""
+import numpy as np
+import pytest
+import torch
+
+from _systems import load_manifest_symbols, oracle_eval
+
+pytestmark = pytest.mark.gpu
+SYMS = load_manifest_symbols()
+SI = SYMS.index('Si')
+F_TOL = 1e-4     # eV/A, north_star
+E_RTOL = 2e-6
+S_TOL = 2e-6     # eV/A^3
+
+
+@pytest.fixture(scope='module')
+def model():
+    from sevennet_finetuning_amd.model import E3GNNModel
+    assert torch.cuda.is_available(), 'GPU tests need a HIP device'
+    return E3GNNModel(device='cuda:0')
+
+
+@pytest.fixture(scope='module')
+def cell8():
+    """Displaced 8-atom Si cell: GPU result (host neighbour list) + oracle check."""
+    from sevennet_finetuning_amd.structures import si_diamond
+    from sevennet_finetuning_amd.neighbor import neighbor_list
+    pos, cell = si_diamond((1, 1, 1), sigma=0.05)
+    types = np.full(len(pos), SI)
+    ref = oracle_eval(pos, cell, types)
+    return pos, cell, types, ref
+
+
+def eval_box(model, pos, cell, types):
+    """Device neighbour list + e3gnn_energy_forces; host numpy results."""
+    from sevennet_finetuning_amd.neighbor import DeviceNeighborList
+    dev = model.device
+    nl = DeviceNeighborList(dev)
+    c, nb, _, vec = nl(pos, cell, model.cutoff)
+    ty = torch.as_tensor(types, dtype=torch.int32, device=dev)
+    out = model.energy_forces(ty, c, nb, vec)
+    vol = abs(np.linalg.det(cell))
+    res = {'energy': float(out['energy']), 'forces': out['forces'].cpu().numpy(),
+           'stress': out['virial'].cpu().numpy() / vol, 'n_edges': int(c.numel())}
+    del c, nb, vec, out
+    return res
+
+
+def small(model, pos, cell, types):
+    from sevennet_finetuning_amd.neighbor import neighbor_list
+    ei, sh = neighbor_list(pos, cell, model.cutoff)
+    out = model({'x': torch.tensor(types), 'pos': torch.tensor(pos, dtype=torch.float32),
+                 'edge_index': torch.tensor(ei), 'pbc_shift': torch.tensor(sh, dtype=torch.float32),
+                 'cell_lattice_vectors': torch.tensor(cell, dtype=torch.float32)})
+    return {'energy': float(out['inferred_total_energy']),
+            'forces': out['inferred_force'].cpu().numpy(),
+            'stress': out['inferred_stress'].cpu().numpy()}
+
+
+@pytest.mark.parametrize('k', [23, 46], ids=['97k', '778k'])
+def test_supercell_property(model, cell8, k):
+    """E = k^3 E_cell, forces repeat per image, stress equal (k = 23: config 3,
+    97,336 atoms; k = 46: config 4's 778,688 atoms on ONE device)."""
+    from sevennet_finetuning_amd.structures import tile
+    pos, cell, types, ref = cell8
+    one = small(model, pos, cell, types)
+    assert abs(one['energy'] - ref['energy']) <= E_RTOL * abs(ref['energy'])
+    assert np.abs(one['forces'] - ref['forces']).max() <= F_TOL
+    posk, cellk = tile(pos, cell, (k, k, k))
+    big = eval_box(model, posk, cellk, np.tile(types, k ** 3))
+    assert big['n_edges'] == 28 * len(posk)
+    assert abs(big['energy'] - k ** 3 * one['energy']) <= E_RTOL * abs(big['energy'])
+    fk = big['forces'].reshape(k ** 3, len(pos), 3)
+    assert np.abs(fk - one['forces'][None]).max() <= F_TOL
+    assert np.abs(big['stress'] - one['stress']).max() <= S_TOL
+    # and against the fp64 oracle directly
+    assert np.abs(fk - ref['forces'][None]).max() <= F_TOL
+    assert abs(big['energy'] / k ** 3 - ref['energy']) <= E_RTOL * abs(ref['energy'])
+
+
+@pytest.fixture(scope='module')
+def bench_box():
+    from sevennet_finetuning_amd.structures import si_diamond
+    pos, cell = si_diamond((23, 23, 23), sigma=0.05)
+    return pos, cell, np.full(len(pos), SI)
+
+
+def test_fused_matches_v1_at_97k(model, bench_box):
+    """Config 3 box (random per-atom displacements): the fused kernels and the
+    independent unfused v1 kernels (w materialised in HBM) agree."""
+    pos, cell, types = bench_box
+    try:
+        model.set_impl('v1')
+        a = eval_box(model, pos, cell, types)
+    finally:
+        model.set_impl('fused')
+    b = eval_box(model, pos, cell, types)
+    assert a['n_edges'] == b['n_edges'] == 2725408
+    assert abs(a['energy'] - b['energy']) <= E_RTOL * abs(a['energy'])
+    assert np.abs(a['forces'] - b['forces']).max() <= 5e-5
+    assert np.abs(a['stress'] - b['stress']).max() <= 1e-6
+    assert np.abs(b['forces'].sum(0)).max() < 1e-2   # sum of 97k f32 forces
+
+
+def test_bitwise_determinism_at_97k(model, bench_box):
+    pos, cell, types = bench_box
+    a = eval_box(model, pos, cell, types)
+    b = eval_box(model, pos, cell, types)
+    assert a['energy'] == b['energy']
+    assert np.array_equal(a['forces'], b['forces'])
+    assert np.array_equal(a['stress'], b['stress'])

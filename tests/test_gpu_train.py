@@ -198,11 +198,14 @@ def test_rehearsal_ewc_steps_reduce_loss(models):
 
 def test_graphed_rehearsal_step_equals_eager():
     """The HIP-graph-captured rehearsal step (train.GraphedRehearsalStep)
-    reproduces the eager step: same parameters after three steps on changing
-    batches of one shape, and a new shape is captured separately."""
+    reproduces the eager step: same losses and parameters after steps on
+    changing batches of one shape (one with its edges in a random order: the
+    graphed step sorts them by centre like the eager model), a new shape is
+    captured separately, and once hip_graph_max shapes are cached a further
+    shape runs eagerly with the same result as the eager trainer."""
     from sevennet_finetuning_amd.nn import SevenNetTrainable
 
-    def run(graph, batches):
+    def run(graph, batches, third):
         m = SevenNetTrainable(device=DEV)
         fisher = {n: torch.full_like(p, 1e-3) for n, p in m.named_parameters()}
         opt = {n: p.detach().clone() for n, p in m.named_parameters()}
@@ -210,12 +213,16 @@ def test_graphed_rehearsal_step_equals_eager():
                'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
                'optim_param': {'lr': 1e-4}, 'scheduler': 'exponentiallr',
                'scheduler_param': {'gamma': 0.99}, 'device': DEV, 'hip_graph': graph,
-               'continue': {'fisher_information': fisher, 'opt_params': opt,
-                            'ewc_lambda': 1e2}}
+               'hip_graph_max': 2, 'continue': {'fisher_information': fisher,
+                                                'opt_params': opt, 'ewc_lambda': 1e2}}
         tr = train.Trainer(m, cfg)
         m.train(True)
         losses = [tuple(float(x) for x in tr.rehearsal_step(b, mm)) for b, mm in batches]
-        return m.flat.detach().double().cpu(), losses, tr
+        cached = len(tr._graphed.cache) if graph else 0
+        losses.append(tuple(float(x) for x in tr.rehearsal_step(*third)))
+        if graph:   # the third shape ran eagerly: nothing new captured
+            assert len(tr._graphed.cache) == cached == 2
+        return m.flat.detach().double().cpu(), losses
 
     def coll(seeds, cells=(3, 3, 3)):
         return train.collate(_batch(seeds, cells), device=DEV, dtype=torch.float32)
@@ -223,14 +230,17 @@ def test_graphed_rehearsal_step_equals_eager():
                (coll([10], (2, 2, 2)), coll([11]))]
     # one label NaN: the static (masked) loss drops it like the eager one
     batches[1][0][KEY.FORCE][3, 1] = float('nan')
-    theta0 = SevenNetTrainable(device=DEV).flat.detach().double().cpu()
-    fe, le, _ = run(False, batches)
-    fg, lg, tr = run(True, batches)
-    assert len(tr._graphed.cache) == 2
-    tr._graphed.max_graphs = 2      # a third shape now runs eagerly
+    # edges of one batch in a random order
+    b2 = batches[2][0]
+    perm = torch.as_tensor(np.random.default_rng(0).permutation(b2[KEY.EDGE_IDX].shape[1]),
+                           device=DEV)
+    for k in (KEY.EDGE_IDX, KEY.EDGE_VEC):
+        b2[k] = b2[k][:, perm] if k == KEY.EDGE_IDX else b2[k][perm]
     third = (coll([12], (2, 2, 1)), coll([13], (2, 2, 1)))
-    assert all(torch.isfinite(t).all() for t in tr.rehearsal_step(*third))
-    assert len(tr._graphed.cache) == 2
+    theta0 = SevenNetTrainable(device=DEV).flat.detach().double().cpu()
+    fe, le = run(False, batches, third)
+    fg, lg = run(True, batches, third)
+    assert len(le) == len(lg) == 5
     for a, b in zip(le, lg):
         assert abs(a[0] - b[0]) <= 1e-5 * abs(a[0]) and abs(a[1] - b[1]) <= 1e-5 * abs(a[1])
     # Adam normalises every component: where a gradient is ~0, fp32 rounding

@@ -82,6 +82,8 @@ def test_decomposed_matches_single_process_oracle(world, name, tmp_path):
     ref = oracle_eval(pos, cell, types)
     got = _run(world, name, 'cpu', tmp_path)
     assert got['n_ghost'][0] > 0
+    # three evaluations of one neighbour list: one upload, identical results
+    assert got['uploads'][0] == 1 and got['repeat_same'][0]
     vol = abs(np.linalg.det(cell))
     assert abs(got['energy'] - ref['energy']) <= 1e-10 * abs(ref['energy'])
     assert np.abs(got['forces'] - ref['forces']).max() < 1e-9
@@ -97,6 +99,7 @@ def test_decomposed_hip_matches_single_device(tmp_path):
     name = 'mixed_3x3x3'
     pos, cell, types = system(name, SYMS)
     got = _run(2, name, 'hip', tmp_path)
+    assert got['repeat_same'][0]
     m = E3GNNModel(device='cuda:0')
     ei, sh = neighbor_list(pos, cell, 5.0)
     vec = torch.tensor(pos[ei[1]] + sh @ cell - pos[ei[0]], dtype=torch.float32)

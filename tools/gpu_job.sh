@@ -16,7 +16,10 @@ step() {  # step <name> <seconds> <cmd...>
 }
 for s in "$@"; do
   case $s in
-    tests) step tests 600 python -m pytest tests -m gpu -x -q ;;
+    tests) step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    fullsize) step fullsize 600 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
+    benchstrong) step benchstrong 600 python bench.py --strong --steps 3 --warmup 1 --no-cpu-baseline ;;
+    profstrong) step profstrong 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profstrong -o run --output-format csv -- python bench.py --strong --steps 2 --warmup 1 --profile-only --no-parity-check ;;
     testsall) step tests 900 python -m pytest tests -m gpu -q ;;
     layer) step layer 300 python -m pytest tests -m gpu -q -k layerwise ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
