@@ -77,6 +77,10 @@ def make_box(cells, device):
     from sevennet_finetuning_amd.neighbor import neighbor_list
     from sevennet_finetuning_amd.structures import si_diamond
     pos, cell = si_diamond((cells,) * 3, sigma=0.05)
+    order = os.environ.get('E3GNN_BENCH_ORDER')   # experiment: atom order of the box
+    if order == 'morton':
+        from sevennet_finetuning_amd.structures import morton_order
+        pos = pos[morton_order(pos, cell, 2.7)]
     t0 = time.perf_counter()
     ei, sh = neighbor_list(pos, cell, 5.0)
     host_nl_s = time.perf_counter() - t0

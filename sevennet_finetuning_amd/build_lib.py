@@ -55,6 +55,7 @@ def build(force=False, verbose=False, out=None, defines=()):
 
     with ThreadPoolExecutor(max_workers=4) as ex:
         objs = list(ex.map(compile_one, SOURCES))
+    os.makedirs(os.path.dirname(os.path.abspath(lib)), exist_ok=True)
     tmp = lib + '.tmp'
     cmd = [HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -33,6 +33,22 @@ __device__ __forceinline__ float sum_rows4(float v) {
   return s + t;
 }
 
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs
+// (b and b + 8 share one, MI355X_MICROARCH.md "Workgroup dispatch"), so
+// consecutive blocks land on different L2s.  This bijection gives each XCD a
+// contiguous 1/8 of the index range instead, so the rows its blocks gather
+// (spatial neighbours of consecutive centres / edges) are shared in its L2.
+// Placement only: any dispatch order gives the same results.
+#ifndef E3GNN_XCD_REMAP
+#define E3GNN_XCD_REMAP 0
+#endif
+__device__ __forceinline__ int xcd_block() {
+  const int b = blockIdx.x;
+  if (!E3GNN_XCD_REMAP) return b;
+  const int nb = gridDim.x, q = nb >> 3, r = nb & 7, x = b & 7;
+  return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -385,16 +385,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
                                                   float* __restrict__ agg, MlpW W, int n_centers,
                                                   int n_nodes, float denom) {
   __shared__ float lds[4][160];
+  // the centre's message sum over its tiles stays in LDS (first tile stores,
+  // later tiles add: no global read-back), one coalesced copy out at the end
+  __shared__ __attribute__((aligned(16))) float aggl[4][L::DM];
   const int wid = threadIdx.x >> 6;
-  const int c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wid);
+  const int c = __builtin_amdgcn_readfirstlane(xcd_block() * 4 + wid);
   if (c >= n_centers) return;
   float* ybuf = lds[wid];
+  float* acl = aggl[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
   const int beg = row_ptr[c], end = row_ptr[c + 1];
   float* out = agg + (int64_t)c * L::DM;
   const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rh = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
-  const __amdgpu_buffer_rsrc_t Ro = rsrc_bytes(out, L::DM * 4);
   const float rden = 1.0f / denom;
   for (int e0 = beg; e0 < end || e0 == beg; e0 += 16) {
     const bool first_tile = e0 == beg;
@@ -430,9 +433,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
             if constexpr (p.l1 == I) {
               constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
               phase();
-              // previous tiles' sum of this block (read early, added at the end)
-              float prev[D3];
-              if (!first_tile) ldv<D3>(Ro, col * D3 * 4, (p.moff + 16 * j * D3) * 4, prev);
               const f32x4 wv = w2_block<true>(hq, wq);
               {  // operands of the next block load under this block's tensor product
                 const int nc = next_block_col<L, I, pi>(j);
@@ -454,8 +454,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
                 float v = acc[k];
                 v = sum_rows4(v) * rden;
                 if (g == 0) {
-                  const int so = (p.moff + 16 * j * D3 + k) * 4, vo = col * D3 * 4;
-                  stw(first_tile ? v : prev[k] + v, Ro, vo, so);
+                  float* a = acl + p.moff + (16 * j + col) * D3 + k;
+                  *a = first_tile ? v : *a + v;
                 }
               }
             }
@@ -464,6 +464,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
       }
     });
     if (end <= beg) break;
+  }
+  phase();
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  {
+    const float4* src = reinterpret_cast<const float4*>(acl);
+    float4* dst = reinterpret_cast<float4*>(out);
+    for (int t = lane; t < L::DM / 4; t += 64) dst[t] = src[t];
   }
 }
 
@@ -560,11 +568,17 @@ __device__ __forceinline__ void prefetch_gm(float* gmN, __amdgpu_buffer_rsrc_t R
 // block (transposed product w^T = W2^T H2^T: D[channel 4g+r][edge c]).  One
 // edge per lane keeps dE/dY in 8 registers; dE/dx[j] is summed over the 16
 // edge lanes of a row (DPP) once per block and accumulated in LDS.
-// EDGE = true: one wave per fixed tile of 16 consecutive (CSR-order) edges
-// instead of one per neighbour node -- the centres' dE/dagg rows are then read
-// in order (L2-resident) rather than scattered -- and dE/dx is written per
-// edge to dxc (summed per neighbour by the transposed-CSR gather).
-template <class L, bool EDGE>
+// MODE 0: one wave per NEIGHBOUR node over its incoming edges, dE/dx[j]
+// summed in LDS and written once.
+// MODE 1: one wave per fixed tile of 16 consecutive (CSR-order) edges -- the
+// centres' dE/dagg rows are then read in order (L2-resident) rather than
+// scattered -- and dE/dx is written per edge to dxc (summed per neighbour by
+// the transposed-CSR gather).
+// MODE 2: one wave per CENTRE over its CSR edges in tiles of 16 (the forward
+// kernel's mapping), the centre's dE/dagg row (DM floats) staged in LDS once:
+// the 60 per-path-block dE/dagg reads of a middle block become LDS reads
+// instead of dependent global gathers; dE/dx per edge to dxc as in MODE 1.
+template <class L, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_WAVES, E3GNN_BWDX_WAVES))) void k_conv_bwd_x(const int* __restrict__ src_ptr,
                                                     const int* __restrict__ src_perm,
                                                     const int* __restrict__ center,
@@ -575,15 +589,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
                                                     float* __restrict__ dh,
                                                     float* __restrict__ dgu, int n_nodes,
                                                     int n_centers, const int* __restrict__ nbr,
-                                                    float* __restrict__ dxc, int n_edges) {
-  __shared__ float lds[4][EDGE ? 1 : L::DX];  // dE/dx[j] of the wave's node
+                                                    float* __restrict__ dxc, int n_edges,
+                                                    const int* __restrict__ row_ptr) {
+  constexpr bool EDGE = MODE != 0;  // per-edge dE/dx output (dxc)
+  // MODE 0: dE/dx[j] of the wave's node; MODE 2: dE/dagg row of its centre
+  __shared__ __attribute__((aligned(16))) float lds[4][MODE == 0 ? L::DX : (MODE == 2 ? L::DM : 1)];
   const int wid = threadIdx.x >> 6;
-  const int jn = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wid);
-  if (EDGE ? jn * 16 >= n_edges : jn >= n_nodes) return;
+  const int jn = __builtin_amdgcn_readfirstlane(xcd_block() * 4 + wid);
+  if (MODE == 1 ? jn * 16 >= n_edges : jn >= (MODE == 2 ? n_centers : n_nodes)) return;
   float* dacc = lds[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
-  const int qb = EDGE ? jn * 16 : src_ptr[jn];
-  const int qe = EDGE ? min(jn * 16 + 16, n_edges) : src_ptr[jn + 1];
+  const int qb = MODE == 1 ? jn * 16 : (MODE == 2 ? row_ptr[jn] : src_ptr[jn]);
+  const int qe = MODE == 1 ? min(jn * 16 + 16, n_edges) : (MODE == 2 ? row_ptr[jn + 1] : src_ptr[jn + 1]);
+  if constexpr (MODE == 2) {
+    // stage the centre's dE/dagg row: DM / 4 float4 per wave, all in flight
+    const float4* src = reinterpret_cast<const float4*>(gagg + (int64_t)jn * L::DM);
+    float4* dst = reinterpret_cast<float4*>(dacc);
+    for (int t = lane; t < L::DM / 4; t += 64) dst[t] = src[t];
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  }
   const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rx =
       EDGE ? rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4) : rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
@@ -593,7 +618,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
   // at any system size; per neighbour node (last block, DM = 224): whole array
   // (the host checks n_centers * 224 * 4 < 2^31)
   const __amdgpu_buffer_rsrc_t RgAll = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
-  if constexpr (!EDGE)
+  if constexpr (MODE == 0)
     for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
 
   for (int q0 = qb; q0 < qe; q0 += 16) {
@@ -605,12 +630,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
     // EDGE: the slot's gathered row (padded slots: row 0, w = 0 there)
     const int vx = EDGE ? (er >= 0 ? nbr[er] : 0) * L::DX * 4 : 0;
     int cb = 0, nc = n_centers;  // centre rows [cb, cb + nc) under the descriptor
-    if constexpr (EDGE) {
+    if constexpr (MODE == 1) {
       cb = __builtin_amdgcn_readfirstlane(center[q0]);
       nc = __builtin_amdgcn_readfirstlane(center[qe - 1]) - cb + 1;
     }
     const __amdgpu_buffer_rsrc_t Rg =
-        EDGE ? rsrc_bytes(gagg + (int64_t)cb * L::DM, (int64_t)nc * L::DM * 4) : RgAll;
+        MODE == 1 ? rsrc_bytes(gagg + (int64_t)cb * L::DM, (int64_t)nc * L::DM * 4) : RgAll;
     // padded slots read past the end of the descriptor: 0
     const int vg = (er >= 0 ? (center[er] - cb) * L::DM : nc * L::DM) * 4;
     float y[9];
@@ -660,6 +685,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
 #pragma unroll
                 for (int k = 0; k < 4 * D3; ++k) gm[k] = gmN[k];
                 prefetch_gm<L, I, pi>(gmN, Rg, vg, g, jj);
+              } else if constexpr (MODE == 2) {
+                // the centre's row in LDS: 4 D3 contiguous floats per lane group
+                const float* gl = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
+#pragma unroll
+                for (int k = 0; k < 4 * D3; ++k) gm[k] = gl[k];
               } else {
                 load_gm<L, pi>(gm, Rg, vg, g, jj);
               }
@@ -731,7 +761,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
       o[2] += gz;
     }
   }
-  if constexpr (!EDGE) {
+  if constexpr (MODE == 0) {
     phase();
     __builtin_amdgcn_s_waitcnt(0);
     float* dhj = dh + (int64_t)jn * L::DX;
@@ -807,7 +837,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_
   // per wave: two dw transpose tiles [16 slots][DWS] + Y of the tile [16][9]
   __shared__ __attribute__((aligned(16))) float lds[4][2 * DWB + 160];
   const int wid = threadIdx.x >> 6;
-  const int e0 = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wid) * 16);
+  const int e0 = __builtin_amdgcn_readfirstlane((xcd_block() * 4 + wid) * 16);
   if (e0 >= n_edges) return;
   const int end = n_edges;
   float* dwbuf = lds[wid];
@@ -950,21 +980,32 @@ static hipError_t fwd_impl(const FusedArgs& a, hipStream_t s) {
                      a.nbr, a.emb, a.Y, a.h, a.agg, a.W, a.n_centers, a.n_nodes, a.denom);
   return hipGetLastError();
 }
+// E3GNN_BWDX_MODE: 2 (default) per-centre tiles with the dE/dagg row in LDS,
+// 1 fixed 16-edge tiles with gathered dE/dagg (round-1 kernel)
+#ifndef E3GNN_BWDX_MODE
+#define E3GNN_BWDX_MODE 2
+#endif
 template <class L>
 static hipError_t bwd_x_impl(const FusedArgs& a, hipStream_t s) {
   if (a.n_nodes <= 0 || a.n_edges <= 0) return hipSuccess;
-  if (a.edge_order) {  // edge-ordered tiles, per-edge dE/dx (caller gathers)
-    const int tiles = (a.n_edges + 15) / 16;
-    hipLaunchKernelGGL((k_conv_bwd_x<L, true>), dim3((tiles + 3) / 4), dim3(256), 0, s, a.src_ptr,
-                       a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
-                       a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges);
+  if (a.edge_order) {  // per-edge dE/dx (caller gathers)
+    if (E3GNN_BWDX_MODE == 2) {
+      hipLaunchKernelGGL((k_conv_bwd_x<L, 2>), dim3((a.n_centers + 3) / 4), dim3(256), 0, s,
+                         a.src_ptr, a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh,
+                         a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr);
+    } else {
+      const int tiles = (a.n_edges + 15) / 16;
+      hipLaunchKernelGGL((k_conv_bwd_x<L, 1>), dim3((tiles + 3) / 4), dim3(256), 0, s, a.src_ptr,
+                         a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
+                         a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr);
+    }
     return hipGetLastError();
   }
   // first block: dE/dx of the embedding is not needed (scratch sink), only dE/du
-  hipLaunchKernelGGL((k_conv_bwd_x<L, false>), dim3((a.n_nodes + 3) / 4), dim3(256), 0, s,
+  hipLaunchKernelGGL((k_conv_bwd_x<L, 0>), dim3((a.n_nodes + 3) / 4), dim3(256), 0, s,
                      a.src_ptr, a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W,
                      a.dh ? a.dh : a.scratch_dh, a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc,
-                     a.n_edges);
+                     a.n_edges, a.row_ptr);
   return hipGetLastError();
 }
 template <class L>

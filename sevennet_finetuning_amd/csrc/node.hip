@@ -378,7 +378,7 @@ __global__ void k_gather_rows(int n, int D, const int* __restrict__ ptr, const i
 __global__ void k_gather_rows4(int n, int D4, const int* __restrict__ ptr,
                                const int* __restrict__ perm, const float4* __restrict__ src,
                                float4* __restrict__ dst) {
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int j = xcd_block() * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
   const int b = ptr[j], en = ptr[j + 1];

@@ -66,6 +66,25 @@ def tile(pos, cell, reps):
     return big.reshape(-1, 3), cell * np.array(reps, dtype=np.float64)[:, None]
 
 
+def morton_order(pos, cell, bin_width):
+    """Permutation that sorts atoms by the Z-order (Morton) index of their
+    spatial bin (bins of ~bin_width along each lattice vector), ascending atom
+    id inside a bin -- the spatial sort LAMMPS applies (atom_modify sort), so
+    that atoms close in space are close in memory."""
+    pos = np.asarray(pos, dtype=np.float64)
+    cell = np.asarray(cell, dtype=np.float64)
+    frac = pos @ np.linalg.inv(cell)
+    frac -= np.floor(frac)
+    lens = np.linalg.norm(cell, axis=1)
+    nb = np.maximum((lens / bin_width).astype(np.int64), 1)
+    b = np.minimum((frac * nb).astype(np.int64), nb - 1)
+    code = np.zeros(len(pos), dtype=np.int64)
+    for bit in range(21):
+        for k in range(3):
+            code |= ((b[:, k] >> bit) & 1) << (3 * bit + k)
+    return np.lexsort((np.arange(len(pos)), code))
+
+
 def mixed_symbols(n, seed=1):
     rng = np.random.default_rng(seed)
     return [MIXED_SYMBOLS[i] for i in rng.integers(0, len(MIXED_SYMBOLS), n)]
