@@ -87,6 +87,7 @@ def build_native(lib=LIB, verbose=False):
 
 
 if __name__ == '__main__':
+    sys.stdout.reconfigure(line_buffering=True)
     args = sys.argv[1:]
     out = args[args.index('--out') + 1] if '--out' in args else None
     defs = [a[2:] for a in args if a.startswith('-D')]

@@ -174,11 +174,16 @@ class SevenNetTrainable(torch.nn.Module):
 
     def __init__(self, model_dir=os.path.join(ASSETS, 'sevennet0'), device='cuda',
                  train_shift_scale=False, train_denominator=False, train_radial_coeffs=True,
-                 conv_backend=None, dtype=torch.float32):
+                 conv_backend=None, dtype=torch.float32, manifest=None, weights=None):
+        """Parameters from a deployment directory (manifest.json +
+        weights.bin), or from ``manifest`` (dict) + ``weights`` (flat fp32
+        array in manifest tensor order) -- what model_build produces."""
         super().__init__()
         self.dtype = dtype
-        with open(os.path.join(model_dir, 'manifest.json')) as f:
-            man = json.load(f)
+        if manifest is None:
+            with open(os.path.join(model_dir, 'manifest.json')) as f:
+                manifest = json.load(f)
+        man = manifest
         self.manifest = man
         self.chemical_symbols = list(man['chemical_symbols'])
         self.nsp = int(man['num_species'])
@@ -189,7 +194,8 @@ class SevenNetTrainable(torch.nn.Module):
         self.nlayer = int(man['num_convolution_layer'])
         self.conv_backend = conv_backend if conv_backend is not None \
             else conv_ops.HipConvBackend()
-        flat_host = np.fromfile(os.path.join(model_dir, 'weights.bin'), dtype='<f4')
+        flat_host = np.fromfile(os.path.join(model_dir, 'weights.bin'), dtype='<f4') \
+            if weights is None else np.ascontiguousarray(weights, dtype='<f4').reshape(-1)
         total = sum(t['numel'] for t in man['tensors'])
         self.flat = torch.empty(total, dtype=dtype, device=device)
         self.flat_grad = torch.zeros(total, dtype=dtype, device=device)
