@@ -120,6 +120,24 @@ float* e3gnn_grad_ptr(e3gnn_ctx* c, int layer);
  * rank-local virial6 and optional edge_grad[E*3]. */
 int e3gnn_forces(e3gnn_ctx* c, float* forces, float* virial6, float* edge_grad, void* stream);
 
+/* ---- halo overlap (the forward_comm / reverse_comm loop of
+ * pair_e3gnn_parallel.cpp:371-454, overlapped instead of serialised) ----
+ * Owned centres [0, n_interior) have no ghost neighbour (the rank-graph
+ * builder orders them first; checked at the next e3gnn_graph_set, which it
+ * must precede).  e3gnn_layer_forward = part 0 then part 1, where part 0
+ * reads only the OWNED rows of the block's input features (self_interaction_1
+ * of the owned rows, the interior centres' convolution) -- run it while the
+ * ghost rows are exchanged -- and part 1 the rest.  e3gnn_layer_backward =
+ * part 0 then part 1, where part 0 produces everything the GHOST rows of
+ * dE/dfeatures need (boundary centres' edges, the ghost rows' gather and
+ * self_interaction_1 backward) -- start the reverse exchange after it -- and
+ * part 1 the interior centres and the owned rows (accumulate the received
+ * ghost contributions after part 1).  n_interior = 0 (default): part 0 of
+ * the forward is the owned rows' self_interaction_1 only. */
+int e3gnn_set_interior(e3gnn_ctx* c, int64_t n_interior);
+int e3gnn_layer_forward_part(e3gnn_ctx* c, int layer, int part, void* stream);
+int e3gnn_layer_backward_part(e3gnn_ctx* c, int layer, int part, void* stream);
+
 /* ---- halo kernels ---- */
 /* dst[r*dim + k] = src[idx[r]*src_stride + k], r < n */
 int e3gnn_halo_pack(const int32_t* idx, int64_t n, int dim, const float* src, int64_t src_stride,

@@ -35,6 +35,9 @@ SIGNATURES = {
     'e3gnn_feature_dim': (_c_int, [_vp, _c_int]),
     'e3gnn_readout': (_c_int, [_vp, _vp, _vp, _vp]),
     'e3gnn_layer_backward': (_c_int, [_vp, _c_int, _vp]),
+    'e3gnn_set_interior': (_c_int, [_vp, _c_i64]),
+    'e3gnn_layer_forward_part': (_c_int, [_vp, _c_int, _c_int, _vp]),
+    'e3gnn_layer_backward_part': (_c_int, [_vp, _c_int, _c_int, _vp]),
     'e3gnn_grad_ptr': (_vp, [_vp, _c_int]),
     'e3gnn_forces': (_c_int, [_vp, _vp, _vp, _vp, _vp]),
     'e3gnn_halo_pack': (_c_int, [_vp, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),

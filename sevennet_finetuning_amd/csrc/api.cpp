@@ -236,6 +236,9 @@ double tp_flops_per_edge(int kind) {
 struct e3gnn_ctx {
   e3gnn_model* m;
   int64_t n = 0, nl = 0, E = 0;
+  // halo overlap: owned centres [0, n_int) have no ghost neighbour; their
+  // edges are [0, e_int) (e3gnn_set_interior, effective at graph_set)
+  int64_t n_interior_req = 0, n_int = 0, e_int = 0;
   // graph
   DBuf type, center, nbr, vec, row_ptr, src_ptr, src_perm, cnt, err;
   DBuf Y, emb, dY, dgu, demb, fe;
@@ -807,6 +810,9 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   c->nl = nl;
   c->E = E;
   c->readout_done = 0;
+  if (c->n_interior_req > nl) return fail(E3GNN_ERR_ARG, "n_interior exceeds n_local");
+  c->n_int = c->n_interior_req;
+  c->e_int = 0;
   const size_t F = sizeof(float);
   // workspace (grow-only)
   HIPCHK(c->type.ensure(n * 4));
@@ -869,21 +875,26 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   {
     Region r(c, s, C_GRAPH, 0, (double)E * 24 + n * 12);
     HIPCHK(launch_build_graph(E, (int)nl, (int)n, c->center.i(), c->nbr.i(), c->row_ptr.i(),
-                              c->src_ptr.i(), c->src_perm.i(), c->cnt.i(), c->err.i(), s));
+                              c->src_ptr.i(), c->src_perm.i(), c->cnt.i(), c->err.i(), s,
+                              (int)c->n_int));
   }
   {
     Region r(c, s, C_EMBED_NODE, 0, (double)n * 128 * 4);
     HIPCHK(launch_embed((int)n, c->type.i(), m->nsp, m->embed.f(), c->x[0].f(), c->err.i(), s));
   }
-  int err = 0;
+  int err = 0, e_int = 0;
   HIPCHK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, s));
+  if (c->n_int > 0)
+    HIPCHK(hipMemcpyAsync(&e_int, c->row_ptr.i() + c->n_int, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  c->e_int = e_int;
   if (err) {
     std::string msg = "invalid graph:";
     if (err & 1) msg += " edge_center not sorted non-decreasing;";
     if (err & 2) msg += " edge_center out of [0, n_local);";
     if (err & 4) msg += " edge_nbr out of [0, n_local+n_ghost);";
     if (err & 8) msg += " species index out of range;";
+    if (err & 16) msg += " an interior centre (below n_interior) has a ghost neighbour;";
     return fail(E3GNN_ERR_GRAPH, msg);
   }
   {
@@ -899,10 +910,17 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   return E3GNN_OK;
 }
 
-int e3gnn_layer_forward(e3gnn_ctx* c, int t, void* stream) {
+// Parts of one interaction block for the halo overlap (e3gnn.h):
+// part 0 needs only the owned rows of the block's input features (it runs
+// while the ghost rows are in flight): self_interaction_1 of the owned rows and
+// the convolution of the interior centres [0, n_int); part 1: the ghost rows'
+// self_interaction_1, the boundary centres [n_int, n_local), si2 +
+// self-connection + gate.  The v1 kernels run whole in part 1.
+int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
   if (!c) return fail(E3GNN_ERR_ARG, "null context");
   e3gnn_model* m = c->m;
   if (t < 0 || t >= m->nlayer) return fail(E3GNN_ERR_ARG, "layer out of range");
+  if (part != 0 && part != 1) return fail(E3GNN_ERR_ARG, "part must be 0 or 1");
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
   const int64_t n = c->n, nl = c->nl, E = c->E;
@@ -910,16 +928,13 @@ int e3gnn_layer_forward(e3gnn_ctx* c, int t, void* stream) {
   const int dm = irreps_dim(m->mid[t]), W = m->W[t];
   const bool last = t == m->nlayer - 1;
   const int kind = t == 0 ? 0 : (last ? 2 : 1);
-  // self_interaction_1 on owned + ghost rows
-  {
-    Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], n));
-    HIPCHK(launch_gemm(lin_fwd(*m->si1[t], c->x[t].f(), dx, c->h[t].f(), dx, n, 0), s));
-  }
-  if (c->graph_impl == 0) {
-    // fused radial MLP + tensor product + segmented sum (fused.hip)
+  const bool fused = c->graph_impl == 0;
+  const int64_t n_int = fused ? c->n_int : 0;
+  auto conv_fwd = [&](int64_t c0, int64_t c1, double e_share) -> int {
+    if (c1 <= c0) return E3GNN_OK;
     Region r(c, s, C_CONV_FWD + kind,
-             tp_flops_per_edge(kind) * E + 2.0 * E * (8 * 64 + 64 * 64 + 64 * W),
-             (double)E * 4 * (8 + 9 + 2 + dx) + nl * 4.0 * dm);
+             e_share * (tp_flops_per_edge(kind) + 2.0 * (8 * 64 + 64 * 64 + 64 * W)),
+             e_share * 4 * (8 + 9 + 2 + dx) + (c1 - c0) * 4.0 * dm);
     FusedArgs a;
     std::memset(&a, 0, sizeof(a));
     a.row_ptr = c->row_ptr.i();
@@ -932,7 +947,31 @@ int e3gnn_layer_forward(e3gnn_ctx* c, int t, void* stream) {
     a.n_centers = (int)nl;
     a.n_nodes = (int)n;
     a.denom = m->denom[t];
+    a.c_begin = (int)c0;
+    a.c_end = (int)c1;
     HIPCHK(launch_conv_fwd(kind, a, s));
+    return E3GNN_OK;
+  };
+  if (part == 0) {
+    if (!fused) return E3GNN_OK;
+    {
+      Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], nl));
+      HIPCHK(launch_gemm(lin_fwd(*m->si1[t], c->x[t].f(), dx, c->h[t].f(), dx, nl, 0), s));
+    }
+    return conv_fwd(0, n_int, (double)c->e_int);
+  }
+  // ---- part 1
+  {
+    const int64_t r0 = fused ? nl : 0;  // rows not done in part 0
+    Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], n - r0));
+    if (n > r0)
+      HIPCHK(launch_gemm(lin_fwd(*m->si1[t], c->x[t].f() + r0 * dx, dx, c->h[t].f() + r0 * dx, dx,
+                                 n - r0, 0), s));
+  }
+  if (fused) {
+    // fused radial MLP + tensor product + segmented sum (fused.hip)
+    const int rc = conv_fwd(n_int, nl, (double)(E - c->e_int));
+    if (rc) return rc;
   } else {
   // radial MLP: emb -> 64 -> 64 -> W  (convolution.py:97-106)
   {
@@ -989,6 +1028,11 @@ int e3gnn_layer_forward(e3gnn_ctx* c, int t, void* stream) {
   return E3GNN_OK;
 }
 
+int e3gnn_layer_forward(e3gnn_ctx* c, int t, void* stream) {
+  const int rc = e3gnn_layer_forward_part(c, t, 0, stream);
+  return rc ? rc : e3gnn_layer_forward_part(c, t, 1, stream);
+}
+
 int e3gnn_readout(e3gnn_ctx* c, float* energy, float* atomic_energy, void* stream) {
   if (!c) return fail(E3GNN_ERR_ARG, "null context");
   e3gnn_model* m = c->m;
@@ -1010,10 +1054,16 @@ int e3gnn_readout(e3gnn_ctx* c, float* energy, float* atomic_energy, void* strea
   return E3GNN_OK;
 }
 
-int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
+// Parts of a block's backward for the halo overlap (e3gnn.h): part 0 makes
+// everything the GHOST rows of dE/dx need (gate + si2 backward of the owned
+// rows, the boundary centres' edges, the ghost rows' gather and
+// self_interaction_1 backward), so the reverse exchange can start; part 1 does
+// the interior centres and the owned rows.  The v1 kernels run whole in part 0.
+int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
   if (!c) return fail(E3GNN_ERR_ARG, "null context");
   e3gnn_model* m = c->m;
   if (t < 0 || t >= m->nlayer) return fail(E3GNN_ERR_ARG, "layer out of range");
+  if (part != 0 && part != 1) return fail(E3GNN_ERR_ARG, "part must be 0 or 1");
   if (!c->readout_done) return fail(E3GNN_ERR_ARG, "e3gnn_readout must precede the backward");
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
@@ -1022,15 +1072,23 @@ int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
   const int dm = irreps_dim(m->mid[t]), W = m->W[t];
   const bool last = t == m->nlayer - 1;
   const int kind = t == 0 ? 0 : (last ? 2 : 1);
-  {
-    Region r(c, s, C_GATE_BWD, 0, nl * 4.0 * (2 * dg + irreps_dim(m->irreps[t + 1])));
-    HIPCHK(launch_gate_bwd((int)nl, last, c->y[t].f(), c->grad[t + 1].f(), c->dy.f(), s));
+  const bool fused = c->graph_impl == 0;
+  if (!fused && part == 1) return E3GNN_OK;
+  const int64_t n_int = c->n_int, e_int = c->e_int;
+  if (part == 0) {
+    {
+      Region r(c, s, C_GATE_BWD, 0, nl * 4.0 * (2 * dg + irreps_dim(m->irreps[t + 1])));
+      HIPCHK(launch_gate_bwd((int)nl, last, c->y[t].f(), c->grad[t + 1].f(), c->dy.f(), s));
+    }
+    {
+      Region r(c, s, C_LINEAR, lin_flops(*m->si2[t], nl));
+      HIPCHK(launch_gemm(lin_bwd(*m->si2[t], c->dy.f(), dg, c->agg.f(), dm, nl, 0), s));
+    }
   }
-  {
-    Region r(c, s, C_LINEAR, lin_flops(*m->si2[t], nl));
-    HIPCHK(launch_gemm(lin_bwd(*m->si2[t], c->dy.f(), dg, c->agg.f(), dm, nl, 0), s));
-  }
-  if (c->graph_impl == 0) {
+  // per-edge dE/dx + transposed-CSR gather (edge-ordered kernels) or dE/dx
+  // written per neighbour node (the last block)
+  const bool gather = !fused || (c->graph_bwd_edge && !last);
+  if (fused) {
     FusedArgs a;
     std::memset(&a, 0, sizeof(a));
     a.row_ptr = c->row_ptr.i();
@@ -1053,17 +1111,25 @@ int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
     a.W = mlp_ptrs(m, t);
     a.n_centers = (int)nl;
     a.n_nodes = (int)n;
+    // part 0: boundary centres / their edges / ghost neighbour nodes
+    a.c_begin = (int)(part == 0 ? n_int : 0);
+    a.c_end = (int)(part == 0 ? nl : n_int);
+    a.e_begin = (int)(part == 0 ? e_int : 0);
+    a.e_end = (int)(part == 0 ? E : e_int);
+    a.node_begin = (int)(part == 0 ? nl : 0);
+    a.node_end = (int)(part == 0 ? n : nl);
+    const double ef = (double)(a.e_end - a.e_begin);
     // algorithmic FLOP (the forward radial MLP the dE/dx kernel recomputes is
     // not counted): dE/dx + dE/dY = 2 x TP; dE/dw = TP, dH2 = dw W2^T, MLP chain
     {
-      Region r(c, s, C_CONV_BWD_X + kind, 2.0 * tp_flops_per_edge(kind) * E,
-               (double)E * 4 * (8 + 9 + 2 + 3) + nl * 4.0 * dm + n * 4.0 * 2 * dx);
+      Region r(c, s, C_CONV_BWD_X + kind, 2.0 * tp_flops_per_edge(kind) * ef,
+               ef * 4 * (8 + 9 + 2 + 3) + (a.c_end - a.c_begin) * 4.0 * dm);
       HIPCHK(launch_conv_bwd_x(kind, a, s));
     }
     {
       Region r(c, s, C_CONV_BWD_W + kind,
-               tp_flops_per_edge(kind) * E + 2.0 * E * (64 * W + 64 * 64 + 8 * 64),
-               (double)E * 4 * (8 + 9 + 2 + 8 + dx) + nl * 4.0 * dm);
+               tp_flops_per_edge(kind) * ef + 2.0 * ef * (64 * W + 64 * 64 + 8 * 64),
+               ef * 4 * (8 + 9 + 2 + 8 + dx));
       HIPCHK(launch_conv_bwd_w(kind, a, s));
     }
   } else {
@@ -1110,18 +1176,28 @@ int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
   }
   }
   if (t > 0) {
-    // per-edge dE/dx (v1, or the edge-ordered fused kernel) -> dh by the
-    // transposed CSR; the per-neighbour fused kernel wrote dh itself
-    if (c->graph_impl == 1 || (c->graph_bwd_edge && t != m->nlayer - 1)) {
-      Region r(c, s, C_GATHER, 0, (double)E * 4 * (dx + 1) + n * 4.0 * dx);
-      HIPCHK(launch_gather_rows((int)n, dx, c->src_ptr.i(), c->src_perm.i(), c->dxc.f(),
-                                c->dh.f(), s));
+    // rows of this part: ghosts [nl, n) in part 0, owned [0, nl) in part 1
+    // (the v1 kernels: all rows, in part 0)
+    const int64_t r0 = !fused ? 0 : (part == 0 ? nl : 0), r1 = !fused ? n : (part == 0 ? n : nl);
+    if (gather && r1 > r0) {
+      Region r(c, s, C_GATHER, 0, (double)E * 4 * (dx + 1) * (r1 - r0) / std::max<int64_t>(n, 1) +
+                                      (r1 - r0) * 4.0 * dx);
+      HIPCHK(launch_gather_rows_range((int)r0, (int)r1, dx, c->src_ptr.i(), c->src_perm.i(),
+                                      c->dxc.f(), c->dh.f(), s));
     }
-    Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], n) + lin_flops(*m->sc[t], nl));
-    HIPCHK(launch_gemm(lin_bwd(*m->si1[t], c->dh.f(), dx, c->grad[t].f(), dx, n, 0), s));
-    HIPCHK(launch_gemm(lin_bwd(*m->sc[t], c->dy.f(), dg, c->grad[t].f(), dx, nl, 1), s));
+    const bool owned = !fused || part == 1;
+    Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], r1 - r0) + (owned ? lin_flops(*m->sc[t], nl) : 0));
+    if (r1 > r0)
+      HIPCHK(launch_gemm(lin_bwd(*m->si1[t], c->dh.f() + r0 * dx, dx, c->grad[t].f() + r0 * dx, dx,
+                                 r1 - r0, 0), s));
+    if (owned) HIPCHK(launch_gemm(lin_bwd(*m->sc[t], c->dy.f(), dg, c->grad[t].f(), dx, nl, 1), s));
   }
   return E3GNN_OK;
+}
+
+int e3gnn_layer_backward(e3gnn_ctx* c, int t, void* stream) {
+  const int rc = e3gnn_layer_backward_part(c, t, 0, stream);
+  return rc ? rc : e3gnn_layer_backward_part(c, t, 1, stream);
 }
 
 int e3gnn_forces(e3gnn_ctx* c, float* forces, float* virial6, float* edge_grad, void* stream) {
@@ -1454,6 +1530,13 @@ int e3gnn_nlist_fetch(e3gnn_nlist* h, int32_t* center, int32_t* nbr, int32_t* sh
   HIPCHK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (herr & 2) return fail(E3GNN_ERR_GRAPH, "periodic image shift beyond +-1024 cells");
+  return E3GNN_OK;
+}
+
+int e3gnn_set_interior(e3gnn_ctx* c, int64_t n_interior) {
+  if (!c) return fail(E3GNN_ERR_ARG, "null context");
+  if (n_interior < 0) return fail(E3GNN_ERR_ARG, "negative n_interior");
+  c->n_interior_req = n_interior;
   return E3GNN_OK;
 }
 

@@ -45,6 +45,11 @@ struct FusedArgs {
   int n_edges;
   int n_nodes;
   float denom;
+  // work range of one launch (halo overlap splits a layer into parts):
+  // centres [c_begin, c_end) (forward, per-centre dE/dx), edges [e_begin,
+  // e_end) (dE/dw, edge tiles), neighbour nodes [node_begin, node_end)
+  // (per-node dE/dx); the host sets them to the whole graph by default
+  int c_begin, c_end, e_begin, e_end, node_begin, node_end;
 };
 
 hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s);

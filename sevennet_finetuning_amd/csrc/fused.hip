@@ -382,15 +382,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
                                                   const float* __restrict__ emb,
                                                   const float* __restrict__ Y,
                                                   const float* __restrict__ h,
-                                                  float* __restrict__ agg, MlpW W, int n_centers,
-                                                  int n_nodes, float denom) {
+                                                  float* __restrict__ agg, MlpW W, int c_begin,
+                                                  int c_end, int n_nodes, float denom) {
   __shared__ float lds[4][160];
   // the centre's message sum over its tiles stays in LDS (first tile stores,
   // later tiles add: no global read-back), one coalesced copy out at the end
   __shared__ __attribute__((aligned(16))) float aggl[4][L::DM];
   const int wid = threadIdx.x >> 6;
-  const int c = __builtin_amdgcn_readfirstlane(xcd_block() * 4 + wid);
-  if (c >= n_centers) return;
+  const int c = __builtin_amdgcn_readfirstlane(c_begin + xcd_block() * 4 + wid);
+  if (c >= c_end) return;
   float* ybuf = lds[wid];
   float* acl = aggl[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
@@ -590,17 +590,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
                                                     float* __restrict__ dgu, int n_nodes,
                                                     int n_centers, const int* __restrict__ nbr,
                                                     float* __restrict__ dxc, int n_edges,
-                                                    const int* __restrict__ row_ptr) {
+                                                    const int* __restrict__ row_ptr, int r_begin,
+                                                    int r_end) {
   constexpr bool EDGE = MODE != 0;  // per-edge dE/dx output (dxc)
   // MODE 0: dE/dx[j] of the wave's node; MODE 2: dE/dagg row of its centre
   __shared__ __attribute__((aligned(16))) float lds[4][MODE == 0 ? L::DX : (MODE == 2 ? L::DM : 1)];
   const int wid = threadIdx.x >> 6;
-  const int jn = __builtin_amdgcn_readfirstlane(xcd_block() * 4 + wid);
-  if (MODE == 1 ? jn * 16 >= n_edges : jn >= (MODE == 2 ? n_centers : n_nodes)) return;
+  // wave index: node (MODE 0), 16-edge tile of [r_begin, r_end) (MODE 1), centre (MODE 2)
+  const int jn = __builtin_amdgcn_readfirstlane((MODE == 1 ? 0 : r_begin) + xcd_block() * 4 + wid);
+  if (MODE == 1 ? r_begin + jn * 16 >= r_end : jn >= r_end) return;
   float* dacc = lds[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
-  const int qb = MODE == 1 ? jn * 16 : (MODE == 2 ? row_ptr[jn] : src_ptr[jn]);
-  const int qe = MODE == 1 ? min(jn * 16 + 16, n_edges) : (MODE == 2 ? row_ptr[jn + 1] : src_ptr[jn + 1]);
+  const int qb = MODE == 1 ? r_begin + jn * 16 : (MODE == 2 ? row_ptr[jn] : src_ptr[jn]);
+  const int qe = MODE == 1 ? min(qb + 16, r_end) : (MODE == 2 ? row_ptr[jn + 1] : src_ptr[jn + 1]);
   if constexpr (MODE == 2) {
     // stage the centre's dE/dagg row: DM / 4 float4 per wave, all in flight
     const float4* src = reinterpret_cast<const float4*>(gagg + (int64_t)jn * L::DM);
@@ -832,14 +834,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_
                                                     const float* __restrict__ Y,
                                                     const float* __restrict__ h,
                                                     const float* __restrict__ gagg, MlpW W,
-                                                    float* __restrict__ demb, int n_edges,
-                                                    int n_nodes, int n_centers) {
+                                                    float* __restrict__ demb, int e_begin,
+                                                    int e_end, int n_nodes, int n_centers) {
   // per wave: two dw transpose tiles [16 slots][DWS] + Y of the tile [16][9]
   __shared__ __attribute__((aligned(16))) float lds[4][2 * DWB + 160];
   const int wid = threadIdx.x >> 6;
-  const int e0 = __builtin_amdgcn_readfirstlane((xcd_block() * 4 + wid) * 16);
-  if (e0 >= n_edges) return;
-  const int end = n_edges;
+  const int e0 = __builtin_amdgcn_readfirstlane(e_begin + (xcd_block() * 4 + wid) * 16);
+  if (e0 >= e_end) return;
+  const int end = e_end;
   float* dwbuf = lds[wid];
   float* ybuf = lds[wid] + 2 * DWB;
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
@@ -975,9 +977,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_
 
 template <class L>
 static hipError_t fwd_impl(const FusedArgs& a, hipStream_t s) {
-  if (a.n_centers <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_conv_fwd<L>, dim3((a.n_centers + 3) / 4), dim3(256), 0, s, a.row_ptr,
-                     a.nbr, a.emb, a.Y, a.h, a.agg, a.W, a.n_centers, a.n_nodes, a.denom);
+  const int nc = a.c_end - a.c_begin;  // centre range of this launch
+  if (nc <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_conv_fwd<L>, dim3((nc + 3) / 4), dim3(256), 0, s, a.row_ptr, a.nbr, a.emb,
+                     a.Y, a.h, a.agg, a.W, a.c_begin, a.c_end, a.n_nodes, a.denom);
   return hipGetLastError();
 }
 // E3GNN_BWDX_MODE: 2 (default) per-centre tiles with the dE/dagg row in LDS,
@@ -990,30 +993,39 @@ static hipError_t bwd_x_impl(const FusedArgs& a, hipStream_t s) {
   if (a.n_nodes <= 0 || a.n_edges <= 0) return hipSuccess;
   if (a.edge_order) {  // per-edge dE/dx (caller gathers)
     if (E3GNN_BWDX_MODE == 2) {
-      hipLaunchKernelGGL((k_conv_bwd_x<L, 2>), dim3((a.n_centers + 3) / 4), dim3(256), 0, s,
-                         a.src_ptr, a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh,
-                         a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr);
+      const int nc = a.c_end - a.c_begin;
+      if (nc <= 0) return hipSuccess;
+      hipLaunchKernelGGL((k_conv_bwd_x<L, 2>), dim3((nc + 3) / 4), dim3(256), 0, s, a.src_ptr,
+                         a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
+                         a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr, a.c_begin,
+                         a.c_end);
     } else {
-      const int tiles = (a.n_edges + 15) / 16;
+      const int tiles = (a.e_end - a.e_begin + 15) / 16;
+      if (tiles <= 0) return hipSuccess;
       hipLaunchKernelGGL((k_conv_bwd_x<L, 1>), dim3((tiles + 3) / 4), dim3(256), 0, s, a.src_ptr,
                          a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
-                         a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr);
+                         a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr, a.e_begin,
+                         a.e_end);
     }
     return hipGetLastError();
   }
-  // first block: dE/dx of the embedding is not needed (scratch sink), only dE/du
-  hipLaunchKernelGGL((k_conv_bwd_x<L, 0>), dim3((a.n_nodes + 3) / 4), dim3(256), 0, s,
-                     a.src_ptr, a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W,
+  // per neighbour node over [node_begin, node_end); first block: dE/dx of the
+  // embedding is not needed (scratch sink), only dE/du
+  const int nn = a.node_end - a.node_begin;
+  if (nn <= 0) return hipSuccess;
+  hipLaunchKernelGGL((k_conv_bwd_x<L, 0>), dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr,
+                     a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W,
                      a.dh ? a.dh : a.scratch_dh, a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc,
-                     a.n_edges, a.row_ptr);
+                     a.n_edges, a.row_ptr, a.node_begin, a.node_end);
   return hipGetLastError();
 }
 template <class L>
 static hipError_t bwd_w_impl(const FusedArgs& a, hipStream_t s) {
-  if (a.n_nodes <= 0 || a.n_edges <= 0) return hipSuccess;
-  const int tiles = (a.n_edges + 15) / 16;
+  const int tiles = (a.e_end - a.e_begin + 15) / 16;  // edge range of this launch
+  if (a.n_nodes <= 0 || tiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_conv_bwd_w<L>, dim3((tiles + 3) / 4), dim3(256), 0, s, a.center, a.nbr,
-                     a.emb, a.Y, a.h, a.gagg, a.W, a.demb, a.n_edges, a.n_nodes, a.n_centers);
+                     a.emb, a.Y, a.h, a.gagg, a.W, a.demb, a.e_begin, a.e_end, a.n_nodes,
+                     a.n_centers);
   return hipGetLastError();
 }
 

@@ -13,8 +13,8 @@ hipError_t launch_edge_force(int64_t E, const float* vec, const float* coeffs, f
 hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, const int* src_ptr,
                              const int* src_perm, const float* fe, float* F, hipStream_t s);
 hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* center,
-                              const int* nbr, int* row_ptr, int* src_ptr, int* src_perm,
-                              int* cnt, int* err, hipStream_t s);
+                              const int* nbr, int* row_ptr, int* src_ptr, int* src_perm, int* cnt,
+                              int* err, hipStream_t s, int n_interior = 0);
 hipError_t launch_embed(int n, const int* type, int nsp, const float* W, float* x, int* err,
                         hipStream_t s);
 hipError_t launch_gate_fwd(int n, bool last, const float* y, float* x, hipStream_t s);
@@ -29,6 +29,9 @@ hipError_t launch_sum(int64_t n, const float* a, float* part, float* out, hipStr
 hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStream_t s);
 hipError_t launch_gather_rows(int n, int D, const int* ptr, const int* perm, const float* src,
                               float* dst, hipStream_t s);
+// the same over neighbour nodes [j_begin, j_end) only
+hipError_t launch_gather_rows_range(int j_begin, int j_end, int D, const int* ptr, const int* perm,
+                                    const float* src, float* dst, hipStream_t s);
 hipError_t launch_pack(int64_t n, int dim, const int* idx, const float* src, int64_t ss, float* dst,
                        hipStream_t s);
 hipError_t launch_unpack(int64_t n, int dim, const int* idx, const float* src, float* dst,

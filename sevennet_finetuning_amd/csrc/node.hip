@@ -146,10 +146,11 @@ __global__ void k_atom_force(int n_nodes, int n_centers, const int* __restrict__
 
 // ------------------------------------------------------------ graph indices
 // row_ptr of the centre-sorted edge list + validation (edge_index[0] sorted,
-// indices in range).  err bits: 1 unsorted, 2 centre out of range, 4 nbr out of range.
-__global__ void k_row_ptr(int64_t E, int n_centers, int n_nodes, const int* __restrict__ center,
-                          const int* __restrict__ nbr, int* __restrict__ row_ptr,
-                          int* __restrict__ err) {
+// indices in range).  err bits: 1 unsorted, 2 centre out of range, 4 nbr out
+// of range, 16 a centre below n_interior has a ghost neighbour.
+__global__ void k_row_ptr(int64_t E, int n_centers, int n_nodes, int n_interior,
+                          const int* __restrict__ center, const int* __restrict__ nbr,
+                          int* __restrict__ row_ptr, int* __restrict__ err) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E) return;
   const int c = center[e];
@@ -159,6 +160,7 @@ __global__ void k_row_ptr(int64_t E, int n_centers, int n_nodes, const int* __re
     return;
   }
   if (j < 0 || j >= n_nodes) atomicOr(err, 4);
+  if (c < n_interior && j >= n_centers) atomicOr(err, 16);  // interior centre with a ghost neighbour
   const int prev = e ? center[e - 1] : -1;
   if (c < prev) {
     atomicOr(err, 1);
@@ -360,9 +362,10 @@ __global__ __launch_bounds__(256) void k_final_sum(int nb, int k, const float* _
 }
 
 // dh[j] = sum_{e: nbr[e] == j} dxc[e]  (transposed CSR, ascending edge order)
-__global__ void k_gather_rows(int n, int D, const int* __restrict__ ptr, const int* __restrict__ perm,
-                              const float* __restrict__ src, float* __restrict__ dst) {
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+__global__ void k_gather_rows(int j_begin, int n, int D, const int* __restrict__ ptr,
+                              const int* __restrict__ perm, const float* __restrict__ src,
+                              float* __restrict__ dst) {
+  const int j = j_begin + blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
   const int b = ptr[j], en = ptr[j + 1];
@@ -375,10 +378,10 @@ __global__ void k_gather_rows(int n, int D, const int* __restrict__ ptr, const i
 
 // same sum, 4 columns per lane (D % 4 == 0) and 4 rows in flight; the adds
 // keep the ascending edge order, so the result is bitwise that of k_gather_rows
-__global__ void k_gather_rows4(int n, int D4, const int* __restrict__ ptr,
+__global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict__ ptr,
                                const int* __restrict__ perm, const float4* __restrict__ src,
                                float4* __restrict__ dst) {
-  const int j = xcd_block() * 4 + (threadIdx.x >> 6);
+  const int j = j_begin + xcd_block() * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
   const int b = ptr[j], en = ptr[j + 1];
@@ -453,9 +456,9 @@ hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, con
 }
 hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* center,
                               const int* nbr, int* row_ptr, int* src_ptr, int* src_perm,
-                              int* cnt, int* err, hipStream_t s) {
+                              int* cnt, int* err, hipStream_t s, int n_interior) {
   LAUNCH(k_fill_int, nblk(n_centers + 1), n_centers + 1, 0, row_ptr);
-  LAUNCH(k_row_ptr, nblk(E), E, n_centers, n_nodes, center, nbr, row_ptr, err);
+  LAUNCH(k_row_ptr, nblk(E), E, n_centers, n_nodes, n_interior, center, nbr, row_ptr, err);
   LAUNCH(k_fill_int, nblk(n_nodes), n_nodes, 0, cnt);
   LAUNCH(k_count_nbr, nblk(E), E, nbr, n_nodes, cnt);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, n_nodes, cnt, src_ptr);
@@ -513,13 +516,18 @@ hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStr
 }
 hipError_t launch_gather_rows(int n, int D, const int* ptr, const int* perm, const float* src,
                               float* dst, hipStream_t s) {
+  return launch_gather_rows_range(0, n, D, ptr, perm, src, dst, s);
+}
+hipError_t launch_gather_rows_range(int j_begin, int j_end, int D, const int* ptr, const int* perm,
+                                    const float* src, float* dst, hipStream_t s) {
+  const int n = j_end - j_begin;
   if (n <= 0) return hipGetLastError();
   if (D % 4 == 0) {
-    hipLaunchKernelGGL(k_gather_rows4, dim3((n + 3) / 4), dim3(256), 0, s, n, D / 4, ptr, perm,
-                       (const float4*)src, (float4*)dst);
+    hipLaunchKernelGGL(k_gather_rows4, dim3((n + 3) / 4), dim3(256), 0, s, j_begin, j_end, D / 4,
+                       ptr, perm, (const float4*)src, (float4*)dst);
   } else {
-    hipLaunchKernelGGL(k_gather_rows, dim3((n + 3) / 4), dim3(256), 0, s, n, D, ptr, perm, src,
-                       dst);
+    hipLaunchKernelGGL(k_gather_rows, dim3((n + 3) / 4), dim3(256), 0, s, j_begin, j_end, D, ptr,
+                       perm, src, dst);
   }
   return hipGetLastError();
 }

@@ -24,7 +24,11 @@ Here, one process per GPU:
 * ``Halo`` moves rows with one ``all_to_all_single`` per exchange (RCCL over
   xGMI with backend "nccl"; host-staged with "gloo"), packing and unpacking
   with the library's halo kernels.  Reverse exchanges accumulate per peer
-  block in rank order (deterministic; no atomics).
+  block in rank order (deterministic; no atomics).  Exchanges are started
+  asynchronously and overlapped with the work that does not need them: the
+  interior centres (owned atoms without ghost neighbours, ordered first) in
+  the forward, the interior centres and owned rows in the backward
+  (e3gnn_layer_forward_part / _backward_part).
 * ``ParallelE3GNN.set_graph`` uploads a rank graph once per neighbour list;
   ``evaluate`` runs one evaluation: graph_set, 5 x (halo forward, layer
   forward), readout, 5 x (layer backward, halo reverse), forces, reverse of
@@ -77,7 +81,8 @@ class RankGraph:
     rank: int
     world: int
     grid: tuple
-    owned: np.ndarray            # global ids of owned atoms (sorted) -> rows [0, n_local)
+    owned: np.ndarray            # global ids of owned atoms -> rows [0, n_local):
+                                 # interior atoms first, then boundary, each by id
     ghosts: np.ndarray           # global ids of ghost rows [n_local, n_local + n_ghost)
     types: np.ndarray            # int32 [n_local + n_ghost]
     center: np.ndarray           # int32 [E] (sorted, < n_local)
@@ -85,7 +90,8 @@ class RankGraph:
     vec: np.ndarray              # float64 [E, 3] = x_j - x_i (+ image); engines cast
     recv_counts: np.ndarray      # ghosts received from each rank
     recv_rows: np.ndarray        # ghost rows, grouped by owner rank
-    req_rows: np.ndarray         # owners' local rows of those ghosts (what we ask for)
+    req_ids: np.ndarray          # global ids of those ghosts (what we ask the owners for)
+    n_interior: int = 0          # owned rows [0, n_interior) have no ghost neighbour
     send_counts: np.ndarray = field(default=None)  # rows each peer asks of us
     send_rows: np.ndarray = field(default=None)    # our local rows, grouped by peer
 
@@ -99,26 +105,30 @@ class RankGraph:
 
 
 def build_rank_graph(pos, cell, types, cutoff, grid, rank, pbc=(True, True, True)):
-    """Local graph of ``rank`` (no communication; see ``handshake``)."""
+    """Local graph of ``rank`` (no communication; see ``handshake``).  Owned
+    atoms whose neighbours are all owned (interior) come first, so the
+    library can convolve them while the halo is in flight (e3gnn_set_interior)."""
     pos = np.asarray(pos, dtype=np.float64)
     cell = np.asarray(cell, dtype=np.float64)
     types = np.asarray(types)
     world = int(np.prod(grid))
     own = owners(pos, cell, grid)
-    owned = np.nonzero(own == rank)[0]
-    ei, sh = neighbor_list(pos, cell, cutoff, pbc=pbc, centers=owned)
+    mine = np.nonzero(own == rank)[0]
+    ei, sh = neighbor_list(pos, cell, cutoff, pbc=pbc, centers=mine)
     i, j = ei
+    boundary = np.zeros(len(pos), dtype=bool)
+    boundary[i[own[j] != rank]] = True
+    owned = np.concatenate([mine[~boundary[mine]], mine[boundary[mine]]])
+    n_interior = int((~boundary[mine]).sum())
     gj = np.unique(j[own[j] != rank])
     ghosts = gj[np.lexsort((gj, own[gj]))]
     lid = np.full(len(pos), -1, dtype=np.int64)
     lid[owned] = np.arange(len(owned))
     lid[ghosts] = len(owned) + np.arange(len(ghosts))
+    # CSR by local centre row (stable: each centre keeps the (j, S) order)
+    order = np.argsort(lid[i], kind='stable')
+    i, j, sh = i[order], j[order], sh[order]
     vec = pos[j] + sh @ cell - pos[i]
-    # owner-local row of every atom (its index among its owner's sorted atoms)
-    order = np.lexsort((np.arange(len(pos)), own))
-    start = np.concatenate([[0], np.cumsum(np.bincount(own, minlength=world))])
-    owner_row = np.empty(len(pos), dtype=np.int64)
-    owner_row[order] = np.arange(len(pos)) - start[own[order]]
     return RankGraph(
         rank=rank, world=world, grid=tuple(grid), owned=owned, ghosts=ghosts,
         types=np.concatenate([types[owned], types[ghosts]]).astype(np.int32),
@@ -126,11 +136,12 @@ def build_rank_graph(pos, cell, types, cutoff, grid, rank, pbc=(True, True, True
         vec=vec,
         recv_counts=np.bincount(own[ghosts], minlength=world).astype(np.int64),
         recv_rows=(len(owned) + np.arange(len(ghosts))).astype(np.int64),
-        req_rows=owner_row[ghosts].astype(np.int64))
+        req_ids=ghosts.astype(np.int64), n_interior=n_interior)
 
 
 def handshake(rg, group=None, device='cpu'):
-    """Tell every owner which of its rows we need (one-time, per graph)."""
+    """Tell every owner which of its atoms we need (global ids, one-time per
+    graph); the owner turns them into its local rows."""
     w = rg.world
     if w == 1:
         rg.send_counts = np.zeros(1, dtype=np.int64)
@@ -140,12 +151,21 @@ def handshake(rg, group=None, device='cpu'):
     sc = torch.empty_like(rc)
     dist.all_to_all_single(sc, rc, group=group)
     send_counts = sc.cpu().numpy()
-    req = torch.as_tensor(rg.req_rows, dtype=torch.int64, device=device)
-    rows = torch.empty(int(send_counts.sum()), dtype=torch.int64, device=device)
-    dist.all_to_all_single(rows, req, output_split_sizes=send_counts.tolist(),
+    req = torch.as_tensor(rg.req_ids, dtype=torch.int64, device=device)
+    ids = torch.empty(int(send_counts.sum()), dtype=torch.int64, device=device)
+    dist.all_to_all_single(ids, req, output_split_sizes=send_counts.tolist(),
                            input_split_sizes=rg.recv_counts.tolist(), group=group)
+    ids = ids.cpu().numpy()
+    local_of = {int(g): r for r, g in enumerate(rg.owned)} if len(ids) < 4096 else None
+    if local_of is not None:
+        rows = np.array([local_of[int(g)] for g in ids], dtype=np.int64)
+    else:   # vectorised: owned ids sorted, positions mapped back to rows
+        srt = np.argsort(rg.owned)
+        rows = srt[np.searchsorted(rg.owned, ids, sorter=srt)].astype(np.int64)
+    if len(ids) and not np.array_equal(rg.owned[rows], ids):
+        raise RuntimeError('halo handshake: a peer asked for an atom this rank does not own')
     rg.send_counts = send_counts
-    rg.send_rows = rows.cpu().numpy()
+    rg.send_rows = rows
     return rg
 
 
@@ -166,39 +186,68 @@ class Halo:
         self.rc = [int(x) for x in rg.recv_counts]
         self.soff = np.concatenate([[0], np.cumsum(self.sc)]).astype(np.int64)
 
-    def _a2a(self, out, inp, out_splits, in_splits):
+    def _a2a_start(self, out, inp, out_splits, in_splits):
+        """Start an all_to_all (async on the device with RCCL: ordered after
+        the pack on the current stream, waited for on the stream in finish)."""
         if self.staged:
             o = torch.empty(out.shape, dtype=out.dtype)
-            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
-            out.copy_(o)
-        else:
-            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+            w = dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group,
+                                       async_op=True)
+            return (w, o, out)
+        w = dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group,
+                                   async_op=True)
+        return (w, None, out)
 
-    def forward(self, kind, t):
-        """Ghost rows of buffer (kind, t) <- their owners' rows."""
+    @staticmethod
+    def _a2a_wait(h):
+        w, o, out = h
+        w.wait()
+        if o is not None:
+            out.copy_(o)
+
+    def forward_start(self, kind, t):
+        """Ghost rows of buffer (kind, t) <- their owners' rows: pack + start."""
         if self.rg.world == 1:
-            return
+            return None
         dim = self.eng.dim(kind, t)
         sbuf = self.eng.empty(sum(self.sc), dim)
         rbuf = self.eng.empty(sum(self.rc), dim)
         self.eng.pack(kind, t, self.send_rows, sbuf)
-        self._a2a(rbuf, sbuf, self.rc, self.sc)
+        return (kind, t, rbuf, sbuf, self._a2a_start(rbuf, sbuf, self.rc, self.sc))
+
+    def forward_finish(self, h):
+        if h is None:
+            return
+        kind, t, rbuf, _, a2a = h
+        self._a2a_wait(a2a)
         self.eng.unpack(kind, t, self.recv_rows, rbuf, accumulate=False)
 
-    def reverse(self, kind, t):
-        """Owner rows of buffer (kind, t) += the ghost rows peers hold for them."""
+    def reverse_start(self, kind, t):
+        """Owner rows of buffer (kind, t) += the ghost rows peers hold: pack + start."""
         if self.rg.world == 1:
-            return
+            return None
         dim = self.eng.dim(kind, t)
         sbuf = self.eng.empty(sum(self.rc), dim)
         rbuf = self.eng.empty(sum(self.sc), dim)
         self.eng.pack(kind, t, self.recv_rows, sbuf)
-        self._a2a(rbuf, sbuf, self.sc, self.rc)
+        return (kind, t, rbuf, sbuf, self._a2a_start(rbuf, sbuf, self.sc, self.rc))
+
+    def reverse_finish(self, h):
+        if h is None:
+            return
+        kind, t, rbuf, _, a2a = h
+        self._a2a_wait(a2a)
         # one accumulate per peer block: unique rows inside a block, fixed order
         for p in range(self.rg.world):
             a, b = int(self.soff[p]), int(self.soff[p + 1])
             if b > a:
                 self.eng.unpack(kind, t, self.send_rows[a:b], rbuf[a:b], accumulate=True)
+
+    def forward(self, kind, t):
+        self.forward_finish(self.forward_start(kind, t))
+
+    def reverse(self, kind, t):
+        self.reverse_finish(self.reverse_start(kind, t))
 
 
 # ------------------------------------------------------------------ engines
@@ -227,6 +276,7 @@ class HipSegmentEngine:
         self.n_ghost = rg.n_ghost
         self._in = (t32(rg.types), t32(rg.center), t32(rg.nbr),
                     torch.as_tensor(np.asarray(rg.vec, dtype=np.float32), device=dev))
+        _lib.check(self.lib.e3gnn_set_interior(self.ctx, int(rg.n_interior)))
 
     def graph_set(self):
         """Per evaluation: CSR indices, transposed CSR, edge embedding and
@@ -266,6 +316,12 @@ class HipSegmentEngine:
 
     def layer_forward(self, t):
         _lib.check(self.lib.e3gnn_layer_forward(self.ctx, t, self._s()))
+
+    def layer_forward_part(self, t, part):
+        _lib.check(self.lib.e3gnn_layer_forward_part(self.ctx, t, part, self._s()))
+
+    def layer_backward_part(self, t, part):
+        _lib.check(self.lib.e3gnn_layer_backward_part(self.ctx, t, part, self._s()))
 
     def readout(self):
         e = torch.empty(1, device=self.device)
@@ -316,13 +372,25 @@ class ParallelE3GNN:
         eng.graph_set()
         for t in range(L):
             if t > 0:
-                halo.forward('x', t)          # forward_comm of the layer-t features
-            eng.layer_forward(t)
+                # forward_comm of the layer-t features, overlapped with the
+                # owned rows' work (interior centres)
+                h = halo.forward_start('x', t)
+                eng.layer_forward_part(t, 0)
+                halo.forward_finish(h)
+                eng.layer_forward_part(t, 1)
+            else:
+                eng.layer_forward(t)
         e_local, atomic = eng.readout()
         for t in reversed(range(L)):
-            eng.layer_backward(t)
             if t > 0:
-                halo.reverse('grad', t)       # reverse_comm of dE/dx_ghost
+                # ghost rows of dE/dx first, their reverse_comm overlapped with
+                # the interior centres and owned rows
+                eng.layer_backward_part(t, 0)
+                h = halo.reverse_start('grad', t)
+                eng.layer_backward_part(t, 1)
+                halo.reverse_finish(h)
+            else:
+                eng.layer_backward(t)
         forces, vir = eng.forces()
         halo.reverse('force', 0)              # ghost forces -> owners (newton on)
         tot = torch.cat([e_local.reshape(1), vir.reshape(6)]).to(torch.float64)

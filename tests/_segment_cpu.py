@@ -96,6 +96,18 @@ class CpuSegmentEngine:
         nxt[:nl] = out.detach()
         self.x[t + 1] = nxt
 
+    # halo-overlap parts: the oracle engine computes a block in one go (part 1
+    # of the forward, part 0 of the backward), which keeps the driver's data
+    # dependencies (ghost rows needed by forward part 1, produced by backward
+    # part 0)
+    def layer_forward_part(self, t, part):
+        if part == 1:
+            self.layer_forward(t)
+
+    def layer_backward_part(self, t, part):
+        if part == 0:
+            self.layer_backward(t)
+
     def readout(self):
         r, nl, L = self.ref, self.nl, self.num_layers
         xl = self.x[L].detach().requires_grad_(True)

@@ -58,6 +58,10 @@ def test_rank_graphs_partition_the_global_graph(world):
         # ghosts grouped by owner, each group sorted by id
         go = own[rg.ghosts]
         assert np.all(np.diff(go) >= 0)
+        # interior owned atoms first: their edges never reach a ghost row
+        assert np.all(rg.nbr[rg.center < rg.n_interior] < rg.n_local)
+        bnd = np.unique(rg.center[rg.nbr >= rg.n_local])
+        assert np.all(bnd >= rg.n_interior)
         edges.append(np.concatenate([np.stack([ids[rg.center], ids[rg.nbr]], 1), rg.vec], 1))
     assert np.all(seen == 1)
     key = lambda a: np.lexsort((np.round(a[:, 4], 6), np.round(a[:, 3], 6),
@@ -76,7 +80,14 @@ def _run(world, name, engine, tmp_path):
     return np.load(out)
 
 
-@pytest.mark.parametrize('world,name', [(2, 'si_rng0_2x2x2'), (4, 'mixed_2x2x2')])
+def test_interior_atoms_exist_in_thick_slabs():
+    pos, cell, types = system('si_rng0_6x2x2', SYMS)
+    rg = build_rank_graph(pos, cell, types, 5.0, brick_grid(2), 0)
+    assert 0 < rg.n_interior < rg.n_local
+
+
+@pytest.mark.parametrize('world,name', [(2, 'si_rng0_2x2x2'), (4, 'mixed_2x2x2'),
+                                        (2, 'si_rng0_6x2x2')])
 def test_decomposed_matches_single_process_oracle(world, name, tmp_path):
     pos, cell, types = system(name, SYMS)
     ref = oracle_eval(pos, cell, types)
@@ -92,11 +103,13 @@ def test_decomposed_matches_single_process_oracle(world, name, tmp_path):
 
 
 @pytest.mark.gpu
-def test_decomposed_hip_matches_single_device(tmp_path):
+@pytest.mark.parametrize('name', ['mixed_3x3x3', 'si_rng0_6x2x2'])
+def test_decomposed_hip_matches_single_device(tmp_path, name):
     """Two ranks on the box's GPU (gloo, host-staged halo) vs the
-    single-process HIP evaluation and the oracle."""
+    single-process HIP evaluation and the oracle; si_rng0_6x2x2 has interior
+    atoms, so the library's overlapped parts (interior / boundary centres,
+    ghost / owned rows) are exercised."""
     from sevennet_finetuning_amd.model import E3GNNModel
-    name = 'mixed_3x3x3'
     pos, cell, types = system(name, SYMS)
     got = _run(2, name, 'hip', tmp_path)
     assert got['repeat_same'][0]
