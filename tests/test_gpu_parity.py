@@ -240,3 +240,48 @@ def test_high_degree_centres(model):
     # forces here are O(10-100) eV/A: relative tolerance on this unphysical packing
     fscale = max(1.0, float(np.abs(ref['forces']).max()))
     assert np.abs(got['forces'] - ref['forces']).max() <= F_TOL * fscale
+
+
+def test_batched_branch_per_graph_energy_and_stress(model):
+    """AtomGraphSequential.set_is_batch_data(True) (sequential.py:38-46): a
+    PyG-style batch of three graphs (edge_index offset, ``batch`` vector,
+    stacked cells) gives per-graph energies and stresses equal to the
+    one-graph evaluations (and the oracle's)."""
+    from sevennet_finetuning_amd.neighbor import neighbor_list
+    names = ['si_rng0_2x2x1', 'mixed_2x2x2', 'hfo2_resdat']
+    parts, off = [], 0
+    for b, nm in enumerate(names):
+        pos, cell, types = system(nm, SYMS)
+        ei, sh = neighbor_list(pos, cell, model.cutoff)
+        parts.append((pos, cell, types, ei + off, sh, b))
+        off += len(pos)
+    data = {
+        'x': torch.tensor(np.concatenate([p[2] for p in parts])),
+        'pos': torch.tensor(np.concatenate([p[0] for p in parts]), dtype=torch.float32),
+        'edge_index': torch.tensor(np.concatenate([p[3] for p in parts], 1)),
+        'pbc_shift': torch.tensor(np.concatenate([p[4] for p in parts]), dtype=torch.float32),
+        'cell_lattice_vectors': torch.tensor(np.stack([p[1] for p in parts]), dtype=torch.float32),
+        'batch': torch.tensor(np.concatenate([np.full(len(p[0]), p[5]) for p in parts])),
+        'cell_volume': torch.tensor([abs(np.linalg.det(p[1])) for p in parts], dtype=torch.float32),
+        'num_atoms': torch.tensor([len(p[0]) for p in parts]),
+    }
+    try:
+        model.set_is_batch_data(True)
+        out = model(data)
+    finally:
+        model.set_is_batch_data(False)
+    e = out['inferred_total_energy'].cpu().numpy()
+    s = out['inferred_stress'].cpu().numpy()
+    f = out['inferred_force'].cpu().numpy()
+    assert e.shape == (3,) and s.shape == (3, 6)
+    off = 0
+    for b, nm in enumerate(names):
+        pos, cell, types = system(nm, SYMS)
+        one = run(model, pos, cell, types)
+        ref = oracle_eval(pos, cell, types)
+        assert abs(e[b] - one['energy']) <= 2e-6 * abs(one['energy'])
+        assert abs(e[b] - ref['energy']) <= E_RTOL * abs(ref['energy'])
+        assert np.abs(s[b] - one['stress']).max() <= S_TOL
+        assert np.abs(s[b] - ref['stress']).max() <= S_TOL
+        assert np.abs(f[off:off + len(pos)] - ref['forces']).max() <= F_TOL
+        off += len(pos)
