@@ -178,7 +178,7 @@ struct e3gnn_model {
   std::vector<std::unique_ptr<Linear>> sc, si1, si2;
   struct Mlp {
     DBuf w0, w1, w2, w0t, w1t, w2t;
-    DBuf w1p, w2p, w2q;  // MFMA-operand orders of the fused kernels (fused.h)
+    DBuf w1p, w2p, w2q, w2r;  // MFMA-operand orders of the fused kernels (fused.h)
     DBuf w2b;            // 3-way bf16 split of w2 in 16x16x32 operand order (fused.h)
     DBuf w2c;            // 3-way bf16 split of w2, dE/dw-kernel block pairs (fused.h)
   };
@@ -250,6 +250,13 @@ struct e3gnn_ctx {
     return (v && std::string(v) == "node") ? 0 : 1;
   }();
   int graph_bwd_edge = 1;
+  // per-centre dE/dx kernel also computes dE/dw -> dH2 -> dE/demb (one
+  // backward launch per block; 1, default) or a separate dE/dw kernel over
+  // edge tiles (0; E3GNN_BWD_FUSE=0)
+  int bwd_fuse = [] {
+    const char* v = std::getenv("E3GNN_BWD_FUSE");
+    return (v && std::string(v) == "0") ? 0 : 1;
+  }();
   // 0: fused radial-MLP + TP kernels (fused.hip); 1: the unfused v1 kernels
   // (materialised per-edge weights; kept as an independent cross-check)
   int impl = [] {
@@ -493,7 +500,8 @@ void dense_cg(float* out) {
 MlpW mlp_ptrs(const e3gnn_model* m, int t) {
   const auto& mm = m->mlp[t];
   return MlpW{mm.w0.f(),  mm.w1.f(),  mm.w2.f(),  mm.w2t.f(),
-              mm.w1p.f(), mm.w2p.f(), mm.w2q.f(), static_cast<const uint16_t*>(mm.w2b.p),
+              mm.w1p.f(), mm.w2p.f(), mm.w2q.f(), mm.w2r.f(),
+              static_cast<const uint16_t*>(mm.w2b.p),
               static_cast<const uint16_t*>(mm.w2c.p)};
 }
 
@@ -682,6 +690,15 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
                 for (int sx = 0; sx < 4; ++sx)
                   q2[((size_t)(cb * 4 + bh) * 64 + g * 16 + c) * 4 + sx] =
                       a2[(size_t)(16 * bh + c) * W + 16 * cb + 4 * sx + g];
+        // w2r: the same blocks with channel 4g + r (the fused backward's dE/dw layout)
+        std::vector<float> r2((size_t)W * 64);
+        for (int cb = 0; cb < W / 16; ++cb)
+          for (int bh = 0; bh < 4; ++bh)
+            for (int g = 0; g < 4; ++g)
+              for (int c = 0; c < 16; ++c)
+                for (int r = 0; r < 4; ++r)
+                  r2[((size_t)(cb * 4 + bh) * 64 + g * 16 + c) * 4 + r] =
+                      a2[(size_t)(16 * bh + c) * W + 16 * cb + 4 * g + r];
         // w2b (MlpW::w2b): w2 = p0 + p1 + p2 exactly (bf16 pieces, round to
         // nearest even); element t of lane (g, c) in k-half m of column block cb
         // is w2[16(2m + t/4) + 4g + t%4][16 cb + c]
@@ -726,6 +743,7 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
         if (upload(mm.w2c, c2) != hipSuccess) throw std::runtime_error("upload mlp (w2c)");
         if (W % 16 || upload(mm.w1p, kperm(a1, 64)) != hipSuccess ||
             upload(mm.w2p, kperm(a2, W)) != hipSuccess || upload(mm.w2q, q2) != hipSuccess ||
+            upload(mm.w2r, r2) != hipSuccess ||
             upload(mm.w2b, b2) != hipSuccess)
           throw std::runtime_error("upload mlp (packed)");
       }
@@ -1105,6 +1123,8 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     // the last block (224 message channels) is faster per neighbour node
     a.edge_order = c->graph_bwd_edge && kind != 2;
     a.dxc = (a.edge_order && t > 0) ? c->dxc.f() : nullptr;
+    // per-centre dE/dx kernel also does dE/dw (first and middle blocks)
+    a.fuse_w = a.edge_order && c->bwd_fuse;
     a.scratch_dh = c->dh.f();
     a.dgu = c->dgu.f();
     a.demb = c->demb.f();
@@ -1121,12 +1141,17 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     const double ef = (double)(a.e_end - a.e_begin);
     // algorithmic FLOP (the forward radial MLP the dE/dx kernel recomputes is
     // not counted): dE/dx + dE/dY = 2 x TP; dE/dw = TP, dH2 = dw W2^T, MLP chain
-    {
-      Region r(c, s, C_CONV_BWD_X + kind, 2.0 * tp_flops_per_edge(kind) * ef,
-               ef * 4 * (8 + 9 + 2 + 3) + (a.c_end - a.c_begin) * 4.0 * dm);
+    // empty ranges launch nothing (and are not counted as launches)
+    const bool any_x = a.edge_order ? a.c_end > a.c_begin : a.node_end > a.node_begin;
+    if (any_x) {
+      // fused (a.fuse_w): + dE/dw = TP, dH2 = dw W2^T and the MLP chain backward
+      const double xf = 2.0 * tp_flops_per_edge(kind) +
+                        (a.fuse_w ? tp_flops_per_edge(kind) + 2.0 * (64 * W + 64 * 64 + 8 * 64) : 0.0);
+      Region r(c, s, C_CONV_BWD_X + kind, xf * ef,
+               ef * 4 * (8 + 9 + 2 + 3 + (a.fuse_w ? 8 : 0)) + (a.c_end - a.c_begin) * 4.0 * dm);
       HIPCHK(launch_conv_bwd_x(kind, a, s));
     }
-    {
+    if (ef > 0 && !a.fuse_w) {
       Region r(c, s, C_CONV_BWD_W + kind,
                tp_flops_per_edge(kind) * ef + 2.0 * ef * (64 * W + 64 * 64 + 8 * 64),
                ef * 4 * (8 + 9 + 2 + 8 + dx));

@@ -14,6 +14,7 @@ struct MlpW {
   const float* w1p;  // [n<64][g][q][t] = w1[16q + 4g + t][n]
   const float* w2p;  // [n<W][g][q][t]  = w2[16q + 4g + t][n]
   const float* w2q;  // [n/16][bh][g][c][s] = w2[16bh + c][16(n/16) + 4s + g]
+  const float* w2r;  // [n/16][bh][g][c][r] = w2[16bh + c][16(n/16) + 4g + r] (fused bwd)
   // w2 as three bf16 pieces (w2 = p0 + p1 + p2, exact) in v_mfma_f32_16x16x32_bf16
   // operand order: [n/16][piece][m][g][c][t] = piece of w2[16(2m + t/4) + 4g + t%4][n]
   const uint16_t* w2b;
@@ -38,6 +39,7 @@ struct FusedArgs {
   float* scratch_dh;   // [n_nodes, DX] sink used when dh is null
   float* dxc;          // [E, DX] per-edge dE/dx (edge-ordered dE/dx kernel; nullable)
   int edge_order;      // dE/dx kernel over CSR edge tiles (writes dxc) vs per neighbour
+  int fuse_w;          // per-centre dE/dx kernel also does dE/dw -> dE/demb (no bwd_w launch)
   float* dgu;         // bwd in/out [E, 3]  dE/du accumulated over layers
   float* demb;        // bwd in/out [E, 8]  dE/demb accumulated over layers
   MlpW W;

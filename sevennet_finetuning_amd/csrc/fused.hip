@@ -58,6 +58,11 @@
 #ifndef E3GNN_BWDX_WAVES
 #define E3GNN_BWDX_WAVES 3
 #endif
+// the fused dE/dx + dE/dw kernel (MODE 3) holds dH2 accumulators and the
+// block's W2 operands on top: 2 waves/SIMD without spills
+#ifndef E3GNN_BWDXW_WAVES
+#define E3GNN_BWDXW_WAVES 2
+#endif
 
 namespace e3gnn {
 namespace {
@@ -104,7 +109,7 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // does not hoist hundreds of 64-bit addresses out of the centre loop (which it
 // did, and spilled).  Offsets outside the descriptor read 0 (padded rows).
 struct WRes {
-  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b, w2c;
+  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b, w2c, w2r;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int nfloats) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
@@ -112,7 +117,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int nfloa
 __device__ __forceinline__ WRes make_wres(const MlpW& W, int width) {
   return {rsrc(W.w0, 8 * 64), rsrc(W.w1, 64 * 64), rsrc(W.w2p, 64 * width), rsrc(W.w2q, 64 * width),
           rsrc(W.w1p, 64 * 64), rsrc((const float*)W.w2b, 64 * width * 3 / 2),
-          rsrc((const float*)W.w2c, 64 * width * 3 / 2)};
+          rsrc((const float*)W.w2c, 64 * width * 3 / 2), rsrc(W.w2r, 64 * width)};
 }
 __device__ __forceinline__ float ldw(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
   // the builtin returns the raw 32 bits (an unsigned int): reinterpret, never convert
@@ -525,6 +530,35 @@ __device__ __forceinline__ float tp_bwd_w(const float* x, const float* y, const 
   });
   return dwv;
 }
+// tp_bwd_x and dE/dw of the same (edge, channel) in one pass: with
+// t'_ij = sum_k C_ijk g_k and u_i = sum_j t'_ij y_j,
+//   dE/dx_i += w u_i,  dE/dy_j += t'_ij (w x_i),  dE/dw = sum_i x_i u_i
+// (no x_i y_j products: those are shared by the paths of an (l1, l2) pair, and
+// the compiler kept them live across paths; the fused backward, MODE 3)
+template <int L1, int L2, int L3>
+__device__ __forceinline__ float tp_bwd_xw(const float* x, const float* y, float w, const float* gm,
+                                           float* dx, float* dy) {
+  using C = CG<L1, L2, L3>;
+  float dwv = 0.f;
+  sfor<2 * L1 + 1>([&](auto i) {
+    float ui = 0.f;
+    const float wx = w * x[i];
+    sfor<2 * L2 + 1>([&](auto j) {
+      if constexpr (cg_pair<C, i, j>()) {
+        float tp = 0.f;
+        sfor<C::n>([&](auto q) {
+          if constexpr (C::e[q].i == i && C::e[q].j == j) tp += C::e[q].c * gm[C::e[q].k];
+        });
+        ui += tp * y[j];
+        dy[j] += tp * wx;
+      }
+    });
+    dx[i] += w * ui;
+    dwv += x[i] * ui;
+  });
+  return dwv;
+}
+
 // sum over the 16 lanes of a DPP row (fixed order; every lane gets the total)
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float x) {
@@ -564,6 +598,56 @@ __device__ __forceinline__ void prefetch_gm(float* gmN, __amdgpu_buffer_rsrc_t R
   }
 }
 
+// MLP chain backward of a 16-edge tile [e0, min(e0 + 16, end)) from dH2^T
+// (D[hidden 16 bh + 4g + r][edge slot c]): pre-activations recomputed, dA2,
+// dH1^T = W1 dA2^T, demb^T = W0 dA1^T, demb += (rows < 8)
+__device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __restrict__ emb, int e0,
+                                              int end, int lane, const f32x4 (&dh2)[4],
+                                              float* __restrict__ demb) {
+  const int g = lane >> 4, col = lane & 15;
+  MlpT m;
+  mlp_pre(R, emb, e0, end, lane, m);
+
+  f32x4 da2[4], dh1[4];
+#pragma unroll
+  for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) da2[bb][r] = dh2[bb][r] * act_grad(m.a2[bb][r]);
+  // dH1^T = W1 dA2^T  (A[i = h_in][k = h_out] = W1s[h_in][h_out])
+  const int vb = (col * 64 + 4 * g) * 4;
+#pragma unroll
+  for (int bi = 0; bi < 4; ++bi) {
+    phase();
+    float a[16];  // W1s[16 bi + c][16q + 4g + t]: 4 contiguous per q
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = ldw4(R.w1, vb, (16 * bi * 64 + 16 * q) * 4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[4 * q + t] = v[t];
+    }
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = mfma(a[s], da2[s >> 2][s & 3], acc);
+    dh1[bi] = acc;
+  }
+  // demb^T = W0 dA1^T (rows n < 8; lanes c >= 8 read 0 outside the descriptor)
+  f32x4 de = zero4();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 a4 = ldw4(R.w0, vb, 16 * q * 4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      de = mfma(a4[t], dh1[q][t] * act_grad(m.a1[q][t]), de);
+  }
+  {
+    const int e = e0 + col;
+    if (g < 2 && e < end) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) demb[(int64_t)e * 8 + 4 * g + r] += de[r];
+    }
+  }
+}
+
 // B1: lane (g, c) = edge slot c of the tile x channels 4g..4g+3 of a 16-channel
 // block (transposed product w^T = W2^T H2^T: D[channel 4g+r][edge c]).  One
 // edge per lane keeps dE/dY in 8 registers; dE/dx[j] is summed over the 16
@@ -579,7 +663,7 @@ __device__ __forceinline__ void prefetch_gm(float* gmN, __amdgpu_buffer_rsrc_t R
 // the 60 per-path-block dE/dagg reads of a middle block become LDS reads
 // instead of dependent global gathers; dE/dx per edge to dxc as in MODE 1.
 template <class L, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_WAVES, E3GNN_BWDX_WAVES))) void k_conv_bwd_x(const int* __restrict__ src_ptr,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ? E3GNN_BWDXW_WAVES : E3GNN_BWDX_WAVES, MODE == 3 ? E3GNN_BWDXW_WAVES : E3GNN_BWDX_WAVES))) void k_conv_bwd_x(const int* __restrict__ src_ptr,
                                                     const int* __restrict__ src_perm,
                                                     const int* __restrict__ center,
                                                     const float* __restrict__ emb,
@@ -591,19 +675,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
                                                     int n_centers, const int* __restrict__ nbr,
                                                     float* __restrict__ dxc, int n_edges,
                                                     const int* __restrict__ row_ptr, int r_begin,
-                                                    int r_end) {
+                                                    int r_end, float* __restrict__ demb) {
   constexpr bool EDGE = MODE != 0;  // per-edge dE/dx output (dxc)
+  constexpr bool CTR = MODE >= 2;   // one wave per centre, dE/dagg row in LDS
+  constexpr bool FW = MODE == 3;    // + dE/dw -> dH2 -> MLP chain -> dE/demb
   // MODE 0: dE/dx[j] of the wave's node; MODE 2: dE/dagg row of its centre
-  __shared__ __attribute__((aligned(16))) float lds[4][MODE == 0 ? L::DX : (MODE == 2 ? L::DM : 1)];
+  __shared__ __attribute__((aligned(16))) float lds[4][MODE == 0 ? L::DX : (CTR ? L::DM : 1)];
   const int wid = threadIdx.x >> 6;
   // wave index: node (MODE 0), 16-edge tile of [r_begin, r_end) (MODE 1), centre (MODE 2)
   const int jn = __builtin_amdgcn_readfirstlane((MODE == 1 ? 0 : r_begin) + xcd_block() * 4 + wid);
   if (MODE == 1 ? r_begin + jn * 16 >= r_end : jn >= r_end) return;
   float* dacc = lds[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
-  const int qb = MODE == 1 ? r_begin + jn * 16 : (MODE == 2 ? row_ptr[jn] : src_ptr[jn]);
-  const int qe = MODE == 1 ? min(qb + 16, r_end) : (MODE == 2 ? row_ptr[jn + 1] : src_ptr[jn + 1]);
-  if constexpr (MODE == 2) {
+  const int qb = MODE == 1 ? r_begin + jn * 16 : (CTR ? row_ptr[jn] : src_ptr[jn]);
+  const int qe = MODE == 1 ? min(qb + 16, r_end) : (CTR ? row_ptr[jn + 1] : src_ptr[jn + 1]);
+  if constexpr (CTR) {
     // stage the centre's dE/dagg row: DM / 4 float4 per wave, all in flight
     const float4* src = reinterpret_cast<const float4*>(gagg + (int64_t)jn * L::DM);
     float4* dst = reinterpret_cast<float4*>(dacc);
@@ -657,6 +743,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
         for (int r = 0; r < 4; ++r) h2[bb][r] = act_fwd(m.a2[bb][r]);
       split_h2(h2, hq);
     }
+    // MODE 3: dH2^T of the tile's edges (D[hidden 16 bh + 4g + r][edge c]),
+    // accumulated over the visited blocks
+    f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
     float dYa[9];  // dE/dY of edge c over this lane's channels (index 0 unused)
 #pragma unroll
     for (int q = 0; q < 9; ++q) dYa[q] = 0.f;
@@ -687,7 +776,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
 #pragma unroll
                 for (int k = 0; k < 4 * D3; ++k) gm[k] = gmN[k];
                 prefetch_gm<L, I, pi>(gmN, Rg, vg, g, jj);
-              } else if constexpr (MODE == 2) {
+              } else if constexpr (CTR) {
                 // the centre's row in LDS: 4 D3 contiguous floats per lane group
                 const float* gl = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
 #pragma unroll
@@ -695,6 +784,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
               } else {
                 load_gm<L, pi>(gm, Rg, vg, g, jj);
               }
+              // MODE 3: W2 operands of this block's dH2 product, issued now and
+              // consumed after the tensor product
+              f32x4 bq[4];
+              if constexpr (FW) load_w2q(bq, R.w2r, lane, p.woff + 16 * jj);
+              float dwr[4];
               // w^T block: A = W2s[:, col0 + i]^T (w2p order), B = H2^T
               const f32x4 wv = w2_block<false>(hq, wq);
               {
@@ -707,9 +801,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
                 float dy[2 * p.l2 + 1];
 #pragma unroll
                 for (int q = 0; q < 2 * p.l2 + 1; ++q) dy[q] = 0.f;
-                // padded slots: w = 0 and g = 0
-                tp_bwd_x<p.l1, p.l2, p.l3>(x + r * D1, y + yoff(p.l2), wv[r], gm + r * D3,
-                                           dx + r * D1, dy);
+                // padded slots: w = 0 and g = 0 (MODE 3: y = 0, so dE/dw = 0)
+                if constexpr (FW)
+                  dwr[r] = tp_bwd_xw<p.l1, p.l2, p.l3>(x + r * D1, y + yoff(p.l2), wv[r],
+                                                       gm + r * D3, dx + r * D1, dy);
+                else
+                  tp_bwd_x<p.l1, p.l2, p.l3>(x + r * D1, y + yoff(p.l2), wv[r], gm + r * D3,
+                                             dx + r * D1, dy);
                 if constexpr (p.l2 > 0) {
 #pragma unroll
                   for (int q = 0; q < 2 * p.l2 + 1; ++q) dYa[yoff(p.l2) + q] += dy[q];
@@ -719,6 +817,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
               }
               pin<4 * D1>(dx);
               pin<8>(dYa + 1);
+              if constexpr (FW) {
+                // dH2^T += W2[:, block] dw^T: k = lane group g, channel 4g + r
+#pragma unroll
+                for (int bh = 0; bh < 4; ++bh)
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) dh2[bh] = mfma(bq[bh][r], dwr[r], dh2[bh]);
+              }
             }
           });
           phase();
@@ -761,6 +866,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDX_
       o[0] += gx;
       o[1] += gy;
       o[2] += gz;
+    }
+    if constexpr (FW) {
+      phase();
+      mlp_bwd_chain(R, emb, q0, qe, lane, dh2, demb);
     }
   }
   if constexpr (MODE == 0) {
@@ -931,46 +1040,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_
   }
   // ---- MLP chain backward (pre-activations recomputed)
   phase();
-  MlpT m;
-  mlp_pre(R, emb, e0, end, lane, m);
-  f32x4 da2[4], dh1[4];
-#pragma unroll
-  for (int bb = 0; bb < 4; ++bb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) da2[bb][r] = dh2[bb][r] * act_grad(m.a2[bb][r]);
-  // dH1^T = W1 dA2^T  (A[i = h_in][k = h_out] = W1s[h_in][h_out])
-  const int vb = (col * 64 + 4 * g) * 4;
-#pragma unroll
-  for (int bi = 0; bi < 4; ++bi) {
-    phase();
-    float a[16];  // W1s[16 bi + c][16q + 4g + t]: 4 contiguous per q
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 v = ldw4(R.w1, vb, (16 * bi * 64 + 16 * q) * 4);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) a[4 * q + t] = v[t];
-    }
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc = mfma(a[s], da2[s >> 2][s & 3], acc);
-    dh1[bi] = acc;
-  }
-  // demb^T = W0 dA1^T (rows n < 8; lanes c >= 8 read 0 outside the descriptor)
-  f32x4 de = zero4();
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x4 a4 = ldw4(R.w0, vb, 16 * q * 4);
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-      de = mfma(a4[t], dh1[q][t] * act_grad(m.a1[q][t]), de);
-  }
-  {
-    const int e = e0 + col;
-    if (g < 2 && e < end) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) demb[(int64_t)e * 8 + 4 * g + r] += de[r];
-    }
-  }
+  mlp_bwd_chain(R, emb, e0, end, lane, dh2, demb);
 }
 
 }  // namespace
@@ -992,20 +1062,27 @@ template <class L>
 static hipError_t bwd_x_impl(const FusedArgs& a, hipStream_t s) {
   if (a.n_nodes <= 0 || a.n_edges <= 0) return hipSuccess;
   if (a.edge_order) {  // per-edge dE/dx (caller gathers)
-    if (E3GNN_BWDX_MODE == 2) {
+    if (a.fuse_w) {  // dE/dx, dE/du and dE/dw -> dE/demb in one pass
+      const int nc = a.c_end - a.c_begin;
+      if (nc <= 0) return hipSuccess;
+      hipLaunchKernelGGL((k_conv_bwd_x<L, 3>), dim3((nc + 3) / 4), dim3(256), 0, s, a.src_ptr,
+                         a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
+                         a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr, a.c_begin,
+                         a.c_end, a.demb);
+    } else if (E3GNN_BWDX_MODE == 2) {
       const int nc = a.c_end - a.c_begin;
       if (nc <= 0) return hipSuccess;
       hipLaunchKernelGGL((k_conv_bwd_x<L, 2>), dim3((nc + 3) / 4), dim3(256), 0, s, a.src_ptr,
                          a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
                          a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr, a.c_begin,
-                         a.c_end);
+                         a.c_end, a.demb);
     } else {
       const int tiles = (a.e_end - a.e_begin + 15) / 16;
       if (tiles <= 0) return hipSuccess;
       hipLaunchKernelGGL((k_conv_bwd_x<L, 1>), dim3((tiles + 3) / 4), dim3(256), 0, s, a.src_ptr,
                          a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
                          a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr, a.e_begin,
-                         a.e_end);
+                         a.e_end, a.demb);
     }
     return hipGetLastError();
   }
@@ -1016,13 +1093,13 @@ static hipError_t bwd_x_impl(const FusedArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((k_conv_bwd_x<L, 0>), dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr,
                      a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W,
                      a.dh ? a.dh : a.scratch_dh, a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc,
-                     a.n_edges, a.row_ptr, a.node_begin, a.node_end);
+                     a.n_edges, a.row_ptr, a.node_begin, a.node_end, a.demb);
   return hipGetLastError();
 }
 template <class L>
 static hipError_t bwd_w_impl(const FusedArgs& a, hipStream_t s) {
   const int tiles = (a.e_end - a.e_begin + 15) / 16;  // edge range of this launch
-  if (a.n_nodes <= 0 || tiles <= 0) return hipSuccess;
+  if (a.n_nodes <= 0 || tiles <= 0 || a.fuse_w) return hipSuccess;  // fused: done in bwd_x
   hipLaunchKernelGGL(k_conv_bwd_w<L>, dim3((tiles + 3) / 4), dim3(256), 0, s, a.center, a.nbr,
                      a.emb, a.Y, a.h, a.gagg, a.W, a.demb, a.e_begin, a.e_end, a.n_nodes,
                      a.n_centers);

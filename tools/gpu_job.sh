@@ -26,6 +26,7 @@ for s in "$@"; do
     bench) step bench 600 python bench.py --steps 5 --warmup 2 ;;
     benchq) step bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10 ;;
     benchf) step benchf 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
+    benchnofuse) step benchnofuse 600 env E3GNN_BWD_FUSE=0 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchsplit) step benchsplit 600 env E3GNN_BWD=split python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchmorton) step benchmorton 600 env E3GNN_BENCH_ORDER=morton python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchmorton_*) v=${s#benchmorton_}; step benchmorton_$v 600 env E3GNN_BENCH_ORDER=morton E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
