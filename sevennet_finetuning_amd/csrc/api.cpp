@@ -181,6 +181,7 @@ struct e3gnn_model {
     DBuf w1p, w2p, w2q, w2r;  // MFMA-operand orders of the fused kernels (fused.h)
     DBuf w2b;            // 3-way bf16 split of w2 in 16x16x32 operand order (fused.h)
     DBuf w2c;            // 3-way bf16 split of w2, dE/dw-kernel block pairs (fused.h)
+    DBuf w2d;            // the same for the fused backward's pairs (fused.h)
   };
   std::vector<Mlp> mlp;
 };
@@ -502,7 +503,7 @@ MlpW mlp_ptrs(const e3gnn_model* m, int t) {
   return MlpW{mm.w0.f(),  mm.w1.f(),  mm.w2.f(),  mm.w2t.f(),
               mm.w1p.f(), mm.w2p.f(), mm.w2q.f(), mm.w2r.f(),
               static_cast<const uint16_t*>(mm.w2b.p),
-              static_cast<const uint16_t*>(mm.w2c.p)};
+              static_cast<const uint16_t*>(mm.w2c.p), static_cast<const uint16_t*>(mm.w2d.p)};
 }
 
 }  // namespace
@@ -741,6 +742,24 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
                   }
                 }
         if (upload(mm.w2c, c2) != hipSuccess) throw std::runtime_error("upload mlp (w2c)");
+        // w2d (MlpW::w2d): element t of lane (g, c) for hidden block bh is
+        // w2[16 bh + c][col], col = cols[2P] + 4g + t (t < 4) or cols[2P + 1] + 4g + t - 4
+        std::vector<float> d2((size_t)W * 64 * 3 / 2);
+        uint16_t* d2h = reinterpret_cast<uint16_t*>(d2.data());
+        for (size_t P = 0; P < cols.size() / 2; ++P)
+          for (int bh = 0; bh < 4; ++bh)
+            for (int g = 0; g < 4; ++g)
+              for (int c = 0; c < 16; ++c)
+                for (int t8 = 0; t8 < 8; ++t8) {
+                  const int col = t8 < 4 ? cols[2 * P] + 4 * g + t8 : cols[2 * P + 1] + 4 * g + t8 - 4;
+                  float v = a2[(size_t)(16 * bh + c) * W + col];
+                  for (int pc = 0; pc < 3; ++pc) {
+                    const uint16_t hb = bf16_rne(v);
+                    d2h[(((P * 3 + pc) * 4 + bh) * 64 + g * 16 + c) * 8 + t8] = hb;
+                    v -= bf16_to_f32(hb);
+                  }
+                }
+        if (upload(mm.w2d, d2) != hipSuccess) throw std::runtime_error("upload mlp (w2d)");
         if (W % 16 || upload(mm.w1p, kperm(a1, 64)) != hipSuccess ||
             upload(mm.w2p, kperm(a2, W)) != hipSuccess || upload(mm.w2q, q2) != hipSuccess ||
             upload(mm.w2r, r2) != hipSuccess ||

@@ -22,6 +22,10 @@ struct MlpW {
   // consecutive visited 16-column blocks: [pair][piece][bh][g][c][t] = piece of
   // w2[16 bh + c][column of k = 8g + t] (api.cpp bwd_w_block_cols)
   const uint16_t* w2c;
+  // the fused backward's (MODE 3) pairs: [pair][piece][bh][g][c][t] = piece of
+  // w2[16 bh + c][col], col = channel 4g + t of the pair's first block (t < 4)
+  // or 4g + t - 4 of its second
+  const uint16_t* w2d;
 };
 
 struct FusedArgs {

@@ -63,6 +63,21 @@
 #ifndef E3GNN_BWDXW_WAVES
 #define E3GNN_BWDXW_WAVES 2
 #endif
+// MODE 3 register diet (experiment): W2 bf16 operands loaded at use instead of
+// a block ahead, dH2 operands loaded per hidden block just before its MFMAs --
+// fits 3 waves/SIMD (167 VGPRs) but measured slower (+1.2 ms/step at 3 waves,
+// +4 ms at 2): the exposed load latency costs more than the occupancy gains
+#ifndef E3GNN_BWDXW_LEAN
+#define E3GNN_BWDXW_LEAN 0
+#endif
+// MODE 3 dH2 = dw W2^T product: 0 (default) f32 MFMA per block; 1 bf16x6 over
+// PAIRS of consecutive visited blocks (K = 32 channels: 24 x 16 MFMA cycles per
+// pair instead of 2 x 16 x 32) -- measured slower (57.4 -> 59.5 ms/step): the
+// kernel is bound by tensor-product VALU issue, not by the MFMA pipe, and the
+// splits and just-in-time operand loads add to the VALU side
+#ifndef E3GNN_BWDXW_DH2BF
+#define E3GNN_BWDXW_DH2BF 0
+#endif
 
 namespace e3gnn {
 namespace {
@@ -109,7 +124,7 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // does not hoist hundreds of 64-bit addresses out of the centre loop (which it
 // did, and spilled).  Offsets outside the descriptor read 0 (padded rows).
 struct WRes {
-  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b, w2c, w2r;
+  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b, w2c, w2r, w2d;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int nfloats) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
@@ -117,7 +132,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int nfloa
 __device__ __forceinline__ WRes make_wres(const MlpW& W, int width) {
   return {rsrc(W.w0, 8 * 64), rsrc(W.w1, 64 * 64), rsrc(W.w2p, 64 * width), rsrc(W.w2q, 64 * width),
           rsrc(W.w1p, 64 * 64), rsrc((const float*)W.w2b, 64 * width * 3 / 2),
-          rsrc((const float*)W.w2c, 64 * width * 3 / 2), rsrc(W.w2r, 64 * width)};
+          rsrc((const float*)W.w2c, 64 * width * 3 / 2), rsrc(W.w2r, 64 * width),
+          rsrc((const float*)W.w2d, 64 * width * 3 / 2)};
 }
 __device__ __forceinline__ float ldw(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
   // the builtin returns the raw 32 bits (an unsigned int): reinterpret, never convert
@@ -648,6 +664,17 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
   }
 }
 
+// W2 pieces of the fused backward's dH2 product for block pair P, hidden block
+// bh (w2d order: [P][piece][bh][g][c][t] = piece of w2[16 bh + c][column of
+// element t of lane group g], MlpW::w2d)
+__device__ __forceinline__ void load_w2d(bf16x8 (&a)[3], __amdgpu_buffer_rsrc_t w2d, int lane, int P,
+                                         int bh) {
+#pragma unroll
+  for (int pc = 0; pc < 3; ++pc)
+    a[pc] = __builtin_bit_cast(
+        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2d, lane * 16, ((P * 3 + pc) * 4 + bh) * 1024, 0));
+}
+
 // B1: lane (g, c) = edge slot c of the tile x channels 4g..4g+3 of a 16-channel
 // block (transposed product w^T = W2^T H2^T: D[channel 4g+r][edge c]).  One
 // edge per lane keeps dE/dY in 8 registers; dE/dx[j] is summed over the 16
@@ -712,7 +739,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
   for (int q0 = qb; q0 < qe; q0 += 16) {
     phase();
     Op3 wq;
-    load_w2b(wq, R.w2b, lane, L::P[0].woff);
+    if (!(FW && E3GNN_BWDXW_LEAN)) load_w2b(wq, R.w2b, lane, L::P[0].woff);
     // edge of slot c
     const int er = (q0 + col < qe) ? (EDGE ? q0 + col : src_perm[q0 + col]) : -1;
     // EDGE: the slot's gathered row (padded slots: row 0, w = 0 there)
@@ -746,6 +773,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
     // MODE 3: dH2^T of the tile's edges (D[hidden 16 bh + 4g + r][edge c]),
     // accumulated over the visited blocks
     f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
+    constexpr bool DBF = FW && E3GNN_BWDXW_DH2BF;
+    int nb = 0;     // visited blocks of the tile (DBF: pairs (2P, 2P + 1))
+    float dwp[4];   // DBF: dE/dw of the pair's first block
     float dYa[9];  // dE/dY of edge c over this lane's channels (index 0 unused)
 #pragma unroll
     for (int q = 0; q < 9; ++q) dYa[q] = 0.f;
@@ -787,11 +817,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
               // MODE 3: W2 operands of this block's dH2 product, issued now and
               // consumed after the tensor product
               f32x4 bq[4];
-              if constexpr (FW) load_w2q(bq, R.w2r, lane, p.woff + 16 * jj);
+              if constexpr (FW && !DBF && !E3GNN_BWDXW_LEAN) load_w2q(bq, R.w2r, lane, p.woff + 16 * jj);
+              // DBF: the pair's W2 pieces of hidden block 0, issued at its second block
+              bf16x8 pa[3];
+              if constexpr (DBF) {
+                if (nb & 1) load_w2d(pa, R.w2d, lane, nb >> 1, 0);
+              }
               float dwr[4];
+              if constexpr (FW && E3GNN_BWDXW_LEAN) load_w2b(wq, R.w2b, lane, p.woff + 16 * jj);
               // w^T block: A = W2s[:, col0 + i]^T (w2p order), B = H2^T
               const f32x4 wv = w2_block<false>(hq, wq);
-              {
+              if constexpr (!(FW && E3GNN_BWDXW_LEAN)) {
                 const int nc = next_block_col<L, I, pi>(jj);
                 if (nc >= 0) load_w2b(wq, R.w2b, lane, nc);
               }
@@ -817,12 +853,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
               }
               pin<4 * D1>(dx);
               pin<8>(dYa + 1);
-              if constexpr (FW) {
+              if constexpr (DBF) {
+                if (nb & 1) {
+                  // dH2^T += W2[:, pair] dw^T, K = 32: element t of lane (g, c) is
+                  // channel 4g + t of the first block (t < 4) or 4g + t - 4 of the second
+                  bf16x8 d[3];
+#pragma unroll
+                  for (int t = 0; t < 8; ++t) {
+                    float v = t < 4 ? dwp[t] : dwr[t - 4];
+#pragma unroll
+                    for (int pc = 0; pc < 3; ++pc) {
+                      const __bf16 b = (__bf16)v;
+                      d[pc][t] = b;
+                      v -= (float)b;
+                    }
+                  }
+                  constexpr int PI_[6] = {2, 1, 0, 1, 0, 0}, PJ_[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+                  for (int bh = 0; bh < 4; ++bh) {
+                    bf16x8 pn[3];
+                    if (bh < 3) load_w2d(pn, R.w2d, lane, nb >> 1, bh + 1);
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) dh2[bh] = mfma16(pa[PI_[q]], d[PJ_[q]], dh2[bh]);
+                    if (bh < 3) {
+#pragma unroll
+                      for (int pc = 0; pc < 3; ++pc) pa[pc] = pn[pc];
+                    }
+                  }
+                } else {
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) dwp[r] = dwr[r];
+                }
+                ++nb;
+              } else if constexpr (FW) {
                 // dH2^T += W2[:, block] dw^T: k = lane group g, channel 4g + r
 #pragma unroll
-                for (int bh = 0; bh < 4; ++bh)
+                for (int bh = 0; bh < 4; ++bh) {
+                  if constexpr (E3GNN_BWDXW_LEAN)
+                    bq[bh] = ldw4(R.w2r, ((lane >> 4) * 16 + (lane & 15)) * 16,
+                                  ((p.woff + 16 * jj) / 16 * 4 + bh) * 1024);
 #pragma unroll
                   for (int r = 0; r < 4; ++r) dh2[bh] = mfma(bq[bh][r], dwr[r], dh2[bh]);
+                }
               }
             }
           });
