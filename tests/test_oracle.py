@@ -61,3 +61,56 @@ def test_oracle_forces_are_energy_gradient():
         e1 = oracle_eval(p1, cell, types)['energy']
         e2 = oracle_eval(p2, cell, types)['energy']
         assert abs(-(e1 - e2) / (2 * h) - res['forces'][atom, comp]) < 1e-6
+
+
+# ------------------------------------------------ the nequip-family restatement
+def _nequip(model):
+    import os
+    from oracle.nequip_ref import NequIPRef
+    root = os.path.join(os.path.dirname(GOLD), '..', 'sevennet_finetuning_amd', 'assets', model)
+    return NequIPRef(root)
+
+
+def test_nequip_oracle_matches_hfo2_example_kat():
+    """The generic restatement on the HfO2 example deployment (sevenn 0.8.6:
+    odd parity, nequip self-connection, polynomial cutoff, raw-vector SH)
+    against the reference's own frozen-model energy and force on res.dat."""
+    import json
+    from oracle.neighbor import neighbor_list
+    kat = json.load(open(f'{GOLD}/kat_reference.json'))['kats_hfo2_example']
+    ref = _nequip(kat['model'])
+    d = np.load(f'{GOLD}/hfo2_resdat.npz')
+    types = np.array([ref.symbols.index(str(s)) for s in d['symbols']])
+    ei, sh = neighbor_list(d['pos'], d['cell'], ref.cutoff)
+    assert ei.shape[1] == kat['n_edges']
+    out = ref(torch.tensor(d['pos']), torch.tensor(types), torch.tensor(ei),
+              torch.tensor(sh), torch.tensor(d['cell']))
+    # the reference value is fp32 (ulp at 2.8e3 eV: 2.4e-4): 1e-6 relative
+    assert abs(float(out['energy']) - kat['energy']) <= 1e-6 * abs(kat['energy'])
+    assert np.abs(out['forces'][0].numpy() - np.array(kat['force0'])).max() < 2e-5
+    assert float(out['forces'].sum(0).abs().max()) < 1e-9
+
+
+def test_nequip_oracle_reproduces_sevennet0_oracle():
+    """SevenNet-0 is an instance of the generic restatement: both oracles agree
+    to fp64 round-off (and hence both sit on the SevenNet-0 KATs)."""
+    from oracle.neighbor import neighbor_list
+    from oracle.sevennet_ref import SevenNet0Ref
+    pos, cell, types = system('mixed_1x1x1', SYMS)
+    ei, sh = neighbor_list(pos, cell, 5.0)
+    args = (torch.tensor(pos), torch.tensor(types), torch.tensor(ei), torch.tensor(sh),
+            torch.tensor(cell))
+    a = _nequip('sevennet0')(*args)
+    b = SevenNet0Ref(dtype=torch.float64)(*args)
+    assert abs(float(a['energy'] - b['energy'])) < 1e-9 * abs(float(b['energy']))
+    assert float((a['forces'] - b['forces']).abs().max()) < 1e-10
+    assert float((a['stress'] - b['stress']).abs().max()) < 1e-12
+
+
+def test_oracle_cg_matches_hfo2_frozen_w3j():
+    """The HfO2 deployment froze wigner_3j(1,1,1) itself (a parity-odd path of
+    the 1o x 1o product): the oracle's coupling / sqrt(3) equals it."""
+    import math
+    from oracle.cg import tp_cg
+    w = np.load(f'{GOLD}/hfo2_frozen_w3j111.npz')['w3j_111']
+    assert np.abs(tp_cg(1, 1, 1) / math.sqrt(3.0) - w).max() < 1e-7

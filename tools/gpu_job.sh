@@ -44,8 +44,8 @@ for s in "$@"; do
     nativetests) step nativetests 300 python -m pytest tests/test_gpu_native.py -x -q -s --timeout 200 --timeout-method thread ;;
     md) step md 300 native/e3gnn_md sevennet_finetuning_amd/assets/sevennet0/weights.bin sevennet_finetuning_amd/assets/sevennet0/manifest.json 23 5 1.0 ;;
     prof10k) step prof10k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof10k -o run --output-format csv -- python bench.py --cells 11 --steps 3 --warmup 1 --profile-only ;;
-    pmcf) step pmcf 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 1 --warmup 1 --profile-only ;;
-    pmcw) step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 1 --warmup 1 --profile-only ;;
+    pmcf) step pmcf 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
+    pmcw) step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     slp) step slp_build 600 env E3GNN_FUSED_FLAGS=" " python -c "import sevennet_finetuning_amd.build_lib as b; b.build(force=True)" && step benchslp 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     ptest) step ptest 600 python -m pytest tests/test_parallel.py -q ;;
     bench2) step bench2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --cells 11 --same-device --no-cpu-baseline ;;
