@@ -179,6 +179,27 @@ int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_
                         const float* h, const float* Y, const float* w, const float* gagg,
                         float* dh, float* dY, float* dw, float* dxc, void* stream);
 
+/* ---- generic path tables: the convolution of any nequip-family model ----
+ * Same contract as e3gnn_conv_forward / _backward (IrrepsConvolution,
+ * sevenn/nn/convolution.py:36-123), with the instruction list given at run
+ * time instead of the SevenNet-0 kinds: paths[8 * n_paths] = per instruction
+ * (l1, l2, l3, mul, x offset, Y offset, w column offset, agg offset), l <= 2,
+ * uvu coupling wigner_3j * sqrt(2 l3 + 1); h [n x dx], Y [E x dy], w [E x dw],
+ * agg [n x dm].  Serves e.g. the reference's HfO2 example deployment
+ * (odd parity, lmax 1; example_inputs/md_serial_example).  The handle lives on
+ * the device current at creation. */
+typedef struct e3gnn_gtp e3gnn_gtp;
+e3gnn_gtp* e3gnn_gtp_create(int n_paths, const int32_t* paths, int dx, int dy, int dw, int dm);
+void e3gnn_gtp_free(e3gnn_gtp* g);
+int e3gnn_gtp_dims(const e3gnn_gtp* g, int* dx, int* dy, int* dw, int* dm);
+int e3gnn_gtp_forward(const e3gnn_gtp* g, int64_t n_nodes, const int32_t* row_ptr,
+                      const int32_t* edge_nbr, const float* h, const float* Y, const float* w,
+                      float* agg, void* stream);
+int e3gnn_gtp_backward(const e3gnn_gtp* g, int64_t n_nodes, int64_t n_edges, const int32_t* row_ptr,
+                       const int32_t* edge_nbr, const int32_t* src_ptr, const int32_t* src_perm,
+                       const float* h, const float* Y, const float* w, const float* gagg,
+                       float* dh, float* dY, float* dw, float* dxc, void* stream);
+
 /* Scaled SiLU of the trainable model (y = scale * silu(x); e3nn normalize2mom,
  * SevenNet's act_radial / act_scalar / act_gate, silu_norm 1.6792), element-
  * wise over n floats: op 0 out0 = y(x); op 1 out0 = g * y'(x); op 2 (the

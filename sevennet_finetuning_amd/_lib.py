@@ -47,6 +47,12 @@ SIGNATURES = {
     'e3gnn_conv_forward': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_conv_backward': (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      _vp, _vp, _vp, _vp, _vp, _vp]),
+    'e3gnn_gtp_create': (_vp, [_c_int, _vp, _c_int, _c_int, _c_int, _c_int]),
+    'e3gnn_gtp_free': (None, [_vp]),
+    'e3gnn_gtp_dims': (_c_int, [_vp, _P(_c_int), _P(_c_int), _P(_c_int), _P(_c_int)]),
+    'e3gnn_gtp_forward': (_c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'e3gnn_gtp_backward': (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _vp, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_act': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_f, _vp]),
     'e3gnn_gate': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_f, _vp]),
     'e3gnn_d3_create': (_vp, [_c_int, _c_int, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp, _vp, _vp]),

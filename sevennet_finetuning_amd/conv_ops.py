@@ -134,6 +134,83 @@ class HipConvBackend:
         return dh, dY, dw
 
 
+class GenericHipConvBackend(HipConvBackend):
+    """Runtime path tables (gtp.hip, e3gnn_gtp_*): the convolution of any
+    nequip-family block (irreps with parity, lmax <= 2), one table per block;
+    ``kind`` is the block index.  Same build / forward / backward contract as
+    the SevenNet-0 kernels, so the double-backward op above serves it too."""
+    generic = True
+
+    def __init__(self, tables=None):
+        self.lib = _lib.load()
+        self.dims, self.ydims, self.handles = {}, {}, []
+        if tables is not None:
+            self.configure(tables)
+
+    def configure(self, tables):
+        """tables: per block (paths int32 [P, 8], dx, dy, dw, dm) (nn.path_table)."""
+        import numpy as np
+        self._free()
+        for k, (paths, dx, dy, dw, dm) in enumerate(tables):
+            arr = np.ascontiguousarray(paths, dtype=np.int32)
+            h = self.lib.e3gnn_gtp_create(len(arr), arr.ctypes.data, dx, dy, dw, dm)
+            if not h:
+                raise _lib.E3GNNError(f'gtp block {k}: {self.lib.e3gnn_last_error().decode()}')
+            self.handles.append(h)
+            self.dims[k] = (dx, dw, dm)
+            self.ydims[k] = dy
+
+    def _free(self):
+        for h in getattr(self, 'handles', []):
+            self.lib.e3gnn_gtp_free(h)
+        self.handles = []
+
+    def __del__(self):
+        try:
+            self._free()
+        except Exception:
+            pass
+
+    def _check(self, kind, g, h, Y, w):
+        dx, dw, _ = self.dims[kind]
+        for name, t, shape in (('h', h, (g.n_nodes, dx)), ('Y', Y, (g.n_edges, self.ydims[kind])),
+                               ('w', w, (g.n_edges, dw))):
+            if tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_cuda:
+                raise _lib.E3GNNError(f'gtp block {kind}: {name} must be float32 {shape} on the '
+                                      f'GPU, got {t.dtype} {tuple(t.shape)} on {t.device}')
+
+    def forward(self, kind, g, h, Y, w):
+        self._check(kind, g, h, Y, w)
+        h, Y, w = h.contiguous(), Y.contiguous(), w.contiguous()
+        agg = torch.empty(g.n_nodes, self.dims[kind][2], device=h.device)
+        a = g.aux
+        _lib.check(self.lib.e3gnn_gtp_forward(
+            self.handles[kind], g.n_nodes, a['row_ptr'].data_ptr(), a['nbr'].data_ptr(),
+            h.data_ptr(), Y.data_ptr(), w.data_ptr(), agg.data_ptr(), self._stream(h)))
+        return agg
+
+    def backward(self, kind, g, h, Y, w, gagg, need_h=True):
+        self._check(kind, g, h, Y, w)
+        dx, dwd, dm = self.dims[kind]
+        h, Y, w = h.contiguous(), Y.contiguous(), w.contiguous()
+        gagg = gagg.to(torch.float32).contiguous()
+        if tuple(gagg.shape) != (g.n_nodes, dm):
+            raise _lib.E3GNNError(f'gtp block {kind}: gagg must be {(g.n_nodes, dm)}')
+        dev, E = h.device, g.n_edges
+        dY = torch.empty(E, self.ydims[kind], device=dev)
+        dw = torch.empty(E, dwd, device=dev)
+        dh = torch.empty(g.n_nodes, dx, device=dev) if need_h else None
+        dxc = torch.empty(E, dx, device=dev) if need_h and E else None
+        a = g.aux
+        _lib.check(self.lib.e3gnn_gtp_backward(
+            self.handles[kind], g.n_nodes, E, a['row_ptr'].data_ptr(), a['nbr'].data_ptr(),
+            a['src_ptr'].data_ptr(), a['src_perm'].data_ptr(), h.data_ptr(), Y.data_ptr(),
+            w.data_ptr(), gagg.data_ptr(), dh.data_ptr() if dh is not None else None,
+            dY.data_ptr(), dw.data_ptr(), dxc.data_ptr() if dxc is not None else None,
+            self._stream(h)))
+        return dh, dY, dw
+
+
 def _add(acc, t):
     if t is None:
         return acc

@@ -29,6 +29,7 @@
 #include "train_ops.h"
 #include "common.h"
 #include "fused.h"
+#include "gtp.h"
 #include "minijson.h"
 #include "node.h"
 #include "neighbor.h"
@@ -1398,6 +1399,126 @@ int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_
   a.denom = 1.0f;
   HIPCHK(launch_tp_bwd(kind, a, s));
   if (dh) HIPCHK(launch_gather_rows((int)n_nodes, dx, src_ptr, src_perm, dxc, dh, s));
+  return E3GNN_OK;
+}
+
+// ------------------------------------------------------------ generic path tables
+// (gtp.hip): the convolution of any nequip-family model from its instruction list
+namespace {
+void cg_entries(int l1, int l2, int l3, std::vector<CGEntry>& out) {
+  auto add = [&](const CGEntry* e, int n) { out.assign(e, e + n); };
+#define E3GNN_CG_CASE(a, b, c) \
+  if (l1 == a && l2 == b && l3 == c) return add(CG<a, b, c>::e, CG<a, b, c>::n);
+  E3GNN_CG_CASE(0, 0, 0) E3GNN_CG_CASE(0, 1, 1) E3GNN_CG_CASE(0, 2, 2)
+  E3GNN_CG_CASE(1, 0, 1) E3GNN_CG_CASE(1, 1, 0) E3GNN_CG_CASE(1, 1, 1) E3GNN_CG_CASE(1, 1, 2)
+  E3GNN_CG_CASE(1, 2, 1) E3GNN_CG_CASE(1, 2, 2) E3GNN_CG_CASE(2, 0, 2) E3GNN_CG_CASE(2, 1, 1)
+  E3GNN_CG_CASE(2, 1, 2) E3GNN_CG_CASE(2, 2, 0) E3GNN_CG_CASE(2, 2, 1) E3GNN_CG_CASE(2, 2, 2)
+#undef E3GNN_CG_CASE
+  out.clear();
+}
+}  // namespace
+
+struct e3gnn_gtp {
+  int device = 0;
+  GtpTables T{};
+  DBuf by[4], ptr[4];
+};
+
+e3gnn_gtp* e3gnn_gtp_create(int n_paths, const int32_t* paths, int dx, int dy, int dw, int dm) {
+  if (n_paths <= 0 || !paths || dx <= 0 || dy <= 0 || dw <= 0 || dm <= 0) {
+    fail(E3GNN_ERR_ARG, "gtp: empty path table or dimensions");
+    return nullptr;
+  }
+  std::vector<GtpTerm> terms;
+  std::vector<CGEntry> cg;
+  for (int p = 0; p < n_paths; ++p) {
+    const int32_t* q = paths + 8 * p;
+    const int l1 = q[0], l2 = q[1], l3 = q[2], mul = q[3], xo = q[4], yo = q[5], wo = q[6], mo = q[7];
+    if (l1 < 0 || l2 < 0 || l3 < 0 || l1 > 2 || l2 > 2 || l3 > 2 || l3 < std::abs(l1 - l2) ||
+        l3 > l1 + l2 || mul <= 0 || xo < 0 || yo < 0 || wo < 0 || mo < 0 ||
+        xo + mul * (2 * l1 + 1) > dx || yo + 2 * l2 + 1 > dy || wo + mul > dw ||
+        mo + mul * (2 * l3 + 1) > dm) {
+      fail(E3GNN_ERR_ARG, "gtp: path " + std::to_string(p) + " out of range (l <= 2, offsets within dims)");
+      return nullptr;
+    }
+    cg_entries(l1, l2, l3, cg);
+    for (int u = 0; u < mul; ++u)
+      for (auto& e : cg)
+        terms.push_back({xo + u * (2 * l1 + 1) + e.i, yo + e.j, wo + u, mo + u * (2 * l3 + 1) + e.k, e.c});
+  }
+  auto* g = new e3gnn_gtp;
+  if (hipGetDevice(&g->device) != hipSuccess) {
+    delete g;
+    fail(E3GNN_ERR_HIP, "gtp: no device");
+    return nullptr;
+  }
+  const int dims[4] = {dm, dw, dx, dy};
+  const GtpTerm* dev_by[4];
+  const int* dev_ptr[4];
+  for (int o = 0; o < 4; ++o) {
+    // stable order by the output each term feeds (fixed summation order)
+    auto key = [o](const GtpTerm& t) { return o == 0 ? t.m : (o == 1 ? t.w : (o == 2 ? t.x : t.y)); };
+    std::vector<GtpTerm> s = terms;
+    std::stable_sort(s.begin(), s.end(), [&](const GtpTerm& a, const GtpTerm& b) { return key(a) < key(b); });
+    std::vector<int> ptr(dims[o] + 1, 0);
+    for (auto& t : s) ptr[key(t) + 1]++;
+    for (int i = 0; i < dims[o]; ++i) ptr[i + 1] += ptr[i];
+    if (g->by[o].ensure(s.size() * sizeof(GtpTerm)) != hipSuccess ||
+        g->ptr[o].ensure(ptr.size() * 4) != hipSuccess ||
+        hipMemcpy(g->by[o].p, s.data(), s.size() * sizeof(GtpTerm), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(g->ptr[o].p, ptr.data(), ptr.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+      delete g;
+      fail(E3GNN_ERR_HIP, "gtp: table upload failed");
+      return nullptr;
+    }
+    dev_by[o] = static_cast<const GtpTerm*>(g->by[o].p);
+    dev_ptr[o] = static_cast<const int*>(g->ptr[o].p);
+  }
+  g->T = GtpTables{dx, dy, dw, dm, dev_by[0], dev_ptr[0], dev_by[1], dev_ptr[1],
+                   dev_by[2], dev_ptr[2], dev_by[3], dev_ptr[3]};
+  (void)hipGetLastError();
+  return g;
+}
+
+void e3gnn_gtp_free(e3gnn_gtp* g) { delete g; }
+
+int e3gnn_gtp_dims(const e3gnn_gtp* g, int* dx, int* dy, int* dw, int* dm) {
+  if (!g) return fail(E3GNN_ERR_ARG, "null gtp");
+  if (dx) *dx = g->T.dx;
+  if (dy) *dy = g->T.dy;
+  if (dw) *dw = g->T.dw;
+  if (dm) *dm = g->T.dm;
+  return E3GNN_OK;
+}
+
+int e3gnn_gtp_forward(const e3gnn_gtp* g, int64_t n_nodes, const int32_t* row_ptr,
+                      const int32_t* edge_nbr, const float* h, const float* Y, const float* w,
+                      float* agg, void* stream) {
+  if (!g) return fail(E3GNN_ERR_ARG, "null gtp");
+  if (n_nodes <= 0) return E3GNN_OK;
+  if (n_nodes >= (int64_t)1 << 31) return fail(E3GNN_ERR_ARG, "gtp: too many nodes");
+  if (!row_ptr || !h || !Y || !w || !agg) return fail(E3GNN_ERR_ARG, "null gtp operand");
+  HIPCHK(launch_gtp_fwd((int)n_nodes, row_ptr, edge_nbr, h, Y, w, g->T, agg, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_gtp_backward(const e3gnn_gtp* g, int64_t n_nodes, int64_t n_edges, const int32_t* row_ptr,
+                       const int32_t* edge_nbr, const int32_t* src_ptr, const int32_t* src_perm,
+                       const float* h, const float* Y, const float* w, const float* gagg,
+                       float* dh, float* dY, float* dw, float* dxc, void* stream) {
+  if (!g) return fail(E3GNN_ERR_ARG, "null gtp");
+  hipStream_t s = (hipStream_t)stream;
+  if (dh && n_nodes > 0) HIPCHK(hipMemsetAsync(dh, 0, n_nodes * g->T.dx * 4, s));
+  if (n_edges <= 0 || n_nodes <= 0) return E3GNN_OK;
+  if (n_nodes >= (int64_t)1 << 31 || n_edges >= (int64_t)1 << 31)
+    return fail(E3GNN_ERR_ARG, "gtp: graph size out of int32 range");
+  if (!row_ptr || !edge_nbr || !h || !Y || !w || !gagg || !dY || !dw)
+    return fail(E3GNN_ERR_ARG, "null gtp operand");
+  if (dh && (!dxc || !src_ptr || !src_perm))
+    return fail(E3GNN_ERR_ARG, "dh needs dxc scratch and the transposed CSR");
+  HIPCHK(launch_gtp_bwd((int)n_nodes, row_ptr, edge_nbr, h, Y, w, gagg, g->T, dw, dh ? dxc : nullptr,
+                        dY, s));
+  if (dh) HIPCHK(launch_gather_rows((int)n_nodes, g->T.dx, src_ptr, src_perm, dxc, dh, s));
   return E3GNN_OK;
 }
 

@@ -217,3 +217,94 @@ class E3GNNModel:
                 vol = torch.abs(torch.linalg.det(cell)).to(torch.float32)
                 out[KEY.PRED_STRESS] = res['virial'] / vol
         return out
+
+
+class GenericE3GNNModel:
+    """Any other member of the nequip family (e.g. the reference's HfO2 example
+    deployment: odd parity, lmax 1, FCTP self-connection, polynomial cutoff):
+    the trainable model of nn.py in eval mode on the runtime-path-table HIP
+    convolution (gtp.hip, e3gnn_gtp_*), with the E3GNNModel call surface
+    (``energy_forces`` on device tensors, the ``AtomGraphSequential`` dict
+    contract, ``type_map``, ``cutoff``).  Forces and virial are the edge-vector
+    gradient scattered as ForceStressOutputFromEdge does (force_output.py:158-215);
+    the SevenNet-0 architecture keeps the fully native E3GNNModel."""
+
+    def __init__(self, model_dir, device=None):
+        from .nn import SevenNetTrainable
+        if device is None:
+            device = torch.device('cuda', torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != 'cuda':
+            raise _lib.E3GNNError(f'the HIP path needs a GPU device, got {self.device}')
+        self.model_dir = model_dir
+        self.net = SevenNetTrainable(model_dir=model_dir, device=self.device)
+        self.net.eval()
+        for p in self.net.parameters():
+            p.requires_grad_(False)
+        self.manifest = self.net.manifest
+        self.chemical_symbols = self.net.chemical_symbols
+        self.cutoff = self.net.cutoff
+        self.num_species, self.num_layers = self.net.nsp, self.net.nlayer
+        self.is_batch_data = False
+
+    type_map = E3GNNModel.type_map
+
+    def set_is_batch_data(self, flag: bool):
+        self.is_batch_data = bool(flag)
+
+    def energy_forces(self, types, edge_center, edge_nbr, edge_vec, want_edge_grad=False):
+        dev = self.device
+        n = int(types.shape[0])
+        ei = torch.stack([edge_center.to(dev).long(), edge_nbr.to(dev).long()])
+        data = {KEY.NODE_FEATURE: types.to(dev).long(), KEY.EDGE_IDX: ei,
+                KEY.EDGE_VEC: edge_vec.to(dev, torch.float32),
+                KEY.NUM_ATOMS: torch.tensor([n], device=dev),
+                KEY.CELL_VOLUME: torch.ones(1, device=dev)}
+        out = self.net(data)
+        # with a unit volume the model's stress is the virial (xx,yy,zz,xy,yz,zx)
+        res = {'energy': out[KEY.PRED_TOTAL_ENERGY].detach()[0],
+               'atomic_energy': out[KEY.ATOMIC_ENERGY].detach().view(n),
+               'forces': out[KEY.PRED_FORCE].detach(),
+               'virial': out[KEY.PRED_STRESS].detach().view(6)}
+        if want_edge_grad:
+            raise _lib.E3GNNError('edge gradients are exposed by the SevenNet-0 engine only')
+        return res
+
+    def __call__(self, data):
+        return self.forward(data)
+
+    def forward(self, data):
+        """AtomGraphSequential contract (sequential.py:82-89) on a dict."""
+        dev = self.device
+        d = dict(data)
+        d[KEY.NODE_FEATURE] = torch.as_tensor(data[KEY.NODE_FEATURE]).to(dev).long()
+        ei = torch.as_tensor(data[KEY.EDGE_IDX]).to(dev).long()
+        d[KEY.EDGE_IDX] = ei
+        if KEY.EDGE_VEC not in data or data[KEY.EDGE_VEC] is None:
+            pos = torch.as_tensor(data[KEY.POS]).to(dev, torch.float32)
+            vec = pos[ei[1]] - pos[ei[0]]
+            if KEY.CELL_SHIFT in data and data[KEY.CELL_SHIFT] is not None:
+                shift = torch.as_tensor(data[KEY.CELL_SHIFT]).to(dev, torch.float32)
+                cell = torch.as_tensor(data[KEY.CELL]).to(dev, torch.float32).view(3, 3)
+                vec = vec + shift @ cell
+            d[KEY.EDGE_VEC] = vec
+        if KEY.CELL_VOLUME not in d and KEY.CELL in data and data[KEY.CELL] is not None:
+            cell = torch.as_tensor(data[KEY.CELL]).to(dev, torch.float64).view(3, 3)
+            d[KEY.CELL_VOLUME] = torch.abs(torch.linalg.det(cell)).to(torch.float32).view(1)
+        out = self.net(d)
+        if not self.is_batch_data:
+            out[KEY.PRED_TOTAL_ENERGY] = out[KEY.PRED_TOTAL_ENERGY][0]
+            if KEY.PRED_STRESS in out:
+                out[KEY.PRED_STRESS] = out[KEY.PRED_STRESS][0]
+        return out
+
+
+def load_model(model_dir=os.path.join(ASSETS, 'sevennet0'), device=None):
+    """The engine for a deployment: the native SevenNet-0 engine (E3GNNModel)
+    for that architecture, GenericE3GNNModel for the rest of the family."""
+    with open(os.path.join(model_dir, 'manifest.json')) as f:
+        man = json.load(f)
+    if man.get('family', 'sevennet0') == 'sevennet0' and \
+            man.get('self_connection_type', 'linear') == 'linear' and not man.get('is_parity'):
+        return E3GNNModel(model_dir, device)
+    return GenericE3GNNModel(model_dir, device)

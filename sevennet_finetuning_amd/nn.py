@@ -42,17 +42,21 @@ ASSETS = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'assets')
 
 
 def parse_irreps(s):
+    """'4x0o+4x1e' -> [(4, 0, -1), (4, 1, 1)] (mul, l, parity)"""
     out = []
     for term in s.split('+'):
         mul, ir = term.strip().split('x')
-        if ir[-1] != 'e':
-            raise ValueError(f'{s}: the SevenNet-0 path is even parity only')
-        out.append((int(mul), int(ir[:-1])))
+        out.append((int(mul), int(ir[:-1]), 1 if ir[-1] == 'e' else -1))
     return out
 
 
 def _offsets(irreps):
-    return np.cumsum([0] + [m * (2 * l + 1) for m, l in irreps]).tolist()
+    return np.cumsum([0] + [t[0] * (2 * t[1] + 1) for t in irreps]).tolist()
+
+
+def _ir(t):
+    """(l, p) of an irreps entry (mul, l[, p]); parity defaults to even"""
+    return (t[1], t[2] if len(t) > 2 else 1)
 
 
 class _Linear:
@@ -69,8 +73,8 @@ class _Linear:
 
     def __init__(self, irreps_in, irreps_out):
         self.irreps_in, self.irreps_out = irreps_in, irreps_out
-        self.ins = [(i, j) for i, (_, li) in enumerate(irreps_in)
-                    for j, (_, lo) in enumerate(irreps_out) if li == lo]
+        self.ins = [(i, j) for i, a in enumerate(irreps_in)
+                    for j, b in enumerate(irreps_out) if _ir(a) == _ir(b)]
         fan = {j: sum(irreps_in[i][0] for i, jj in self.ins if jj == j) for _, j in self.ins}
         self.alpha = {j: 1.0 / math.sqrt(f) for j, f in fan.items()}
         self.in_off, self.out_off = _offsets(irreps_in), _offsets(irreps_out)
@@ -85,15 +89,15 @@ class _Linear:
             else:
                 runs.append([(i, k)])
         # x split points: every input irrep boundary
-        self.x_sizes = [m * (2 * l + 1) for m, l in irreps_in]
+        self.x_sizes = [t[0] * (2 * t[1] + 1) for t in irreps_in]
 
     def __call__(self, x, w_flat):
         n = x.shape[0]
         xs = x.split(self.x_sizes, dim=1) if len(self.x_sizes) > 1 else (x,)
         ws = w_flat.split(self.w_sizes) if len(self.w_sizes) > 1 else (w_flat,)
         parts = []
-        for j, (mo, l) in enumerate(self.irreps_out):
-            d = 2 * l + 1
+        for j, to in enumerate(self.irreps_out):
+            mo, d = to[0], 2 * to[1] + 1
             acc = None
             for run in self.groups.get(j, []):
                 mul = sum(self.irreps_in[i][0] for i, _ in run)
@@ -120,8 +124,8 @@ class _Linear:
     def _scale(self, out):
         if not hasattr(self, '_alpha_cols'):
             cols = []
-            for j, (mo, l) in enumerate(self.irreps_out):
-                cols += [self.alpha.get(j, 0.0)] * (mo * (2 * l + 1))
+            for j, to in enumerate(self.irreps_out):
+                cols += [self.alpha.get(j, 0.0)] * (to[0] * (2 * to[1] + 1))
             self._alpha64 = torch.tensor(cols, dtype=torch.float64)
             self._alpha_cols = self._alpha64
         if self._alpha_cols.device != out.device or self._alpha_cols.dtype != out.dtype:
@@ -130,37 +134,77 @@ class _Linear:
 
 
 def _gate_irreps(irreps_out):
-    """e3nn Gate.irreps_in for EquivariantGate (equivariant_gate.py:48-55)."""
-    scal = [(m, l) for m, l in irreps_out if l == 0]
-    gated = [(m, l) for m, l in irreps_out if l > 0]
-    full = scal + [(m, 0) for m, _ in gated] + gated
+    """e3nn Gate.irreps_in for EquivariantGate (equivariant_gate.py:48-55):
+    [scalars (the l = 0 output irreps, in order) | one 0e gate per gated
+    channel | gated irreps], equal neighbours merged (the scalars and gates
+    sort ahead of every l > 0 irrep, odd before even)."""
+    scal = [t for t in irreps_out if t[1] == 0]
+    gated = [t for t in irreps_out if t[1] > 0]
+    ng = sum(t[0] for t in gated)
+    full = scal + ([(ng, 0, 1)] if ng else []) + gated
     simp = []
-    for m, l in sorted(full, key=lambda t: t[1]):
-        if simp and simp[-1][1] == l:
-            simp[-1] = (simp[-1][0] + m, l)
+    for t in full:
+        m, (l, p) = t[0], _ir(t)
+        if simp and _ir(simp[-1]) == (l, p):
+            simp[-1] = (simp[-1][0] + m, l, p)
         else:
-            simp.append((m, l))
+            simp.append((m, l, p))
     return simp, scal, gated
 
 
-def _conv_mid(irreps_x, lmax_out):
-    """Sorted mid irreps of IrrepsConvolution (convolution.py:72-95)."""
-    ins = [(mul, l3) for mul, l1 in irreps_x for l2 in range(3)
-           for l3 in range(abs(l1 - l2), l1 + l2 + 1) if l3 <= lmax_out]
-    return [ins[k] for k in sorted(range(len(ins)), key=lambda k: (ins[k][1], k))]
+def conv_instructions(irreps_x, lmax_filter, filter_parity, irreps_out):
+    """IrrepsConvolution instructions (convolution.py:72-95): every (x irrep,
+    filter irrep l2 of parity filter_parity^l2, output) whose output irrep is
+    in the block's output irreps, as (i_x, l2, l3, p3, mul) in weight order;
+    the mid irreps are the outputs stable-sorted by (l, p) (odd first), perm[k]
+    the slot of instruction k."""
+    allowed = {_ir(t) for t in irreps_out}
+    ins = []
+    for i, t in enumerate(irreps_x):
+        mul, (l1, p1) = t[0], _ir(t)
+        for l2 in range(lmax_filter + 1):
+            p3 = p1 * filter_parity ** l2
+            for l3 in range(abs(l1 - l2), l1 + l2 + 1):
+                if (l3, p3) in allowed:
+                    ins.append((i, l2, l3, p3, mul))
+    order = sorted(range(len(ins)), key=lambda k: (ins[k][2], ins[k][3], k))
+    perm = [0] * len(ins)
+    for slot, k in enumerate(order):
+        perm[k] = slot
+    mid = [(ins[k][4], ins[k][2], ins[k][3]) for k in order]
+    return ins, mid, perm
 
 
-def spherical_harmonics(vec):
-    """e3nn SphericalHarmonics(0e+1e+2e, normalize=True, 'component')
-    (edge_embedding.py:177-198)."""
-    r = torch.linalg.norm(vec, dim=-1, keepdim=True)
-    u = vec / r
+def path_table(irreps_x, lmax_filter, filter_parity, irreps_out):
+    """Runtime path table of e3gnn_gtp_create: per instruction (l1, l2, l3,
+    mul, x offset, Y offset, w offset, agg offset), plus (dx, dy, dw, dm)."""
+    ins, mid, perm = conv_instructions(irreps_x, lmax_filter, filter_parity, irreps_out)
+    xo, mo = _offsets(irreps_x), _offsets(mid)
+    rows, woff = [], 0
+    for k, (i, l2, l3, _, mul) in enumerate(ins):
+        rows.append((irreps_x[i][1], l2, l3, mul, xo[i], l2 * l2, woff, mo[perm[k]]))
+        woff += mul
+    return (np.asarray(rows, dtype=np.int32).reshape(-1, 8), xo[-1], (lmax_filter + 1) ** 2,
+            woff, mo[-1]), mid
+
+
+def spherical_harmonics(vec, lmax=2, normalize=True):
+    """e3nn SphericalHarmonics(0e+1p+2e, 'component') (edge_embedding.py:177-198);
+    ``normalize`` False (sevenn < 0.9 checkpoints, util.py:143-144) evaluates
+    the same homogeneous polynomials on the raw edge vector."""
+    if normalize:
+        u = vec / torch.linalg.norm(vec, dim=-1, keepdim=True)
+    else:
+        u = vec
     x, y, z = u[:, 0], u[:, 1], u[:, 2]
     s3, s5, s15 = math.sqrt(3.0), math.sqrt(5.0), math.sqrt(15.0)
-    return torch.stack([
-        torch.ones_like(x), s3 * x, s3 * y, s3 * z,
-        s15 * x * z, s15 * x * y, s5 * (y * y - 0.5 * (x * x + z * z)), s15 * y * z,
-        0.5 * s15 * (z * z - x * x)], dim=-1)
+    parts = [torch.ones_like(x)]
+    if lmax >= 1:
+        parts += [s3 * x, s3 * y, s3 * z]
+    if lmax >= 2:
+        parts += [s15 * x * z, s15 * x * y, s5 * (y * y - 0.5 * (x * x + z * z)), s15 * y * z,
+                  0.5 * s15 * (z * z - x * x)]
+    return torch.stack(parts, dim=-1)
 
 
 class SevenNetTrainable(torch.nn.Module):
@@ -188,12 +232,20 @@ class SevenNetTrainable(torch.nn.Module):
         self.chemical_symbols = list(man['chemical_symbols'])
         self.nsp = int(man['num_species'])
         self.cutoff = float(man['cutoff'])
-        self.r_on = float(man['cutoff_function']['cutoff_on'])
+        self.cut = dict(man['cutoff_function'])
+        self.r_on = float(self.cut.get('cutoff_on', self.cutoff))
         self.silu_norm = float(man['silu_norm'])
+        self.tanh_norm = float(man.get('act_norm', {}).get('tanh', 1.0))
         self.irreps = [parse_irreps(s) for s in man['irreps_manual']]
         self.nlayer = int(man['num_convolution_layer'])
-        self.conv_backend = conv_backend if conv_backend is not None \
-            else conv_ops.HipConvBackend()
+        # the nequip family's other knobs (sevenn 0.8.6 HfO2 example:
+        # odd parity, raw-vector SH, FCTP self-connection, tanh odd scalars)
+        self.lmax_edge = int(man.get('lmax_edge', man.get('lmax', 2)))
+        self.filter_parity = -1 if man.get('is_parity', False) else 1
+        self.sh_normalize = bool(man.get('sh_normalize', True))
+        self.sc_type = man.get('self_connection_type', 'linear')
+        self.readout_hidden = int(man.get('readout_hidden', self.irreps[-1][0][0] // 2))
+        self.conv_backend = conv_backend
         flat_host = np.fromfile(os.path.join(model_dir, 'weights.bin'), dtype='<f4') \
             if weights is None else np.ascontiguousarray(weights, dtype='<f4').reshape(-1)
         total = sum(t['numel'] for t in man['tensors'])
@@ -258,27 +310,57 @@ class SevenNetTrainable(torch.nn.Module):
         self.is_batch_data = bool(flag)
 
     # ------------------------------------------------------------ structure
+    def _sevennet0_kinds(self):
+        """The SevenNet-0 kernel kinds (csrc/tp.h) of the blocks, or None when
+        the architecture is another member of the family."""
+        if self.filter_parity != 1 or self.lmax_edge != 2 or not self.sh_normalize or \
+                self.sc_type != 'linear':
+            return None
+        kinds = [0 if t == 0 else (2 if t == self.nlayer - 1 else 1) for t in range(self.nlayer)]
+        want = {0: ([(128, 0, 1)], [(128, 0, 1), (64, 1, 1), (32, 2, 1)]),
+                1: ([(128, 0, 1), (64, 1, 1), (32, 2, 1)],) * 2,
+                2: ([(128, 0, 1), (64, 1, 1), (32, 2, 1)], [(128, 0, 1)])}
+        for t, k in enumerate(kinds):
+            if (self.irreps[t], self.irreps[t + 1]) != want[k]:
+                return None
+        return kinds
+
     def _build_layers(self):
         irr = self.irreps
         self.blocks = []
+        tables = []
         for t in range(self.nlayer):
             x_ir, out_ir = irr[t], irr[t + 1]
-            last = t == self.nlayer - 1
             gin, scal, gated = _gate_irreps(out_ir)
-            mid = _conv_mid(x_ir, 0 if last else 2)
-            kind = 0 if t == 0 else (2 if last else 1)
-            dx, dw, dm = self.conv_backend.dims[kind]
-            xdim = _offsets(x_ir)[-1]
-            wdim = sum(m for m, l1 in x_ir for l2 in range(3)
-                       for l3 in range(abs(l1 - l2), l1 + l2 + 1) if l3 <= (0 if last else 2))
-            if (dx, dw, dm) != (xdim, wdim, _offsets(mid)[-1]):
-                raise ValueError(f'block {t}: irreps {x_ir} -> {out_ir} have no kernel path '
-                                 f'table (kind {kind} is {dx}/{dw}/{dm})')
+            table, mid = path_table(x_ir, self.lmax_edge, self.filter_parity, out_ir)
+            tables.append(table)
             self.blocks.append({
-                'kind': kind, 'gate': (gin, scal, gated),
+                'kind': t, 'gate': (gin, scal, gated), 'sc_irreps': (x_ir, gin),
                 'sc': _Linear(x_ir, gin), 'si1': _Linear(x_ir, x_ir), 'si2': _Linear(mid, gin)})
-        self.readout1 = _Linear(irr[-1], [(irr[-1][0][0] // 2, 0)])
-        self.readout2 = _Linear([(irr[-1][0][0] // 2, 0)], [(1, 0)])
+        kinds = self._sevennet0_kinds()
+        be = self.conv_backend
+        if be is None:
+            # SevenNet-0: the specialised kernels (compile-time path tables);
+            # any other member of the family: the runtime path tables (gtp.hip)
+            be = conv_ops.HipConvBackend() if kinds is not None \
+                else conv_ops.GenericHipConvBackend(tables)
+        elif getattr(be, 'generic', False):
+            be.configure(tables)
+        self.conv_backend = be
+        if not getattr(be, 'generic', False):
+            if kinds is None:
+                raise ValueError('this architecture has no SevenNet-0 kernel path table; use the '
+                                 'generic (runtime path table) backend')
+            for blk, k in zip(self.blocks, kinds):
+                blk['kind'] = k
+        for blk, table in zip(self.blocks, tables):
+            _, dx, _, dw, dm = table
+            if tuple(be.dims[blk['kind']]) != (dx, dw, dm):
+                raise ValueError(f'block {blk["kind"]}: backend dims {be.dims[blk["kind"]]} != '
+                                 f'{(dx, dw, dm)}')
+        hid = self.readout_hidden
+        self.readout1 = _Linear(irr[-1], [(hid, 0, 1)])
+        self.readout2 = _Linear([(hid, 0, 1)], [(1, 0, 1)])
 
     def act(self, x):
         # HIP kernels on the GPU (one launch per derivative order); the CPU
@@ -295,38 +377,82 @@ class SevenNetTrainable(torch.nn.Module):
 
     def gate(self, x, gate_irreps):
         # e3nn nn.Gate (equivariant_gate.py:59-61); split, not sliced (one cat
-        # in the backward instead of a zero-fill + copy per slice)
+        # in the backward instead of a zero-fill + copy per slice).  Odd
+        # scalars take tanh (act_scalar 'o'), everything else scaled SiLU.
         _, scal, gated = gate_irreps
         n = x.shape[0]
-        ns = sum(m for m, _ in scal)
-        ng = sum(m for m, _ in gated)
-        if ng > 0 and x.is_cuda and x.dtype == torch.float32 and len(gated) <= 2:
+        ns = sum(t[0] for t in scal)
+        ng = sum(t[0] for t in gated)
+        odd = any(_ir(t)[1] == -1 for t in scal)
+        if ng > 0 and not odd and x.is_cuda and x.dtype == torch.float32 and len(gated) <= 2:
             key = id(gate_irreps)
             if key not in self._gate_dims:
-                self._gate_dims[key] = conv_ops.gate_dims(scal, gated)
+                self._gate_dims[key] = conv_ops.gate_dims([t[:2] for t in scal],
+                                                          [t[:2] for t in gated])
             return conv_ops.gate(x, self._gate_dims[key], self.silu_norm, self._act_lib())
-        if ng == 0:
-            return self.act(x[:, :ns] if x.shape[1] != ns else x)
-        sizes = [ns, ng] + [m * (2 * l + 1) for m, l in gated]
-        pieces = x.split(sizes, dim=1)
-        outs = [self.act(pieces[0])]
-        gs = self.act(pieces[1]).split([m for m, _ in gated], dim=1)
-        for k, (m, l) in enumerate(gated):
-            blk = pieces[2 + k].view(n, m, 2 * l + 1)
-            outs.append((gs[k].unsqueeze(-1) * blk).reshape(n, -1))
-        return torch.cat(outs, dim=1)
+        sizes = [t[0] for t in scal] + ([ng] if ng else []) + \
+            [t[0] * (2 * t[1] + 1) for t in gated]
+        pieces = x.split(sizes, dim=1) if len(sizes) > 1 else (x[:, :ns],)
+        outs = []
+        for k, t in enumerate(scal):
+            outs.append(self.act(pieces[k]) if _ir(t)[1] == 1
+                        else torch.tanh(pieces[k]) * self.tanh_norm)
+        if ng:
+            gs = self.act(pieces[len(scal)]).split([t[0] for t in gated], dim=1)
+            for k, t in enumerate(gated):
+                blk = pieces[len(scal) + 1 + k].view(n, t[0], 2 * t[1] + 1)
+                outs.append((gs[k].unsqueeze(-1) * blk).reshape(n, -1))
+        return torch.cat(outs, dim=1) if len(outs) > 1 else outs[0]
 
     def _edge_basis(self, r):
-        # BesselBasis (edge_embedding.py:114-116) * XPLORCutoff (:163-173)
-        rc, ron = self.cutoff, self.r_on
+        # BesselBasis (edge_embedding.py:114-116) * XPLORCutoff (:163-173) or
+        # PolynomialCutoff (:131-145)
+        rc = self.cutoff
         coeffs = self.param('edge_embedding.basis_function.coeffs')
         ur = r.unsqueeze(-1)
         bessel = (2.0 / rc) * torch.sin(coeffs * ur) / ur
+        if self.cut.get('name', 'XPLOR') == 'poly_cut':
+            p = float(self.cut['p'])
+            x = r / rc
+            env = 1.0 - (p + 1.0) * (p + 2.0) / 2.0 * x ** p + p * (p + 2.0) * x ** (p + 1) \
+                - p * (p + 1.0) / 2.0 * x ** (p + 2)
+            return bessel * env.unsqueeze(-1)
+        ron = self.r_on
         r2 = r * r
         env = torch.where(r < ron, torch.ones_like(r),
                           (rc * rc - r2) ** 2 * (rc * rc + 2 * r2 - 3 * ron * ron)
                           / (rc * rc - ron * ron) ** 3)
         return bessel * env.unsqueeze(-1)
+
+    def self_connection(self, t, blk, x, types):
+        """SelfConnectionLinearIntro (self_connection.py:42-62) or, for the
+        'nequip' type, SelfConnectionIntro = FullyConnectedTensorProduct(x,
+        one-hot) (:11-38): per (i_x, i_out) of equal irrep a (mul_x, nsp,
+        mul_out) weight block, path weight 1/sqrt(sum of mul_x nsp into i_out)
+        -- with a one-hot operand, row n uses the block of its species."""
+        if self.sc_type != 'nequip':
+            return blk['sc'](x, self.param(f'{t}_self_connection_intro.linear.weight'))
+        x_ir, gin = blk['sc_irreps']
+        w = self.param(f'{t}_self_connection_intro.fc_tensor_product.weight')
+        n, nsp = x.shape[0], self.nsp
+        xo = _offsets(x_ir)
+        ins = [(i, j) for i, a in enumerate(x_ir) for j, b in enumerate(gin) if _ir(a) == _ir(b)]
+        fan = {}
+        for i, j in ins:
+            fan[j] = fan.get(j, 0) + x_ir[i][0] * nsp
+        outs = [None] * len(gin)
+        woff = 0
+        for i, j in ins:
+            mi, l, mo = x_ir[i][0], x_ir[i][1], gin[j][0]
+            wb = w[woff:woff + mi * nsp * mo].view(mi, nsp, mo)
+            woff += mi * nsp * mo
+            xi = x[:, xo[i]:xo[i + 1]].reshape(n, mi, 2 * l + 1)
+            # (n, mo, 2l+1): the species' (mi, mo) block per row
+            y = torch.einsum('nui,unw->nwi', xi, wb[:, types, :]) / math.sqrt(fan[j])
+            outs[j] = y if outs[j] is None else outs[j] + y
+        parts = [o.reshape(n, -1) if o is not None else x.new_zeros(n, t_[0] * (2 * t_[1] + 1))
+                 for o, t_ in zip(outs, gin)]
+        return torch.cat(parts, dim=1)
 
     # ------------------------------------------------------------ forward
     def forward(self, data, graph=None):
@@ -354,16 +480,19 @@ class SevenNetTrainable(torch.nn.Module):
 
         r = torch.linalg.norm(vec_k, dim=-1)
         emb = self._edge_basis(r)
-        Y = spherical_harmonics(vec_k)
+        Y = spherical_harmonics(vec_k, self.lmax_edge, self.sh_normalize)
         P = self.param
         x = P('onehot_to_feature_x.linear.weight').view(self.nsp, -1)[types] / math.sqrt(self.nsp)
         for t, blk in enumerate(self.blocks):
-            sc = blk['sc'](x, P(f'{t}_self_connection_intro.linear.weight'))
+            sc = self.self_connection(t, blk, x, types)
             h = blk['si1'](x, P(f'{t}_self_interaction_1.linear.weight'))
             pre = f'{t}_convolution'
-            hid = self.act(emb @ (P(f'{pre}.weight_nn.layer0.weight') / math.sqrt(8.0)))
-            hid = self.act(hid @ (P(f'{pre}.weight_nn.layer1.weight') / 8.0))
-            w = hid @ (P(f'{pre}.weight_nn.layer2.weight') / 8.0)
+            w0 = P(f'{pre}.weight_nn.layer0.weight')
+            hid = self.act(emb @ (w0 / math.sqrt(w0.shape[0])))
+            w1 = P(f'{pre}.weight_nn.layer1.weight')
+            hid = self.act(hid @ (w1 / math.sqrt(w1.shape[0])))
+            w2 = P(f'{pre}.weight_nn.layer2.weight')
+            w = hid @ (w2 / math.sqrt(w2.shape[0]))
             agg = conv_ops.conv(h, Y, w, blk['kind'], graph) / P(f'{pre}.denominator')
             y = blk['si2'](agg, P(f'{t}_self_interaction_2.linear.weight')) + sc
             x = self.gate(y, blk['gate'])

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from . import _keys as KEY
-from .model import E3GNNModel
+from .model import load_model
 from .util import pretrained_name_to_path, unlabeled_atoms_to_graph
 
 try:  # pragma: no cover - ase is not installed in this image
@@ -46,7 +46,9 @@ class SevenNetCalculator(Calculator):
         self.device = torch.device(device)
         import os
         path = model if os.path.isdir(str(model)) else pretrained_name_to_path(model)
-        self.model = E3GNNModel(path, device=self.device)
+        # the native SevenNet-0 engine, or the generic one for other models of
+        # the family (e.g. the HfO2 example deployment)
+        self.model = load_model(path, device=self.device)
         self.type_map = self.model.type_map()
         self.cutoff = self.model.cutoff
         self.sevennet_config = sevennet_config

@@ -60,3 +60,36 @@ class CpuConvBackend:
         dY = dY if dY is not None else zero(Y)
         dw = dw if dw is not None else zero(w)
         return (dh if need_h else None), dY, dw
+
+
+class GenericCpuConvBackend:
+    """CPU double of conv_ops.GenericHipConvBackend: the runtime path tables
+    (nn.path_table rows: l1, l2, l3, mul, x/Y/w/agg offsets) evaluated with
+    the oracle's coupling tables, any dtype."""
+    generic = True
+
+    def __init__(self):
+        self.dims, self.tables = {}, {}
+
+    def configure(self, tables):
+        for k, (paths, dx, dy, dw, dm) in enumerate(tables):
+            self.dims[k] = (dx, dw, dm)
+            self.tables[k] = (np.asarray(paths), dm)
+
+    def build(self, g, into=None):
+        return {} if into is None else into
+
+    def forward(self, kind, g, h, Y, w):
+        paths, dm = self.tables[kind]
+        xs = h[g.edge_nbr.long()]
+        e = xs.shape[0]
+        msg = torch.zeros(e, dm, dtype=h.dtype)
+        for l1, l2, l3, mul, xo, yo, wo, mo in paths.tolist():
+            xi = xs[:, xo:xo + mul * (2 * l1 + 1)].reshape(e, mul, 2 * l1 + 1)
+            c = torch.as_tensor(tp_cg(l1, l2, l3), dtype=h.dtype)
+            m = torch.einsum('eui,ej,ijk->euk', xi, Y[:, yo:yo + 2 * l2 + 1], c) * \
+                w[:, wo:wo + mul].unsqueeze(-1)
+            msg = msg.index_add(1, torch.arange(mo, mo + mul * (2 * l3 + 1)), m.reshape(e, -1))
+        return torch.zeros(g.n_nodes, dm, dtype=h.dtype).index_add(0, g.edge_center.long(), msg)
+
+    backward = CpuConvBackend.backward

@@ -1,0 +1,207 @@
+"""The rest of the nequip family on the GPU: the runtime-path-table
+convolution (gtp.hip, e3gnn_gtp_*) and the reference's HfO2 example deployment
+(sevenn 0.8.6: odd parity, lmax 1, FCTP self-connection, polynomial cutoff,
+raw-vector SH) served through it.  Needs an MI355X: ``pytest -m gpu``.
+
+Oracles: the float64 CPU double of the same op (tests/_conv_cpu.py, the
+oracle's coupling tables) for the kernels; oracle/nequip_ref.py (pinned by the
+reference-run KAT of this deployment, tests/test_oracle.py) for the model.
+Tolerances: op outputs and first / second derivatives 2e-5 relative to the
+output's max magnitude; energies 2e-6 relative, forces 1e-4 eV/A, stress
+2e-6 eV/A^3 (north_star), against the fp64 oracle.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from _conv_cpu import GenericCpuConvBackend
+from _systems import GOLD, load_manifest_symbols, system
+from sevennet_finetuning_amd import _keys as KEY
+from sevennet_finetuning_amd import conv_ops
+from sevennet_finetuning_amd.nn import parse_irreps, path_table
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HFO2 = os.path.join(ROOT, 'sevennet_finetuning_amd', 'assets', 'hfo2_example')
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _tables():
+    """Block tables of the HfO2 deployment + a SevenNet-0 middle block (lmax 2,
+    even parity, 960-wide weights) for the same kernels."""
+    man = json.load(open(os.path.join(HFO2, 'manifest.json')))
+    irr = [parse_irreps(s) for s in man['irreps_manual']]
+    tabs = [path_table(irr[t], 1, -1, irr[t + 1])[0] for t in range(4)]
+    mid = parse_irreps('128x0e+64x1e+32x2e')
+    tabs.append(path_table(mid, 2, 1, mid)[0])
+    return tabs
+
+
+def _problem(table, n=53, seed=0):
+    _, dx, dy, dw, dm = table
+    rng = np.random.default_rng(seed)
+    deg = rng.integers(0, 12, n)
+    deg[::7] = 0
+    deg[3] = 40
+    center = np.repeat(np.arange(n), deg)
+    e = len(center)
+    nbr = rng.integers(0, n, e)
+    ops = [rng.normal(size=(n, dx)), rng.normal(size=(e, dy)), rng.normal(size=(e, dw))]
+    g = rng.normal(size=(n, dm))
+    probe = [rng.normal(size=(n, dx)), rng.normal(size=(e, dy)), rng.normal(size=(e, dw))]
+    return center, nbr, ops, g, probe
+
+
+def _derivs(kind, graph, ops, g, probe, dtype, device):
+    t = [torch.tensor(a, dtype=dtype, device=device, requires_grad=True) for a in ops]
+    gt = torch.tensor(g, dtype=dtype, device=device)
+    pt = [torch.tensor(a, dtype=dtype, device=device) for a in probe]
+    agg = conv_ops.conv(*t, kind, graph)
+    d1 = torch.autograd.grad((agg * gt).sum(), t, create_graph=True)
+    s = sum((di * pi).sum() for di, pi in zip(d1, pt))
+    d2 = torch.autograd.grad(s, t)
+    return agg, d1, d2
+
+
+@pytest.fixture(scope='module')
+def backends():
+    assert torch.cuda.is_available(), 'GPU tests need a HIP device'
+    tabs = _tables()
+    cpu = GenericCpuConvBackend()
+    cpu.configure(tabs)
+    return tabs, conv_ops.GenericHipConvBackend(tabs), cpu
+
+
+@pytest.mark.parametrize('kind', [0, 1, 2, 3, 4])
+def test_gtp_op_first_and_second_derivatives(backends, kind):
+    """Runtime-path-table kernels vs the float64 CPU double: value, first and
+    second derivatives (all operands), ragged graph with empty and busy nodes."""
+    tabs, hip, cpu = backends
+    center, nbr, ops, g, probe = _problem(tabs[kind], seed=kind)
+    gc = conv_ops.ConvGraph(len(g), torch.tensor(center), torch.tensor(nbr), cpu)
+    gh = conv_ops.ConvGraph(len(g), torch.tensor(center, device=DEV),
+                            torch.tensor(nbr, device=DEV), hip)
+    ref = _derivs(kind, gc, ops, g, probe, torch.float64, 'cpu')
+    got = _derivs(kind, gh, ops, g, probe, torch.float32, DEV)
+    assert _rel(got[0], ref[0]) < 2e-5
+    for a, b in zip(got[1], ref[1]):
+        assert _rel(a, b) < 2e-5
+    for a, b in zip(got[2], ref[2]):
+        assert _rel(a, b) < 2e-5
+
+
+def test_gtp_deterministic_and_rejects_bad_tables(backends):
+    from sevennet_finetuning_amd import _lib
+    tabs, hip, _ = backends
+    center, nbr, ops, g, _ = _problem(tabs[4], seed=9)
+    gh = conv_ops.ConvGraph(len(g), torch.tensor(center, device=DEV),
+                            torch.tensor(nbr, device=DEV), hip)
+    t = [torch.tensor(a, dtype=torch.float32, device=DEV) for a in ops]
+    gt = torch.tensor(g, dtype=torch.float32, device=DEV)
+    a1 = hip.forward(4, gh, *t)
+    b1 = hip.backward(4, gh, *t, gt)
+    a2 = hip.forward(4, gh, *t)
+    b2 = hip.backward(4, gh, *t, gt)
+    assert torch.equal(a1, a2)
+    assert all(torch.equal(x, y) for x, y in zip(b1, b2))
+    bad = np.array([[3, 0, 3, 4, 0, 0, 0, 0]], dtype=np.int32)   # l = 3
+    lib = _lib.load()
+    assert not lib.e3gnn_gtp_create(1, bad.ctypes.data, 64, 4, 4, 64)
+    assert 'out of range' in lib.e3gnn_last_error().decode()
+
+
+def _hfo2_oracle(pos, cell, types):
+    from oracle.neighbor import neighbor_list
+    from oracle.nequip_ref import NequIPRef
+    ref = NequIPRef(HFO2)
+    ei, sh = neighbor_list(pos, cell, ref.cutoff)
+    return ref(torch.tensor(pos), torch.tensor(types), torch.tensor(ei), torch.tensor(sh),
+               torch.tensor(cell))
+
+
+@pytest.fixture(scope='module')
+def hfo2():
+    from sevennet_finetuning_amd.model import GenericE3GNNModel, load_model
+    m = load_model(HFO2, device=DEV)
+    assert isinstance(m, GenericE3GNNModel)
+    assert isinstance(m.net.conv_backend, conv_ops.GenericHipConvBackend)
+    return m
+
+
+def _run(model, pos, cell, types):
+    from sevennet_finetuning_amd.neighbor import neighbor_list
+    ei, sh = neighbor_list(pos, cell, model.cutoff)
+    vec = pos[ei[1]] + sh @ cell - pos[ei[0]]
+    t = lambda a, dt=torch.int32: torch.as_tensor(a, dtype=dt, device=DEV)  # noqa: E731
+    r = model.energy_forces(t(types), t(ei[0]), t(ei[1]), t(vec, torch.float32))
+    vol = abs(np.linalg.det(cell))
+    return {'energy': float(r['energy']), 'forces': r['forces'].cpu().numpy(),
+            'stress': r['virial'].cpu().numpy() / vol}
+
+
+def test_hfo2_example_vs_oracle_and_reference_kat(hfo2):
+    """The HfO2 example deployment on res.dat (96 atoms, triclinic, 2,248
+    edges): energy / forces / stress against the fp64 oracle, and the
+    reference's own frozen-model energy and F[0]."""
+    kat = json.load(open(f'{GOLD}/kat_reference.json'))['kats_hfo2_example']
+    d = np.load(f'{GOLD}/hfo2_resdat.npz')
+    types = np.array([hfo2.chemical_symbols.index(str(s)) for s in d['symbols']])
+    got = _run(hfo2, d['pos'], d['cell'], types)
+    ref = _hfo2_oracle(d['pos'], d['cell'], types)
+    assert abs(got['energy'] - float(ref['energy'])) <= 2e-6 * abs(float(ref['energy']))
+    assert np.abs(got['forces'] - ref['forces'].numpy()).max() <= 1e-4
+    assert np.abs(got['stress'] - ref['stress'].numpy()).max() <= 2e-6
+    assert abs(got['energy'] - kat['energy']) <= 2e-6 * abs(kat['energy'])
+    assert np.abs(got['forces'][0] - np.array(kat['force0'])).max() <= 1e-4
+
+
+def test_hfo2_example_supercell_and_calculator(hfo2):
+    """res.dat replicated 2x2x1 (the in.lmp MD example replicates it): E = 4 E,
+    forces periodic; the ASE calculator surface routes the deployment to the
+    generic engine."""
+    from sevennet_finetuning_amd.sevennet_calculator import SevenNetCalculator
+    from sevennet_finetuning_amd.structures import Atoms, tile
+    d = np.load(f'{GOLD}/hfo2_resdat.npz')
+    types = np.array([hfo2.chemical_symbols.index(str(s)) for s in d['symbols']])
+    one = _run(hfo2, d['pos'], d['cell'], types)
+    pos4, cell4 = tile(d['pos'], d['cell'], (2, 2, 1))
+    four = _run(hfo2, pos4, cell4, np.tile(types, 4))
+    assert abs(four['energy'] - 4 * one['energy']) <= 2e-6 * abs(four['energy'])
+    f = four['forces'].reshape(4, len(types), 3)
+    assert np.abs(f - one['forces'][None]).max() <= 1e-4
+    calc = SevenNetCalculator(HFO2, device=DEV)
+    atoms = Atoms(symbols=[str(s) for s in d['symbols']], positions=d['pos'], cell=d['cell'])
+    calc.calculate(atoms)
+    r = calc.results
+    assert abs(r['energy'] - one['energy']) <= 2e-6 * abs(one['energy'])
+    assert np.abs(r['forces'] - one['forces']).max() <= 1e-4
+    assert np.abs(r['stress'] - (-one['stress'][[0, 1, 2, 4, 5, 3]])).max() <= 2e-6
+
+
+def test_generic_kernels_serve_sevennet0_like_the_specialised_ones():
+    """SevenNet-0 through the runtime path tables equals SevenNet-0 through its
+    compile-time kernels (two independent HIP implementations of the same
+    convolution)."""
+    from sevennet_finetuning_amd import train
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    syms = load_manifest_symbols()
+    pos, cell, types = system('mixed_2x1x1', syms)
+    g = train.collate([train.labeled_graph(pos, cell, types, 5.0)], device=DEV,
+                      dtype=torch.float32)
+    a = SevenNetTrainable(device=DEV)
+    b = SevenNetTrainable(device=DEV, conv_backend=conv_ops.GenericHipConvBackend())
+    assert isinstance(b.conv_backend, conv_ops.GenericHipConvBackend)
+    a.eval()
+    b.eval()
+    ra, rb = a(g), b(g)
+    ea, eb = float(ra[KEY.PRED_TOTAL_ENERGY][0]), float(rb[KEY.PRED_TOTAL_ENERGY][0])
+    assert abs(ea - eb) <= 2e-6 * abs(ea)
+    assert float((ra[KEY.PRED_FORCE] - rb[KEY.PRED_FORCE]).abs().max()) <= 1e-4
