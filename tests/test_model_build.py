@@ -55,16 +55,27 @@ def test_derived_irreps_and_refusals():
     cfg = mb.resolve_config(c)
     assert [mb._irreps_str(i) for i in cfg['_irreps']] == \
         ['128x0e'] + ['128x0e+128x1e+128x2e'] * 4 + ['128x0e']
-    with pytest.raises(NotImplementedError, match='SevenNet-0 architecture'):
-        mb._check_kernel_support(mb.model_manifest(cfg))
+    # other family members are served by the runtime path tables (gtp.hip)
+    mb._check_kernel_support(mb.model_manifest(cfg))
     c = ft_config()
     c['cutoff_function'] = {'cutoff_function_name': 'poly_cut'}
-    with pytest.raises(NotImplementedError, match='XPLOR'):
-        mb._check_kernel_support(mb.model_manifest(mb.resolve_config(c)))
+    man = mb.model_manifest(mb.resolve_config(c))
+    mb._check_kernel_support(man)
+    assert man['cutoff_function'] == {'name': 'poly_cut', 'p': 6.0}
     c = ft_config()
     c['self_connection_type'] = 'nequip'
-    with pytest.raises(NotImplementedError, match='nequip'):
+    man = mb.model_manifest(mb.resolve_config(c))
+    assert man['family'] == 'nequip'
+    assert any(t['name'] == '0_self_connection_intro.fc_tensor_product.weight'
+               for t in man['tensors'])
+    c = ft_config()
+    c['self_connection_type'] = 'mace'
+    with pytest.raises(NotImplementedError, match='mace'):
         mb.model_manifest(mb.resolve_config(c))
+    c = ft_config()
+    c['irreps_manual'] = ['128x0e'] + ['128x0e+64x1e+32x3e'] * 4 + ['128x0e']
+    with pytest.raises(NotImplementedError, match='l > 2'):
+        mb._check_kernel_support(mb.model_manifest(mb.resolve_config(c)))
     c = ft_config()
     c['conv_denominator'] = 'avg_num_neigh'
     with pytest.raises(ValueError, match='dataset statistic'):
@@ -121,3 +132,26 @@ def test_checkpoint_and_deploy_round_trips(tmp_path):
     assert torch.equal(m3.flat, m.flat)
     raw = np.fromfile(os.path.join(out, 'weights.bin'), dtype='<f4')
     assert np.array_equal(raw, m.flat.numpy())
+
+
+def test_hfo2_example_config_builds_the_exported_parameter_table():
+    """The reference config of the HfO2 example deployment (sevenn 0.8.6:
+    channel 4, lmax 1, is_parity, nequip self-connection, poly_cut, 4 blocks,
+    full irreps in the last block) through model_build gives exactly the
+    parameter table exported from the frozen archive (tools/export_hfo2.py)."""
+    import json
+    import os
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        'sevennet_finetuning_amd', 'assets', 'hfo2_example')
+    ref = json.load(open(os.path.join(root, 'manifest.json')))
+    cfg = mb.resolve_config({
+        'chemical_species': 'Hf O', 'cutoff': 4.0, 'channel': 4, 'lmax': 1, 'is_parity': True,
+        'num_convolution_layer': 4, 'irreps_manual': ref['irreps_manual'],
+        'self_connection_type': 'nequip', 'conv_denominator': ref['conv_denominator'][0],
+        '_normalize_sph': False,
+        'cutoff_function': {'cutoff_function_name': 'poly_cut', 'poly_cut_p_value': 6}})
+    man = mb.model_manifest(cfg)
+    assert [(t['name'], t['numel']) for t in man['tensors']] == \
+        [(t['name'], t['numel']) for t in ref['tensors']]
+    assert man['family'] == 'nequip' and man['sh_normalize'] is False
+    assert man['readout_hidden'] == ref['readout_hidden']
