@@ -183,6 +183,7 @@ struct e3gnn_model {
     DBuf w2b;            // 3-way bf16 split of w2 in 16x16x32 operand order (fused.h)
     DBuf w2c;            // 3-way bf16 split of w2, dE/dw-kernel block pairs (fused.h)
     DBuf w2d;            // the same for the fused backward's pairs (fused.h)
+    DBuf w2v;            // w2b's column blocks in visiting order (fused.h)
   };
   std::vector<Mlp> mlp;
 };
@@ -504,7 +505,8 @@ MlpW mlp_ptrs(const e3gnn_model* m, int t) {
   return MlpW{mm.w0.f(),  mm.w1.f(),  mm.w2.f(),  mm.w2t.f(),
               mm.w1p.f(), mm.w2p.f(), mm.w2q.f(), mm.w2r.f(),
               static_cast<const uint16_t*>(mm.w2b.p),
-              static_cast<const uint16_t*>(mm.w2c.p), static_cast<const uint16_t*>(mm.w2d.p)};
+              static_cast<const uint16_t*>(mm.w2c.p), static_cast<const uint16_t*>(mm.w2d.p),
+              static_cast<const uint16_t*>(mm.w2v.p)};
 }
 
 }  // namespace
@@ -761,6 +763,14 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
                   }
                 }
         if (upload(mm.w2d, d2) != hipSuccess) throw std::runtime_error("upload mlp (w2d)");
+        // w2v (MlpW::w2v): w2b's blocks in the visiting order of the kernels
+        {
+          std::vector<float> v2(b2.size());
+          const size_t blk = (size_t)64 * 16 * 3 / 2;   // floats per column block
+          for (size_t k = 0; k < cols.size(); ++k)
+            std::memcpy(v2.data() + k * blk, b2.data() + (size_t)(cols[k] / 16) * blk, blk * 4);
+          if (upload(mm.w2v, v2) != hipSuccess) throw std::runtime_error("upload mlp (w2v)");
+        }
         if (W % 16 || upload(mm.w1p, kperm(a1, 64)) != hipSuccess ||
             upload(mm.w2p, kperm(a2, W)) != hipSuccess || upload(mm.w2q, q2) != hipSuccess ||
             upload(mm.w2r, r2) != hipSuccess ||

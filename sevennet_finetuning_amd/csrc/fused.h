@@ -26,6 +26,9 @@ struct MlpW {
   // w2[16 bh + c][col], col = channel 4g + t of the pair's first block (t < 4)
   // or 4g + t - 4 of its second
   const uint16_t* w2d;
+  // w2b's column blocks in the kernels' visiting order (block k at column 16 k):
+  // the software-pipelined loops fetch the operand of the block after next
+  const uint16_t* w2v;
 };
 
 struct FusedArgs {

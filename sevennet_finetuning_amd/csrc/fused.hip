@@ -78,6 +78,13 @@
 #ifndef E3GNN_BWDXW_DH2BF
 #define E3GNN_BWDXW_DH2BF 0
 #endif
+// dE/dx kernels: the radial weights w of the NEXT visited block are formed
+// (MFMA) before this block's tensor product (VALU), so the matrix pipe works
+// under the VALU stream instead of the tensor product waiting on it (1), or
+// w of a block just before its use (0)
+#ifndef E3GNN_BWDX_PIPE
+#define E3GNN_BWDX_PIPE 1
+#endif
 
 namespace e3gnn {
 namespace {
@@ -124,7 +131,7 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // does not hoist hundreds of 64-bit addresses out of the centre loop (which it
 // did, and spilled).  Offsets outside the descriptor read 0 (padded rows).
 struct WRes {
-  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b, w2c, w2r, w2d;
+  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b, w2c, w2r, w2d, w2v;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int nfloats) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
@@ -133,7 +140,8 @@ __device__ __forceinline__ WRes make_wres(const MlpW& W, int width) {
   return {rsrc(W.w0, 8 * 64), rsrc(W.w1, 64 * 64), rsrc(W.w2p, 64 * width), rsrc(W.w2q, 64 * width),
           rsrc(W.w1p, 64 * 64), rsrc((const float*)W.w2b, 64 * width * 3 / 2),
           rsrc((const float*)W.w2c, 64 * width * 3 / 2), rsrc(W.w2r, 64 * width),
-          rsrc((const float*)W.w2d, 64 * width * 3 / 2)};
+          rsrc((const float*)W.w2d, 64 * width * 3 / 2),
+          rsrc((const float*)W.w2v, 64 * width * 3 / 2)};
 }
 __device__ __forceinline__ float ldw(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
   // the builtin returns the raw 32 bits (an unsigned int): reinterpret, never convert
@@ -775,6 +783,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
     f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
     constexpr bool DBF = FW && E3GNN_BWDXW_DH2BF;
     int nb = 0;     // visited blocks of the tile (DBF: pairs (2P, 2P + 1))
+    // PIPE: w of the current block (formed during the previous one) and of the
+    // next; wq then holds the operand of the block after the next (w2v: the
+    // bf16 pieces in visiting order, block nb at column 16 nb)
+    constexpr bool PIPE = E3GNN_BWDX_PIPE && !E3GNN_BWDXW_LEAN;
+    constexpr int NBLK = L::W / 16;
+    f32x4 wcur = zero4(), wnxt = zero4();
+    if constexpr (PIPE) {
+      wcur = w2_block<false>(hq, wq);
+      if (NBLK > 1) load_w2b(wq, R.w2v, lane, 16);
+    }
     float dwp[4];   // DBF: dE/dw of the pair's first block
     float dYa[9];  // dE/dY of edge c over this lane's channels (index 0 unused)
 #pragma unroll
@@ -818,16 +836,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
               // consumed after the tensor product
               f32x4 bq[4];
               if constexpr (FW && !DBF && !E3GNN_BWDXW_LEAN) load_w2q(bq, R.w2r, lane, p.woff + 16 * jj);
-              // DBF: the pair's W2 pieces of hidden block 0, issued at its second block
+              // DBF: the pair's W2 pieces (hidden block 0, or all four with
+              // E3GNN_BWDXW_DH2BF == 2), issued at its second block under its TP
               bf16x8 pa[3];
+              bf16x8 pall[E3GNN_BWDXW_DH2BF == 2 ? 4 : 1][3];
               if constexpr (DBF) {
-                if (nb & 1) load_w2d(pa, R.w2d, lane, nb >> 1, 0);
+                if (nb & 1) {
+                  if constexpr (E3GNN_BWDXW_DH2BF == 2) {
+#pragma unroll
+                    for (int bh = 0; bh < 4; ++bh) load_w2d(pall[bh], R.w2d, lane, nb >> 1, bh);
+                  } else {
+                    load_w2d(pa, R.w2d, lane, nb >> 1, 0);
+                  }
+                }
               }
               float dwr[4];
               if constexpr (FW && E3GNN_BWDXW_LEAN) load_w2b(wq, R.w2b, lane, p.woff + 16 * jj);
               // w^T block: A = W2s[:, col0 + i]^T (w2p order), B = H2^T
-              const f32x4 wv = w2_block<false>(hq, wq);
-              if constexpr (!(FW && E3GNN_BWDXW_LEAN)) {
+              f32x4 wv;
+              if constexpr (PIPE) {
+                wv = wcur;
+                if (nb + 1 < NBLK) wnxt = w2_block<false>(hq, wq);
+                if (nb + 2 < NBLK) load_w2b(wq, R.w2v, lane, 16 * (nb + 2));
+              } else {
+                wv = w2_block<false>(hq, wq);
+              }
+              if constexpr (!PIPE && !(FW && E3GNN_BWDXW_LEAN)) {
                 const int nc = next_block_col<L, I, pi>(jj);
                 if (nc >= 0) load_w2b(wq, R.w2b, lane, nc);
               }
@@ -869,6 +903,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
                     }
                   }
                   constexpr int PI_[6] = {2, 1, 0, 1, 0, 0}, PJ_[6] = {0, 1, 2, 0, 1, 0};
+                  if constexpr (E3GNN_BWDXW_DH2BF == 2) {
+#pragma unroll
+                    for (int bh = 0; bh < 4; ++bh)
+#pragma unroll
+                      for (int q = 0; q < 6; ++q)
+                        dh2[bh] = mfma16(pall[bh][PI_[q]], d[PJ_[q]], dh2[bh]);
+                  } else {
 #pragma unroll
                   for (int bh = 0; bh < 4; ++bh) {
                     bf16x8 pn[3];
@@ -879,6 +920,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
 #pragma unroll
                       for (int pc = 0; pc < 3; ++pc) pa[pc] = pn[pc];
                     }
+                  }
                   }
                 } else {
 #pragma unroll
@@ -895,6 +937,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
 #pragma unroll
                   for (int r = 0; r < 4; ++r) dh2[bh] = mfma(bq[bh][r], dwr[r], dh2[bh]);
                 }
+              }
+              if constexpr (PIPE) {
+                wcur = wnxt;
+                if constexpr (!DBF) ++nb;   // (DBF counts its pairs above)
               }
             }
           });

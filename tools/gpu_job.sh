@@ -38,6 +38,8 @@ for s in "$@"; do
     proftrain) step proftrain 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_train -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 && mkdir -p gpurun_out/prof_train && cp /tmp/prof_train/*/*stats* /tmp/prof_train/*stats* gpurun_out/prof_train/ 2>/dev/null; ls gpurun_out/prof_train ;;
     traintests) step traintests 400 python -m pytest tests/test_gpu_train.py -x -q --timeout 200 --timeout-method thread ;;
     benchtrain) step benchtrain 300 python bench_train.py --steps 10 --warmup 3 ;;
+    benchtrain2) step benchtrain2 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    benchtraineager) step benchtraineager 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline --eager ;;
     benchd3) step benchd3 300 python bench_d3.py ;;
     profd3) step profd3 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_d3 -o run --output-format csv -- python bench_d3.py --no-cpu-baseline && mkdir -p gpurun_out/prof_d3 && cp /tmp/prof_d3/*/*stats* /tmp/prof_d3/*stats* gpurun_out/prof_d3/ 2>/dev/null; ls gpurun_out/prof_d3 ;;
     d3tests) step d3tests 300 python -m pytest tests/test_gpu_d3.py -x -q --timeout 200 --timeout-method thread ;;
