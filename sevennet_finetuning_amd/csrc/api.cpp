@@ -951,9 +951,11 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
                              c->emb.f(), s));
   }
   if (E > 0) {
-    HIPCHK(hipMemsetAsync(c->dY.p, 0, E * 9 * F, s));
-    HIPCHK(hipMemsetAsync(c->dgu.p, 0, E * 3 * F, s));
-    HIPCHK(hipMemsetAsync(c->demb.p, 0, E * 8 * F, s));
+    // zero kernels, not hipMemsetAsync: the evaluation stays correct when a
+    // host captures it in a HIP graph (launch_zero, node.hip)
+    HIPCHK(launch_zero(c->dY.f(), E * 9, s));
+    HIPCHK(launch_zero(c->dgu.f(), E * 3, s));
+    HIPCHK(launch_zero(c->demb.f(), E * 8, s));
   }
   return E3GNN_OK;
 }
@@ -1388,13 +1390,13 @@ int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_
   int dx, W, dm;
   if (!conv_kind_dims(kind, &dx, &W, &dm)) return fail(E3GNN_ERR_ARG, "conv kind must be 0, 1 or 2");
   hipStream_t s = (hipStream_t)stream;
-  if (dh && n_nodes > 0) HIPCHK(hipMemsetAsync(dh, 0, n_nodes * dx * 4, s));
+  if (dh && n_nodes > 0) HIPCHK(launch_zero(dh, n_nodes * dx, s));
   if (n_edges <= 0 || n_nodes <= 0) return E3GNN_OK;
   if (!row_ptr || !edge_nbr || !h || !Y || !w || !gagg || !dY || !dw)
     return fail(E3GNN_ERR_ARG, "null conv operand");
   if (dh && (!dxc || !src_ptr || !src_perm))
     return fail(E3GNN_ERR_ARG, "dh needs dxc scratch and the transposed CSR");
-  HIPCHK(hipMemsetAsync(dY, 0, n_edges * 9 * 4, s));
+  HIPCHK(launch_zero(dY, n_edges * 9, s));
   TpArgs a{};
   a.row_ptr = row_ptr;
   a.nbr = edge_nbr;
@@ -1518,7 +1520,7 @@ int e3gnn_gtp_backward(const e3gnn_gtp* g, int64_t n_nodes, int64_t n_edges, con
                        float* dh, float* dY, float* dw, float* dxc, void* stream) {
   if (!g) return fail(E3GNN_ERR_ARG, "null gtp");
   hipStream_t s = (hipStream_t)stream;
-  if (dh && n_nodes > 0) HIPCHK(hipMemsetAsync(dh, 0, n_nodes * g->T.dx * 4, s));
+  if (dh && n_nodes > 0) HIPCHK(launch_zero(dh, n_nodes * g->T.dx, s));
   if (n_edges <= 0 || n_nodes <= 0) return E3GNN_OK;
   if (n_nodes >= (int64_t)1 << 31 || n_edges >= (int64_t)1 << 31)
     return fail(E3GNN_ERR_ARG, "gtp: graph size out of int32 range");

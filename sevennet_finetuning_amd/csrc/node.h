@@ -27,6 +27,7 @@ hipError_t launch_readout_bwd(int n, const float* v, const int* type, const floa
 int sum_blocks(int64_t n);
 hipError_t launch_sum(int64_t n, const float* a, float* part, float* out, hipStream_t s);
 hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStream_t s);
+hipError_t launch_zero(float* p, int64_t n, hipStream_t s);
 hipError_t launch_gather_rows(int n, int D, const int* ptr, const int* perm, const float* src,
                               float* dst, hipStream_t s);
 // the same over neighbour nodes [j_begin, j_end) only

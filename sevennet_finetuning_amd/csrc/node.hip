@@ -454,6 +454,21 @@ hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, con
   LAUNCH(k_atom_force, nblk(n_nodes), n_nodes, n_centers, row_ptr, src_ptr, src_perm, fe, F);
   return hipGetLastError();
 }
+// zero fill as a KERNEL: ops that a HIP graph may capture (the fine-tune
+// step's convolution backward) zero their accumulators with this rather than
+// hipMemsetAsync -- a captured memset node did not re-zero the buffer on
+// replay here (the graphed step then accumulated into stale values)
+__global__ void k_zero(int64_t n, float* __restrict__ p) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = 0.f;
+}
+hipError_t launch_zero(float* p, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t b = std::min<int64_t>((n + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_zero, dim3((unsigned)b), dim3(256), 0, s, n, p);
+  return hipGetLastError();
+}
 hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* center,
                               const int* nbr, int* row_ptr, int* src_ptr, int* src_perm,
                               int* cnt, int* err, hipStream_t s, int n_interior) {
@@ -499,8 +514,7 @@ int sum_blocks(int64_t n) { return nblk(n); }
 hipError_t launch_sum(int64_t n, const float* a, float* part, float* out, hipStream_t s) {
   const int nb = nblk(n);
   if (nb == 0) {
-    (void)hipMemsetAsync(out, 0, sizeof(float), s);
-    return hipGetLastError();
+    return launch_zero(out, 1, s);
   }
   LAUNCH(k_block_sum, nb, n, a, part);
   hipLaunchKernelGGL(k_final_sum, dim3(1), dim3(TPB), 0, s, nb, 1, part, out);
@@ -508,8 +522,7 @@ hipError_t launch_sum(int64_t n, const float* a, float* part, float* out, hipStr
 }
 hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStream_t s) {
   if (nb == 0) {
-    (void)hipMemsetAsync(out, 0, sizeof(float) * k, s);
-    return hipGetLastError();
+    return launch_zero(out, k, s);
   }
   hipLaunchKernelGGL(k_final_sum, dim3(1), dim3(TPB), 0, s, nb, k, part, out);
   return hipGetLastError();

@@ -457,6 +457,10 @@ class Trainer:
         for loss_def, _ in self.loss_functions:
             if isinstance(loss_def, EWCLoss) and loss_def.device is None:
                 loss_def.to(self.device)
+            if isinstance(loss_def, EWCLoss) and hasattr(self.model, 'flat'):
+                # the flat (F, theta*) terms now, on this stream: never inside a
+                # graphed step's side-stream warm-up or capture
+                loss_def._flat_terms(self.model)
             loss_def.static = self.hip_graph
         self._graphed = GraphedRehearsalStep(self, config.get('hip_graph_max', 16)) \
             if self.hip_graph else None

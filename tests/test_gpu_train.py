@@ -250,6 +250,44 @@ def test_graphed_rehearsal_step_equals_eager():
     assert float((de - dg).norm() / de.norm()) < 1e-2
 
 
+def test_graphed_step_replays_of_equal_shapes_equal_eager():
+    """Many replays of ONE captured graph whose new and memory batches have
+    the same shapes (bench_train's case: the graph's memory plan then reuses
+    the first pass's buffers in the second): every step's losses and the
+    parameters equal the eager trainer's.  (A captured hipMemsetAsync node did
+    not re-zero the convolution backward's accumulators on replay; the ops now
+    zero them with a kernel.)"""
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+
+    def make(graph):
+        m = SevenNetTrainable(device=DEV)
+        fisher = {n: torch.full_like(p, 1e-3) for n, p in m.named_parameters()}
+        opt = {n: p.detach().clone() for n, p in m.named_parameters()}
+        cfg = {'loss': 'huber', 'loss_param': {'delta': 0.01}, 'force_loss_weight': 1.0,
+               'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
+               'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
+               'scheduler_param': {'gamma': 0.99}, 'device': DEV, 'hip_graph': graph,
+               'continue': {'fisher_information': fisher, 'opt_params': opt,
+                            'ewc_lambda': 1e5}}
+        tr = train.Trainer(m, cfg)
+        m.train(True)
+        return m, tr
+
+    def coll(seeds):
+        return train.collate(_batch(seeds), device=DEV, dtype=torch.float32)
+    pairs = [(coll([1, 2]), coll([3, 4])), (coll([5, 6]), coll([7, 8]))]
+    assert all(a[KEY.EDGE_IDX].shape == b[KEY.EDGE_IDX].shape for a, b in pairs)
+    me, te = make(False)
+    le = [[float(x) for x in te.rehearsal_step(*pairs[i % 2])] for i in range(5)]
+    mg, tg = make(True)
+    lg = [[float(x) for x in tg.rehearsal_step(*pairs[i % 2])] for i in range(5)]
+    for i in range(5):
+        for a, c in zip(le[i], lg[i]):
+            assert abs(a - c) <= 1e-5 * abs(a), (i, le[i], lg[i])
+    assert len(tg._graphed.cache) == 1
+    assert float((me.flat - mg.flat).abs().max()) < 1e-5
+
+
 def test_scaled_silu_op_derivatives():
     """e3gnn_act (fused scale * silu) against torch's composite in float64:
     value, first and second derivatives."""

@@ -53,6 +53,16 @@ for s in "$@"; do
     bench2) step bench2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --cells 11 --same-device --no-cpu-baseline ;;
     report) step report 300 python tools/parity_report.py ;;
     trainops) step trainops 300 python tools/prof_train_ops.py ;;
+    diaggraph) step diaggraph 300 python tools/diag_graph_train.py ;;
+    diaggraph2) step diaggraph2 300 python tools/diag_graph_train2.py ;;
+    diag3) step diag3 300 python tools/diag_graph_train3.py ;;
+    diag4) step diag4 300 python tools/diag_graph_train4.py ;;
+    diag5) step diag5 300 python tools/diag_graph_train5.py ;;
+    diag5_*) v=${s#diag5_}; step diag5_$v 300 python tools/diag_graph_train5.py $v ;;
+    diag6) step diag6 300 python tools/diag_graph_train6.py ;;
+    diag7) step diag7 300 python tools/diag_graph_train7.py ;;
+    diagparts) step diagparts 300 python tools/diag_graph_parts.py ;;
+    diaggraph2lt) step diaggraph2lt 300 python tools/diag_graph_train2.py hipblaslt ;;
     pmctcp) step pmctcp 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum --kernel-trace --output-format csv -d gpurun_out/pmc_tcp -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
     pmctcc) step pmctcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum --kernel-trace --output-format csv -d gpurun_out/pmc_tcc -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
     listc) step listc 120 rocprofv3 -L ;;
