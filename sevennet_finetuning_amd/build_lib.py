@@ -36,6 +36,8 @@ def build(force=False, verbose=False, out=None, defines=()):
     built with extra ``-D`` ``defines``)."""
     lib = out or LIB
     if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _deps_mtime():
+        if out is None:
+            build_native(lib, verbose, only_stale=True)
         return lib
     objdir = OBJDIR if out is None else os.path.join(OBJDIR, os.path.basename(out))
     os.makedirs(objdir, exist_ok=True)
@@ -70,20 +72,31 @@ def build(force=False, verbose=False, out=None, defines=()):
 NATIVE = os.path.join(os.path.dirname(HERE), 'native')
 
 
-def build_native(lib=LIB, verbose=False):
-    """native/e3gnn_md: the C++ MD host over the C ABI (no Python), linked
-    against the in-tree library with an $ORIGIN-relative rpath."""
-    src = os.path.join(NATIVE, 'e3gnn_md.cpp')
-    exe = os.path.join(NATIVE, 'e3gnn_md')
-    cmd = [HIPCC, '-O2', '-std=c++17', f'-I{INCLUDE}', src, '-o', exe,
-           f'-L{os.path.dirname(lib)}', '-le3gnn_hip',
-           "-Wl,-rpath,$ORIGIN/../sevennet_finetuning_amd"]
-    if verbose:
-        print(' '.join(cmd))
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
-    if r.returncode != 0:
-        raise RuntimeError(f'hipcc failed on e3gnn_md.cpp:\n{r.stdout}\n{r.stderr}')
-    return exe
+NATIVE_HOSTS = ('e3gnn_md', 'e3gnn_md_parallel')
+
+
+def build_native(lib=LIB, verbose=False, only_stale=False):
+    """native/e3gnn_md (serial MD host) and native/e3gnn_md_parallel (the
+    pair_e3gnn_parallel call sequence over N in-process sub-domains): C++ over
+    the C ABI (no Python), linked against the in-tree library with an
+    $ORIGIN-relative rpath."""
+    exes = []
+    for name in NATIVE_HOSTS:
+        src = os.path.join(NATIVE, name + '.cpp')
+        exe = os.path.join(NATIVE, name)
+        exes.append(exe)
+        if (only_stale and os.path.exists(exe)
+                and os.path.getmtime(exe) >= max(os.path.getmtime(src), os.path.getmtime(lib))):
+            continue
+        cmd = [HIPCC, '-O2', '-std=c++17', f'-I{INCLUDE}', src, '-o', exe,
+               f'-L{os.path.dirname(lib)}', '-le3gnn_hip',
+               "-Wl,-rpath,$ORIGIN/../sevennet_finetuning_amd"]
+        if verbose:
+            print(' '.join(cmd))
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f'hipcc failed on {name}.cpp:\n{r.stdout}\n{r.stderr}')
+    return exes
 
 
 if __name__ == '__main__':

@@ -1,6 +1,10 @@
-"""The native C++ host (native/e3gnn_md.cpp) over the C ABI -- the compiled
-stand-in for the LAMMPS pair_style e3gnn shim: device
-neighbour list + e3gnn_energy_forces inside a velocity-Verlet loop, no Python.
+"""The native C++ hosts over the C ABI -- the compiled stand-ins for the LAMMPS
+pair styles, no Python:
+- native/e3gnn_md.cpp (pair_style e3gnn): device neighbour list +
+  e3gnn_energy_forces inside a velocity-Verlet loop;
+- native/e3gnn_md_parallel.cpp (pair_style e3gnn/parallel): the segment-API call
+  sequence over N brick sub-domains with device-side halo exchanges, checked
+  against the serial evaluation of the same graph.
 Needs an MI355X: ``pytest -m gpu``.
 
 Checks: the step-0 potential energy of the perfect 64-atom Si box equals the
@@ -19,6 +23,7 @@ import torch
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, 'native', 'e3gnn_md')
+EXE_PAR = os.path.join(ROOT, 'native', 'e3gnn_md_parallel')
 ASSET = os.path.join(ROOT, 'sevennet_finetuning_amd', 'assets', 'sevennet0')
 
 
@@ -53,3 +58,22 @@ def test_native_md_energy_conservation_and_python_parity():
                  'cell_lattice_vectors': torch.tensor(cell, dtype=torch.float32)})
     e_py = float(out['inferred_total_energy'])
     assert abs(rows[0]['epot'] - e_py) <= 1e-6 * abs(e_py)
+
+
+@pytest.mark.parametrize('grid', [(1, 1, 1), (2, 1, 1), (2, 2, 1), (3, 1, 1), (2, 2, 2)])
+def test_native_parallel_host_matches_serial(grid):
+    """pair_e3gnn_parallel.cpp:207-541 restated over the segment API: per-layer
+    forward_comm of ghost features, reverse_comm of ghost gradients and ghost
+    forces.  The decomposed energy/forces/virial equal the serial ones up to
+    fp32 summation order (forces: the north-star 1e-4 eV/A bar)."""
+    assert os.path.exists(EXE_PAR), 'native/e3gnn_md_parallel not built (build_lib.build)'
+    r = subprocess.run([EXE_PAR, os.path.join(ASSET, 'weights.bin'),
+                        os.path.join(ASSET, 'manifest.json'), '3', *map(str, grid), '2'],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out['n_atoms'] == 216 and out['ranks'] == int(np.prod(grid))
+    assert (out['ghosts'] == 0) == (grid == (1, 1, 1))
+    assert out['energy_rel_diff'] < 1e-6
+    assert out['max_force_diff'] < 1e-4
+    assert out['max_virial_diff'] <= 1e-5 * max(1.0, out['max_virial'])

@@ -45,6 +45,7 @@ for s in "$@"; do
     d3tests) step d3tests 300 python -m pytest tests/test_gpu_d3.py -x -q --timeout 200 --timeout-method thread ;;
     nativetests) step nativetests 300 python -m pytest tests/test_gpu_native.py -x -q -s --timeout 200 --timeout-method thread ;;
     md) step md 300 native/e3gnn_md sevennet_finetuning_amd/assets/sevennet0/weights.bin sevennet_finetuning_amd/assets/sevennet0/manifest.json 23 5 1.0 ;;
+    mdpar) step mdpar 300 native/e3gnn_md_parallel sevennet_finetuning_amd/assets/sevennet0/weights.bin sevennet_finetuning_amd/assets/sevennet0/manifest.json 23 2 2 2 3 ;;
     prof10k) step prof10k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof10k -o run --output-format csv -- python bench.py --cells 11 --steps 3 --warmup 1 --profile-only ;;
     pmcf) step pmcf 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     pmcw) step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
