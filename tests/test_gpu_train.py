@@ -285,7 +285,13 @@ def test_graphed_step_replays_of_equal_shapes_equal_eager():
         for a, c in zip(le[i], lg[i]):
             assert abs(a - c) <= 1e-5 * abs(a), (i, le[i], lg[i])
     assert len(tg._graphed.cache) == 1
-    assert float((me.flat - mg.flat).abs().max()) < 1e-5
+    # Adam normalises each gradient entry: one whose gradient is ~0 moves by up
+    # to lr per step in the direction of its rounding noise (torch's atomic
+    # scatter-adds differ run to run), so the bound on any entry is 2 lr x steps;
+    # all but a handful agree to fp32 rounding
+    d = (me.flat - mg.flat).abs()
+    assert float(d.max()) <= 2 * 1e-5 * 5
+    assert float((d > 1e-6).float().mean()) < 1e-3
 
 
 def test_scaled_silu_op_derivatives():
