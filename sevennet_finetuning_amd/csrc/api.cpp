@@ -161,7 +161,20 @@ struct LinBlock {
 struct Linear {
   std::vector<LinBlock> blocks;
   DBuf W, WT;  // W: per block [K x N] row-major; WT: [N x K]
+  std::vector<float> W_h, WT_h;  // host copies (pair construction at load)
   int din = 0, dout = 0;
+};
+
+// Node-linear problems for k_nodelin (gemm.hip): each block one output irrep
+// block, from one linear (K2 = 0) or two K-concatenated linears writing the
+// same block; `W` holds [K1 + K2 x N] per block (16-byte aligned).
+struct PairBlock {
+  int l, N, out_off, K1, off1, K2, off2, w_off;
+};
+struct LinPair {
+  std::vector<PairBlock> blocks;
+  DBuf W;
+  bool ok = false;
 };
 
 }  // namespace
@@ -177,6 +190,9 @@ struct e3gnn_model {
   std::vector<float> denom;
   DBuf coeffs, embed, readout_v, scale, shift;
   std::vector<std::unique_ptr<Linear>> sc, si1, si2;
+  // k_nodelin problem sets: si1, si1^T, si2^T, si2 + sc (forward, gate
+  // epilogue), si1^T + sc^T (backward)
+  std::vector<std::unique_ptr<LinPair>> nl_si1, nl_si1t, nl_si2t, nl_fwd, nl_bwd;
   struct Mlp {
     DBuf w0, w1, w2, w0t, w1t, w2t;
     DBuf w1p, w2p, w2q, w2r;  // MFMA-operand orders of the fused kernels (fused.h)
@@ -258,6 +274,13 @@ struct e3gnn_ctx {
   // edge tiles (0; E3GNN_BWD_FUSE=0)
   int bwd_fuse = [] {
     const char* v = std::getenv("E3GNN_BWD_FUSE");
+    return (v && std::string(v) == "0") ? 0 : 1;
+  }();
+  // node linears on k_nodelin (node-aligned tiles, si2 + sc in one problem,
+  // gate in the epilogue; 1, default) or the grouped k_gemm + k_gate kernels
+  // (0; E3GNN_NODELIN=0)
+  int nodelin = [] {
+    const char* v = std::getenv("E3GNN_NODELIN");
     return (v && std::string(v) == "0") ? 0 : 1;
   }();
   // 0: fused radial-MLP + TP kernels (fused.hip); 1: the unfused v1 kernels
@@ -403,6 +426,49 @@ double lin_flops(const Linear& L, int64_t rows) {
   return f;
 }
 
+// k_nodelin batch over rows [0, rows) of A (+ A2) -> C for the blocks of P
+// selected by `sel` (0 all, 1 the l = 0 block, 2 the l > 0 blocks); `fix`
+// fills the epilogue fields per block.  false: not expressible (the caller
+// takes the k_gemm path).
+struct NoFix {
+  void operator()(NlProb&, const PairBlock&) const {}
+};
+template <class Fix = NoFix>
+bool nl_batch(NlBatch& b, LinPair& P, const float* A, int64_t lda, const float* A2, int64_t lda2,
+              float* C, int64_t ldc, int64_t rows, int epi, int sel = 0, Fix fix = Fix()) {
+  std::memset(&b, 0, sizeof(b));
+  if (!P.ok) return false;
+  for (auto& k : P.blocks) {
+    if ((sel == 1 && k.l != 0) || (sel == 2 && k.l == 0)) continue;
+    NlProb q;
+    std::memset(&q, 0, sizeof(q));
+    q.A = A;
+    q.lda = lda;
+    q.a_off = k.off1;
+    q.A2 = k.K2 ? A2 : nullptr;
+    q.lda2 = lda2;
+    q.a_off2 = k.off2;
+    q.K1 = k.K1;
+    q.K = k.K1 + k.K2;
+    q.B = P.W.f() + k.w_off;
+    q.C = C;
+    q.ldc = ldc;
+    q.c_off = k.out_off;
+    q.N = k.N;
+    q.R = 2 * k.l + 1;
+    q.nodes = (int)rows;
+    q.epi = epi;
+    fix(q, k);
+    if (!add_nl(b, q)) return false;
+  }
+  return true;
+}
+double pair_flops(const LinPair& P, int64_t rows) {
+  double f = 0;
+  for (auto& k : P.blocks) f += 2.0 * rows * (2 * k.l + 1) * (k.K1 + k.K2) * k.N;
+  return f;
+}
+
 // ------------------------------------------------------------ model loading
 int build_linear(Linear& L, const Irreps& in, const Irreps& out, const float* w, size_t numel,
                  double extra_scale_t) {
@@ -433,6 +499,47 @@ int build_linear(Linear& L, const Irreps& in, const Irreps& out, const float* w,
   }
   if (woff != numel) return -1;
   if (upload(L.W, W) != hipSuccess || upload(L.WT, WT) != hipSuccess) return -2;
+  L.W_h = std::move(W);
+  L.WT_h = std::move(WT);
+  return 0;
+}
+
+// One linear (forward: in -> out with W, or transposed: out -> in with WT) plus
+// optionally a second one into the same output blocks (K-concatenated).
+// ok = false when a block of the second has no partner in the first.
+int build_pair(LinPair& P, const Linear& a, bool ta, const Linear* b, bool tb) {
+  std::vector<float> W;
+  size_t matched = 0;
+  for (auto& k : a.blocks) {
+    PairBlock pb;
+    pb.l = k.l;
+    pb.N = ta ? k.K : k.N;
+    pb.out_off = ta ? k.in_off : k.out_off;
+    pb.K1 = ta ? k.N : k.K;
+    pb.off1 = ta ? k.out_off : k.in_off;
+    pb.K2 = 0;
+    pb.off2 = 0;
+    pb.w_off = (int)W.size();
+    const float* w1 = ta ? a.WT_h.data() + k.wt_off : a.W_h.data() + k.w_off;
+    W.insert(W.end(), w1, w1 + (size_t)pb.K1 * pb.N);
+    if (b) {
+      for (auto& q : b->blocks) {
+        const int n2 = tb ? q.K : q.N, o2 = tb ? q.in_off : q.out_off;
+        if (q.l != k.l || o2 != pb.out_off) continue;
+        if (n2 != pb.N || pb.K2) return 0;
+        pb.K2 = tb ? q.N : q.K;
+        pb.off2 = tb ? q.out_off : q.in_off;
+        const float* w2 = tb ? b->WT_h.data() + q.wt_off : b->W_h.data() + q.w_off;
+        W.insert(W.end(), w2, w2 + (size_t)pb.K2 * pb.N);
+        ++matched;
+      }
+    }
+    while (W.size() % 4) W.push_back(0.f);
+    P.blocks.push_back(pb);
+  }
+  if (b && matched != b->blocks.size()) return 0;
+  if (upload(P.W, W) != hipSuccess) return -2;
+  P.ok = true;
   return 0;
 }
 
@@ -643,6 +750,16 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
       m->si1.push_back(mk(p + "_self_interaction_1.linear.weight", xin, xin, 1.0));
       // backward of si2 feeds dE/dagg_raw = dE/dagg / denominator (convolution.py:117-118)
       m->si2.push_back(mk(p + "_self_interaction_2.linear.weight", mid, gin, 1.0 / den));
+      auto pair = [&](const Linear& a, bool ta, const Linear* b, bool tb) {
+        auto P = std::make_unique<LinPair>();
+        if (build_pair(*P, a, ta, b, tb) < 0) throw std::runtime_error("upload");
+        return P;
+      };
+      m->nl_si1.push_back(pair(*m->si1[t], false, nullptr, false));
+      m->nl_si1t.push_back(pair(*m->si1[t], true, nullptr, false));
+      m->nl_si2t.push_back(pair(*m->si2[t], true, nullptr, false));
+      m->nl_fwd.push_back(pair(*m->si2[t], false, m->sc[t].get(), false));
+      m->nl_bwd.push_back(pair(*m->si1[t], true, m->sc[t].get(), true));
       // radial MLP (e3nn FullyConnectedNet, weights / sqrt(fan_in))
       const float* w0 = get(p + "_convolution.weight_nn.layer0.weight", 8 * 64);
       const float* w1 = get(p + "_convolution.weight_nn.layer1.weight", 64 * 64);
@@ -1006,7 +1123,11 @@ int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     if (!fused) return E3GNN_OK;
     {
       Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], nl));
-      HIPCHK(launch_gemm(lin_fwd(*m->si1[t], c->x[t].f(), dx, c->h[t].f(), dx, nl, 0), s));
+      NlBatch nb;
+      if (c->nodelin && nl_batch(nb, *m->nl_si1[t], c->x[t].f(), dx, nullptr, 0, c->h[t].f(), dx, nl, 0))
+        HIPCHK(launch_nodelin(nb, s));
+      else
+        HIPCHK(launch_gemm(lin_fwd(*m->si1[t], c->x[t].f(), dx, c->h[t].f(), dx, nl, 0), s));
     }
     return conv_fwd(0, n_int, (double)c->e_int);
   }
@@ -1014,7 +1135,12 @@ int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
   {
     const int64_t r0 = fused ? nl : 0;  // rows not done in part 0
     Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], n - r0));
-    if (n > r0)
+    NlBatch nb;
+    if (n > r0 && c->nodelin &&
+        nl_batch(nb, *m->nl_si1[t], c->x[t].f() + r0 * dx, dx, nullptr, 0, c->h[t].f() + r0 * dx, dx,
+                 n - r0, 0))
+      HIPCHK(launch_nodelin(nb, s));
+    else if (n > r0)
       HIPCHK(launch_gemm(lin_fwd(*m->si1[t], c->x[t].f() + r0 * dx, dx, c->h[t].f() + r0 * dx, dx,
                                  n - r0, 0), s));
   }
@@ -1065,7 +1191,43 @@ int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     HIPCHK(launch_tp_fwd(kind, a, s));
   }
   }
-  // self_interaction_2 + self_connection (intro/outro)
+  // self_interaction_2 + self_connection (intro/outro) + gate: on k_nodelin
+  // one K-concatenated problem per output block, the 0e block first (its
+  // epilogue activates the scalars and stores the gate pre-activations), then
+  // the gated blocks (epilogue: x = act(gate) * y)
+  {
+    const Irreps& gin = m->gin[t];
+    const Irreps& xo = m->irreps[t + 1];
+    int nscal = 0;
+    for (auto& i : xo)
+      if (i.l == 0) nscal += i.mul;
+    const bool gate_ok = !gin.empty() && gin[0].l == 0 && !xo.empty() && xo[0].l == 0;
+    auto gate_fix = [&](NlProb& q, const PairBlock& k) {
+      q.xo = c->x[t + 1].f();
+      q.ldxo = irreps_dim(xo);
+      if (k.l == 0) {
+        q.n_act = nscal;
+        return;
+      }
+      int off = gin[0].mul, gmul = 0, gdim = 0;
+      for (size_t i = 1; i < gin.size() && off != k.out_off; ++i) {
+        gmul += gin[i].mul;
+        gdim += gin[i].mul * (2 * gin[i].l + 1);
+        off += gin[i].mul * (2 * gin[i].l + 1);
+      }
+      q.gate_off = nscal + gmul;
+      q.xo_off = nscal + gdim;
+    };
+    NlBatch b0, b1;
+    if (c->nodelin && gate_ok &&
+        nl_batch(b0, *m->nl_fwd[t], c->agg.f(), dm, c->x[t].f(), dx, c->y[t].f(), dg, nl, 2, 1, gate_fix) &&
+        nl_batch(b1, *m->nl_fwd[t], c->agg.f(), dm, c->x[t].f(), dx, c->y[t].f(), dg, nl, 3, 2, gate_fix)) {
+      Region r(c, s, C_LINEAR, pair_flops(*m->nl_fwd[t], nl));
+      HIPCHK(launch_nodelin(b0, s));
+      HIPCHK(launch_nodelin(b1, s));
+      return E3GNN_OK;
+    }
+  }
   {
     Region r(c, s, C_LINEAR, lin_flops(*m->si2[t], nl) + lin_flops(*m->sc[t], nl));
     HIPCHK(launch_gemm(lin_fwd(*m->si2[t], c->agg.f(), dm, c->y[t].f(), dg, nl, 0), s));
@@ -1132,7 +1294,11 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     }
     {
       Region r(c, s, C_LINEAR, lin_flops(*m->si2[t], nl));
-      HIPCHK(launch_gemm(lin_bwd(*m->si2[t], c->dy.f(), dg, c->agg.f(), dm, nl, 0), s));
+      NlBatch nb;
+      if (c->nodelin && nl_batch(nb, *m->nl_si2t[t], c->dy.f(), dg, nullptr, 0, c->agg.f(), dm, nl, 0))
+        HIPCHK(launch_nodelin(nb, s));
+      else
+        HIPCHK(launch_gemm(lin_bwd(*m->si2[t], c->dy.f(), dg, c->agg.f(), dm, nl, 0), s));
     }
   }
   // per-edge dE/dx + transposed-CSR gather (edge-ordered kernels) or dE/dx
@@ -1244,10 +1410,22 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     }
     const bool owned = !fused || part == 1;
     Region r(c, s, C_LINEAR, lin_flops(*m->si1[t], r1 - r0) + (owned ? lin_flops(*m->sc[t], nl) : 0));
-    if (r1 > r0)
-      HIPCHK(launch_gemm(lin_bwd(*m->si1[t], c->dh.f() + r0 * dx, dx, c->grad[t].f() + r0 * dx, dx,
-                                 r1 - r0, 0), s));
-    if (owned) HIPCHK(launch_gemm(lin_bwd(*m->sc[t], c->dy.f(), dg, c->grad[t].f(), dx, nl, 1), s));
+    // k_nodelin: owned rows [0, nl) as one si1^T + sc^T problem per block,
+    // the remaining rows (ghosts) si1^T alone
+    NlBatch b0, b1;
+    const int64_t p1 = owned ? nl : r0;  // first row of the si1^T-only range
+    if (c->nodelin && (!owned || r0 == 0) && r1 >= p1 &&
+        (!owned || nl_batch(b0, *m->nl_bwd[t], c->dh.f(), dx, c->dy.f(), dg, c->grad[t].f(), dx, nl, 0)) &&
+        (r1 == p1 || nl_batch(b1, *m->nl_si1t[t], c->dh.f() + p1 * dx, dx, nullptr, 0,
+                              c->grad[t].f() + p1 * dx, dx, r1 - p1, 0))) {
+      if (owned) HIPCHK(launch_nodelin(b0, s));
+      if (r1 > p1) HIPCHK(launch_nodelin(b1, s));
+    } else {
+      if (r1 > r0)
+        HIPCHK(launch_gemm(lin_bwd(*m->si1[t], c->dh.f() + r0 * dx, dx, c->grad[t].f() + r0 * dx, dx,
+                                   r1 - r0, 0), s));
+      if (owned) HIPCHK(launch_gemm(lin_bwd(*m->sc[t], c->dy.f(), dg, c->grad[t].f(), dx, nl, 1), s));
+    }
   }
   return E3GNN_OK;
 }

@@ -82,4 +82,40 @@ struct GemmBatch {
 };
 hipError_t launch_gemm(const GemmBatch& b, hipStream_t s);
 
+// ---------------------------------------------------------------- node linears
+// One irrep block of an e3nn linear (or of two linears into the same output
+// block, K-concatenated: self_interaction_2 + self_connection forward,
+// self_interaction_1^T + self_connection^T backward), node-aligned tiles
+// (gemm.hip k_nodelin):
+//   A(node, m, k) = k < K1 ? A [node * lda  + a_off  + k * R + m]
+//                          : A2[node * lda2 + a_off2 + (k - K1) * R + m]
+//   B(k, col)     = B[k * N + col]          (rows 0..K1-1 then K1..K-1)
+//   C(node, m, col) = C[node * ldc + c_off + col * R + m]
+// epi: 0 store, 1 accumulate, 2 store + xo[node, col] = act(v) for
+// col < n_act (gate scalars / last block), 3 store + xo[node, xo_off + col * R
+// + m] = act(C[node, gate_off + col]) * v (gated irreps; the gate columns were
+// stored by an earlier launch).
+struct NlProb {
+  const float* A;
+  const float* A2;
+  const float* B;
+  float* C;
+  float* xo;
+  int64_t lda, lda2, ldc, ldxo;
+  int a_off, a_off2, c_off, xo_off;
+  int K1, K, N, R, nodes;
+  int epi, n_act, gate_off;
+  int wn, tpn, rows, tile_begin, tiles_n;  // set by add_nl
+};
+constexpr int NL_MAX_PROBS = 4;
+struct NlBatch {
+  NlProb p[NL_MAX_PROBS];
+  int nprob;
+  int total_tiles;
+};
+// false when the problem does not meet the kernel's layout assumptions
+// (16-byte alignment of rows / offsets, K1 % 32 when split, R in {1, 3, 5})
+bool add_nl(NlBatch& b, const NlProb& p);
+hipError_t launch_nodelin(const NlBatch& b, hipStream_t s);
+
 }  // namespace e3gnn

@@ -15,6 +15,8 @@
 // (lane l: A[row l&31][k l>>5], B[k l>>5][col l&31]) are unit-stride.
 #include "common.h"
 
+#include <cstring>
+
 namespace e3gnn {
 
 namespace {
@@ -122,11 +124,387 @@ __global__ __launch_bounds__(256) void k_gemm(GemmBatch batch) {
     default: gemm_tile<0>(P, local, As, Bs); break;
   }
 }
+// ---------------------------------------------------------------- node linears
+// k_nodelin: the e3nn linears of the interaction block (self_interaction_1/2,
+// self_connection; linear.py:46-49) as node-aligned tiles.  A tile covers
+// T = BM / R whole nodes, so the A operand of one k-step is T contiguous runs
+// of BK * R floats (the node's [mul][m] block) loaded as float4 and scattered
+// k-major into LDS; BK = 32 with a double-buffered LDS stage (one barrier per
+// k-step).  Two linears writing the same output block run as one problem with
+// K = K1 + K2 (A switches source at K1), and the gate (equivariant_gate.py:
+// 59-61) is the epilogue: the 0e block writes act(scalars) to the next
+// features, the l > 0 blocks multiply by act(gate) read back from the
+// pre-activation columns the 0e launch stored.  Shapes: BN = 64 / BM = 64
+// (4 waves 2 x 2) or, for N <= 32 (the 2e block), BN = 32 / BM = 128 (4 x 1).
+#ifndef E3GNN_NL_BK
+#define E3GNN_NL_BK 16
+#endif
+#ifndef E3GNN_NL_XCD
+#define E3GNN_NL_XCD 0
+#endif
+// occupancy target of k_nodelin (LDS allows 7 workgroups per CU)
+#ifndef E3GNN_NL_WAVES
+#define E3GNN_NL_WAVES 5
+#endif
+#ifndef E3GNN_NL_ROWS
+#define E3GNN_NL_ROWS 0
+#endif
+constexpr int NL_BK = E3GNN_NL_BK;
+template <int WN>
+struct NlShape {
+  static constexpr int BN = 32 * WN, BM = 128 / WN;
+  static constexpr int LDA = BM + 4, LDB = BN + 4;  // 16-byte LDS rows
+  static constexpr int A_FLOATS = NL_BK * LDA, STAGE = A_FLOATS + NL_BK * LDB;
+};
+constexpr int NL_LDS = 2 * (NlShape<1>::STAGE > NlShape<2>::STAGE ? NlShape<1>::STAGE
+                                                                   : NlShape<2>::STAGE);
+
+// Epilogue through LDS: each node's output is one contiguous run of BN * R
+// floats, written as float4 (the MFMA layout would scatter 4-byte stores R
+// floats apart).  Starts with a barrier: the caller's LDS readers are done.
+template <int WN, int R>
+__device__ __forceinline__ void nl_epilogue(const NlProb& P, const f32x16& acc, int node0, int n0,
+                                            float* lds) {
+  using S = NlShape<WN>;
+  constexpr int BM = S::BM, BN = S::BN;
+  constexpr int T = BM / R, ROWS = T * R;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  __syncthreads();
+  constexpr int LDC = BN + 1;
+  static_assert(ROWS * LDC <= NL_LDS, "C tile must fit the LDS stages");
+  float* Cs = lds;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = wr * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+    if (row < ROWS) Cs[row * LDC + wc * 32 + (lane & 31)] = acc[reg];
+  }
+  __syncthreads();
+  constexpr int SEGC = BN * R / 4, UC = T * SEGC;
+  const int ncol = P.N - n0 < BN ? P.N - n0 : BN;
+#pragma unroll 1
+  for (int u = tid; u < UC; u += 256) {
+    const int nl = u / SEGC, j = 4 * (u - nl * SEGC);
+    const int node = node0 + nl;
+    if (node >= P.nodes) continue;
+    float v[4];
+    int cl[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      cl[q] = (j + q) / R;
+      const int m = (j + q) - cl[q] * R;
+      v[q] = cl[q] < ncol ? Cs[(nl * R + m) * LDC + cl[q]] : 0.f;
+    }
+    if (cl[0] >= ncol) continue;
+    const bool full = cl[3] < ncol;
+    const int64_t nrow = (int64_t)node * P.ldc;
+    float* cp = P.C + nrow + P.c_off + n0 * R + j;
+    if (P.epi == 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (cl[q] < ncol) v[q] += cp[q];
+    }
+    if (full) {
+      *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (cl[q] < ncol) cp[q] = v[q];
+    }
+    if (P.epi == 2) {  // R == 1: element q is column n0 + j + q
+      float* xp = P.xo + (int64_t)node * P.ldxo + P.xo_off + n0 + j;
+      if (full && n0 + j + 3 < P.n_act) {
+        *reinterpret_cast<float4*>(xp) =
+            make_float4(act_fwd(v[0]), act_fwd(v[1]), act_fwd(v[2]), act_fwd(v[3]));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (cl[q] < ncol && n0 + j + q < P.n_act) xp[q] = act_fwd(v[q]);
+      }
+    } else if (P.epi == 3) {
+      const float* gp = P.C + nrow + P.gate_off + n0;
+      float w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = cl[q] < ncol ? act_fwd(gp[cl[q]]) * v[q] : 0.f;
+      float* xp = P.xo + (int64_t)node * P.ldxo + P.xo_off + n0 * R + j;
+      if (full) {
+        *reinterpret_cast<float4*>(xp) = make_float4(w[0], w[1], w[2], w[3]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (cl[q] < ncol) xp[q] = w[q];
+      }
+    }
+  }
+}
+
+
+template <int WN, int R>
+__device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) {
+  using S = NlShape<WN>;
+  constexpr int BM = S::BM, BN = S::BN, BK = NL_BK;
+  constexpr int T = BM / R, ROWS = T * R;
+  constexpr int SEG4 = BK * R / 4;  // float4 per node per k-step
+  constexpr int UA = T * SEG4, NA = (UA + 255) / 256;
+  constexpr int UB = BK * BN / 4, NB = (UB + 255) / 256;
+  static_assert(BK % 4 == 0, "tile shape");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const int tm = local / P.tiles_n, tn = local - tm * P.tiles_n;
+  const int node0 = tm * T, n0 = tn * BN;
+
+  float4 ra[NA], rb[NB];
+  auto load = [&](int k0) {
+    const bool second = k0 >= P.K1;
+    const float* src = second ? P.A2 : P.A;
+    const int64_t ld = second ? P.lda2 : P.lda;
+    const int kk0 = second ? k0 - P.K1 : k0;
+    const int kend = second ? P.K - P.K1 : P.K1;
+    const int off = (second ? P.a_off2 : P.a_off) + kk0 * R;
+    const bool full = kk0 + BK <= kend;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int u = tid + 256 * i;
+      const int nl = u / SEG4, j = 4 * (u - nl * SEG4);
+      const int node = node0 + nl;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if ((UA % 256 == 0 || u < UA) && node < P.nodes) {
+        const float* p = src + (int64_t)node * ld + off + j;
+        if (full) {
+          v = *reinterpret_cast<const float4*>(p);
+        } else {  // K tail: element-wise, masked
+          v.x = kk0 + (j + 0) / R < kend ? p[0] : 0.f;
+          v.y = kk0 + (j + 1) / R < kend ? p[1] : 0.f;
+          v.z = kk0 + (j + 2) / R < kend ? p[2] : 0.f;
+          v.w = kk0 + (j + 3) / R < kend ? p[3] : 0.f;
+        }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int u = tid + 256 * i;
+      const int k = u / (BN / 4), c = 4 * (u - k * (BN / 4));
+      const int gk = k0 + k, col = n0 + c;
+      rb[i] = ((UB % 256 == 0 || u < UB) && gk < P.K && col < P.N) ? *reinterpret_cast<const float4*>(P.B + (int64_t)gk * P.N + col)
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](int buf) {
+    float* As = lds + buf * S::STAGE;
+    float* Bs = As + S::A_FLOATS;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int u = tid + 256 * i;
+      if (UA % 256 != 0 && u >= UA) continue;
+      const int nl = u / SEG4, j = 4 * (u - nl * SEG4);
+      const float e[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = (j + q) / R, m = (j + q) - k * R;
+        As[k * S::LDA + nl * R + m] = e[q];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int u = tid + 256 * i;
+      if (UB % 256 != 0 && u >= UB) continue;
+      const int k = u / (BN / 4), c = 4 * (u - k * (BN / 4));
+      *reinterpret_cast<float4*>(Bs + k * S::LDB + c) = rb[i];
+    }
+  };
+
+  // two accumulators when K is split: the second linear's sum is formed on
+  // its own and added once at the end (the rounding of two separate GEMMs
+  // summed, not 128 small terms added to a large partial sum)
+  const int nk = (P.K + BK - 1) / BK;
+  const int nk1 = P.K > P.K1 ? P.K1 / BK : nk;
+  auto step = [&](int kt, f32x16& c) {
+    if (kt + 1 < nk) load((kt + 1) * BK);
+    const float* As = lds + (kt & 1) * S::STAGE;
+    const float* Bs = As + S::A_FLOATS;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      const float a = As[(kk + (lane >> 5)) * S::LDA + wr * 32 + (lane & 31)];
+      const float b = Bs[(kk + (lane >> 5)) * S::LDB + wc * 32 + (lane & 31)];
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+    }
+    if (kt + 1 < nk) store((kt + 1) & 1);
+    __syncthreads();
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk1; ++kt) step(kt, acc);
+  if (nk1 < nk) {
+    // the second linear's sum on its own, added once (the rounding of two
+    // GEMMs summed, not its terms added one by one to a large partial sum)
+    f32x16 acc2;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc2[i] = 0.f;
+    for (int kt = nk1; kt < nk; ++kt) step(kt, acc2);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] += acc2[i];
+  }
+
+  nl_epilogue<WN, R>(P, acc, node0, n0, lds);
+}
+
+// Row-block mode for small K (<= 64: the transposed self_interaction_2 of the
+// l > 0 blocks, K = 64 / 32 against N = 384 / 352): one workgroup per row
+// tile walks all N tiles.  Its A operand is staged once and then held in
+// registers (32 rows x K per wave), B comes from L2 straight into the MFMA
+// operand registers; only the epilogue uses LDS per N tile.
+template <int WN, int R>
+__device__ __forceinline__ void nl_rows(const NlProb& P, int tm, float* lds) {
+  using S = NlShape<WN>;
+  constexpr int BM = S::BM, BN = S::BN, T = BM / R;
+  constexpr int KMAX = 64, KS = KMAX / 2, LDA = BM + 4;
+  static_assert(KMAX * LDA <= NL_LDS, "A block must fit the LDS stages");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const int node0 = tm * T, K = P.K;
+  const int seg4 = K * R / 4;  // float4 per node (K % 4 == 0)
+#pragma unroll 1
+  for (int u = tid; u < T * seg4; u += 256) {
+    const int nl = u / seg4, j = 4 * (u - nl * seg4);
+    const int node = node0 + nl;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (node < P.nodes) v = *reinterpret_cast<const float4*>(P.A + (int64_t)node * P.lda + P.a_off + j);
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = (j + q) / R, m = (j + q) - k * R;
+      lds[k * LDA + nl * R + m] = e[q];
+    }
+  }
+  __syncthreads();
+  float a[KS];
+#pragma unroll
+  for (int i = 0; i < KS; ++i) {
+    const int k = 2 * i + (lane >> 5);
+    a[i] = k < K ? lds[k * LDA + wr * 32 + (lane & 31)] : 0.f;
+  }
+  const int ks = (K + 1) / 2;
+#pragma unroll 1
+  for (int tn = 0; tn < P.tiles_n; ++tn) {
+    const int n0 = tn * BN, col = n0 + wc * 32 + (lane & 31);
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+      if (i < ks) {
+        const int k = 2 * i + (lane >> 5);
+        const float b = (k < K && col < P.N) ? P.B[(int64_t)k * P.N + col] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b, acc, 0, 0, 0);
+      }
+    }
+    nl_epilogue<WN, R>(P, acc, node0, n0, lds);
+  }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_NL_WAVES, 8))) void k_nodelin(NlBatch batch) {
+  __shared__ __attribute__((aligned(16))) float lds[NL_LDS];
+  // XCD-aware order (gridDim.x is a multiple of 8): each XCD takes a
+  // contiguous eighth of the tiles, so the N tiles of one row block share
+  // their A rows in one L2
+  const int b = blockIdx.x, per = gridDim.x >> 3;
+  const int tile = E3GNN_NL_XCD ? (b & 7) * per + (b >> 3) : b;
+  if (tile >= batch.total_tiles) return;
+  int pi = 0;
+#pragma unroll 1
+  for (int i = 1; i < batch.nprob; ++i)
+    if (tile >= batch.p[i].tile_begin) pi = i;
+  const NlProb& P = batch.p[pi];
+  const int local = tile - P.tile_begin;
+  if (P.wn == 1) {
+    switch (P.R) {
+      case 1: nl_tile<1, 1>(P, local, lds); break;
+      case 3: nl_tile<1, 3>(P, local, lds); break;
+      default: nl_tile<1, 5>(P, local, lds); break;
+    }
+  } else {
+    switch (P.R) {
+      case 1: nl_tile<2, 1>(P, local, lds); break;
+      case 3: nl_tile<2, 3>(P, local, lds); break;
+      default: nl_tile<2, 5>(P, local, lds); break;
+    }
+  }
+}
+// the row-block problems in their own kernel (its A registers would lower the
+// occupancy of k_nodelin)
+__global__ __launch_bounds__(256) void k_nodelin_rows(NlBatch batch) {
+  __shared__ __attribute__((aligned(16))) float lds[NL_LDS];
+  const int tile = blockIdx.x;
+  if (tile >= batch.total_tiles) return;
+  int pi = 0;
+#pragma unroll 1
+  for (int i = 1; i < batch.nprob; ++i)
+    if (tile >= batch.p[i].tile_begin) pi = i;
+  const NlProb& P = batch.p[pi];
+  const int local = tile - P.tile_begin;
+  switch (P.R) {
+    case 1: nl_rows<2, 1>(P, local, lds); break;
+    case 3: nl_rows<2, 3>(P, local, lds); break;
+    default: nl_rows<2, 5>(P, local, lds); break;
+  }
+}
 }  // namespace
 
 hipError_t launch_gemm(const GemmBatch& b, hipStream_t s) {
   if (b.total_tiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_gemm, dim3(b.total_tiles), dim3(256), 0, s, b);
+  return hipGetLastError();
+}
+
+bool add_nl(NlBatch& b, const NlProb& p) {
+  if (b.nprob >= NL_MAX_PROBS) return false;
+  if (p.R != 1 && p.R != 3 && p.R != 5) return false;
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (!al(p.A) || !al(p.B) || !al(p.C) || p.lda % 4 || p.a_off % 4 || p.N % 4 || p.ldc % 4 ||
+      p.c_off % 4)
+    return false;
+  if (p.epi >= 2 && (!al(p.xo) || p.ldxo % 4 || p.xo_off % 4 || (p.epi == 2 && p.R != 1)))
+    return false;
+  if (p.K > p.K1 && (!al(p.A2) || p.lda2 % 4 || p.a_off2 % 4 || p.K1 % NL_BK)) return false;
+  NlProb q = p;
+  q.wn = p.N <= 32 ? 1 : 2;
+  const int BM = 128 / q.wn, BN = 32 * q.wn;
+  q.tpn = BM / p.R;
+  const int tm = (p.nodes + q.tpn - 1) / q.tpn, tn = (p.N + BN - 1) / BN;
+  if (tm <= 0 || tn <= 0) return true;
+  // small K, several N tiles: one workgroup per row tile (nl_rows)
+  q.rows = E3GNN_NL_ROWS && p.K == p.K1 && p.K <= 64 && p.K % 4 == 0 && tn > 1 && q.wn == 2;
+  q.tiles_n = tn;
+  q.tile_begin = b.total_tiles;
+  b.p[b.nprob++] = q;
+  b.total_tiles += q.rows ? tm : tm * tn;
+  return true;
+}
+
+hipError_t launch_nodelin(const NlBatch& b, hipStream_t s) {
+  if (b.total_tiles <= 0) return hipSuccess;
+  // tile-mode and row-block problems as two launches
+  NlBatch t, r;
+  std::memset(&t, 0, sizeof(t));
+  std::memset(&r, 0, sizeof(r));
+  for (int i = 0; i < b.nprob; ++i) {
+    NlProb q = b.p[i];
+    NlBatch& d = q.rows ? r : t;
+    const int tm = (q.nodes + q.tpn - 1) / q.tpn;
+    q.tile_begin = d.total_tiles;
+    d.p[d.nprob++] = q;
+    d.total_tiles += q.rows ? tm : tm * q.tiles_n;
+  }
+  if (t.total_tiles > 0) {
+    const int grid = (t.total_tiles + 7) / 8 * 8;
+    hipLaunchKernelGGL(k_nodelin, dim3(grid), dim3(256), 0, s, t);
+  }
+  if (r.total_tiles > 0) hipLaunchKernelGGL(k_nodelin_rows, dim3(r.total_tiles), dim3(256), 0, s, r);
   return hipGetLastError();
 }
 

@@ -5,6 +5,8 @@ Tolerances (fp32 kernels vs the fp64 oracle, BASELINE.json north_star):
 forces 1e-4 eV/A (absolute, per component), energy 2e-6 relative,
 stress 2e-6 eV/A^3, integer graph work bit-exact.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -214,6 +216,30 @@ def test_fused_matches_v1_kernels(model, name):
     b = run(model, pos, cell, types)
     assert abs(a['energy'] - b['energy']) <= 2e-6 * abs(a['energy'])
     assert np.abs(a['forces'] - b['forces']).max() <= 5e-5
+    assert np.abs(a['stress'] - b['stress']).max() <= 1e-6
+
+
+@pytest.mark.parametrize('name', ['si_rng0_3x3x3', 'hfo2_resdat', 'mixed_2x2x2'])
+def test_nodelin_matches_grouped_gemm(model, name):
+    """The node-linear kernel (k_nodelin: node-aligned tiles, si2 + sc as one
+    K-concatenated problem, gate in the epilogue, si1^T + sc^T) against the
+    grouped k_gemm + k_gate kernels (E3GNN_NODELIN=0 at context creation):
+    two HIP implementations of the same linears, equal to fp32 rounding."""
+    from sevennet_finetuning_amd.model import E3GNNModel
+    pos, cell, types = system(name, SYMS)
+    old = os.environ.get('E3GNN_NODELIN')
+    os.environ['E3GNN_NODELIN'] = '0'
+    try:
+        legacy = E3GNNModel(device='cuda:0')
+    finally:
+        if old is None:
+            del os.environ['E3GNN_NODELIN']
+        else:
+            os.environ['E3GNN_NODELIN'] = old
+    a = run(legacy, pos, cell, types)
+    b = run(model, pos, cell, types)
+    assert abs(a['energy'] - b['energy']) <= 1e-6 * abs(a['energy'])
+    assert np.abs(a['forces'] - b['forces']).max() <= 2e-5
     assert np.abs(a['stress'] - b['stress']).max() <= 1e-6
 
 

@@ -24,6 +24,8 @@ for s in "$@"; do
     layer) step layer 300 python -m pytest tests -m gpu -q -k layerwise ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 5 --warmup 2 ;;
+    benchnl0) step benchnl0 600 env E3GNN_NODELIN=0 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    benchnl) step benchnl 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     benchq) step bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10 ;;
     benchf) step benchf 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchnofuse) step benchnofuse 600 env E3GNN_BWD_FUSE=0 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
@@ -35,6 +37,8 @@ for s in "$@"; do
     testsn) step testsn 600 env E3GNN_BWD_X=node python -m pytest tests/test_gpu_parity.py -q -x ;;
     bench10k) step bench10k 300 python bench.py --cells 11 --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --profile-only --no-parity-check ;;
+    proftrace) step proftrace 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/proftrace -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
+    highdeg) step highdeg 300 python tools/diag_highdeg.py && step highdeg0 300 env E3GNN_NODELIN=0 python tools/diag_highdeg.py ;;
     proftrain) step proftrain 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_train -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 && mkdir -p gpurun_out/prof_train && cp /tmp/prof_train/*/*stats* /tmp/prof_train/*stats* gpurun_out/prof_train/ 2>/dev/null; ls gpurun_out/prof_train ;;
     traintests) step traintests 400 python -m pytest tests/test_gpu_train.py -x -q --timeout 200 --timeout-method thread ;;
     benchtrain) step benchtrain 300 python bench_train.py --steps 10 --warmup 3 ;;
