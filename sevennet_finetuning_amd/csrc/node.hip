@@ -267,35 +267,50 @@ __global__ void k_gate_fwd(int n, const float* __restrict__ y, float* __restrict
   else v = act_fwd(yr[192 + (c - 320) / 5]) * yr[416 + (c - 320)];
   x[idx] = v;
 }
-__global__ void k_gate_bwd(int n, const float* __restrict__ y, const float* __restrict__ dx,
-                           float* __restrict__ dy) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)n * 576) return;
-  const int64_t i = idx / 576;
-  const int c = (int)(idx - i * 576);
-  const float* yr = y + i * 576;
-  const float* dr = dx + i * 480;
-  float v;
-  if (c < 128) {
-    v = dr[c] * act_grad(yr[c]);
-  } else if (c < 192) {  // gate of 1e channel u
-    const int u = c - 128;
-    float s = 0.f;
+// Gate backward, one wave per node: the y (576) and dE/dx (480) rows staged
+// in LDS with float4 loads, 9 outputs per lane, coalesced stores.
+__global__ __launch_bounds__(256) void k_gate_bwd_rows(int n, const float* __restrict__ y,
+                                                       const float* __restrict__ dx,
+                                                       float* __restrict__ dy) {
+  __shared__ float4 sh[4][(576 + 480) / 4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 4 + w;
+  if (i >= n) return;  // whole wave: no block-level barrier below
+  float4* yr4 = sh[w];
+  float4* dr4 = sh[w] + 576 / 4;
+  const float4* yg = reinterpret_cast<const float4*>(y + (int64_t)i * 576);
+  const float4* dg = reinterpret_cast<const float4*>(dx + (int64_t)i * 480);
+  for (int k = lane; k < 144; k += 64) yr4[k] = yg[k];
+  for (int k = lane; k < 120; k += 64) dr4[k] = dg[k];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const float* yr = reinterpret_cast<const float*>(yr4);
+  const float* dr = reinterpret_cast<const float*>(dr4);
+  float* out = dy + (int64_t)i * 576;
 #pragma unroll
-    for (int m = 0; m < 3; ++m) s += dr[128 + 3 * u + m] * yr[224 + 3 * u + m];
-    v = s * act_grad(yr[c]);
-  } else if (c < 224) {  // gate of 2e channel u
-    const int u = c - 192;
-    float s = 0.f;
+  for (int q = 0; q < 9; ++q) {
+    const int c = lane + 64 * q;
+    float v;
+    if (c < 128) {
+      v = dr[c] * act_grad(yr[c]);
+    } else if (c < 192) {
+      const int u = c - 128;
+      const float s = dr[128 + 3 * u] * yr[224 + 3 * u] + dr[129 + 3 * u] * yr[225 + 3 * u] +
+                      dr[130 + 3 * u] * yr[226 + 3 * u];
+      v = s * act_grad(yr[c]);
+    } else if (c < 224) {
+      const int u = c - 192;
+      float s = 0.f;
 #pragma unroll
-    for (int m = 0; m < 5; ++m) s += dr[320 + 5 * u + m] * yr[416 + 5 * u + m];
-    v = s * act_grad(yr[c]);
-  } else if (c < 416) {
-    v = dr[128 + (c - 224)] * act_fwd(yr[128 + (c - 224) / 3]);
-  } else {
-    v = dr[320 + (c - 416)] * act_fwd(yr[192 + (c - 416) / 5]);
+      for (int m = 0; m < 5; ++m) s += dr[320 + 5 * u + m] * yr[416 + 5 * u + m];
+      v = s * act_grad(yr[c]);
+    } else if (c < 416) {
+      v = dr[128 + (c - 224)] * act_fwd(yr[128 + (c - 224) / 3]);
+    } else {
+      v = dr[320 + (c - 416)] * act_fwd(yr[192 + (c - 416) / 5]);
+    }
+    out[c] = v;
   }
-  dy[idx] = v;
 }
 // last layer: 128 scalars, all activated
 __global__ void k_act_fwd(int64_t n, const float* __restrict__ y, float* __restrict__ x) {
@@ -495,7 +510,8 @@ hipError_t launch_gate_fwd(int n, bool last, const float* y, float* x, hipStream
 hipError_t launch_gate_bwd(int n, bool last, const float* y, const float* dx, float* dy,
                            hipStream_t s) {
   if (last) LAUNCH(k_act_bwd, nblk((int64_t)n * 128), (int64_t)n * 128, y, dx, dy);
-  else LAUNCH(k_gate_bwd, nblk((int64_t)n * 576), n, y, dx, dy);
+  else if (n > 0)
+    hipLaunchKernelGGL(k_gate_bwd_rows, dim3((n + 3) / 4), dim3(256), 0, s, n, y, dx, dy);
   return hipGetLastError();
 }
 hipError_t launch_readout(int n, const float* x, const float* v, const int* type,
