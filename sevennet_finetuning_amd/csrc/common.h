@@ -105,7 +105,7 @@ struct NlProb {
   int a_off, a_off2, c_off, xo_off;
   int K1, K, N, R, nodes;
   int epi, n_act, gate_off;
-  int wn, tpn, rows, tile_begin, tiles_n;  // set by add_nl
+  int wn, ns, tpn, tile_begin, tiles_n;  // set by add_nl
 };
 constexpr int NL_MAX_PROBS = 4;
 struct NlBatch {

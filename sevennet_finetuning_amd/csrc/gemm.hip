@@ -129,49 +129,50 @@ __global__ __launch_bounds__(256) void k_gemm(GemmBatch batch) {
 // self_connection; linear.py:46-49) as node-aligned tiles.  A tile covers
 // T = BM / R whole nodes, so the A operand of one k-step is T contiguous runs
 // of BK * R floats (the node's [mul][m] block) loaded as float4 and scattered
-// k-major into LDS; BK = 32 with a double-buffered LDS stage (one barrier per
+// k-major into LDS; BK = 16 with a double-buffered LDS stage (one barrier per
 // k-step).  Two linears writing the same output block run as one problem with
-// K = K1 + K2 (A switches source at K1), and the gate (equivariant_gate.py:
-// 59-61) is the epilogue: the 0e block writes act(scalars) to the next
-// features, the l > 0 blocks multiply by act(gate) read back from the
-// pre-activation columns the 0e launch stored.  Shapes: BN = 64 / BM = 64
-// (4 waves 2 x 2) or, for N <= 32 (the 2e block), BN = 32 / BM = 128 (4 x 1).
+// K = K1 + K2 (A switches source at K1; separate partial sums), and the gate
+// (equivariant_gate.py:59-61) is the epilogue: the 0e block writes
+// act(scalars) to the next features, the l > 0 blocks multiply by act(gate)
+// read back from the pre-activation columns the 0e launch stored.
+// Shapes (4 waves): WN waves across N, each NS x 32 columns; BM = 128 / WN.
+//   WN = 2, NS = 1: 64 x 64 (default); WN = 1: 128 x 32 (N <= 32, the 2e
+//   block); WN = 2, NS = 2: 64 x 128 (K <= 64 with N >= 128, the transposed
+//   si2 of the l > 0 blocks: half the tiles, A staged once per 128 columns).
 #ifndef E3GNN_NL_BK
 #define E3GNN_NL_BK 16
 #endif
-#ifndef E3GNN_NL_XCD
-#define E3GNN_NL_XCD 0
-#endif
-// occupancy target of k_nodelin (LDS allows 7 workgroups per CU)
+// occupancy target of k_nodelin (LDS allows 6 workgroups per CU)
 #ifndef E3GNN_NL_WAVES
 #define E3GNN_NL_WAVES 5
 #endif
-#ifndef E3GNN_NL_ROWS
-#define E3GNN_NL_ROWS 0
+#ifndef E3GNN_NL_WIDE
+#define E3GNN_NL_WIDE 1
 #endif
 constexpr int NL_BK = E3GNN_NL_BK;
-template <int WN>
+template <int WN, int NS>
 struct NlShape {
-  static constexpr int BN = 32 * WN, BM = 128 / WN;
+  static constexpr int BN = 32 * WN * NS, BM = 128 / WN;
   static constexpr int LDA = BM + 4, LDB = BN + 4;  // 16-byte LDS rows
   static constexpr int A_FLOATS = NL_BK * LDA, STAGE = A_FLOATS + NL_BK * LDB;
 };
-constexpr int NL_LDS = 2 * (NlShape<1>::STAGE > NlShape<2>::STAGE ? NlShape<1>::STAGE
-                                                                   : NlShape<2>::STAGE);
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int NL_LDS =
+    2 * cmax(NlShape<1, 1>::STAGE, cmax(NlShape<2, 1>::STAGE, NlShape<2, 2>::STAGE));
 
-// Epilogue through LDS: each node's output is one contiguous run of BN * R
-// floats, written as float4 (the MFMA layout would scatter 4-byte stores R
-// floats apart).  Starts with a barrier: the caller's LDS readers are done.
+// Epilogue through LDS, one 64- (or 32-) column chunk at a time: each node's
+// output is one contiguous run of CW * R floats, written as float4 (the MFMA
+// layout would scatter 4-byte stores R floats apart).  Starts with a barrier:
+// the caller's LDS readers are done.
 template <int WN, int R>
 __device__ __forceinline__ void nl_epilogue(const NlProb& P, const f32x16& acc, int node0, int n0,
                                             float* lds) {
-  using S = NlShape<WN>;
-  constexpr int BM = S::BM, BN = S::BN;
+  constexpr int BM = 128 / WN, CW = 32 * WN;
   constexpr int T = BM / R, ROWS = T * R;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WN, wc = wave % WN;
   __syncthreads();
-  constexpr int LDC = BN + 1;
+  constexpr int LDC = CW + 1;
   static_assert(ROWS * LDC <= NL_LDS, "C tile must fit the LDS stages");
   float* Cs = lds;
 #pragma unroll
@@ -180,8 +181,9 @@ __device__ __forceinline__ void nl_epilogue(const NlProb& P, const f32x16& acc, 
     if (row < ROWS) Cs[row * LDC + wc * 32 + (lane & 31)] = acc[reg];
   }
   __syncthreads();
-  constexpr int SEGC = BN * R / 4, UC = T * SEGC;
-  const int ncol = P.N - n0 < BN ? P.N - n0 : BN;
+  constexpr int SEGC = CW * R / 4, UC = T * SEGC;
+  const int ncol = P.N - n0 < CW ? P.N - n0 : CW;
+  if (ncol <= 0) return;
 #pragma unroll 1
   for (int u = tid; u < UC; u += 256) {
     const int nl = u / SEGC, j = 4 * (u - nl * SEGC);
@@ -238,12 +240,11 @@ __device__ __forceinline__ void nl_epilogue(const NlProb& P, const f32x16& acc, 
   }
 }
 
-
-template <int WN, int R>
+template <int WN, int NS, int R>
 __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) {
-  using S = NlShape<WN>;
+  using S = NlShape<WN, NS>;
   constexpr int BM = S::BM, BN = S::BN, BK = NL_BK;
-  constexpr int T = BM / R, ROWS = T * R;
+  constexpr int T = BM / R;
   constexpr int SEG4 = BK * R / 4;  // float4 per node per k-step
   constexpr int UA = T * SEG4, NA = (UA + 255) / 256;
   constexpr int UB = BK * BN / 4, NB = (UB + 255) / 256;
@@ -286,8 +287,9 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
       const int u = tid + 256 * i;
       const int k = u / (BN / 4), c = 4 * (u - k * (BN / 4));
       const int gk = k0 + k, col = n0 + c;
-      rb[i] = ((UB % 256 == 0 || u < UB) && gk < P.K && col < P.N) ? *reinterpret_cast<const float4*>(P.B + (int64_t)gk * P.N + col)
-                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      rb[i] = ((UB % 256 == 0 || u < UB) && gk < P.K && col < P.N)
+                  ? *reinterpret_cast<const float4*>(P.B + (int64_t)gk * P.N + col)
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
   auto store = [&](int buf) {
@@ -314,107 +316,58 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
     }
   };
 
-  // two accumulators when K is split: the second linear's sum is formed on
-  // its own and added once at the end (the rounding of two separate GEMMs
-  // summed, not 128 small terms added to a large partial sum)
   const int nk = (P.K + BK - 1) / BK;
-  const int nk1 = P.K > P.K1 ? P.K1 / BK : nk;
-  auto step = [&](int kt, f32x16& c) {
+  const int nk1 = (NS == 1 && P.K > P.K1) ? P.K1 / BK : nk;
+  // wave (wr, wc), sub-tile s: columns s * 32 * WN + wc * 32 + (0..31), so
+  // chunk s of the epilogue is one contiguous 32 * WN column range
+  auto step = [&](int kt, f32x16 (&c)[NS]) {
     if (kt + 1 < nk) load((kt + 1) * BK);
     const float* As = lds + (kt & 1) * S::STAGE;
     const float* Bs = As + S::A_FLOATS;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       const float a = As[(kk + (lane >> 5)) * S::LDA + wr * 32 + (lane & 31)];
-      const float b = Bs[(kk + (lane >> 5)) * S::LDB + wc * 32 + (lane & 31)];
-      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+#pragma unroll
+      for (int sub = 0; sub < NS; ++sub) {
+        const float b = Bs[(kk + (lane >> 5)) * S::LDB + sub * 32 * WN + wc * 32 + (lane & 31)];
+        c[sub] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c[sub], 0, 0, 0);
+      }
     }
     if (kt + 1 < nk) store((kt + 1) & 1);
     __syncthreads();
   };
-  f32x16 acc;
+  f32x16 acc[NS];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int sub = 0; sub < NS; ++sub)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[sub][i] = 0.f;
   load(0);
   store(0);
   __syncthreads();
   for (int kt = 0; kt < nk1; ++kt) step(kt, acc);
-  if (nk1 < nk) {
+  // (wide tiles are only chosen for unsplit K: add_nl)
+  if (NS == 1 && nk1 < nk) {
     // the second linear's sum on its own, added once (the rounding of two
     // GEMMs summed, not its terms added one by one to a large partial sum)
-    f32x16 acc2;
+    f32x16 acc2[NS];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc2[i] = 0.f;
+    for (int sub = 0; sub < NS; ++sub)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc2[sub][i] = 0.f;
     for (int kt = nk1; kt < nk; ++kt) step(kt, acc2);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] += acc2[i];
+    for (int sub = 0; sub < NS; ++sub)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[sub][i] += acc2[sub][i];
   }
-
-  nl_epilogue<WN, R>(P, acc, node0, n0, lds);
+#pragma unroll
+  for (int sub = 0; sub < NS; ++sub) nl_epilogue<WN, R>(P, acc[sub], node0, n0 + sub * 32 * WN, lds);
 }
 
-// Row-block mode for small K (<= 64: the transposed self_interaction_2 of the
-// l > 0 blocks, K = 64 / 32 against N = 384 / 352): one workgroup per row
-// tile walks all N tiles.  Its A operand is staged once and then held in
-// registers (32 rows x K per wave), B comes from L2 straight into the MFMA
-// operand registers; only the epilogue uses LDS per N tile.
-template <int WN, int R>
-__device__ __forceinline__ void nl_rows(const NlProb& P, int tm, float* lds) {
-  using S = NlShape<WN>;
-  constexpr int BM = S::BM, BN = S::BN, T = BM / R;
-  constexpr int KMAX = 64, KS = KMAX / 2, LDA = BM + 4;
-  static_assert(KMAX * LDA <= NL_LDS, "A block must fit the LDS stages");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave / WN, wc = wave % WN;
-  const int node0 = tm * T, K = P.K;
-  const int seg4 = K * R / 4;  // float4 per node (K % 4 == 0)
-#pragma unroll 1
-  for (int u = tid; u < T * seg4; u += 256) {
-    const int nl = u / seg4, j = 4 * (u - nl * seg4);
-    const int node = node0 + nl;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (node < P.nodes) v = *reinterpret_cast<const float4*>(P.A + (int64_t)node * P.lda + P.a_off + j);
-    const float e[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int k = (j + q) / R, m = (j + q) - k * R;
-      lds[k * LDA + nl * R + m] = e[q];
-    }
-  }
-  __syncthreads();
-  float a[KS];
-#pragma unroll
-  for (int i = 0; i < KS; ++i) {
-    const int k = 2 * i + (lane >> 5);
-    a[i] = k < K ? lds[k * LDA + wr * 32 + (lane & 31)] : 0.f;
-  }
-  const int ks = (K + 1) / 2;
-#pragma unroll 1
-  for (int tn = 0; tn < P.tiles_n; ++tn) {
-    const int n0 = tn * BN, col = n0 + wc * 32 + (lane & 31);
-    f32x16 acc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-    for (int i = 0; i < KS; ++i) {
-      if (i < ks) {
-        const int k = 2 * i + (lane >> 5);
-        const float b = (k < K && col < P.N) ? P.B[(int64_t)k * P.N + col] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b, acc, 0, 0, 0);
-      }
-    }
-    nl_epilogue<WN, R>(P, acc, node0, n0, lds);
-  }
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_NL_WAVES, 8))) void k_nodelin(NlBatch batch) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_NL_WAVES, 8))) void
+k_nodelin(NlBatch batch) {
   __shared__ __attribute__((aligned(16))) float lds[NL_LDS];
-  // XCD-aware order (gridDim.x is a multiple of 8): each XCD takes a
-  // contiguous eighth of the tiles, so the N tiles of one row block share
-  // their A rows in one L2
-  const int b = blockIdx.x, per = gridDim.x >> 3;
-  const int tile = E3GNN_NL_XCD ? (b & 7) * per + (b >> 3) : b;
-  if (tile >= batch.total_tiles) return;
+  const int tile = blockIdx.x;
   int pi = 0;
 #pragma unroll 1
   for (int i = 1; i < batch.nprob; ++i)
@@ -423,34 +376,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_NL_WA
   const int local = tile - P.tile_begin;
   if (P.wn == 1) {
     switch (P.R) {
-      case 1: nl_tile<1, 1>(P, local, lds); break;
-      case 3: nl_tile<1, 3>(P, local, lds); break;
-      default: nl_tile<1, 5>(P, local, lds); break;
+      case 1: nl_tile<1, 1, 1>(P, local, lds); break;
+      case 3: nl_tile<1, 1, 3>(P, local, lds); break;
+      default: nl_tile<1, 1, 5>(P, local, lds); break;
+    }
+  } else if (P.ns == 2) {
+    switch (P.R) {
+      case 1: nl_tile<2, 2, 1>(P, local, lds); break;
+      case 3: nl_tile<2, 2, 3>(P, local, lds); break;
+      default: nl_tile<2, 2, 5>(P, local, lds); break;
     }
   } else {
     switch (P.R) {
-      case 1: nl_tile<2, 1>(P, local, lds); break;
-      case 3: nl_tile<2, 3>(P, local, lds); break;
-      default: nl_tile<2, 5>(P, local, lds); break;
+      case 1: nl_tile<2, 1, 1>(P, local, lds); break;
+      case 3: nl_tile<2, 1, 3>(P, local, lds); break;
+      default: nl_tile<2, 1, 5>(P, local, lds); break;
     }
-  }
-}
-// the row-block problems in their own kernel (its A registers would lower the
-// occupancy of k_nodelin)
-__global__ __launch_bounds__(256) void k_nodelin_rows(NlBatch batch) {
-  __shared__ __attribute__((aligned(16))) float lds[NL_LDS];
-  const int tile = blockIdx.x;
-  if (tile >= batch.total_tiles) return;
-  int pi = 0;
-#pragma unroll 1
-  for (int i = 1; i < batch.nprob; ++i)
-    if (tile >= batch.p[i].tile_begin) pi = i;
-  const NlProb& P = batch.p[pi];
-  const int local = tile - P.tile_begin;
-  switch (P.R) {
-    case 1: nl_rows<2, 1>(P, local, lds); break;
-    case 3: nl_rows<2, 3>(P, local, lds); break;
-    default: nl_rows<2, 5>(P, local, lds); break;
   }
 }
 }  // namespace
@@ -473,38 +414,21 @@ bool add_nl(NlBatch& b, const NlProb& p) {
   if (p.K > p.K1 && (!al(p.A2) || p.lda2 % 4 || p.a_off2 % 4 || p.K1 % NL_BK)) return false;
   NlProb q = p;
   q.wn = p.N <= 32 ? 1 : 2;
-  const int BM = 128 / q.wn, BN = 32 * q.wn;
+  q.ns = (E3GNN_NL_WIDE && q.wn == 2 && p.K == p.K1 && p.K <= 64 && p.N >= 128) ? 2 : 1;
+  const int BM = 128 / q.wn, BN = 32 * q.wn * q.ns;
   q.tpn = BM / p.R;
   const int tm = (p.nodes + q.tpn - 1) / q.tpn, tn = (p.N + BN - 1) / BN;
   if (tm <= 0 || tn <= 0) return true;
-  // small K, several N tiles: one workgroup per row tile (nl_rows)
-  q.rows = E3GNN_NL_ROWS && p.K == p.K1 && p.K <= 64 && p.K % 4 == 0 && tn > 1 && q.wn == 2;
   q.tiles_n = tn;
   q.tile_begin = b.total_tiles;
   b.p[b.nprob++] = q;
-  b.total_tiles += q.rows ? tm : tm * tn;
+  b.total_tiles += tm * tn;
   return true;
 }
 
 hipError_t launch_nodelin(const NlBatch& b, hipStream_t s) {
   if (b.total_tiles <= 0) return hipSuccess;
-  // tile-mode and row-block problems as two launches
-  NlBatch t, r;
-  std::memset(&t, 0, sizeof(t));
-  std::memset(&r, 0, sizeof(r));
-  for (int i = 0; i < b.nprob; ++i) {
-    NlProb q = b.p[i];
-    NlBatch& d = q.rows ? r : t;
-    const int tm = (q.nodes + q.tpn - 1) / q.tpn;
-    q.tile_begin = d.total_tiles;
-    d.p[d.nprob++] = q;
-    d.total_tiles += q.rows ? tm : tm * q.tiles_n;
-  }
-  if (t.total_tiles > 0) {
-    const int grid = (t.total_tiles + 7) / 8 * 8;
-    hipLaunchKernelGGL(k_nodelin, dim3(grid), dim3(256), 0, s, t);
-  }
-  if (r.total_tiles > 0) hipLaunchKernelGGL(k_nodelin_rows, dim3(r.total_tiles), dim3(256), 0, s, r);
+  hipLaunchKernelGGL(k_nodelin, dim3(b.total_tiles), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 
