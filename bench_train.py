@@ -108,7 +108,7 @@ def main():
            'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
            'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
            'scheduler_param': {'gamma': 0.99}, 'is_ddp': world > 1, 'device': device,
-           'hip_graph': world == 1 and not args.eager,
+           'hip_graph': not args.eager,
            'continue': {'fisher_information': fisher, 'opt_params': opt, 'ewc_lambda': 1e5}}
     tr = train.Trainer(model, cfg)
     n_b = 4

@@ -440,10 +440,11 @@ class Trainer:
         params = [p for p in self.model.parameters() if p.requires_grad]
         opt = optim_dict[config[OPTIMIZER].lower()]
         optim_param = dict(config.get(OPTIM_PARAM, {}))
-        # HIP_GRAPH (this build): replay the rehearsal step as one captured HIP
-        # graph per batch-shape signature (single process); the optimizer then
-        # keeps its step count and lr on the device
-        self.hip_graph = bool(config.get(HIP_GRAPH, False)) and not self.distributed
+        # HIP_GRAPH (this build): replay the rehearsal step as captured HIP
+        # graphs per batch-shape signature (one graph in a single process; three
+        # segments around the two gradient all-reduces with is_ddp); the
+        # optimizer then keeps its step count and lr on the device
+        self.hip_graph = bool(config.get(HIP_GRAPH, False))
         if self.hip_graph:
             if config[OPTIMIZER].lower() not in ('adam', 'adamw'):
                 raise ValueError('hip_graph supports the adam/adamw optimizers')
@@ -478,10 +479,14 @@ class Trainer:
     def backward(self, loss):
         loss.backward()
         if self.distributed:
-            import torch.distributed as dist
-            g = self.model.flat_grad
-            dist.all_reduce(g)
-            g.div_(self.world)
+            self.all_reduce_grad()
+
+    def all_reduce_grad(self):
+        """DDP's gradient average (one all-reduce of the flat gradient buffer)."""
+        import torch.distributed as dist
+        g = self.model.flat_grad
+        dist.all_reduce(g)
+        g.div_(self.world)
 
     def train_step(self, batch):
         """One optimizer step of Trainer.run_one_epoch (trainer.py:55-68)."""
@@ -577,7 +582,12 @@ class Trainer:
 
 class GraphedRehearsalStep:
     """The rehearsal step as ONE captured HIP graph per batch-shape signature
-    (launch-bound at the reference's batch sizes: ~8k kernels per step).
+    (launch-bound at the reference's batch sizes: ~8k kernels per step).  With
+    is_ddp the step is three graphs sharing one memory pool -- [new batch
+    forward + backward], [optimizer step, memory batch forward + backward],
+    [optimizer step] -- replayed around the two eager gradient all-reduces
+    (trainer.py:174-206 with DDP's averaging), so any backend works and every
+    rank issues the same collectives whether its step is graphed or not.
 
     Per call: the batch tensors are copied into the graph's static inputs, the
     two edge CSRs are rebuilt in place (e3gnn_conv_graph, which also validates
@@ -627,6 +637,9 @@ class GraphedRehearsalStep:
         graphs = (self._graph_of(sb), self._graph_of(sm))
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        # warm-ups are local (no collectives: the other ranks may not be
+        # capturing at this step) and rolled back
+        dist_flag, tr.distributed = tr.distributed, False
         with torch.cuda.stream(side):
             first = not tr.optimizer.state
             if first:   # create the optimizer state, then undo the update
@@ -642,11 +655,27 @@ class GraphedRehearsalStep:
             for _ in range(2):
                 tr._rehearsal_body(sb, sm, graphs)
             self._restore(snap)
+        tr.distributed = dist_flag
         torch.cuda.current_stream().wait_stream(side)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            loss, mloss = tr._rehearsal_body(sb, sm, graphs)
-        return {'g': g, 'b': sb, 'm': sm, 'graphs': graphs, 'out': (loss, mloss)}
+        if not tr.distributed:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                loss, mloss = tr._rehearsal_body(sb, sm, graphs)
+            return {'g': [g], 'b': sb, 'm': sm, 'graphs': graphs, 'out': (loss, mloss)}
+        segs = [torch.cuda.CUDAGraph() for _ in range(3)]
+        with torch.cuda.graph(segs[0]):
+            tr.zero_grad()
+            loss = tr.total_loss(tr.model(sb, graph=graphs[0]))
+            loss.backward()
+        pool = segs[0].pool()
+        with torch.cuda.graph(segs[1], pool=pool):
+            tr.optimizer.step()
+            mloss = tr.total_loss(tr.model(sm, graph=graphs[1]))
+            mloss.backward()
+        with torch.cuda.graph(segs[2], pool=pool):
+            tr.optimizer.step()
+        return {'g': segs, 'b': sb, 'm': sm, 'graphs': graphs,
+                'out': (loss.detach(), mloss.detach())}
 
     @staticmethod
     def _centre_sorted(b):
@@ -678,7 +707,10 @@ class GraphedRehearsalStep:
                     dst[k].copy_(v, non_blocking=True)
         for gr, b in zip(ent['graphs'], (ent['b'], ent['m'])):
             gr.rebuild(b[KEY.EDGE_IDX][0], b[KEY.EDGE_IDX][1])
-        ent['g'].replay()
+        for i, g in enumerate(ent['g']):
+            if i:   # between the segments of a multi-rank step
+                self.tr.all_reduce_grad()
+            g.replay()
         return ent['out'][0].detach().clone(), ent['out'][1].detach().clone()
 
 

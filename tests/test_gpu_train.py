@@ -373,3 +373,31 @@ def test_fused_gate_op_derivatives():
     ref = run(composite, torch.float64, 'cpu')
     for a, b in zip(got, ref):
         assert _rel(a, b) < 2e-6
+
+
+def test_multi_rank_graphed_step_equals_eager(tmp_path):
+    """is_ddp + hip_graph: the rehearsal step as three captured segments
+    replayed around the two gradient all-reduces (train.GraphedRehearsalStep),
+    two gloo ranks on the GPU, equals the eager multi-rank step: same losses
+    on every rank and step, ranks hold identical parameters, and the
+    parameters equal the eager run's up to Adam's per-step sign-flip bound."""
+    import socket
+    import torch.multiprocessing as mp
+    from _train_workers import ddp_rehearsal_worker
+    res = {}
+    for graph in (False, True):
+        with socket.socket() as sk:
+            sk.bind(('127.0.0.1', 0))
+            port = sk.getsockname()[1]
+        out = str(tmp_path / f'ddp_{int(graph)}')
+        mp.spawn(ddp_rehearsal_worker, args=(2, port, graph, out), nprocs=2, join=True)
+        res[graph] = [np.load(out + f'.{r}.npz') for r in range(2)]
+    for r in range(2):
+        le, lg = res[False][r]['losses'], res[True][r]['losses']
+        assert np.all(np.abs(le - lg) <= 1e-5 * np.abs(le)), (r, le, lg)
+        assert int(res[True][r]['n_graphs']) == 1
+    for graph in (False, True):   # DDP: every rank holds the same parameters
+        assert np.array_equal(res[graph][0]['flat'], res[graph][1]['flat'])
+    d = np.abs(res[False][0]['flat'] - res[True][0]['flat'])
+    assert d.max() <= 2 * 1e-5 * 4
+    assert (d > 1e-6).mean() < 1e-3
