@@ -279,6 +279,12 @@ struct e3gnn_ctx {
   // node linears on k_nodelin (node-aligned tiles, si2 + sc in one problem,
   // gate in the epilogue; 1, default) or the grouped k_gemm + k_gate kernels
   // (0; E3GNN_NODELIN=0)
+  // the last block's backward in edge order with the fused dE/dw too (1) or
+  // per neighbour node + a separate dE/dw kernel (0, default; E3GNN_LAST_EDGE=1)
+  int last_edge = [] {
+    const char* v = std::getenv("E3GNN_LAST_EDGE");
+    return (v && std::string(v) == "1") ? 1 : 0;
+  }();
   int nodelin = [] {
     const char* v = std::getenv("E3GNN_NODELIN");
     return (v && std::string(v) == "0") ? 0 : 1;
@@ -1303,7 +1309,7 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
   }
   // per-edge dE/dx + transposed-CSR gather (edge-ordered kernels) or dE/dx
   // written per neighbour node (the last block)
-  const bool gather = !fused || (c->graph_bwd_edge && !last);
+  const bool gather = !fused || (c->graph_bwd_edge && (!last || c->last_edge));
   if (fused) {
     FusedArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -1319,7 +1325,7 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     a.src_perm = c->src_perm.i();
     a.dh = t > 0 ? c->dh.f() : nullptr;
     // the last block (224 message channels) is faster per neighbour node
-    a.edge_order = c->graph_bwd_edge && kind != 2;
+    a.edge_order = c->graph_bwd_edge && (kind != 2 || c->last_edge);
     a.dxc = (a.edge_order && t > 0) ? c->dxc.f() : nullptr;
     // per-centre dE/dx kernel also does dE/dw (first and middle blocks)
     a.fuse_w = a.edge_order && c->bwd_fuse;

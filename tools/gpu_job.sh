@@ -38,6 +38,7 @@ for s in "$@"; do
     bench10k) step bench10k 300 python bench.py --cells 11 --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --profile-only --no-parity-check ;;
     proftrace) step proftrace 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/proftrace -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
+    benchlastedge) step benchlastedge 600 env E3GNN_LAST_EDGE=1 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     bench2gloo) step bench2gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --same-device --no-cpu-baseline ;;
     traingraph) step traingraph 600 python -u -m pytest tests/test_gpu_train.py -x -v --timeout 300 --timeout-method thread -k "graph" ;;
     highdeg) step highdeg 300 python tools/diag_highdeg.py && step highdeg0 300 env E3GNN_NODELIN=0 python tools/diag_highdeg.py ;;
