@@ -137,8 +137,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmBatch batch) {
 // read back from the pre-activation columns the 0e launch stored.
 // Shapes (4 waves): WN waves across N, each NS x 32 columns; BM = 128 / WN.
 //   WN = 2, NS = 1: 64 x 64 (default); WN = 1: 128 x 32 (N <= 32, the 2e
-//   block); WN = 2, NS = 2: 64 x 128 (K <= 64 with N >= 128, the transposed
-//   si2 of the l > 0 blocks: half the tiles, A staged once per 128 columns).
+//   block); WN = 2, NS = 2: 64 x 128 (unsplit K with N >= 128: si1 / si2^T
+//   blocks; half the tiles, A staged once per 128 columns).
 #ifndef E3GNN_NL_BK
 #define E3GNN_NL_BK 16
 #endif
@@ -148,6 +148,9 @@ __global__ __launch_bounds__(256) void k_gemm(GemmBatch batch) {
 #endif
 #ifndef E3GNN_NL_WIDE
 #define E3GNN_NL_WIDE 1
+#endif
+#ifndef E3GNN_NL_WIDE_KMAX
+#define E3GNN_NL_WIDE_KMAX 4096
 #endif
 constexpr int NL_BK = E3GNN_NL_BK;
 template <int WN, int NS>
@@ -414,7 +417,7 @@ bool add_nl(NlBatch& b, const NlProb& p) {
   if (p.K > p.K1 && (!al(p.A2) || p.lda2 % 4 || p.a_off2 % 4 || p.K1 % NL_BK)) return false;
   NlProb q = p;
   q.wn = p.N <= 32 ? 1 : 2;
-  q.ns = (E3GNN_NL_WIDE && q.wn == 2 && p.K == p.K1 && p.K <= 64 && p.N >= 128) ? 2 : 1;
+  q.ns = (E3GNN_NL_WIDE && q.wn == 2 && p.K == p.K1 && p.K <= E3GNN_NL_WIDE_KMAX && p.N >= 128) ? 2 : 1;
   const int BM = 128 / q.wn, BN = 32 * q.wn * q.ns;
   q.tpn = BM / p.R;
   const int tm = (p.nodes + q.tpn - 1) / q.tpn, tn = (p.N + BN - 1) / BN;
