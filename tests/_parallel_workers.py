@@ -23,6 +23,8 @@ def worker(rank, world, port, name, engine, out):
     """Evaluate system `name` decomposed over `world` ranks; rank 0 saves
     the gathered energy / virial / forces / atomic energies to `out`."""
     import torch
+    if engine == 'cpu':  # the ranks share the host's cores (no oversubscription)
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
     dist = _init(rank, world, port)
     from _systems import load_manifest_symbols, system
     from sevennet_finetuning_amd.parallel import (ParallelE3GNN, brick_grid, build_rank_graph,
