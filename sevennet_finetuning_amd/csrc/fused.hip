@@ -85,6 +85,20 @@
 #ifndef E3GNN_BWDX_PIPE
 #define E3GNN_BWDX_PIPE 1
 #endif
+// per-centre dE/dx kernels (MODE 2/3): the tensor-product backward on packed
+// f32 over channel pairs (tp_bwd_xw_pk; 1: all products packed, 2: u_i scalar,
+// no y splat pairs), or scalar (0).  Measured on the 97k box: 25.2 (scalar) vs
+// 26.1 (1) and 25.2 (2) ms per three middle-block launches -- ~18 % fewer VALU
+// instructions buy nothing: the kernel is latency-bound at 2 waves/SIMD, not
+// VALU-issue-bound
+#ifndef E3GNN_BWDX_PK
+#define E3GNN_BWDX_PK 0
+#endif
+// forward tensor product on packed f32 over edge pairs (tp_acc_pk, 1):
+// measured 11.4 -> 12.0 ms per three middle-block launches, so off (0)
+#ifndef E3GNN_FWD_PK
+#define E3GNN_FWD_PK 0
+#endif
 
 namespace e3gnn {
 namespace {
@@ -328,6 +342,30 @@ __device__ __forceinline__ void tp_acc(const float* x, const float* y, float w, 
   for (int k = 0; k < 2 * L3 + 1; ++k) acc[k] += w * t[k];
 }
 
+// tp_acc for two edges at once on packed f32 (v_pk_fma_f32): element 0 / 1 of
+// every pair is edge r = 2h / 2h + 1 of the lane group (E3GNN_FWD_PK)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <int L1, int L2, int L3>
+__device__ __forceinline__ void tp_acc_pk(const f32x2* x, const f32x2* y, f32x2 w, f32x2* acc) {
+  using C = CG<L1, L2, L3>;
+  f32x2 t[2 * L3 + 1];
+#pragma unroll
+  for (int k = 0; k < 2 * L3 + 1; ++k) t[k] = f32x2{0.f, 0.f};
+  sfor<2 * L1 + 1>([&](auto i) {
+    sfor<2 * L2 + 1>([&](auto j) {
+      if constexpr (cg_pair<C, i, j>()) {
+        const f32x2 xy = x[i] * y[j];
+        sfor<C::n>([&](auto q) {
+          if constexpr (C::e[q].i == i && C::e[q].j == j)
+            t[C::e[q].k] = __builtin_elementwise_fma(f32x2{C::e[q].c, C::e[q].c}, xy, t[C::e[q].k]);
+        });
+      }
+    });
+  });
+#pragma unroll
+  for (int k = 0; k < 2 * L3 + 1; ++k) acc[k] = __builtin_elementwise_fma(w, t[k], acc[k]);
+}
+
 template <class L, int I>
 constexpr int iblock_mul() {
   for (int p = 0; p < L::NP; ++p)
@@ -469,6 +507,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
               }
               phase();
               float acc[D3];
+              if constexpr (E3GNN_FWD_PK) {
+                // edge pairs (0, 1), (2, 3) of the lane group on packed f32
+                f32x2 accp[D3];
+#pragma unroll
+                for (int k = 0; k < D3; ++k) accp[k] = f32x2{0.f, 0.f};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                  f32x2 xp[D1], yp[D2];
+#pragma unroll
+                  for (int i = 0; i < D1; ++i) xp[i] = f32x2{x[2 * h][i], x[2 * h + 1][i]};
+#pragma unroll
+                  for (int q = 0; q < D2; ++q)
+                    yp[q] = f32x2{ybuf[(4 * g + 2 * h) * 9 + yoff(p.l2) + q],
+                                  ybuf[(4 * g + 2 * h + 1) * 9 + yoff(p.l2) + q]};
+                  tp_acc_pk<p.l1, p.l2, p.l3>(xp, yp, f32x2{wv[2 * h], wv[2 * h + 1]}, accp);
+                }
+#pragma unroll
+                for (int k = 0; k < D3; ++k) acc[k] = accp[k][0] + accp[k][1];
+              } else {
 #pragma unroll
               for (int k = 0; k < D3; ++k) acc[k] = 0.f;
 #pragma unroll
@@ -477,6 +534,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
 #pragma unroll
                 for (int q = 0; q < D2; ++q) y[q] = ybuf[(4 * g + r) * 9 + yoff(p.l2) + q];
                 tp_acc<p.l1, p.l2, p.l3>(x[r], y, wv[r], acc);  // padded edges have w = 0
+              }
               }
 #pragma unroll
               for (int k = 0; k < D3; ++k) {
@@ -581,6 +639,97 @@ __device__ __forceinline__ float tp_bwd_xw(const float* x, const float* y, float
     dwv += x[i] * ui;
   });
   return dwv;
+}
+
+// first CG entry of pair (I, J); first J of row I with an entry (-1: none)
+template <class C, int I, int J>
+__device__ __forceinline__ constexpr int cg_first_q() {
+  for (int q = 0; q < C::n; ++q)
+    if (C::e[q].i == I && C::e[q].j == J) return q;
+  return -1;
+}
+template <class C, int I, int D2>
+__device__ __forceinline__ constexpr int cg_first_j() {
+  for (int j = 0; j < D2; ++j)
+    for (int q = 0; q < C::n; ++q)
+      if (C::e[q].i == I && C::e[q].j == j) return j;
+  return -1;
+}
+// tp_bwd_xw of a lane's 4 channels on packed f32 (v_pk_fma_f32: two lanes of
+// work per VALU issue): channels (0, 1) and (2, 3) of the lane's block form the
+// pairs h = 0, 1.  The CG contraction t'_ij and the u_i / dE/dY products run
+// packed; the per-(i, channel) dE/dx, dE/dw and w x_i products stay scalar
+// (their operands are not pair-adjacent in the [channel][component] layout).
+// gl: the centre's dE/dagg of the block, [D3][4 channels] (LDS, staged so).
+template <class C, int J, int D1>
+__device__ __forceinline__ constexpr int cg_first_i() {
+  for (int i = 0; i < D1; ++i)
+    for (int q = 0; q < C::n; ++q)
+      if (C::e[q].i == i && C::e[q].j == J) return i;
+  return -1;
+}
+template <int L1, int L2, int L3, bool FW>
+__device__ __forceinline__ void tp_bwd_xw_pk(const float* x, const float* y, const f32x4 w,
+                                             const float* gl, float* dx, float* dy, float* dwr) {
+  using C = CG<L1, L2, L3>;
+  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
+  f32x2 gp[2][D3];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < D3; ++k) gp[h][k] = f32x2{gl[4 * k + 2 * h], gl[4 * k + 2 * h + 1]};
+  f32x2 dyp[D2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dwr[r] = 0.f;
+  sfor<D1>([&](auto i) {
+    constexpr int J0 = cg_first_j<C, i, D2>();
+    if constexpr (J0 >= 0) {
+      f32x2 wx[2], u[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        wx[h] = f32x2{w[2 * h] * x[2 * h * D1 + i], w[2 * h + 1] * x[(2 * h + 1) * D1 + i]};
+      sfor<D2>([&](auto j) {
+        constexpr int Q0 = cg_first_q<C, i, j>();
+        if constexpr (Q0 >= 0) {
+          const f32x2 yj = f32x2{y[j], y[j]};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            f32x2 tp = C::e[Q0].c * gp[h][C::e[Q0].k];
+            sfor<C::n>([&](auto q) {
+              if constexpr (q > Q0 && C::e[q].i == i && C::e[q].j == j)
+                tp = __builtin_elementwise_fma(f32x2{C::e[q].c, C::e[q].c}, gp[h][C::e[q].k], tp);
+            });
+            if constexpr (E3GNN_BWDX_PK == 2) {  // u scalar: no y splat pairs
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                if constexpr (j == J0) u[h][e] = tp[e] * y[j];
+                else u[h][e] += tp[e] * y[j];
+              }
+            } else if constexpr (j == J0) {
+              u[h] = tp * yj;
+            } else {
+              u[h] = __builtin_elementwise_fma(tp, yj, u[h]);
+            }
+            if constexpr (L2 > 0) {
+              if (h == 0 && cg_first_i<C, j, D1>() == (int)i) dyp[j] = tp * wx[h];
+              else dyp[j] = __builtin_elementwise_fma(tp, wx[h], dyp[j]);
+            }
+          }
+        }
+      });
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ur = u[r >> 1][r & 1];
+        dx[r * D1 + i] += w[r] * ur;
+        if constexpr (FW) dwr[r] += x[r * D1 + i] * ur;
+      }
+    }
+  });
+  if constexpr (L2 > 0) {
+    sfor<D2>([&](auto j) {
+      if constexpr (cg_first_i<C, j, D1>() >= 0) dy[j] += dyp[j][0] + dyp[j][1];
+    });
+  }
 }
 
 // sum over the 16 lanes of a DPP row (fixed order; every lane gets the total)
@@ -727,8 +876,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
   if constexpr (CTR) {
     // stage the centre's dE/dagg row: DM / 4 float4 per wave, all in flight
     const float4* src = reinterpret_cast<const float4*>(gagg + (int64_t)jn * L::DM);
-    float4* dst = reinterpret_cast<float4*>(dacc);
-    for (int t = lane; t < L::DM / 4; t += 64) dst[t] = src[t];
+    if constexpr (E3GNN_BWDX_PK && !E3GNN_BWDX_GMPF) {
+      // packed tensor product (tp_bwd_xw_pk): every 4-channel x D3 group of a
+      // path segment stored [component][channel], so the channel pairs (0, 1)
+      // and (2, 3) of a component are aligned register pairs of one b128 read
+      sfor<L::NP>([&](auto pi) {
+        constexpr PathDef p = L::P[pi];
+        constexpr int D3 = 2 * p.l3 + 1, Q = 4 * D3;
+        for (int t4 = lane; t4 < p.mul * D3 / 4; t4 += 64) {
+          const float4 v = src[p.moff / 4 + t4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int t = 4 * t4 + e, quad = t / Q, within = t - quad * Q;
+            const int r = within / D3, k = within - r * D3;
+            dacc[p.moff + quad * Q + 4 * k + r] = v[e];
+          }
+        }
+      });
+    } else {
+      float4* dst = reinterpret_cast<float4*>(dacc);
+      for (int t = lane; t < L::DM / 4; t += 64) dst[t] = src[t];
+    }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
   }
@@ -819,8 +987,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
               phase();
               // dE/dagg of the edges' centres (loaded during the previous block);
               // the next block's are issued now
+              constexpr bool PK = CTR && E3GNN_BWDX_PK && !E3GNN_BWDX_GMPF;
               float gm[4 * D3];
-              if constexpr (E3GNN_BWDX_GMPF) {
+              // PK: the block's 4 D3 values are read from LDS in pair order inside
+              const float* glb = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
+              if constexpr (PK) {
+              } else if constexpr (E3GNN_BWDX_GMPF) {
 #pragma unroll
                 for (int k = 0; k < 4 * D3; ++k) gm[k] = gmN[k];
                 prefetch_gm<L, I, pi>(gmN, Rg, vg, g, jj);
@@ -865,6 +1037,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
                 const int nc = next_block_col<L, I, pi>(jj);
                 if (nc >= 0) load_w2b(wq, R.w2b, lane, nc);
               }
+              if constexpr (PK) {
+                phase();
+                tp_bwd_xw_pk<p.l1, p.l2, p.l3, FW>(x, y + yoff(p.l2), wv, glb, dx, dYa + yoff(p.l2),
+                                                   dwr);
+                pin<4 * D1>(dx);
+                pin<8>(dYa + 1);
+              } else
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 phase();
