@@ -46,6 +46,7 @@ for s in "$@"; do
     traintests) step traintests 400 python -m pytest tests/test_gpu_train.py -x -q --timeout 200 --timeout-method thread ;;
     benchtrain) step benchtrain 300 python bench_train.py --steps 10 --warmup 3 ;;
     benchtrain2) step benchtrain2 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    benchtrainblk) step benchtrainblk 300 env E3GNN_TRAIN_DENSE_LINEAR=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchtraineager) step benchtraineager 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline --eager ;;
     benchd3) step benchd3 300 python bench_d3.py ;;
     profd3) step profd3 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_d3 -o run --output-format csv -- python bench_d3.py --no-cpu-baseline && mkdir -p gpurun_out/prof_d3 && cp /tmp/prof_d3/*/*stats* /tmp/prof_d3/*stats* gpurun_out/prof_d3/ 2>/dev/null; ls gpurun_out/prof_d3 ;;
