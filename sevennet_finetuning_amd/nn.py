@@ -91,8 +91,49 @@ class _Linear:
         # x split points: every input irrep boundary
         self.x_sizes = [t[0] * (2 * t[1] + 1) for t in irreps_in]
 
+    # Dense form (the fine-tune step's default): the block-sparse e3nn weight
+    # scattered ONCE per call into a (dim_in, dim_out) matrix -- W[u, v] * alpha_j
+    # on the (u m, v m) diagonals of each (i, j) block, 0 elsewhere -- so the
+    # linear is ONE GEMM forward and one per derivative product, instead of a
+    # GEMM per output irrep plus the splits, cats and scalings around them and
+    # their backward / double-backward copies.  At the fine-tune batch sizes
+    # (hundreds of atoms) the step is launch-bound, so the FLOPs of the zeros
+    # (~7x on 128x0e+64x1e+32x2e) are free.  Only the nonzeros move: a gather of
+    # the flat weight (each element repeated 2l+1 times) and a scatter to unique
+    # positions -- no index with millions of duplicates (a gather from a zero pad
+    # slot that way faulted inside a captured graph's backward on the GPU).
+    dense = os.environ.get('E3GNN_TRAIN_DENSE_LINEAR', '1') != '0'
+
+    def _dense_maps(self, device, dtype):
+        key = (str(device), dtype)
+        if getattr(self, '_dkey', None) != key:
+            dout = self.out_off[-1]
+            pos, src, scl = [], [], []
+            woff = 0
+            for i, j in self.ins:
+                mi = self.irreps_in[i][0]
+                mo, d = self.irreps_out[j][0], 2 * self.irreps_in[i][1] + 1
+                u, v, m = np.meshgrid(np.arange(mi), np.arange(mo), np.arange(d), indexing='ij')
+                pos.append(((self.in_off[i] + u * d + m) * dout + self.out_off[j] + v * d + m).ravel())
+                src.append((woff + u * mo + v).ravel())
+                scl.append(np.full(u.size, self.alpha[j]))
+                woff += mi * mo
+            self._dpos = torch.as_tensor(np.concatenate(pos), device=device)
+            self._dsrc = torch.as_tensor(np.concatenate(src), device=device)
+            self._dscl = torch.as_tensor(np.concatenate(scl), device=device, dtype=dtype)
+            self._dkey = key
+        return self._dpos, self._dsrc, self._dscl
+
+    def _dense_weight(self, w_flat):
+        pos, src, scl = self._dense_maps(w_flat.device, w_flat.dtype)
+        wd = w_flat.new_zeros(self.in_off[-1] * self.out_off[-1])
+        wd = wd.index_put((pos,), w_flat[src] * scl)
+        return wd.view(self.in_off[-1], self.out_off[-1])
+
     def __call__(self, x, w_flat):
         n = x.shape[0]
+        if self.dense and len(self.x_sizes) > 1:
+            return x @ self._dense_weight(w_flat)
         xs = x.split(self.x_sizes, dim=1) if len(self.x_sizes) > 1 else (x,)
         ws = w_flat.split(self.w_sizes) if len(self.w_sizes) > 1 else (w_flat,)
         parts = []
@@ -196,15 +237,41 @@ def spherical_harmonics(vec, lmax=2, normalize=True):
         u = vec / torch.linalg.norm(vec, dim=-1, keepdim=True)
     else:
         u = vec
-    x, y, z = u[:, 0], u[:, 1], u[:, 2]
-    s3, s5, s15 = math.sqrt(3.0), math.sqrt(5.0), math.sqrt(15.0)
-    parts = [torch.ones_like(x)]
-    if lmax >= 1:
-        parts += [s3 * x, s3 * y, s3 * z]
+    # one constant map from the monomials [1, u, u (x) u] (as a GEMM: the
+    # fine-tune step is launch-bound and this keeps the SH and its first and
+    # second derivatives to a handful of launches instead of ~25 element-wise
+    # nodes per derivative order)
+    feats = [torch.ones_like(u[:, :1]), u]
     if lmax >= 2:
-        parts += [s15 * x * z, s15 * x * y, s5 * (y * y - 0.5 * (x * x + z * z)), s15 * y * z,
-                  0.5 * s15 * (z * z - x * x)]
-    return torch.stack(parts, dim=-1)
+        feats.append((u.unsqueeze(-1) * u.unsqueeze(-2)).reshape(-1, 9))
+    return torch.cat(feats, dim=-1) @ _sh_map(lmax, u.device, u.dtype)
+
+
+_SH_MAPS = {}
+
+
+def _sh_map(lmax, device, dtype):
+    """(1 + 3 + 9, (lmax+1)^2) coefficients of the component-normalised real
+    SH (edge_embedding.py:177-198) on the monomials 1, x, y, z, u_a u_b."""
+    key = (lmax, str(device), dtype)
+    if key not in _SH_MAPS:
+        s3, s5, s15 = math.sqrt(3.0), math.sqrt(5.0), math.sqrt(15.0)
+        nf = 4 if lmax < 2 else 13
+        m = np.zeros((nf, (lmax + 1) ** 2))
+        m[0, 0] = 1.0
+        if lmax >= 1:
+            m[1, 1] = m[2, 2] = m[3, 3] = s3
+        if lmax >= 2:
+            q = lambda a, b: 4 + 3 * a + b   # row of u_a u_b (x, y, z = 0, 1, 2)
+            m[q(0, 2), 4] = s15
+            m[q(0, 1), 5] = s15
+            m[q(1, 1), 6] = s5
+            m[q(0, 0), 6] = m[q(2, 2), 6] = -0.5 * s5
+            m[q(1, 2), 7] = s15
+            m[q(2, 2), 8] = 0.5 * s15
+            m[q(0, 0), 8] = -0.5 * s15
+        _SH_MAPS[key] = torch.as_tensor(m[:, :(lmax + 1) ** 2], device=device, dtype=dtype)
+    return _SH_MAPS[key]
 
 
 class SevenNetTrainable(torch.nn.Module):
@@ -510,15 +577,15 @@ class SevenNetTrainable(torch.nn.Module):
         # ForceStressOutputFromEdge (force_output.py:158-215)
         fij, = torch.autograd.grad([energy.sum()], [vec], create_graph=self.training,
                                    allow_unused=False)
+        # (few launches per derivative order: the fine-tune step is launch-bound)
         src, dst = ei[0], ei[1]
-        force = torch.zeros(n, 3, device=dev, dtype=fij.dtype).index_add(0, src, fij) \
-            - torch.zeros(n, 3, device=dev, dtype=fij.dtype).index_add(0, dst, fij)
+        force = torch.zeros(n, 3, device=dev, dtype=fij.dtype).index_add(
+            0, torch.cat([src, dst]), torch.cat([fij, -fij]))
         out[KEY.PRED_FORCE] = force
-        voigt = torch.cat([vec * fij, (vec[:, 0] * fij[:, 1]).unsqueeze(-1),
-                           (vec[:, 1] * fij[:, 2]).unsqueeze(-1),
-                           (vec[:, 2] * fij[:, 0]).unsqueeze(-1)], dim=-1)
-        s_atom = torch.zeros(n, 6, device=dev, dtype=fij.dtype).index_add(0, dst, voigt)
-        s_graph = torch.zeros(nb, 6, device=dev, dtype=fij.dtype).index_add(0, batch, s_atom)
+        # virial terms xx yy zz xy yz zx = r_a f_b for (a, b) = (x,x) .. (z,x),
+        # summed per graph straight from the edges (graph of the edge's dst atom)
+        voigt = vec.repeat(1, 2) * torch.cat([fij, fij.roll(-1, dims=1)], dim=1)
+        s_graph = torch.zeros(nb, 6, device=dev, dtype=fij.dtype).index_add(0, batch[dst], voigt)
         if KEY.CELL_VOLUME in data:
             vol = data[KEY.CELL_VOLUME].to(dev, self.dtype).view(-1)
             out[KEY.PRED_STRESS] = torch.neg(s_graph) / vol.unsqueeze(-1)
