@@ -484,11 +484,12 @@ class SevenNetTrainable(torch.nn.Module):
             env = 1.0 - (p + 1.0) * (p + 2.0) / 2.0 * x ** p + p * (p + 2.0) * x ** (p + 1) \
                 - p * (p + 1.0) / 2.0 * x ** (p + 2)
             return bessel * env.unsqueeze(-1)
-        ron = self.r_on
-        r2 = r * r
-        env = torch.where(r < ron, torch.ones_like(r),
-                          (rc * rc - r2) ** 2 * (rc * rc + 2 * r2 - 3 * ron * ron)
-                          / (rc * rc - ron * ron) ** 3)
+        # XPLOR switch as ONE polynomial in s = max(r^2, r_on^2): it equals 1 at
+        # s = r_on^2, so the clamp is the r < r_on branch (value and derivatives)
+        # without a where/ones_like pair per derivative order
+        ron, rc2 = self.r_on, rc * rc
+        s = torch.clamp(r * r, min=ron * ron)
+        env = (rc2 - s) ** 2 * (2.0 * s + (rc2 - 3.0 * ron * ron)) * (1.0 / (rc2 - ron * ron) ** 3)
         return bessel * env.unsqueeze(-1)
 
     def self_connection(self, t, blk, x, types):
