@@ -132,7 +132,10 @@ class _Linear:
 
     def __call__(self, x, w_flat):
         n = x.shape[0]
-        if self.dense and len(self.x_sizes) > 1:
+        # (dense only where the expanded matrix stays small: <= 4M entries, and
+        # while the zeros' extra FLOPs are cheap against the launches saved)
+        if self.dense and len(self.x_sizes) > 1 and \
+                self.in_off[-1] * self.out_off[-1] <= (1 << 22) and n <= 65536:
             return x @ self._dense_weight(w_flat)
         xs = x.split(self.x_sizes, dim=1) if len(self.x_sizes) > 1 else (x,)
         ws = w_flat.split(self.w_sizes) if len(self.w_sizes) > 1 else (w_flat,)
