@@ -63,6 +63,12 @@
 #ifndef E3GNN_BWDXW_WAVES
 #define E3GNN_BWDXW_WAVES 2
 #endif
+// ... of the first block (x = 128x0e: 169 VGPRs at 2 waves, one over the
+// 3-wave budget; at 3 waves it spills 18 and measured 3.42 -> 3.34 ms, within
+// box noise of the whole step, so 2)
+#ifndef E3GNN_BWDXW_WAVES_FIRST
+#define E3GNN_BWDXW_WAVES_FIRST 2
+#endif
 // MODE 3 register diet (experiment): W2 bf16 operands loaded at use instead of
 // a block ahead, dH2 operands loaded per hidden block just before its MFMAs --
 // fits 3 waves/SIMD (167 VGPRs) but measured slower (+1.2 ms/step at 3 waves,
@@ -847,7 +853,7 @@ __device__ __forceinline__ void load_w2d(bf16x8 (&a)[3], __amdgpu_buffer_rsrc_t 
 // the 60 per-path-block dE/dagg reads of a middle block become LDS reads
 // instead of dependent global gathers; dE/dx per edge to dxc as in MODE 1.
 template <class L, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ? E3GNN_BWDXW_WAVES : E3GNN_BWDX_WAVES, MODE == 3 ? E3GNN_BWDXW_WAVES : E3GNN_BWDX_WAVES))) void k_conv_bwd_x(const int* __restrict__ src_ptr,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ? (L::DX == 128 ? E3GNN_BWDXW_WAVES_FIRST : E3GNN_BWDXW_WAVES) : E3GNN_BWDX_WAVES, MODE == 3 ? (L::DX == 128 ? E3GNN_BWDXW_WAVES_FIRST : E3GNN_BWDXW_WAVES) : E3GNN_BWDX_WAVES))) void k_conv_bwd_x(const int* __restrict__ src_ptr,
                                                     const int* __restrict__ src_perm,
                                                     const int* __restrict__ center,
                                                     const float* __restrict__ emb,
