@@ -230,9 +230,88 @@ def parity_check_parallel(model, cells_total, grid, rank, device):
             'max_force_err': df, 'ok': bool(de <= 2e-6 and df <= 1e-4)}
 
 
+def distributed_report(drv, rg, world, step_ms, device):
+    """Backend, the world the process group saw, per-rank owned / ghost / edge
+    counts, and the halo exchange against the compute: one extra evaluation
+    with every exchange run serially (ParallelE3GNN.evaluate(timing=...)), so
+    exchange_ms is what the exchanges cost on their own, compute_ms the rest
+    of that evaluation, and overlap = (compute + exchange - overlapped step) /
+    exchange: the share of the exchange time the overlapped step hides."""
+    import torch.distributed as dist
+    tm = {}
+    drv.evaluate(timing=tm)
+    x_ms, tot_ms = tm.get('exchange_s', 0.0) * 1e3, tm['total_s'] * 1e3
+    backend = dist.get_backend()
+    comm_dev = device if backend == 'nccl' else torch.device('cpu')
+    mine = torch.tensor([rg.n_local, rg.n_ghost, len(rg.center), rg.n_interior, x_ms,
+                         tot_ms - x_ms], dtype=torch.float64, device=comm_dev)
+    rows = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(rows, mine)
+    ranks = []
+    for r, v in enumerate(rows):
+        owned, ghost, edges, interior, xr, cr = v.tolist()
+        ranks.append({'rank': r, 'owned': int(owned), 'ghosts': int(ghost), 'edges': int(edges),
+                      'interior': int(interior), 'exchange_ms': round(xr, 3),
+                      'compute_ms': round(cr, 3),
+                      'overlap': round(min(1.0, max(0.0, (cr + xr - step_ms) / xr)), 3)
+                      if xr > 0 else None})
+    info = {'backend': backend, 'world_size': dist.get_world_size(),
+            'exchanges_per_step': tm.get('exchanges', 0),
+            'exchange_ms_max': max(r['exchange_ms'] for r in ranks),
+            'compute_ms_max': max(r['compute_ms'] for r in ranks),
+            'overlap_min': min((r['overlap'] for r in ranks if r['overlap'] is not None),
+                               default=None),
+            'ranks': ranks}
+    if backend == 'nccl':
+        try:
+            info['rccl_version'] = '.'.join(str(v) for v in torch.cuda.nccl.version())
+        except Exception:  # version query unavailable: not part of the measurement
+            pass
+    return info
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, n, port):
+    """The torch.distributed.run command that starts `n` local ranks of this
+    script with the same arguments (one process per GPU)."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+            f'--nproc-per-node={n}', '--master-addr=127.0.0.1', f'--master-port={port}',
+            os.path.abspath(__file__), *argv]
+
+
+def maybe_launch(args, argv):
+    """`python bench.py --gpus N` with no launcher around it: start the N ranks
+    as child processes (before anything touches the GPU in this process) and
+    return their exit code; None when this process is a rank itself."""
+    if args.gpus <= 1 or 'WORLD_SIZE' in os.environ:
+        return None
+    import subprocess
+    cmd = launcher_cmd(argv, args.gpus, free_port())
+    log(f'launching {args.gpus} ranks: {" ".join(cmd)}')
+    return subprocess.call(cmd)
+
+
+def check_world(args, world):
+    """A rank must see exactly the --gpus N world it was asked for."""
+    if world != args.gpus:
+        raise RuntimeError(f'bench.py --gpus {args.gpus} but WORLD_SIZE={world}: '
+                           'run it directly or under torch.distributed.run with '
+                           f'--nproc-per-node {args.gpus}')
+
+
 def main():
     args = parse()
+    rc = maybe_launch(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    check_world(args, world)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if args.same_device:  # rehearsal of the N > 1 path on a one-GPU box (gloo)
@@ -349,6 +428,11 @@ def main():
         roofline['rocprof_kernel'] = rp_name
         roofline['traffic'] = pmc_traffic(rp_name, cells)
 
+    distributed = None
+    if world > 1:
+        distributed = distributed_report(drv, rg, world, ms, device)
+        log(f'distributed: {distributed}')
+
     nl = None
     if world == 1 and not args.profile_only:
         nl = device_nl_timing(box, device)
@@ -375,6 +459,7 @@ def main():
             'roofline': roofline,
             'cpu_baseline': cpu,
             'neighbor_list': nl,
+            'distributed': distributed,
             'kernels': kernels,
         }
         print(json.dumps(line), flush=True)

@@ -79,15 +79,23 @@ def simplify(irreps):
 
 
 def gate_irreps(irreps_out):
-    """EquivariantGate (equivariant_gate.py:48-55): input = scalars (the l = 0
-    irreps of the output), one 0e gate per gated channel, the gated irreps;
-    simplified (the scalars and the gates sort together ahead of the l > 0
-    irreps)."""
+    """EquivariantGate (equivariant_gate.py:30-51) + e3nn Gate: scalars (the
+    l = 0 irreps of the output), one gate scalar per gated channel (parity +1
+    when 0e is among the scalars, else -1, :41), the gated irreps; e3nn's Gate
+    stable-sorts [scalars | gates | gated] by (l, p) and merges neighbours.
+    Returns (irreps_in, scalars, gated, gate parity, offset of every piece in
+    the sorted row)."""
     scal = [(m, l, p) for m, l, p in irreps_out if l == 0]
     gated = [(m, l, p) for m, l, p in irreps_out if l > 0]
     ng = sum(m for m, _, _ in gated)
-    full = scal + ([(ng, 0, 1)] if ng else []) + gated
-    return simplify(full), scal, gated
+    gp = 1 if (0, 1) in [(l, p) for _, l, p in scal] else -1
+    pieces = scal + ([(ng, 0, gp)] if ng else []) + gated
+    order = sorted(range(len(pieces)), key=lambda i: pieces[i][1:])
+    offs, off = [0] * len(pieces), 0
+    for i in order:
+        offs[i] = off
+        off += pieces[i][0] * (2 * pieces[i][1] + 1)
+    return simplify([pieces[i] for i in order]), scal, gated, gp, offs
 
 
 def conv_instructions(irreps_x, lmax_filter, filter_parity, irreps_out):
@@ -185,6 +193,8 @@ class NequIPRef:
         self.cutoff = float(man['cutoff'])
         self.cut = man['cutoff_function']
         self.irreps = [parse_irreps(s) for s in man['irreps_manual']]
+        self.conv_out = [parse_irreps(s) for s in man['conv_irreps_out']] \
+            if 'conv_irreps_out' in man else self.irreps[1:]
         self.nlayer = int(man['num_convolution_layer'])
         self.lmax_edge = int(man.get('lmax_edge', man['lmax']))
         self.filter_parity = -1 if man['is_parity'] else 1
@@ -229,22 +239,22 @@ class NequIPRef:
         return bessel * env.unsqueeze(-1)
 
     def gate(self, y, irreps_out):
-        gin, scal, gated = gate_irreps(irreps_out)
+        _, scal, gated, gp, offs = gate_irreps(irreps_out)
         n = y.shape[0]
-        outs, off = [], 0
-        for m, l, p in scal:
-            outs.append(self.act(self.act_scalar['e' if p == 1 else 'o'], y[:, off:off + m]))
-            off += m
+        outs = []
+        for k, (m, l, p) in enumerate(scal):
+            outs.append(self.act(self.act_scalar['e' if p == 1 else 'o'],
+                                 y[:, offs[k]:offs[k] + m]))
         if gated:
             ng = sum(m for m, _, _ in gated)
-            g = self.act(self.act_gate['e'], y[:, off:off + ng])
-            off += ng
+            o = offs[len(scal)]
+            g = self.act(self.act_gate['e' if gp == 1 else 'o'], y[:, o:o + ng])
             goff = 0
-            for m, l, _ in gated:
+            for k, (m, l, _) in enumerate(gated):
                 d = 2 * l + 1
-                blk = y[:, off:off + m * d].reshape(n, m, d)
+                o = offs[len(scal) + 1 + k]
+                blk = y[:, o:o + m * d].reshape(n, m, d)
                 outs.append((g[:, goff:goff + m].unsqueeze(-1) * blk).reshape(n, -1))
-                off += m * d
                 goff += m
         return torch.cat(outs, dim=1)
 
@@ -291,7 +301,7 @@ class NequIPRef:
             / math.sqrt(self.nsp)
         for t in range(self.nlayer):
             irr_x, irr_out = self.irreps[t], self.irreps[t + 1]
-            gin, _, _ = gate_irreps(irr_out)
+            gin = gate_irreps(irr_out)[0]
             if self.sc_type == 'nequip':
                 sc = fctp_scalar(x, irr_x, onehot, gin,
                                  self.p[f'{t}_self_connection_intro.fc_tensor_product.weight'])
@@ -299,7 +309,9 @@ class NequIPRef:
                 sc = e3nn_linear(x, irr_x, gin, self.p[f'{t}_self_connection_intro.linear.weight'])
             h = e3nn_linear(x, irr_x, irr_x, self.p[f'{t}_self_interaction_1.linear.weight'])
             # edge_index[1] is the gathered source, [0] the target (convolution.py:111-113)
-            agg, mid = self.convolution(t, h, emb, sh, dst, src, irr_x, irr_out)
+            # the convolution's output irreps (model_build.py:303-315); without
+            # the key (sevenn < 0.9 deployments) the block's irreps_manual
+            agg, mid = self.convolution(t, h, emb, sh, dst, src, irr_x, self.conv_out[t])
             y = e3nn_linear(agg, mid, gin, self.p[f'{t}_self_interaction_2.linear.weight']) + sc
             x = self.gate(y, irr_out)
         hid = e3nn_linear(x, self.irreps[-1], [(self.hidden, 0, 1)],

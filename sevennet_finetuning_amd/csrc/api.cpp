@@ -668,6 +668,19 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
   try {
     if (man["model_type"].str() != "E3_equivariant_model")
       throw std::runtime_error("unsupported model_type");
+    // the knobs this engine does not read must hold SevenNet-0's values (the
+    // same predicate as nn.sevennet0_kinds; every other architecture is served
+    // by the runtime-path-table model)
+    if (man.has("sh_normalize") && !man["sh_normalize"].boolean())
+      throw std::runtime_error("raw-vector spherical harmonics (sh_normalize false, sevenn < 0.9) "
+                               "are not SevenNet-0's architecture");
+    if (man.has("is_parity") && man["is_parity"].boolean())
+      throw std::runtime_error("odd-parity filters are not SevenNet-0's architecture");
+    if (man.has("self_connection_type") && man["self_connection_type"].str() != "linear")
+      throw std::runtime_error("self_connection_type " + man["self_connection_type"].str() +
+                               " is not SevenNet-0's (linear)");
+    if (man.has("lmax_edge") && (int)man["lmax_edge"].num() != 2)
+      throw std::runtime_error("lmax_edge must be 2 (SevenNet-0)");
     m->nsp = (int)man["num_species"].num();
     m->cutoff = (float)man["cutoff"].num();
     m->r_on = (float)man["cutoff_function"]["cutoff_on"].num();

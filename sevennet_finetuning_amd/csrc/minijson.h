@@ -24,9 +24,14 @@ struct Value {
     if (it == o.end()) throw std::runtime_error("missing key " + k);
     return it->second;
   }
+  bool has(const std::string& k) const { return kind == OBJ && o.count(k) != 0; }
   double num() const {
     if (kind != NUM) throw std::runtime_error("not a number");
     return n;
+  }
+  bool boolean() const {
+    if (kind != BOOL) throw std::runtime_error("not a boolean");
+    return b;
   }
   const std::string& str() const {
     if (kind != STR) throw std::runtime_error("not a string");

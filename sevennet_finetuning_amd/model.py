@@ -302,9 +302,9 @@ class GenericE3GNNModel:
 def load_model(model_dir=os.path.join(ASSETS, 'sevennet0'), device=None):
     """The engine for a deployment: the native SevenNet-0 engine (E3GNNModel)
     for that architecture, GenericE3GNNModel for the rest of the family."""
+    from .nn import sevennet0_kinds
     with open(os.path.join(model_dir, 'manifest.json')) as f:
         man = json.load(f)
-    if man.get('family', 'sevennet0') == 'sevennet0' and \
-            man.get('self_connection_type', 'linear') == 'linear' and not man.get('is_parity'):
+    if sevennet0_kinds(man) is not None:
         return E3GNNModel(model_dir, device)
     return GenericE3GNNModel(model_dir, device)

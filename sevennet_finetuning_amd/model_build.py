@@ -171,18 +171,10 @@ def resolve_config(config):
 
 
 def _gate_irreps(irreps_out):
-    """EquivariantGate irreps_in (equivariant_gate.py:48-55): scalars, one 0e
-    gate per gated irrep, the gated irreps; merged by (l, p)."""
-    scal = [(m, l, p) for m, l, p in irreps_out if l == 0]
-    gated = [(m, l, p) for m, l, p in irreps_out if l > 0]
-    full = scal + [(m, 0, 1) for m, _, _ in gated] + gated
-    out = []
-    for m, l, p in sorted(full, key=lambda t: (t[1], t[2])):
-        if out and out[-1][1:] == (l, p):
-            out[-1] = (out[-1][0] + m, l, p)
-        else:
-            out.append((m, l, p))
-    return out
+    """EquivariantGate irreps_in (equivariant_gate.py:30-51): nn._gate_irreps
+    (gate parity by the scalars, e3nn's (l, p) sort, equal neighbours merged)."""
+    from .nn import _gate_irreps as gate_irreps
+    return gate_irreps(irreps_out)[0]
 
 
 def _conv_instructions(irreps_x, lmax_filter, parity_filter, irreps_out):
@@ -225,11 +217,24 @@ def model_manifest(cfg):
         tensors.append({'name': name, 'shape': list(shape)})
     add('edge_embedding.basis_function.coeffs', [nb])
     add('onehot_to_feature_x.linear.weight', [_linear_numel([(nsp, 0, 1)], irreps[0])])
+    conv_out = []
     for t in range(L):
         last = t == L - 1
         xin, xout = irreps[t], irreps[t + 1]
         gin = _gate_irreps(xout)
-        ins = _conv_instructions(xin, cfg['_lmax_edge'], parity, xout)
+        # the convolution's output irreps (model_build.py:303-315): the full
+        # tensor product's, l <= lmax_node, scalars 0e only in the last block
+        # -- irreps_manual sets only the block's node irreps; sevenn < 0.9
+        # built the convolution on irreps_manual (config key
+        # '_conv_irreps_manual': True; the 0.8.6 HfO2 example deployment)
+        if cfg.get('_conv_irreps_manual', False):
+            tp_out = xout
+        else:
+            tp_out = infer_irreps_out(xin, cfg['_lmax_edge'], parity,
+                                      0 if last else cfg['_lmax_node'],
+                                      'even' if last else 'full', False)
+        conv_out.append(_irreps_str(tp_out))
+        ins = _conv_instructions(xin, cfg['_lmax_edge'], parity, tp_out)
         mid = {}
         for mul, _, _, l3, p3 in ins:
             mid[(l3, p3)] = mid.get((l3, p3), 0) + mul
@@ -263,7 +268,7 @@ def model_manifest(cfg):
         cutoff_function['cutoff_on'] = float(cf.get('cutoff_on', 4.5))
     elif cname == 'poly_cut':
         cutoff_function['p'] = float(cf.get('poly_cut_p_value', 6))
-    return {
+    man = {
         'format': FORMAT,
         'model_type': 'E3_equivariant_model',
         'source_version': BUILD_VERSION,
@@ -279,13 +284,14 @@ def model_manifest(cfg):
         'channel': int(cfg['channel']),
         'num_convolution_layer': L,
         'irreps_manual': [_irreps_str(ir) for ir in irreps],
+        'conv_irreps_out': conv_out,
         'weight_nn_hidden_neurons': hid,
         'act_radial': 'silu',
         'act_scalar': {'e': 'silu', 'o': 'tanh'}, 'act_gate': {'e': 'silu', 'o': 'tanh'},
         'act_norm': {'silu': SILU_NORM, 'tanh': TANH_NORM},
         'silu_norm': SILU_NORM,
         'sh_normalize': bool(cfg['_normalize_sph']),
-        'family': 'sevennet0' if (sc_type == 'linear' and not cfg['is_parity']) else 'nequip',
+        'lmax_edge': int(cfg['_lmax_edge']),
         'readout_hidden': hidden,
         'self_connection_type': sc_type,
         'conv_denominator': cfg['_conv_denominator'],
@@ -293,6 +299,10 @@ def model_manifest(cfg):
         'num_params': off,
         'tensors': tensors,
     }
+    # the same predicate routes the deployment (model.load_model)
+    from .nn import sevennet0_kinds
+    man['family'] = 'sevennet0' if sevennet0_kinds(man) is not None else 'nequip'
+    return man
 
 
 def _check_kernel_support(man):
@@ -368,17 +378,69 @@ def load_state_dict(model, state_dict, strict=True):
     return missing, unused
 
 
+def _patch_old_config(config):
+    """util.py:130-146, the old-checkpoint fixes: XPLOR configs lose a stray
+    ``poly_cut_p_value``; ``train_avg_num_neigh`` is the old name of
+    ``train_denominator``; ``optimize_by_reduce: False`` checkpoints are
+    refused; a missing ``conv_denominator`` is 0.0 (the trained denominator
+    comes from the state dict); a missing ``_normalize_sph`` means the raw
+    edge vector went into the spherical harmonics (sevenn < 0.9, e.g.
+    SevenNet-0 22May2024 and the 0.8.6 HfO2 example)."""
+    cf = config.get('cutoff_function')
+    if isinstance(cf, dict) and cf.get('cutoff_function_name') == 'XPLOR':
+        cf = dict(cf)
+        cf.pop('poly_cut_p_value', None)
+        config['cutoff_function'] = cf
+    if 'train_denominator' not in config:
+        config['train_denominator'] = config.pop('train_avg_num_neigh', False)
+    if config.pop('optimize_by_reduce', None) is False:
+        raise ValueError('This checkpoint(optimize_by_reduce: False) is no longer supported')
+    if 'conv_denominator' not in config:
+        config['conv_denominator'] = 0.0
+    if '_normalize_sph' not in config:
+        config['_normalize_sph'] = False
+    return config
+
+
+def _map_old_model(state_dict):
+    """util.py:149-183: module names before the reference's 240501 rename
+    ('0 convolution.x' -> '0_convolution.x', 'EdgeEmbedding' ->
+    'edge_embedding', ..., 'denumerator' -> 'denominator')."""
+    names = {'EdgeEmbedding': 'edge_embedding',
+             'reducing nn input to hidden': 'reduce_input_to_hidden',
+             'reducing nn hidden to energy': 'reduce_hidden_to_energy',
+             'rescale atomic energy': 'rescale_atomic_energy'}
+    for i in range(10):
+        for old, new in (('self connection intro', 'self_connection_intro'),
+                         ('convolution', 'convolution'),
+                         ('self interaction 2', 'self_interaction_2'),
+                         ('equivariant gate', 'equivariant_gate')):
+            names[f'{i} {old}'] = f'{i}_{new}'
+    out = {}
+    for k, v in state_dict.items():
+        head, _, rest = k.partition('.')
+        rest = rest.replace('denumerator', 'denominator')
+        out[f'{names[head]}.{rest}' if head in names else k] = v
+    return out
+
+
 def model_from_checkpoint(checkpoint, device='cuda'):
     """util.py:186-231: ``{'model_state_dict': ..., 'config': ...}`` (or the
-    path of one, read weights-only) -> (model, config)."""
+    path of one, read weights-only) -> (model, config).  Old configs are
+    patched first (``_patch_old_config``) and old module names mapped when
+    keys are missing (``_map_old_model``), as the reference does."""
     if isinstance(checkpoint, str):
         checkpoint = torch.load(checkpoint, map_location='cpu', weights_only=True)
     elif not isinstance(checkpoint, dict):
         raise ValueError('checkpoint must be either str or dict')
     config = {k: (v.cpu().tolist() if torch.is_tensor(v) else v)
               for k, v in checkpoint['config'].items()}
+    config = _patch_old_config(config)
     model = build_E3_equivariant_model(config, device=device)
-    missing, _ = load_state_dict(model, checkpoint['model_state_dict'], strict=False)
+    sd = checkpoint['model_state_dict']
+    missing, _ = load_state_dict(model, sd, strict=False)
+    if missing:
+        missing, _ = load_state_dict(model, _map_old_model(sd), strict=False)
     assert len(missing) == 0, f'Missing keys: {missing}'
     return model, model.config
 
@@ -387,7 +449,12 @@ def checkpoint_of(model):
     """The reference checkpoint layout of a model: state dict + config."""
     sd = {n: model.flat[o:o + k].detach().cpu().clone().view(shape)
           for n, (o, k, shape) in model.slices.items()}
-    cfg = {k: v for k, v in getattr(model, 'config', {}).items() if not k.startswith('_')}
+    # the user-level keys, '_normalize_sph' included (model_from_checkpoint
+    # reads its absence as a pre-0.9 checkpoint); the keys resolve_config
+    # derives are recomputed on load
+    derived = ('_irreps', '_lmax_edge', '_lmax_node', '_conv_denominator')
+    cfg = {k: v for k, v in getattr(model, 'config', {}).items()
+           if (not k.startswith('_') or k == '_normalize_sph') and k not in derived}
     if not cfg:
         raise ValueError('model has no config (build it with build_E3_equivariant_model)')
     return {'model_state_dict': sd, 'config': cfg}

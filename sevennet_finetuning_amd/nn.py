@@ -178,22 +178,32 @@ class _Linear:
 
 
 def _gate_irreps(irreps_out):
-    """e3nn Gate.irreps_in for EquivariantGate (equivariant_gate.py:48-55):
-    [scalars (the l = 0 output irreps, in order) | one 0e gate per gated
-    channel | gated irreps], equal neighbours merged (the scalars and gates
-    sort ahead of every l > 0 irrep, odd before even)."""
+    """e3nn Gate.irreps_in for EquivariantGate (equivariant_gate.py:30-51):
+    scalars = the l = 0 output irreps, gated = the rest (both in order), one
+    gate scalar per gated channel of parity +1 when '0e' is among the scalars,
+    else -1 (:41); e3nn's Gate stable-sorts [scalars | gates | gated] by
+    (l, p) (odd first) and merges equal neighbours.  Returns (irreps_in,
+    scalars, gated, layout) with layout = (gate parity, the offset of every
+    piece -- each scalar irrep, the gate block, each gated irrep -- in the
+    sorted row, and whether that is the unsorted order)."""
     scal = [t for t in irreps_out if t[1] == 0]
     gated = [t for t in irreps_out if t[1] > 0]
     ng = sum(t[0] for t in gated)
-    full = scal + ([(ng, 0, 1)] if ng else []) + gated
+    gate_p = 1 if any(_ir(t) == (0, 1) for t in scal) else -1
+    pieces = scal + ([(ng, 0, gate_p)] if ng else []) + gated
+    order = sorted(range(len(pieces)), key=lambda i: _ir(pieces[i]))   # stable
+    offs, off = [0] * len(pieces), 0
+    for i in order:
+        offs[i] = off
+        off += pieces[i][0] * (2 * pieces[i][1] + 1)
     simp = []
-    for t in full:
-        m, (l, p) = t[0], _ir(t)
+    for i in order:
+        m, (l, p) = pieces[i][0], _ir(pieces[i])
         if simp and _ir(simp[-1]) == (l, p):
             simp[-1] = (simp[-1][0] + m, l, p)
         else:
             simp.append((m, l, p))
-    return simp, scal, gated
+    return simp, scal, gated, (gate_p, offs, order == list(range(len(pieces))))
 
 
 def conv_instructions(irreps_x, lmax_filter, filter_parity, irreps_out):
@@ -275,6 +285,38 @@ def _sh_map(lmax, device, dtype):
             m[q(0, 0), 8] = -0.5 * s15
         _SH_MAPS[key] = torch.as_tensor(m[:, :(lmax + 1) ** 2], device=device, dtype=dtype)
     return _SH_MAPS[key]
+
+
+def sevennet0_kinds(manifest, conv_only=False):
+    """THE test for SevenNet-0's architecture, shared by every router
+    (model.load_model and model_build's family label; e3gnn_load checks the
+    same knobs): even-parity lmax-2 filters on normalised edge vectors, the
+    XPLOR cutoff, a linear self-connection and exactly
+    128x0e -> 4 x (128x0e+64x1e+32x2e) -> 128x0e.  Returns the kernel kind of
+    every block (0 first, 1 middle, 2 last; csrc/tp.h) or None.
+    ``conv_only``: only what the convolution kernels depend on (filter parity,
+    lmax_edge, irreps) -- the trainable model computes the edge basis, SH and
+    self-connection itself and needs no more for its kernel choice."""
+    man = manifest
+    if man.get('is_parity', False) or int(man.get('lmax_edge', man.get('lmax', 2))) != 2:
+        return None
+    cf = man.get('cutoff_function', {}) or {}
+    if not conv_only and (not bool(man.get('sh_normalize', True)) or
+                          man.get('self_connection_type', 'linear') != 'linear' or
+                          cf.get('name', 'XPLOR') != 'XPLOR'):
+        return None
+    irreps = [parse_irreps(s) for s in man['irreps_manual']]
+    L = int(man['num_convolution_layer'])
+    if len(irreps) != L + 1 or L < 2:
+        return None
+    kinds = [0 if t == 0 else (2 if t == L - 1 else 1) for t in range(L)]
+    want = {0: ([(128, 0, 1)], [(128, 0, 1), (64, 1, 1), (32, 2, 1)]),
+            1: ([(128, 0, 1), (64, 1, 1), (32, 2, 1)],) * 2,
+            2: ([(128, 0, 1), (64, 1, 1), (32, 2, 1)], [(128, 0, 1)])}
+    for t, k in enumerate(kinds):
+        if (irreps[t], irreps[t + 1]) != want[k]:
+            return None
+    return kinds
 
 
 class SevenNetTrainable(torch.nn.Module):
@@ -383,29 +425,25 @@ class SevenNetTrainable(torch.nn.Module):
     def _sevennet0_kinds(self):
         """The SevenNet-0 kernel kinds (csrc/tp.h) of the blocks, or None when
         the architecture is another member of the family."""
-        if self.filter_parity != 1 or self.lmax_edge != 2 or not self.sh_normalize or \
-                self.sc_type != 'linear':
-            return None
-        kinds = [0 if t == 0 else (2 if t == self.nlayer - 1 else 1) for t in range(self.nlayer)]
-        want = {0: ([(128, 0, 1)], [(128, 0, 1), (64, 1, 1), (32, 2, 1)]),
-                1: ([(128, 0, 1), (64, 1, 1), (32, 2, 1)],) * 2,
-                2: ([(128, 0, 1), (64, 1, 1), (32, 2, 1)], [(128, 0, 1)])}
-        for t, k in enumerate(kinds):
-            if (self.irreps[t], self.irreps[t + 1]) != want[k]:
-                return None
-        return kinds
+        return sevennet0_kinds(self.manifest, conv_only=True)
 
     def _build_layers(self):
         irr = self.irreps
+        # the convolution's output irreps per block (model_build: the
+        # reference's irreps_out_tp); deployments without the key (SevenNet-0,
+        # the 0.8.6 HfO2 example) built it on irreps_manual
+        conv_out = [parse_irreps(s) for s in self.manifest['conv_irreps_out']] \
+            if 'conv_irreps_out' in self.manifest else irr[1:]
         self.blocks = []
         tables = []
         for t in range(self.nlayer):
             x_ir, out_ir = irr[t], irr[t + 1]
-            gin, scal, gated = _gate_irreps(out_ir)
-            table, mid = path_table(x_ir, self.lmax_edge, self.filter_parity, out_ir)
+            gate_irreps = _gate_irreps(out_ir)
+            gin = gate_irreps[0]
+            table, mid = path_table(x_ir, self.lmax_edge, self.filter_parity, conv_out[t])
             tables.append(table)
             self.blocks.append({
-                'kind': t, 'gate': (gin, scal, gated), 'sc_irreps': (x_ir, gin),
+                'kind': t, 'gate': gate_irreps, 'sc_irreps': (x_ir, gin),
                 'sc': _Linear(x_ir, gin), 'si1': _Linear(x_ir, x_ir), 'si2': _Linear(mid, gin)})
         kinds = self._sevennet0_kinds()
         be = self.conv_backend
@@ -448,13 +486,14 @@ class SevenNetTrainable(torch.nn.Module):
     def gate(self, x, gate_irreps):
         # e3nn nn.Gate (equivariant_gate.py:59-61); split, not sliced (one cat
         # in the backward instead of a zero-fill + copy per slice).  Odd
-        # scalars take tanh (act_scalar 'o'), everything else scaled SiLU.
-        _, scal, gated = gate_irreps
+        # scalars and odd gates take tanh (act 'o'), the rest scaled SiLU.
+        _, scal, gated, (gate_p, offs, natural) = gate_irreps
         n = x.shape[0]
         ns = sum(t[0] for t in scal)
         ng = sum(t[0] for t in gated)
-        odd = any(_ir(t)[1] == -1 for t in scal)
-        if ng > 0 and not odd and x.is_cuda and x.dtype == torch.float32 and len(gated) <= 2:
+        odd = any(_ir(t)[1] == -1 for t in scal) or gate_p == -1
+        if natural and ng > 0 and not odd and x.is_cuda and x.dtype == torch.float32 and \
+                len(gated) <= 2:
             key = id(gate_irreps)
             if key not in self._gate_dims:
                 self._gate_dims[key] = conv_ops.gate_dims([t[:2] for t in scal],
@@ -462,15 +501,19 @@ class SevenNetTrainable(torch.nn.Module):
             return conv_ops.gate(x, self._gate_dims[key], self.silu_norm, self._act_lib())
         sizes = [t[0] for t in scal] + ([ng] if ng else []) + \
             [t[0] * (2 * t[1] + 1) for t in gated]
-        pieces = x.split(sizes, dim=1) if len(sizes) > 1 else (x[:, :ns],)
+        if natural:
+            pieces = x.split(sizes, dim=1) if len(sizes) > 1 else (x[:, :sizes[0]],)
+        else:   # the row is e3nn's (l, p)-sorted layout: each piece at its offset
+            pieces = [x[:, o:o + w] for o, w in zip(offs, sizes)]
+        act_o = lambda v: torch.tanh(v) * self.tanh_norm   # noqa: E731
         outs = []
         for k, t in enumerate(scal):
-            outs.append(self.act(pieces[k]) if _ir(t)[1] == 1
-                        else torch.tanh(pieces[k]) * self.tanh_norm)
+            outs.append(self.act(pieces[k]) if _ir(t)[1] == 1 else act_o(pieces[k]))
         if ng:
-            gs = self.act(pieces[len(scal)]).split([t[0] for t in gated], dim=1)
+            g = pieces[len(scal)]
+            gs = (self.act(g) if gate_p == 1 else act_o(g)).split([t[0] for t in gated], dim=1)
             for k, t in enumerate(gated):
-                blk = pieces[len(scal) + 1 + k].view(n, t[0], 2 * t[1] + 1)
+                blk = pieces[len(scal) + 1 + k].reshape(n, t[0], 2 * t[1] + 1)
                 outs.append((gs[k].unsqueeze(-1) * blk).reshape(n, -1))
         return torch.cat(outs, dim=1) if len(outs) > 1 else outs[0]
 

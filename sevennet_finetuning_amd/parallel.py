@@ -38,6 +38,7 @@ The per-rank compute is an *engine* with the segment interface of
 include/e3gnn.h (``HipSegmentEngine`` wraps libe3gnn_hip.so; tests plug in a
 CPU engine built on the oracle to check the decomposition itself).
 """
+import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -367,14 +368,39 @@ class ParallelE3GNN:
             return self.eng.device
         return 'cpu'
 
-    def evaluate(self):
+    def _sync(self):
+        if torch.device(self.eng.device).type == 'cuda':
+            torch.cuda.synchronize(self.eng.device)
+
+    def _exchange(self, start, finish, kind, t, timing):
+        """Start an exchange (overlapped: the caller finishes it later).  With
+        ``timing`` (a dict) the exchange instead runs to completion on its own,
+        ranks aligned by a barrier and the device synchronised around it, and
+        its wall time is added to timing['exchange_s']."""
+        if timing is None:
+            return start(kind, t)
+        self._sync()
+        if dist.is_initialized() and self.rg.world > 1:
+            dist.barrier(group=self.group)
+        t0 = time.perf_counter()
+        finish(start(kind, t))
+        self._sync()
+        timing['exchange_s'] = timing.get('exchange_s', 0.0) + time.perf_counter() - t0
+        timing['exchanges'] = timing.get('exchanges', 0) + 1
+        return None
+
+    def evaluate(self, timing=None):
+        """One evaluation.  ``timing``: a dict to fill with the wall time of
+        the halo exchanges run serially (no overlap; see ``_exchange``) and of
+        the whole evaluation, so compute = total - exchange."""
         eng, halo, L = self.eng, self.halo, self.eng.num_layers
+        t_begin = time.perf_counter()
         eng.graph_set()
         for t in range(L):
             if t > 0:
                 # forward_comm of the layer-t features, overlapped with the
                 # owned rows' work (interior centres)
-                h = halo.forward_start('x', t)
+                h = self._exchange(halo.forward_start, halo.forward_finish, 'x', t, timing)
                 eng.layer_forward_part(t, 0)
                 halo.forward_finish(h)
                 eng.layer_forward_part(t, 1)
@@ -386,13 +412,15 @@ class ParallelE3GNN:
                 # ghost rows of dE/dx first, their reverse_comm overlapped with
                 # the interior centres and owned rows
                 eng.layer_backward_part(t, 0)
-                h = halo.reverse_start('grad', t)
+                h = self._exchange(halo.reverse_start, halo.reverse_finish, 'grad', t, timing)
                 eng.layer_backward_part(t, 1)
                 halo.reverse_finish(h)
             else:
                 eng.layer_backward(t)
         forces, vir = eng.forces()
-        halo.reverse('force', 0)              # ghost forces -> owners (newton on)
+        # ghost forces -> owners (newton on)
+        halo.reverse_finish(self._exchange(halo.reverse_start, halo.reverse_finish, 'force', 0,
+                                           timing))
         tot = torch.cat([e_local.reshape(1), vir.reshape(6)]).to(torch.float64)
         if dist.is_initialized() and self.rg.world > 1:
             if self._comm_device() == 'cpu' and tot.device.type != 'cpu':
@@ -401,6 +429,9 @@ class ParallelE3GNN:
                 tot = h.to(tot.device)
             else:
                 dist.all_reduce(tot, group=self.group)
+        if timing is not None:
+            self._sync()
+            timing['total_s'] = time.perf_counter() - t_begin
         nl = self.rg.n_local
         return {'energy': tot[0], 'virial': tot[1:7], 'forces': forces[:nl],
                 'atomic_energy': atomic, 'owned': self.rg.owned}

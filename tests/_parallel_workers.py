@@ -45,15 +45,20 @@ def worker(rank, world, port, name, engine, out):
     # once (set_graph), every evaluation gives the same result
     res = drv.evaluate()
     first = (float(res['energy']), res['forces'].detach().cpu().clone())
-    for _ in range(2):
-        res = drv.evaluate()
+    # the bench's serial-exchange timing pass gives the same result too
+    tm = {}
+    res = drv.evaluate(timing=tm)
     same = first[0] == float(res['energy']) and torch.equal(first[1], res['forces'].detach().cpu())
+    timed_ok = tm.get('exchanges') == 9 and 0 < tm['exchange_s'] < tm['total_s']
+    res = drv.evaluate()
+    same = same and first[0] == float(res['energy']) and torch.equal(first[1],
+                                                                     res['forces'].detach().cpu())
     uploads = getattr(eng, 'uploads', -1)
     f, ea = gather_all(res, len(pos))
     if rank == 0:
         np.savez(out, energy=float(res['energy']), virial=res['virial'].cpu().numpy(),
                  forces=f.numpy(), atomic=ea.numpy(), repeat_same=np.array([same]),
-                 uploads=np.array([uploads]),
+                 uploads=np.array([uploads]), timed_ok=np.array([timed_ok]),
                  n_ghost=np.array([rg.n_ghost]), n_local=np.array([rg.n_local]))
     dist.barrier()
     dist.destroy_process_group()

@@ -148,10 +148,124 @@ def test_hfo2_example_config_builds_the_exported_parameter_table():
         'chemical_species': 'Hf O', 'cutoff': 4.0, 'channel': 4, 'lmax': 1, 'is_parity': True,
         'num_convolution_layer': 4, 'irreps_manual': ref['irreps_manual'],
         'self_connection_type': 'nequip', 'conv_denominator': ref['conv_denominator'][0],
-        '_normalize_sph': False,
+        '_normalize_sph': False, '_conv_irreps_manual': True,   # sevenn 0.8.6
         'cutoff_function': {'cutoff_function_name': 'poly_cut', 'poly_cut_p_value': 6}})
     man = mb.model_manifest(cfg)
     assert [(t['name'], t['numel']) for t in man['tensors']] == \
         [(t['name'], t['numel']) for t in ref['tensors']]
     assert man['family'] == 'nequip' and man['sh_normalize'] is False
     assert man['readout_hidden'] == ref['readout_hidden']
+
+
+def test_old_checkpoint_config_is_patched():
+    """util.py:130-146: a config without ``_normalize_sph`` is a pre-0.9
+    checkpoint (raw-vector SH); the old denominator key is renamed; XPLOR
+    loses a stray p value; optimize_by_reduce False is refused."""
+    c = ft_config()
+    c.pop('train_denominator')
+    c['train_avg_num_neigh'] = True
+    c['cutoff_function'] = dict(c['cutoff_function'], poly_cut_p_value=6)
+    p = mb._patch_old_config(dict(c))
+    assert p['_normalize_sph'] is False and p['train_denominator'] is True
+    assert 'train_avg_num_neigh' not in p and 'poly_cut_p_value' not in p['cutoff_function']
+    man = mb.model_manifest(mb.resolve_config(p))
+    assert man['sh_normalize'] is False
+    # not SevenNet-0's architecture any more: routed to the family model
+    assert man['family'] == 'nequip'
+    from sevennet_finetuning_amd.nn import sevennet0_kinds
+    assert sevennet0_kinds(man) is None and sevennet0_kinds(man, conv_only=True) is not None
+    c2 = ft_config()
+    c2.pop('conv_denominator')
+    assert mb._patch_old_config(c2)['conv_denominator'] == 0.0
+    with pytest.raises(ValueError, match='optimize_by_reduce'):
+        mb._patch_old_config(dict(ft_config(), optimize_by_reduce=False))
+    # a current config keeps its value
+    assert mb._patch_old_config(dict(ft_config(), _normalize_sph=True))['_normalize_sph'] is True
+
+
+def test_old_module_names_are_mapped():
+    sd = {'EdgeEmbedding.basis_function.coeffs': 1, '3 convolution.denumerator': 2,
+          '0 self connection intro.linear.weight': 3, '4 self interaction 2.linear.weight': 4,
+          'reducing nn hidden to energy.linear.weight': 5, '1_self_interaction_1.linear.weight': 6}
+    assert mb._map_old_model(sd) == {
+        'edge_embedding.basis_function.coeffs': 1, '3_convolution.denominator': 2,
+        '0_self_connection_intro.linear.weight': 3, '4_self_interaction_2.linear.weight': 4,
+        'reduce_hidden_to_energy.linear.weight': 5, '1_self_interaction_1.linear.weight': 6}
+
+
+def test_checkpoint_keeps_normalize_sph_and_loads_old_names(monkeypatch):
+    """checkpoint_of keeps ``_normalize_sph`` (else reloading would patch it to
+    False); model_from_checkpoint maps old module names when keys are missing."""
+    m = _build_cpu(2)
+    ck = mb.checkpoint_of(m)
+    assert ck['config']['_normalize_sph'] is True
+    built = {}
+
+    def fake_build(config, device='cuda', **kw):
+        built['cfg'] = config
+        return _build_cpu(5)
+    monkeypatch.setattr(mb, 'build_E3_equivariant_model', fake_build)
+    old = {}
+    for k, v in ck['model_state_dict'].items():
+        head, _, rest = k.partition('.')
+        if head.endswith('_convolution'):
+            head = head.replace('_convolution', ' convolution')
+        if rest == 'denominator':
+            rest = 'denumerator'
+        old[f'{head}.{rest}'] = v
+    m2, _ = mb.model_from_checkpoint({'model_state_dict': old, 'config': ck['config']},
+                                     device='cpu')
+    assert built['cfg']['_normalize_sph'] is True
+    assert torch.equal(m2.flat, m.flat)
+
+
+def test_routing_uses_one_predicate():
+    """model.load_model, model_build's family label and the trainable
+    model's kernel choice agree (nn.sevennet0_kinds)."""
+    from sevennet_finetuning_amd.nn import sevennet0_kinds
+    assert sevennet0_kinds(MAN) == [0, 1, 1, 1, 2]
+    for change in ({'sh_normalize': False}, {'is_parity': True},
+                   {'self_connection_type': 'nequip'}, {'lmax_edge': 1},
+                   {'cutoff_function': {'name': 'poly_cut', 'p': 6.0}}):
+        man = dict(MAN, **change)
+        assert sevennet0_kinds(man) is None, change
+    man = mb.model_manifest(mb.resolve_config(dict(ft_config(), _normalize_sph=True)))
+    assert man['family'] == 'sevennet0' and man['lmax_edge'] == 2
+
+
+def test_convolution_irreps_follow_the_current_reference():
+    """model_build.py:303-315: with irreps_manual the convolution's outputs are
+    still infer_irreps_out(x, filter, lmax_node, 'full'), and only 0e in the
+    last block; the sevenn < 0.9 behaviour (outputs = irreps_manual) is the
+    explicit legacy key.  The HfO2 example's config shows the difference in
+    its last block (full irreps there): 10 paths x 4 = 40 radial weights
+    legacy, the paths into 0e only now."""
+    ref = json.load(open(os.path.join(ROOT, 'sevennet_finetuning_amd', 'assets', 'hfo2_example',
+                                      'manifest.json')))
+    base = {'chemical_species': 'Hf O', 'cutoff': 4.0, 'channel': 4, 'lmax': 1,
+            'is_parity': True, 'num_convolution_layer': 4, 'irreps_manual': ref['irreps_manual'],
+            'self_connection_type': 'nequip', 'conv_denominator': 5.0, '_normalize_sph': False,
+            'cutoff_function': {'cutoff_function_name': 'poly_cut'}}
+    legacy = mb.model_manifest(mb.resolve_config(dict(base, _conv_irreps_manual=True)))
+    now = mb.model_manifest(mb.resolve_config(base))
+    w = lambda m: {t['name']: t['shape'] for t in m['tensors']}['3_convolution.weight_nn.layer2.weight']
+    assert w(legacy) == [64, 40]
+    # last block x = 4x0o+4x0e+4x1o+4x1e, filter 0e+1o: 0e from 0e x 0e and
+    # 1o x 1o (1e x 1o gives 0o, 0o x 0e gives 0o)
+    assert now['conv_irreps_out'][-1] == '8x0e' and w(now) == [64, 8]
+    # middle blocks: every (l <= 1) output of the full product
+    assert legacy['conv_irreps_out'][:3] == ref['irreps_manual'][1:4]
+    assert [mb._parse(s) for s in now['conv_irreps_out'][:3]] == [
+        mb.infer_irreps_out(mb._parse(ref['irreps_manual'][t]), 1, -1, 1, 'full', False)
+        for t in range(3)]
+    # and the trainable model builds and runs either way (CPU double)
+    from _conv_cpu import GenericCpuConvBackend
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    for man, cfg in ((legacy, dict(base, _conv_irreps_manual=True)), (now, base)):
+        r = mb.resolve_config(cfg)
+        m = SevenNetTrainable(device='cpu', conv_backend=GenericCpuConvBackend(), manifest=man,
+                              weights=mb.init_weights(man, r, 0))
+        si2 = m.blocks[-1]['si2']
+        assert {(l, p) for _, l, p in si2.irreps_in} == \
+            {(l, p) for _, l, p in mb._parse(man['conv_irreps_out'][-1])}
+        assert si2.numel == m.slices['3_self_interaction_2.linear.weight'][1]

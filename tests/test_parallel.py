@@ -95,6 +95,7 @@ def test_decomposed_matches_single_process_oracle(world, name, tmp_path):
     assert got['n_ghost'][0] > 0
     # three evaluations of one neighbour list: one upload, identical results
     assert got['uploads'][0] == 1 and got['repeat_same'][0]
+    assert got['timed_ok'][0]   # serial-exchange timing pass: 9 exchanges, same result
     vol = abs(np.linalg.det(cell))
     assert abs(got['energy'] - ref['energy']) <= 1e-10 * abs(ref['energy'])
     assert np.abs(got['forces'] - ref['forces']).max() < 1e-9
