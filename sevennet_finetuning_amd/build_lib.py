@@ -72,7 +72,9 @@ def build(force=False, verbose=False, out=None, defines=()):
 NATIVE = os.path.join(os.path.dirname(HERE), 'native')
 
 
-NATIVE_HOSTS = ('e3gnn_md', 'e3gnn_md_parallel')
+NATIVE_HOSTS = ('e3gnn_md', 'e3gnn_md_parallel', 'e3gnn_pair_check')
+# extra translation units of a host (the LAMMPS pair-style core)
+NATIVE_EXTRA = {'e3gnn_pair_check': ['pair_e3gnn_core.cpp']}
 
 
 def build_native(lib=LIB, verbose=False, only_stale=False):
@@ -82,14 +84,15 @@ def build_native(lib=LIB, verbose=False, only_stale=False):
     $ORIGIN-relative rpath."""
     exes = []
     for name in NATIVE_HOSTS:
-        src = os.path.join(NATIVE, name + '.cpp')
+        srcs = [os.path.join(NATIVE, f) for f in [name + '.cpp'] + NATIVE_EXTRA.get(name, [])]
+        hdrs = [os.path.join(NATIVE, f) for f in os.listdir(NATIVE) if f.endswith('.h')]
         exe = os.path.join(NATIVE, name)
         exes.append(exe)
-        if (only_stale and os.path.exists(exe)
-                and os.path.getmtime(exe) >= max(os.path.getmtime(src), os.path.getmtime(lib))):
+        if (only_stale and os.path.exists(exe) and os.path.getmtime(exe) >=
+                max([os.path.getmtime(f) for f in srcs + hdrs] + [os.path.getmtime(lib)])):
             continue
-        cmd = [HIPCC, '-O2', '-std=c++17', f'-I{INCLUDE}', src, '-o', exe,
-               f'-L{os.path.dirname(lib)}', '-le3gnn_hip',
+        cmd = [HIPCC, '-O2', '-std=c++17', f'-I{INCLUDE}', *srcs, '-o', exe,
+               f'-L{os.path.dirname(lib)}', '-le3gnn_hip', '-lpthread',
                "-Wl,-rpath,$ORIGIN/../sevennet_finetuning_amd"]
         if verbose:
             print(' '.join(cmd))

@@ -285,6 +285,15 @@ struct e3gnn_ctx {
     const char* v = std::getenv("E3GNN_LAST_EDGE");
     return (v && std::string(v) == "1") ? 1 : 0;
   }();
+  // lock-step convolution kernels (4 centres per workgroup, W2 operands staged
+  // per block pair in LDS, dH2 on bf16x6; 1) or the per-wave kernels (0;
+  // E3GNN_CONV=wave)
+  int conv_ls = [] {
+    const char* v = std::getenv("E3GNN_CONV");
+    if (!v) return 0;
+    const std::string m(v);
+    return m == "ls" ? 3 : (m == "lsb" ? 2 : (m == "lsf" ? 1 : 0));
+  }();
   int nodelin = [] {
     const char* v = std::getenv("E3GNN_NODELIN");
     return (v && std::string(v) == "0") ? 0 : 1;
@@ -1135,7 +1144,7 @@ int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     a.denom = m->denom[t];
     a.c_begin = (int)c0;
     a.c_end = (int)c1;
-    HIPCHK(launch_conv_fwd(kind, a, s));
+    HIPCHK((c->conv_ls & 1) ? launch_conv_fwd_ls(kind, a, s) : launch_conv_fwd(kind, a, s));
     return E3GNN_OK;
   };
   if (part == 0) {
@@ -1366,7 +1375,10 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
                         (a.fuse_w ? tp_flops_per_edge(kind) + 2.0 * (64 * W + 64 * 64 + 8 * 64) : 0.0);
       Region r(c, s, C_CONV_BWD_X + kind, xf * ef,
                ef * 4 * (8 + 9 + 2 + 3 + (a.fuse_w ? 8 : 0)) + (a.c_end - a.c_begin) * 4.0 * dm);
-      HIPCHK(launch_conv_bwd_x(kind, a, s));
+      if ((c->conv_ls & 2) && a.edge_order && a.fuse_w)
+        HIPCHK(launch_conv_bwd_ls(kind, a, s));
+      else
+        HIPCHK(launch_conv_bwd_x(kind, a, s));
     }
     if (ef > 0 && !a.fuse_w) {
       Region r(c, s, C_CONV_BWD_W + kind,

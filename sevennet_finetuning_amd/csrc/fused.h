@@ -62,6 +62,10 @@ struct FusedArgs {
 };
 
 hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s);
+// lock-step kernels: 4 centres per workgroup, W2 operands staged per block pair
+// in LDS, dH2 on bf16x6 (fused.hip); the backward writes dxc (first / middle blocks)
+hipError_t launch_conv_fwd_ls(int kind, const FusedArgs& a, hipStream_t s);
+hipError_t launch_conv_bwd_ls(int kind, const FusedArgs& a, hipStream_t s);
 hipError_t launch_conv_bwd(int kind, const FusedArgs& a, hipStream_t s);  // = _x then _w
 hipError_t launch_conv_bwd_x(int kind, const FusedArgs& a, hipStream_t s);  // dE/dx, dE/du
 hipError_t launch_conv_bwd_w(int kind, const FusedArgs& a, hipStream_t s);  // dE/dw -> dE/demb

@@ -372,6 +372,81 @@ __device__ __forceinline__ void tp_acc_pk(const f32x2* x, const f32x2* y, f32x2 
   for (int k = 0; k < 2 * L3 + 1; ++k) acc[k] = __builtin_elementwise_fma(w, t[k], acc[k]);
 }
 
+// The lane's four (edge or channel) slots r = 0..3 in lock-step: every CG
+// product is issued for the four slots back to back, so the dependency chains
+// of the contraction run four-wide (the per-slot form serialises them).
+// Forward: acc[k] += sum_r w[r] sum_ij C_ijk x[r][i] y[r][j]; y[r] = the slot's
+// SH block (stride ys between slots).
+template <int L1, int L2, int L3>
+__device__ __forceinline__ void tp_acc4(const float* x, const float* y, int ys, const f32x4 w,
+                                        float* acc) {
+  using C = CG<L1, L2, L3>;
+  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
+  float yv[4][D2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int q = 0; q < D2; ++q) yv[r][q] = y[r * ys + q];
+  float t[4][D3];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int k = 0; k < D3; ++k) t[r][k] = 0.f;
+  sfor<D1>([&](auto i) {
+    sfor<D2>([&](auto j) {
+      if constexpr (cg_pair<C, i, j>()) {
+        float xy[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xy[r] = x[r * D1 + i] * yv[r][j];
+        sfor<C::n>([&](auto q) {
+          if constexpr (C::e[q].i == i && C::e[q].j == j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[r][C::e[q].k] += C::e[q].c * xy[r];
+          }
+        });
+      }
+    });
+  });
+#pragma unroll
+  for (int k = 0; k < D3; ++k) acc[k] += (w[0] * t[0][k] + w[1] * t[1][k]) + (w[2] * t[2][k] + w[3] * t[3][k]);
+}
+
+// Backward, the lane's 4 channels r of one edge: with t'_rij = sum_k C_ijk
+// g[r][k] and u_ri = sum_j t'_rij y_j,
+//   dx[r][i] += w[r] u_ri,  dy_j += sum_r t'_rij w[r] x[r][i],  dw[r] = sum_i x[r][i] u_ri
+template <int L1, int L2, int L3>
+__device__ __forceinline__ void tp_bwd_xw4(const float* x, const float* y, const f32x4 w,
+                                           const float* gm, float* dx, float* dy, float* dw) {
+  using C = CG<L1, L2, L3>;
+  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dw[r] = 0.f;
+  sfor<D1>([&](auto i) {
+    float u[4] = {0.f, 0.f, 0.f, 0.f}, wx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wx[r] = w[r] * x[r * D1 + i];
+    sfor<D2>([&](auto j) {
+      if constexpr (cg_pair<C, i, j>()) {
+        float tp[4] = {0.f, 0.f, 0.f, 0.f};
+        sfor<C::n>([&](auto q) {
+          if constexpr (C::e[q].i == i && C::e[q].j == j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) tp[r] += C::e[q].c * gm[r * D3 + C::e[q].k];
+          }
+        });
+#pragma unroll
+        for (int r = 0; r < 4; ++r) u[r] += tp[r] * y[j];
+        if constexpr (L2 > 0) dy[j] += (tp[0] * wx[0] + tp[1] * wx[1]) + (tp[2] * wx[2] + tp[3] * wx[3]);
+      }
+    });
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dx[r * D1 + i] += w[r] * u[r];
+      dw[r] += x[r * D1 + i] * u[r];
+    }
+  });
+}
+
 template <class L, int I>
 constexpr int iblock_mul() {
   for (int p = 0; p < L::NP; ++p)
@@ -430,6 +505,22 @@ __device__ __forceinline__ void load_w2q(f32x4 (&b)[4], __amdgpu_buffer_rsrc_t w
   for (int bh = 0; bh < 4; ++bh) b[bh] = ldw4(w2q, v, (col0 / 16 * 4 + bh) * 1024);
 }
 
+// channel groups (input irrep I, 16-channel block j) in visiting order
+template <class L>
+constexpr int mul_of(int I) {
+  for (int p = 0; p < L::NP; ++p)
+    if (L::P[p].l1 == I) return L::P[p].mul;
+  return 0;
+}
+template <class L>
+constexpr int next_I(int I) {
+  for (int i = I + 1; i < 3; ++i)
+    if (mul_of<L>(i) > 0) return i;
+  return -1;
+}
+template <class L>
+constexpr int first_I() { return mul_of<L>(0) > 0 ? 0 : next_I<L>(0); }
+
 // per tile: neighbour ids of the lane group's 4 edges, Y of the 16 edges in LDS
 __device__ __forceinline__ void load_tile_edges(const int* __restrict__ nbr,
                                                 const float* __restrict__ Y, int e0, int end,
@@ -478,6 +569,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
     Op3 wq;
     load_w2b(wq, R.w2b, lane, L::P[0].woff);
     load_tile_edges(nbr, Y, e0, end, lane, src, ybuf);
+    // neighbour rows of the next channel group (4 edges x D1), loaded under the
+    // current group's work
+    float xpf[20];
+    auto load_group = [&](auto Iq, int jq) {
+      constexpr int D1q = 2 * Iq + 1;
+      constexpr int XOq = iblock_xoff<L, Iq>();
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ldv<D1q>(Rh, (src[r] * L::DX + col * D1q) * 4, (XOq + 16 * jq * D1q) * 4, xpf + r * D1q);
+    };
+    load_group(std::integral_constant<int, first_I<L>()>{}, 0);
     Op3 hq;
     {
       MlpT m;
@@ -493,14 +595,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
       constexpr int MUL = iblock_mul<L, I>();
       if constexpr (MUL > 0) {
         constexpr int D1 = 2 * I + 1;
-        constexpr int XOFF = iblock_xoff<L, I>();
         for (int j = 0; j < MUL / 16; ++j) {
-          const int u = 16 * j + col;
           float x[4][D1];
           phase();
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            ldv<D1>(Rh, (src[r] * L::DX + col * D1) * 4, (XOFF + 16 * j * D1) * 4, x[r]);
+#pragma unroll
+            for (int i = 0; i < D1; ++i) x[r][i] = xpf[r * D1 + i];
+          if (j + 1 < MUL / 16) {
+            load_group(I, j + 1);
+          } else {
+            constexpr int IN = next_I<L>(I);
+            if constexpr (IN >= 0) load_group(std::integral_constant<int, IN>{}, 0);
+          }
           sfor<L::NP>([&](auto pi) {
             constexpr PathDef p = L::P[pi];
             if constexpr (p.l1 == I) {
@@ -534,13 +641,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
               } else {
 #pragma unroll
               for (int k = 0; k < D3; ++k) acc[k] = 0.f;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                float y[D2];
-#pragma unroll
-                for (int q = 0; q < D2; ++q) y[q] = ybuf[(4 * g + r) * 9 + yoff(p.l2) + q];
-                tp_acc<p.l1, p.l2, p.l3>(x[r], y, wv[r], acc);  // padded edges have w = 0
-              }
+              // the lane's 4 edges in lock-step (padded edges have Y = 0)
+              tp_acc4<p.l1, p.l2, p.l3>(&x[0][0], ybuf + 4 * g * 9 + yoff(p.l2), 9, wv, acc);
               }
 #pragma unroll
               for (int k = 0; k < D3; ++k) {
@@ -1346,7 +1448,407 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_
   mlp_bwd_chain(R, emb, e0, end, lane, dh2, demb);
 }
 
+// ================================================================ lock-step kernels
+// One workgroup = 4 waves = 4 consecutive centres (one wave per centre, its
+// CSR edges in 16-edge tiles, tile t of the four centres at the same time).
+// The waves walk the same sequence of 16-column weight blocks and share the
+// W2 operands of each block PAIR: staged once per workgroup in LDS (register
+// staging: issued a whole pair ahead, written between two barriers), so each
+// operand crosses the L2 -> CU path once per 4 tiles instead of once per tile
+// and needs no per-wave prefetch registers.  The backward's dH2 = dw W2^T runs
+// on bf16x6 MFMA over the pair (K = 32 channels): 24 x 16 MFMA cycles instead of
+// 2 x 16 x 32 on f32 MFMA.  Two workgroups per CU (LDS), 2 waves per SIMD.
+constexpr int LS_BLK = 6144;            // bytes of one w2v column block (3 pieces x 2 halves x 1 KB)
+constexpr int LS_PAIR_W = 2 * LS_BLK;   // the pair's two w-recompute operand blocks
+constexpr int LS_PAIR_D = 12288;        // the pair's dH2 operand (w2d: 3 pieces x 4 bh x 1 KB)
+
+__device__ __forceinline__ void lds_op3(Op3& o, const char* blk, int lane) {
+#pragma unroll
+  for (int pc = 0; pc < 3; ++pc)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      o.v[pc][m] = *reinterpret_cast<const bf16x8*>(blk + ((pc * 2 + m) * 64 + lane) * 16);
+}
+
+// dH2^T += W2[:, pair] dw^T on bf16x6 (K = 32: element t of lane (g, c) is
+// channel 4g + t of the pair's first block (t < 4) or 4g + t - 4 of its second,
+// the w2d order); A = the W2 pieces (LDS), B = dw split in three pieces
+__device__ __forceinline__ void dh2_pair(f32x4 (&dh2)[4], const float (&da)[4], const float (&db)[4],
+                                         const char* pimg, int lane) {
+  bf16x8 d[3];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    float v = t < 4 ? da[t] : db[t - 4];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+      const __bf16 b = (__bf16)v;
+      d[pc][t] = b;
+      v -= (float)b;
+    }
+  }
+  constexpr int I[6] = {2, 1, 0, 1, 0, 0}, J[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+  for (int bh = 0; bh < 4; ++bh) {
+    bf16x8 a[3];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+      a[pc] = *reinterpret_cast<const bf16x8*>(pimg + ((pc * 4 + bh) * 64 + lane) * 16);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) dh2[bh] = mfma16(a[I[q]], d[J[q]], dh2[bh]);
+  }
+}
+
+// tiles of the workgroup's centres [cb, cb + 4) clipped to c_end: the lock-step
+// loop count (min_one: a centre without edges still has its one (empty) tile)
+__device__ __forceinline__ int ls_tiles(const int* __restrict__ row_ptr, int cb, int c_end,
+                                        bool min_one) {
+  int T = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int cc = cb + w;
+    if (cc < c_end) {
+      const int t = (row_ptr[cc + 1] - row_ptr[cc] + 15) >> 4;
+      T = max(T, min_one ? max(t, 1) : t);
+    }
+  }
+  return __builtin_amdgcn_readfirstlane(T);
+}
+
+// Forward: agg[c] = sum_e TP(h[nbr e], Y_e, w_e) / denom (IrrepsConvolution.forward,
+// convolution.py:104-123); the centre's message sum over its tiles stays in LDS.
+// Per block pair: both blocks' w = H2 W2 (bf16x6) are formed at the pair start,
+// so the second block's MFMAs run under the first block's tensor product; the
+// neighbour rows of the next channel group are loaded under the current one.
+template <class L>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_fwd_ls(
+    const int* __restrict__ row_ptr, const int* __restrict__ nbr, const float* __restrict__ emb,
+    const float* __restrict__ Y, const float* __restrict__ h, float* __restrict__ agg, MlpW W,
+    int c_begin, int c_end, int n_nodes, float denom) {
+  constexpr int NBLK = L::W / 16, NPAIR = NBLK / 2;
+  static_assert(NBLK % 2 == 0, "weight blocks come in pairs");
+  constexpr int NST = LS_PAIR_W / 16 / 256;  // b128 staging chunks per thread
+  // [4 agg rows | 4 x Y of the tile (16 x 9, padded to 160) | pair image]
+  __shared__ __attribute__((aligned(16))) float smem[4 * L::DM + 4 * 160 + LS_PAIR_W / 4];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int cb = c_begin + blockIdx.x * 4;
+  const int c = cb + wid;
+  const bool valid = c < c_end;
+  const int beg = valid ? row_ptr[c] : 0, end = valid ? row_ptr[c + 1] : 0;
+  const int ntile = valid ? max(1, (end - beg + 15) >> 4) : 0;
+  const int T = ls_tiles(row_ptr, cb, c_end, true);
+  float* acl = smem + wid * L::DM;
+  float* ybuf = smem + 4 * L::DM + wid * 160;
+  char* img = reinterpret_cast<char*>(smem + 4 * L::DM + 4 * 160);
+  const WRes R = make_wres(W, L::W);
+  const __amdgpu_buffer_rsrc_t Rh = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
+  const float rden = 1.0f / denom;
+  f32x4 st[NST];
+  auto issue = [&](int P) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) st[i] = ldw4(R.w2v, (tid + 256 * i) * 16, P * LS_PAIR_W);
+  };
+  auto commit = [&]() {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NST; ++i) *reinterpret_cast<f32x4*>(img + (tid + 256 * i) * 16) = st[i];
+    __syncthreads();
+  };
+  issue(0);
+  for (int t = 0; t < T; ++t) {
+    const bool act = t < ntile;   // wave-uniform
+    const bool first_tile = t == 0;
+    const int e0 = beg + 16 * t;
+    int src[4];
+    float xpf[20];   // neighbour rows of the next channel group (4 edges x D1)
+    auto load_group = [&](auto Iq, int jq) {
+      constexpr int D1q = 2 * Iq + 1;
+      constexpr int XOq = iblock_xoff<L, Iq>();
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ldv<D1q>(Rh, (src[r] * L::DX + col * D1q) * 4, (XOq + 16 * jq * D1q) * 4, xpf + r * D1q);
+    };
+    Op3 hq;
+    if (act) {
+      load_tile_edges(nbr, Y, e0, end, lane, src, ybuf);
+      load_group(std::integral_constant<int, first_I<L>()>{}, 0);
+      MlpT m;
+      mlp_pre(R, emb, e0, end, lane, m);
+      f32x4 h2[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h2[b][r] = act_fwd(m.a2[b][r]);
+      split_h2(h2, hq);
+    }
+    int nb = 0;
+    f32x4 wv0 = zero4(), wv1 = zero4();   // w of the pair's two blocks
+    sfor<3>([&](auto I) {
+      constexpr int MUL = iblock_mul<L, I>();
+      if constexpr (MUL > 0) {
+        constexpr int D1 = 2 * I + 1;
+        for (int j = 0; j < MUL / 16; ++j) {
+          float x[4][D1];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int i = 0; i < D1; ++i) x[r][i] = xpf[r * D1 + i];
+          if (act) {
+            if (j + 1 < MUL / 16) {
+              load_group(I, j + 1);
+            } else {
+              constexpr int IN = next_I<L>(I);
+              if constexpr (IN >= 0) load_group(std::integral_constant<int, IN>{}, 0);
+            }
+          }
+          sfor<L::NP>([&](auto pi) {
+            constexpr PathDef p = L::P[pi];
+            if constexpr (p.l1 == I) {
+              constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
+              if ((nb & 1) == 0) {   // pair start: stage it, fetch the next one
+                commit();
+                issue((nb >> 1) + 1 < NPAIR ? (nb >> 1) + 1 : 0);
+                if (act) {
+                  Op3 wq;
+                  lds_op3(wq, img, lane);
+                  wv0 = w2_block<true>(hq, wq);
+                  lds_op3(wq, img + LS_BLK, lane);
+                  wv1 = w2_block<true>(hq, wq);
+                }
+              }
+              if (act) {
+                const f32x4 wv = (nb & 1) ? wv1 : wv0;
+                float acc[D3];
+#pragma unroll
+                for (int k = 0; k < D3; ++k) acc[k] = 0.f;
+                // padded edges: Y = 0
+                tp_acc4<p.l1, p.l2, p.l3>(&x[0][0], ybuf + 4 * g * 9 + yoff(p.l2), 9, wv, acc);
+#pragma unroll
+                for (int k = 0; k < D3; ++k) {
+                  const float v = sum_rows4(acc[k]) * rden;
+                  if (g == 0) {
+                    float* a = acl + p.moff + (16 * j + col) * D3 + k;
+                    *a = first_tile ? v : *a + v;
+                  }
+                }
+              }
+              ++nb;
+            }
+          });
+        }
+      }
+    });
+  }
+  if (valid) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    const float4* s4 = reinterpret_cast<const float4*>(acl);
+    float4* d4 = reinterpret_cast<float4*>(agg + (int64_t)c * L::DM);
+    for (int k = lane; k < L::DM / 4; k += 64) d4[k] = s4[k];
+  }
+}
+
+// Backward of a first / middle block (per-edge dE/dx to dxc, summed per
+// neighbour by the transposed-CSR gather; dE/dY -> dE/du; dE/dw -> dH2 -> MLP
+// chain -> dE/demb), the centre's dE/dagg row staged in LDS once.  Same pair
+// structure as the forward (both blocks' w formed at the pair start, next
+// group's neighbour rows prefetched); dH2 of the pair on bf16x6 at its end.
+template <class L>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_bwd_ls(
+    const int* __restrict__ row_ptr, const int* __restrict__ nbr, const float* __restrict__ emb,
+    const float* __restrict__ Y, const float* __restrict__ h, const float* __restrict__ gagg, MlpW W,
+    float* __restrict__ dxc, float* __restrict__ dgu, float* __restrict__ demb, int c_begin,
+    int c_end, int n_nodes) {
+  constexpr int NBLK = L::W / 16, NPAIR = NBLK / 2;
+  static_assert(NBLK % 2 == 0, "weight blocks come in pairs");
+  constexpr int NW = LS_PAIR_W / 16 / 256, ND = LS_PAIR_D / 16 / 256;
+  __shared__ __attribute__((aligned(16))) float smem[4 * L::DM + (LS_PAIR_W + LS_PAIR_D) / 4];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int cb = c_begin + blockIdx.x * 4;
+  const int c = cb + wid;
+  const bool valid = c < c_end;
+  const int beg = valid ? row_ptr[c] : 0, end = valid ? row_ptr[c + 1] : 0;
+  const int T = ls_tiles(row_ptr, cb, c_end, false);
+  float* dacc = smem + wid * L::DM;
+  char* img = reinterpret_cast<char*>(smem + 4 * L::DM);
+  if (valid && end > beg) {
+    const float4* s4 = reinterpret_cast<const float4*>(gagg + (int64_t)c * L::DM);
+    float4* d4 = reinterpret_cast<float4*>(dacc);
+    for (int k = lane; k < L::DM / 4; k += 64) d4[k] = s4[k];
+  }
+  const WRes R = make_wres(W, L::W);
+  const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
+  f32x4 st[NW + ND];
+  auto issue = [&](int P) {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) st[i] = ldw4(R.w2v, (tid + 256 * i) * 16, P * LS_PAIR_W);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) st[NW + i] = ldw4(R.w2d, (tid + 256 * i) * 16, P * LS_PAIR_D);
+  };
+  auto commit = [&]() {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NW + ND; ++i) *reinterpret_cast<f32x4*>(img + (tid + 256 * i) * 16) = st[i];
+    __syncthreads();
+  };
+  issue(0);
+  for (int t = 0; t < T; ++t) {
+    const int q0 = beg + 16 * t;
+    const bool act = q0 < end;   // wave-uniform
+    const int er = (act && q0 + col < end) ? q0 + col : -1;
+    const int vx = (er >= 0 ? nbr[er] : 0) * L::DX * 4;
+    float xpf[20];   // the lane's 4 channels x D1 of the next channel group
+    auto load_group = [&](auto Iq, int jq) {
+      constexpr int D1q = 2 * Iq + 1;
+      constexpr int XOq = iblock_xoff<L, Iq>();
+      ldv<4 * D1q>(Rx, vx + 4 * g * D1q * 4, (XOq + 16 * jq * D1q) * 4, xpf);
+    };
+    float y[9];
+    Op3 hq;
+    if (act) {
+      load_group(std::integral_constant<int, first_I<L>()>{}, 0);
+#pragma unroll
+      for (int q = 0; q < 9; ++q) y[q] = er >= 0 ? Y[(int64_t)er * 9 + q] : 0.f;
+      float b[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) b[s] = er >= 0 ? emb[(int64_t)er * 8 + 4 * s + g] : 0.f;
+      MlpT m;
+      mlp_chain(R, b, lane, m);
+      f32x4 h2[4];
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h2[bb][r] = act_fwd(m.a2[bb][r]);
+      split_h2(h2, hq);
+    }
+    f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
+    float dYa[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) dYa[q] = 0.f;
+    float dwp[4];   // dE/dw of the pair's first block
+    f32x4 wv0 = zero4(), wv1 = zero4();   // w of the pair's two blocks
+    int nb = 0;
+    sfor<3>([&](auto I) {
+      constexpr int MUL = iblock_mul<L, I>();
+      if constexpr (MUL > 0) {
+        constexpr int D1 = 2 * I + 1;
+        constexpr int XOFF = iblock_xoff<L, I>();
+        for (int jj = 0; jj < MUL / 16; ++jj) {
+          float x[4 * D1], dx[4 * D1];
+#pragma unroll
+          for (int i = 0; i < 4 * D1; ++i) {
+            x[i] = xpf[i];
+            dx[i] = 0.f;
+          }
+          if (act) {
+            if (jj + 1 < MUL / 16) {
+              load_group(I, jj + 1);
+            } else {
+              constexpr int IN = next_I<L>(I);
+              if constexpr (IN >= 0) load_group(std::integral_constant<int, IN>{}, 0);
+            }
+          }
+          sfor<L::NP>([&](auto pi) {
+            constexpr PathDef p = L::P[pi];
+            if constexpr (p.l1 == I) {
+              constexpr int D3 = 2 * p.l3 + 1;
+              if ((nb & 1) == 0) {   // pair start: stage it, fetch the next one
+                commit();
+                issue((nb >> 1) + 1 < NPAIR ? (nb >> 1) + 1 : 0);
+                if (act) {
+                  Op3 wq;
+                  lds_op3(wq, img, lane);
+                  wv0 = w2_block<false>(hq, wq);
+                  lds_op3(wq, img + LS_BLK, lane);
+                  wv1 = w2_block<false>(hq, wq);
+                }
+              }
+              if (act) {
+                const f32x4 wv = (nb & 1) ? wv1 : wv0;
+                float gm[4 * D3];
+                const float* gl = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
+#pragma unroll
+                for (int k = 0; k < 4 * D3; ++k) gm[k] = gl[k];
+                float dwr[4];
+                // padded slots: y = 0, so dE/dx = dE/dw = 0 there
+                tp_bwd_xw4<p.l1, p.l2, p.l3>(x, y + yoff(p.l2), wv, gm, dx, dYa + yoff(p.l2), dwr);
+                pin<4 * D1>(dx);
+                pin<8>(dYa + 1);
+                if (nb & 1) {
+                  dh2_pair(dh2, dwp, dwr, img + LS_PAIR_W, lane);
+                } else {
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) dwp[r] = dwr[r];
+                }
+              }
+              ++nb;
+            }
+          });
+          if (act && dxc && er >= 0) {   // per-edge dE/dx[nbr] (not needed for the first block)
+            float* o = dxc + (int64_t)er * L::DX + XOFF + (16 * jj + 4 * g) * D1;
+#pragma unroll
+            for (int i = 0; i < 4 * D1; ++i) o[i] = dx[i];
+          }
+        }
+      }
+    });
+    if (act) {
+      // dE/dY of edge c: sum over the 4 lane groups, then dE/du through the SH
+      // polynomials (serial_code.py:50-70)
+#pragma unroll
+      for (int q = 1; q < 9; ++q) dYa[q] = sum_rows4(dYa[q]);
+      if (g == 0 && er >= 0) {
+        const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f, c15 = s3 * s5;
+        const float is3 = 0.57735026918962576f;  // 1 / sqrt(3)
+        const float ux = y[1] * is3, uy = y[2] * is3, uz = y[3] * is3;
+        const float* d = dYa + 1;  // d[0..2] = dE/dY_1, d[3..7] = dE/dY_2
+        const float gx = s3 * d[0] + c15 * (uz * d[3] + uy * d[4]) - s5 * ux * d[5] - c15 * ux * d[7];
+        const float gy = s3 * d[1] + c15 * (ux * d[4] + uz * d[6]) + 2.f * s5 * uy * d[5];
+        const float gz = s3 * d[2] + c15 * (ux * d[3] + uy * d[6]) - s5 * uz * d[5] + c15 * uz * d[7];
+        float* o = dgu + (int64_t)er * 3;
+        o[0] += gx;
+        o[1] += gy;
+        o[2] += gz;
+      }
+      mlp_bwd_chain(R, emb, q0, end, lane, dh2, demb);
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_conv_fwd_ls(int kind, const FusedArgs& a, hipStream_t s) {
+  const int nc = a.c_end - a.c_begin;
+  if (nc <= 0) return hipSuccess;
+  const dim3 grid((nc + 3) / 4), block(256);
+  switch (kind) {
+    case 0: hipLaunchKernelGGL(k_conv_fwd_ls<LayerFirst>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb, a.Y,
+                               a.h, a.agg, a.W, a.c_begin, a.c_end, a.n_nodes, a.denom); break;
+    case 1: hipLaunchKernelGGL(k_conv_fwd_ls<LayerMid>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb, a.Y,
+                               a.h, a.agg, a.W, a.c_begin, a.c_end, a.n_nodes, a.denom); break;
+    default: hipLaunchKernelGGL(k_conv_fwd_ls<LayerLast>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb,
+                                a.Y, a.h, a.agg, a.W, a.c_begin, a.c_end, a.n_nodes, a.denom); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_bwd_ls(int kind, const FusedArgs& a, hipStream_t s) {
+  const int nc = a.c_end - a.c_begin;
+  if (nc <= 0 || a.n_nodes <= 0) return hipSuccess;
+  const dim3 grid((nc + 3) / 4), block(256);
+  switch (kind) {
+    case 0: hipLaunchKernelGGL(k_conv_bwd_ls<LayerFirst>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb, a.Y,
+                               a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb, a.c_begin, a.c_end, a.n_nodes);
+      break;
+    case 1: hipLaunchKernelGGL(k_conv_bwd_ls<LayerMid>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb, a.Y,
+                               a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb, a.c_begin, a.c_end, a.n_nodes);
+      break;
+    default: hipLaunchKernelGGL(k_conv_bwd_ls<LayerLast>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb,
+                                a.Y, a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb, a.c_begin, a.c_end,
+                                a.n_nodes);
+      break;
+  }
+  return hipGetLastError();
+}
 
 template <class L>
 static hipError_t fwd_impl(const FusedArgs& a, hipStream_t s) {

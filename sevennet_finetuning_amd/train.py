@@ -196,6 +196,20 @@ class EWCLoss(LossDefinition):
         return ewc
 
 
+def _sum_two_level(v):
+    """Sum of a long 1-D tensor as rows of 1024 reduced per block, then the row
+    sums: no reduction spans blocks.  A single torch.sum over the 842k-entry
+    flat buffer is PyTorch's multi-block global reduction, whose semaphores
+    are re-zeroed by a hipMemsetAsync before each launch; captured in a HIP
+    graph (the graphed rehearsal step) it returned wrong sums on replays that
+    other work ran between (tools/diag_graph_reduce.py, tools/
+    diag_ewc_interleave.py: the reported EWC loss, never the gradients, which
+    _FlatEWC.backward forms element-wise)."""
+    m = v.numel() // 1024 * 1024
+    s = v[:m].view(-1, 1024).sum(1).sum() if m else v.new_zeros(())
+    return s + v[m:].sum() if m < v.numel() else s
+
+
 class _FlatEWC(torch.autograd.Function):
     """sum F (theta - theta*)^2 over the model's flat parameter buffer in one
     pass; the backward adds 2 F (theta - theta*) straight into the flat
@@ -207,7 +221,7 @@ class _FlatEWC(torch.autograd.Function):
         d = model.flat.detach() - o
         ctx.model, ctx.f_train = model, f_train
         ctx.save_for_backward(d)
-        return torch.sum(f * d * d)
+        return _sum_two_level(f * d * d)
 
     @staticmethod
     def backward(ctx, g):

@@ -77,3 +77,28 @@ def test_native_parallel_host_matches_serial(grid):
     assert out['energy_rel_diff'] < 1e-6
     assert out['max_force_diff'] < 1e-4
     assert out['max_virial_diff'] <= 1e-5 * max(1.0, out['max_virial'])
+
+
+EXE_PAIR = os.path.join(ROOT, 'native', 'e3gnn_pair_check')
+
+
+@pytest.mark.parametrize('grid', [(1, 1, 1), (2, 1, 1), (2, 2, 1)])
+def test_lammps_pair_core_matches_device_path(grid):
+    """The LAMMPS pair-style core (native/pair_e3gnn_core.cpp, what
+    native/lammps/pair_e3gnn_hip.cpp and pair_e3gnn_parallel_hip.cpp call) on
+    LAMMPS-shaped inputs -- scrambled atom indices and tags, periodic-image
+    ghosts carrying their owner's tag, full neighbour lists with a skin and
+    NEIGHMASK bits -- serial (pair_e3gnn.cpp:72-275) and on brick sub-domains
+    with threaded ranks and halo exchanges (pair_e3gnn_parallel.cpp:207-933),
+    against the device neighbour list + e3gnn_energy_forces of the same box."""
+    assert os.path.exists(EXE_PAIR), 'native/e3gnn_pair_check not built (build_lib.build)'
+    r = subprocess.run([EXE_PAIR, ASSET, '4', *map(str, grid), '3'], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out['n_atoms'] == 512 and out['ranks'] == int(np.prod(grid))
+    for k in ('serial', 'parallel'):
+        assert out[k]['energy_rel'] < 1e-6, out
+        assert out[k]['eatom_sum_rel'] < 1e-6, out
+        assert out[k]['max_force'] < 1e-4, out
+        assert out[k]['max_virial'] < 1e-3, out

@@ -294,6 +294,72 @@ def test_graphed_step_replays_of_equal_shapes_equal_eager():
     assert float((d > 1e-6).float().mean()) < 1e-3
 
 
+def test_graphed_ewc_step_interleaved_with_eager_trainer():
+    """An eager and a graphed EWC trainer stepped alternately in one process
+    (tools/diag_ewc_interleave.py): every step's losses and the final
+    parameters equal.  Round 2 shipped this broken: the graphed trainer's
+    REPORTED loss came back ~800 (parameters right) once other work ran
+    between its replays -- the EWC term's torch.sum over the 842k-entry flat
+    buffer is a multi-block reduction that did not survive graph replay here;
+    train._sum_two_level keeps every reduction inside one block."""
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+
+    def make(graph):
+        m = SevenNetTrainable(device=DEV)
+        fisher = {n: torch.full_like(p, 1e-3) for n, p in m.named_parameters()}
+        opt = {n: p.detach().clone() for n, p in m.named_parameters()}
+        cfg = {'loss': 'huber', 'loss_param': {'delta': 0.01}, 'force_loss_weight': 1.0,
+               'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
+               'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
+               'scheduler_param': {'gamma': 0.99}, 'device': DEV, 'hip_graph': graph,
+               'continue': {'fisher_information': fisher, 'opt_params': opt,
+                            'ewc_lambda': 1e5}}
+        tr = train.Trainer(m, cfg)
+        m.train(True)
+        return m, tr
+
+    def coll(seeds):
+        return train.collate(_batch(seeds), device=DEV, dtype=torch.float32)
+    pairs = [(coll([1, 2]), coll([3, 4])), (coll([5, 6]), coll([7, 8]))]
+    me, te = make(False)
+    mg, tg = make(True)
+    for i in range(5):
+        le = [float(x) for x in te.rehearsal_step(*pairs[i % 2])]
+        torch.cuda.synchronize()
+        lg = [float(x) for x in tg.rehearsal_step(*pairs[i % 2])]
+        torch.cuda.synchronize()
+        for a, c in zip(le, lg):
+            assert abs(a - c) <= 1e-5 * abs(a), (i, le, lg)
+    d = (me.flat - mg.flat).abs()
+    assert float(d.max()) <= 2 * 1e-5 * 5
+    assert float((d > 1e-6).float().mean()) < 1e-3
+
+
+def test_two_level_sum_in_a_replayed_graph():
+    """The reduction form of the EWC loss reproduces the eager sum on every
+    replay of a captured graph, with other reductions run between replays."""
+    N = 842623
+    x = torch.randn(N, device=DEV)
+    y = torch.randn(N, device=DEV)
+    fn = lambda v: train._sum_two_level(v * v)   # noqa: E731
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn(x)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = fn(x)
+    for _ in range(4):
+        x.mul_(1.01)
+        g.replay()
+        got = out.clone()
+        _ = (y * y).sum()
+        torch.cuda.synchronize()
+        ref = (x.double() ** 2).sum()
+        assert abs(float(got) - float(ref)) <= 1e-5 * float(ref)
+
+
 def test_scaled_silu_op_derivatives():
     """e3gnn_act (fused scale * silu) against torch's composite in float64:
     value, first and second derivatives."""

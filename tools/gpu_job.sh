@@ -62,16 +62,6 @@ for s in "$@"; do
     bench2) step bench2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --cells 11 --same-device --no-cpu-baseline ;;
     report) step report 300 python tools/parity_report.py ;;
     trainops) step trainops 300 python tools/prof_train_ops.py ;;
-    diaggraph) step diaggraph 300 python tools/diag_graph_train.py ;;
-    diaggraph2) step diaggraph2 300 python tools/diag_graph_train2.py ;;
-    diag3) step diag3 300 python tools/diag_graph_train3.py ;;
-    diag4) step diag4 300 python tools/diag_graph_train4.py ;;
-    diag5) step diag5 300 python tools/diag_graph_train5.py ;;
-    diag5_*) v=${s#diag5_}; step diag5_$v 300 python tools/diag_graph_train5.py $v ;;
-    diag6) step diag6 300 python tools/diag_graph_train6.py ;;
-    diag7) step diag7 300 python tools/diag_graph_train7.py ;;
-    diagparts) step diagparts 300 python tools/diag_graph_parts.py ;;
-    diaggraph2lt) step diaggraph2lt 300 python tools/diag_graph_train2.py hipblaslt ;;
     pmctcp) step pmctcp 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum --kernel-trace --output-format csv -d gpurun_out/pmc_tcp -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
     pmctcc) step pmctcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum --kernel-trace --output-format csv -d gpurun_out/pmc_tcc -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
     listc) step listc 120 rocprofv3 -L ;;
@@ -81,6 +71,14 @@ for s in "$@"; do
     testsv_*) v=${s#testsv_}; step tests_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -m pytest tests -m gpu -x -q ;;
     diagewc) step diagewc 400 python tools/diag_ewc_interleave.py ;;
     bench2self) step bench2self 600 python bench.py --gpus 2 --same-device --steps 2 --warmup 1 --cells 11 --no-cpu-baseline ;;
+    parityls) step parityls 600 env E3GNN_CONV=ls python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
+    benchls) step benchls 600 env E3GNN_CONV=ls python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    benchlsb) step benchlsb 600 env E3GNN_CONV=lsb python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    paritydef) step paritydef 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
+    profls) step profls 600 env E3GNN_CONV=ls rocprofv3 --kernel-trace --stats -d gpurun_out/profls -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --profile-only --no-parity-check ;;
+    pmcsqls) step pmcsqls 600 env E3GNN_CONV=ls rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES --kernel-trace --output-format csv -d gpurun_out/pmc_sqls -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
+    pmcsq2ls) step pmcsq2ls 600 env E3GNN_CONV=ls rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM_RD SQ_INSTS_VALU_MFMA_MOPS_F32 --kernel-trace --output-format csv -d gpurun_out/pmc_sq2ls -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
+    reduce) step reduce 300 python tools/diag_graph_reduce.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
