@@ -290,9 +290,9 @@ struct e3gnn_ctx {
   // E3GNN_CONV=wave)
   int conv_ls = [] {
     const char* v = std::getenv("E3GNN_CONV");
-    if (!v) return 0;
+    if (!v) return 2;
     const std::string m(v);
-    return m == "ls" ? 3 : (m == "lsb" ? 2 : (m == "lsf" ? 1 : 0));
+    return m == "ls" ? 3 : (m == "wave" ? 0 : (m == "lsf" ? 1 : 2));
   }();
   int nodelin = [] {
     const char* v = std::getenv("E3GNN_NODELIN");

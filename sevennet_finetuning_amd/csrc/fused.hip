@@ -520,6 +520,25 @@ constexpr int next_I(int I) {
 }
 template <class L>
 constexpr int first_I() { return mul_of<L>(0) > 0 ? 0 : next_I<L>(0); }
+// paths of input irrep I; rank of path pi among them; blocks visited before I
+template <class L>
+constexpr int paths_of(int I) {
+  int n = 0;
+  for (int p = 0; p < L::NP; ++p) n += L::P[p].l1 == I;
+  return n;
+}
+template <class L>
+constexpr int path_rank(int pi) {
+  int n = 0;
+  for (int p = 0; p < pi; ++p) n += L::P[p].l1 == L::P[pi].l1;
+  return n;
+}
+template <class L>
+constexpr int blocks_before(int I) {
+  int n = 0;
+  for (int i = 0; i < I; ++i) n += paths_of<L>(i) * mul_of<L>(i) / 16;
+  return n;
+}
 
 // per tile: neighbour ids of the lane group's 4 edges, Y of the 16 edges in LDS
 __device__ __forceinline__ void load_tile_edges(const int* __restrict__ nbr,
@@ -1662,7 +1681,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   static_assert(NBLK % 2 == 0, "weight blocks come in pairs");
   constexpr int NW = LS_PAIR_W / 16 / 256, ND = LS_PAIR_D / 16 / 256;
   __shared__ __attribute__((aligned(16))) float smem[4 * L::DM + (LS_PAIR_W + LS_PAIR_D) / 4];
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
+  const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int cb = c_begin + blockIdx.x * 4;
   const int c = cb + wid;
   const bool valid = c < c_end;
@@ -1726,68 +1745,76 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int q = 0; q < 9; ++q) dYa[q] = 0.f;
     float dwp[4];   // dE/dw of the pair's first block
     f32x4 wv0 = zero4(), wv1 = zero4();   // w of the pair's two blocks
-    int nb = 0;
     sfor<3>([&](auto I) {
       constexpr int MUL = iblock_mul<L, I>();
       if constexpr (MUL > 0) {
         constexpr int D1 = 2 * I + 1;
         constexpr int XOFF = iblock_xoff<L, I>();
-        for (int jj = 0; jj < MUL / 16; ++jj) {
-          float x[4 * D1], dx[4 * D1];
+        // an odd number of paths: two channel groups per iteration, so the
+        // position of every block in its pair is a compile-time constant (no
+        // branches around the staging: the wait counts stay exact)
+        constexpr int NPI = paths_of<L>(I), U = (NPI & 1) ? 2 : 1, NB0 = blocks_before<L>(I);
+        static_assert((MUL / 16) % U == 0, "channel groups come in pairs");
+        for (int j2 = 0; j2 < MUL / 16; j2 += U) {
+          sfor<U>([&](auto hh) {
+            const int jj = j2 + hh;
+            float x[4 * D1], dx[4 * D1];
 #pragma unroll
-          for (int i = 0; i < 4 * D1; ++i) {
-            x[i] = xpf[i];
-            dx[i] = 0.f;
-          }
-          if (act) {
-            if (jj + 1 < MUL / 16) {
-              load_group(I, jj + 1);
-            } else {
-              constexpr int IN = next_I<L>(I);
-              if constexpr (IN >= 0) load_group(std::integral_constant<int, IN>{}, 0);
+            for (int i = 0; i < 4 * D1; ++i) {
+              x[i] = xpf[i];
+              dx[i] = 0.f;
             }
-          }
-          sfor<L::NP>([&](auto pi) {
-            constexpr PathDef p = L::P[pi];
-            if constexpr (p.l1 == I) {
-              constexpr int D3 = 2 * p.l3 + 1;
-              if ((nb & 1) == 0) {   // pair start: stage it, fetch the next one
-                commit();
-                issue((nb >> 1) + 1 < NPAIR ? (nb >> 1) + 1 : 0);
+            if (act) {
+              if (jj + 1 < MUL / 16) {
+                load_group(I, jj + 1);
+              } else {
+                constexpr int IN = next_I<L>(I);
+                if constexpr (IN >= 0) load_group(std::integral_constant<int, IN>{}, 0);
+              }
+            }
+            sfor<L::NP>([&](auto pi) {
+              constexpr PathDef p = L::P[pi];
+              if constexpr (p.l1 == I) {
+                constexpr int D3 = 2 * p.l3 + 1;
+                constexpr int ODD = (NB0 + hh * NPI + path_rank<L>(pi)) & 1;
+                const int nb = NB0 + jj * NPI + path_rank<L>(pi);
+                if constexpr (!ODD) {   // pair start: stage it, fetch the next one
+                  commit();
+                  issue((nb >> 1) + 1 < NPAIR ? (nb >> 1) + 1 : 0);
+                  if (act) {
+                    Op3 wq;
+                    lds_op3(wq, img, lane);
+                    wv0 = w2_block<false>(hq, wq);
+                    lds_op3(wq, img + LS_BLK, lane);
+                    wv1 = w2_block<false>(hq, wq);
+                  }
+                }
                 if (act) {
-                  Op3 wq;
-                  lds_op3(wq, img, lane);
-                  wv0 = w2_block<false>(hq, wq);
-                  lds_op3(wq, img + LS_BLK, lane);
-                  wv1 = w2_block<false>(hq, wq);
+                  const f32x4 wv = ODD ? wv1 : wv0;
+                  float gm[4 * D3];
+                  const float* gl = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
+#pragma unroll
+                  for (int k = 0; k < 4 * D3; ++k) gm[k] = gl[k];
+                  float dwr[4];
+                  // padded slots: y = 0, so dE/dx = dE/dw = 0 there
+                  tp_bwd_xw4<p.l1, p.l2, p.l3>(x, y + yoff(p.l2), wv, gm, dx, dYa + yoff(p.l2), dwr);
+                  pin<4 * D1>(dx);
+                  pin<8>(dYa + 1);
+                  if constexpr (ODD) {
+                    dh2_pair(dh2, dwp, dwr, img + LS_PAIR_W, lane);
+                  } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dwp[r] = dwr[r];
+                  }
                 }
               }
-              if (act) {
-                const f32x4 wv = (nb & 1) ? wv1 : wv0;
-                float gm[4 * D3];
-                const float* gl = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
+            });
+            if (act && dxc && er >= 0) {   // per-edge dE/dx[nbr] (not needed for the first block)
+              float* o = dxc + (int64_t)er * L::DX + XOFF + (16 * jj + 4 * g) * D1;
 #pragma unroll
-                for (int k = 0; k < 4 * D3; ++k) gm[k] = gl[k];
-                float dwr[4];
-                // padded slots: y = 0, so dE/dx = dE/dw = 0 there
-                tp_bwd_xw4<p.l1, p.l2, p.l3>(x, y + yoff(p.l2), wv, gm, dx, dYa + yoff(p.l2), dwr);
-                pin<4 * D1>(dx);
-                pin<8>(dYa + 1);
-                if (nb & 1) {
-                  dh2_pair(dh2, dwp, dwr, img + LS_PAIR_W, lane);
-                } else {
-#pragma unroll
-                  for (int r = 0; r < 4; ++r) dwp[r] = dwr[r];
-                }
-              }
-              ++nb;
+              for (int i = 0; i < 4 * D1; ++i) o[i] = dx[i];
             }
           });
-          if (act && dxc && er >= 0) {   // per-edge dE/dx[nbr] (not needed for the first block)
-            float* o = dxc + (int64_t)er * L::DX + XOFF + (16 * jj + 4 * g) * D1;
-#pragma unroll
-            for (int i = 0; i < 4 * D1; ++i) o[i] = dx[i];
-          }
         }
       }
     });

@@ -11,7 +11,10 @@ the quantities):
   property ties the full-size result to the oracle;
 * the fused kernels against the independent unfused v1 kernels on the bench
   box (random per-atom displacements, every atom's environment distinct);
-* bitwise run-to-run determinism on the bench box.
+* bitwise run-to-run determinism on the bench box;
+* direct oracle parity inside the random full-size boxes: an atom's energy
+  depends only on atoms within 5 cutoffs (25 A, ~3,500 atoms), so the fp64
+  oracle evaluates that open cluster and must reproduce the HIP value.
 """
 import numpy as np
 import pytest
@@ -123,3 +126,49 @@ def test_bitwise_determinism_at_97k(model, bench_box):
     assert a['energy'] == b['energy']
     assert np.array_equal(a['forces'], b['forces'])
     assert np.array_equal(a['stress'], b['stress'])
+
+
+def _cluster_atomic_energy(pos, cell, types, centre, cutoff, n_layers):
+    """fp64 oracle atomic energy of ``centre`` from the open cluster of every
+    atom image within n_layers * cutoff of it.  E_i depends only on atoms
+    within that radius (each interaction block reaches one cutoff further,
+    nn/convolution.py message passing; the readout after the last block is
+    per atom), so the cluster value is the periodic box's value exactly."""
+    from oracle.neighbor import neighbor_list
+    from oracle.sevennet_ref import SevenNet0Ref
+    r = n_layers * cutoff + 0.25
+    d = pos - pos[centre]
+    f = d @ np.linalg.inv(cell)
+    f -= np.round(f)                       # minimum image: the box is > 2r wide
+    d = f @ cell
+    sel = np.nonzero((d * d).sum(1) <= r * r)[0]
+    box = np.eye(3) * (4 * r + 10)
+    cp = d[sel] + box[0, 0] / 2
+    ei, sh = neighbor_list(cp, box, cutoff, pbc=(False, False, False))
+    ref = SevenNet0Ref(dtype=torch.float64)
+    with torch.no_grad():
+        out = ref.energy(torch.tensor(cp), torch.tensor(types[sel]), torch.tensor(ei),
+                         torch.tensor(sh), torch.tensor(box), False)
+    return float(out['atomic_energy'][int(np.nonzero(sel == centre)[0][0])]), len(sel)
+
+
+@pytest.mark.parametrize('cells,centres', [(23, (0, 48611)), (46, (500001,))],
+                         ids=['97k', '778k'])
+def test_atomic_energies_at_full_size_vs_oracle(model, cells, centres):
+    """Direct oracle parity INSIDE the full-size random boxes (config 3 and
+    config 4's atom count, every atom's environment distinct): the HIP
+    atomic energies of chosen atoms equal the fp64 oracle's on the open
+    cluster that determines them (~3,500 atoms each)."""
+    from sevennet_finetuning_amd.structures import si_diamond
+    from sevennet_finetuning_amd.neighbor import DeviceNeighborList
+    pos, cell = si_diamond((cells,) * 3, sigma=0.05)
+    types = np.full(len(pos), SI)
+    dev = model.device
+    c, nb, _, vec = DeviceNeighborList(dev)(pos, cell, model.cutoff)
+    out = model.energy_forces(torch.as_tensor(types, dtype=torch.int32, device=dev), c, nb, vec)
+    eat = out['atomic_energy'].cpu().numpy()
+    del c, nb, vec, out
+    for i in centres:
+        e_ref, n = _cluster_atomic_energy(pos, cell, types, i, model.cutoff, 5)
+        assert n > 3000
+        assert abs(eat[i] - e_ref) <= 2e-5, (i, eat[i], e_ref)
