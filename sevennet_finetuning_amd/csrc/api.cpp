@@ -197,7 +197,6 @@ struct e3gnn_model {
     DBuf w0, w1, w2, w0t, w1t, w2t;
     DBuf w1p, w2p, w2q, w2r;  // MFMA-operand orders of the fused kernels (fused.h)
     DBuf w2b;            // 3-way bf16 split of w2 in 16x16x32 operand order (fused.h)
-    DBuf w2c;            // 3-way bf16 split of w2, dE/dw-kernel block pairs (fused.h)
     DBuf w2d;            // the same for the fused backward's pairs (fused.h)
     DBuf w2v;            // w2b's column blocks in visiting order (fused.h)
   };
@@ -559,9 +558,9 @@ int build_pair(LinPair& P, const Linear& a, bool ta, const Linear* b, bool tb) {
 }
 
 // Column start of every 16-channel weight block in the order the fused
-// dE/dw kernel visits them (input irrep I, channel block jj, then the paths of
-// I in instruction order): pairs of consecutive blocks form one K = 32 MFMA
-// operand (MlpW::w2c).
+// kernels visit them (input irrep I, channel block jj, then the paths of I in
+// instruction order): pairs of consecutive blocks form one K = 32 MFMA operand
+// of the lock-step backward's dH2 product (MlpW::w2d).
 template <class L>
 std::vector<int> bwd_w_block_cols() {
   std::vector<int> cols;
@@ -627,7 +626,7 @@ MlpW mlp_ptrs(const e3gnn_model* m, int t) {
   return MlpW{mm.w0.f(),  mm.w1.f(),  mm.w2.f(),  mm.w2t.f(),
               mm.w1p.f(), mm.w2p.f(), mm.w2q.f(), mm.w2r.f(),
               static_cast<const uint16_t*>(mm.w2b.p),
-              static_cast<const uint16_t*>(mm.w2c.p), static_cast<const uint16_t*>(mm.w2d.p),
+              static_cast<const uint16_t*>(mm.w2d.p),
               static_cast<const uint16_t*>(mm.w2v.p)};
 }
 
@@ -865,31 +864,13 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
                     v -= bf16_to_f32(hb);
                   }
                 }
-        // w2c (MlpW::w2c): block pair P = visited blocks (2P, 2P + 1); element t
-        // of lane (g, c) for hidden block bh is w2[16 bh + c][column of k = 8g + t]
-        // (k < 16 in block 2P, k >= 16 in block 2P + 1)
+        // the kernels' visiting order of the 16-column blocks (input irrep,
+        // channel block, path): pairs of consecutive blocks
         const std::vector<int> cols = t == 0 ? bwd_w_block_cols<LayerFirst>()
                                              : (last ? bwd_w_block_cols<LayerLast>()
                                                      : bwd_w_block_cols<LayerMid>());
         if ((int)cols.size() * 16 != W || cols.size() % 2)
           throw std::runtime_error("dE/dw block order does not cover the weights");
-        std::vector<float> c2((size_t)W * 64 * 3 / 2);
-        uint16_t* c2h = reinterpret_cast<uint16_t*>(c2.data());
-        for (size_t P = 0; P < cols.size() / 2; ++P)
-          for (int bh = 0; bh < 4; ++bh)
-            for (int g = 0; g < 4; ++g)
-              for (int c = 0; c < 16; ++c)
-                for (int t8 = 0; t8 < 8; ++t8) {
-                  const int k = 8 * g + t8;
-                  const int col = k < 16 ? cols[2 * P] + k : cols[2 * P + 1] + k - 16;
-                  float v = a2[(size_t)(16 * bh + c) * W + col];
-                  for (int pc = 0; pc < 3; ++pc) {
-                    const uint16_t hb = bf16_rne(v);
-                    c2h[(((P * 3 + pc) * 4 + bh) * 64 + g * 16 + c) * 8 + t8] = hb;
-                    v -= bf16_to_f32(hb);
-                  }
-                }
-        if (upload(mm.w2c, c2) != hipSuccess) throw std::runtime_error("upload mlp (w2c)");
         // w2d (MlpW::w2d): element t of lane (g, c) for hidden block bh is
         // w2[16 bh + c][col], col = cols[2P] + 4g + t (t < 4) or cols[2P + 1] + 4g + t - 4
         std::vector<float> d2((size_t)W * 64 * 3 / 2);

@@ -18,11 +18,8 @@ struct MlpW {
   // w2 as three bf16 pieces (w2 = p0 + p1 + p2, exact) in v_mfma_f32_16x16x32_bf16
   // operand order: [n/16][piece][m][g][c][t] = piece of w2[16(2m + t/4) + 4g + t%4][n]
   const uint16_t* w2b;
-  // the same pieces for the dE/dw kernel's K = 32 products over PAIRS of
-  // consecutive visited 16-column blocks: [pair][piece][bh][g][c][t] = piece of
-  // w2[16 bh + c][column of k = 8g + t] (api.cpp bwd_w_block_cols)
-  const uint16_t* w2c;
-  // the fused backward's (MODE 3) pairs: [pair][piece][bh][g][c][t] = piece of
+  // the lock-step backward's dH2 operand over PAIRS of consecutive visited
+  // 16-column blocks (api.cpp bwd_w_block_cols): [pair][piece][bh][g][c][t] = piece of
   // w2[16 bh + c][col], col = channel 4g + t of the pair's first block (t < 4)
   // or 4g + t - 4 of its second
   const uint16_t* w2d;

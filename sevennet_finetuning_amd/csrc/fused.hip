@@ -41,19 +41,8 @@
 #ifndef E3GNN_FWD_WAVES
 #define E3GNN_FWD_WAVES 3
 #endif
-// dE/dw kernel's dH2 = dw W2^T product: 0 f32 MFMA per block (operands
-// prefetched a block ahead), 1 bf16x6 per block pair, 2 the same with the
-// pair's operands loaded under its second block
-#ifndef E3GNN_BWDW_MODE
-#define E3GNN_BWDW_MODE 0
-#endif
 #ifndef E3GNN_BWDW_WAVES
 #define E3GNN_BWDW_WAVES 4
-#endif
-// dE/dx kernel: dE/dagg operands loaded one path block ahead (1; spills 18
-// registers at 3 waves/SIMD: 17.4 -> 20.9 ms per three launches) or at use (0)
-#ifndef E3GNN_BWDX_GMPF
-#define E3GNN_BWDX_GMPF 0
 #endif
 #ifndef E3GNN_BWDX_WAVES
 #define E3GNN_BWDX_WAVES 3
@@ -69,43 +58,6 @@
 #ifndef E3GNN_BWDXW_WAVES_FIRST
 #define E3GNN_BWDXW_WAVES_FIRST 2
 #endif
-// MODE 3 register diet (experiment): W2 bf16 operands loaded at use instead of
-// a block ahead, dH2 operands loaded per hidden block just before its MFMAs --
-// fits 3 waves/SIMD (167 VGPRs) but measured slower (+1.2 ms/step at 3 waves,
-// +4 ms at 2): the exposed load latency costs more than the occupancy gains
-#ifndef E3GNN_BWDXW_LEAN
-#define E3GNN_BWDXW_LEAN 0
-#endif
-// MODE 3 dH2 = dw W2^T product: 0 (default) f32 MFMA per block; 1 bf16x6 over
-// PAIRS of consecutive visited blocks (K = 32 channels: 24 x 16 MFMA cycles per
-// pair instead of 2 x 16 x 32) -- measured slower (57.4 -> 59.5 ms/step): the
-// kernel is bound by tensor-product VALU issue, not by the MFMA pipe, and the
-// splits and just-in-time operand loads add to the VALU side
-#ifndef E3GNN_BWDXW_DH2BF
-#define E3GNN_BWDXW_DH2BF 0
-#endif
-// dE/dx kernels: the radial weights w of the NEXT visited block are formed
-// (MFMA) before this block's tensor product (VALU), so the matrix pipe works
-// under the VALU stream instead of the tensor product waiting on it (1), or
-// w of a block just before its use (0)
-#ifndef E3GNN_BWDX_PIPE
-#define E3GNN_BWDX_PIPE 1
-#endif
-// per-centre dE/dx kernels (MODE 2/3): the tensor-product backward on packed
-// f32 over channel pairs (tp_bwd_xw_pk; 1: all products packed, 2: u_i scalar,
-// no y splat pairs), or scalar (0).  Measured on the 97k box: 25.2 (scalar) vs
-// 26.1 (1) and 25.2 (2) ms per three middle-block launches -- ~18 % fewer VALU
-// instructions buy nothing: the kernel is latency-bound at 2 waves/SIMD, not
-// VALU-issue-bound
-#ifndef E3GNN_BWDX_PK
-#define E3GNN_BWDX_PK 0
-#endif
-// forward tensor product on packed f32 over edge pairs (tp_acc_pk, 1):
-// measured 11.4 -> 12.0 ms per three middle-block launches, so off (0)
-#ifndef E3GNN_FWD_PK
-#define E3GNN_FWD_PK 0
-#endif
-
 namespace e3gnn {
 namespace {
 
@@ -151,15 +103,14 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // does not hoist hundreds of 64-bit addresses out of the centre loop (which it
 // did, and spilled).  Offsets outside the descriptor read 0 (padded rows).
 struct WRes {
-  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b, w2c, w2r, w2d, w2v;
+  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b, w2r, w2d, w2v;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int nfloats) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
 }
 __device__ __forceinline__ WRes make_wres(const MlpW& W, int width) {
   return {rsrc(W.w0, 8 * 64), rsrc(W.w1, 64 * 64), rsrc(W.w2p, 64 * width), rsrc(W.w2q, 64 * width),
-          rsrc(W.w1p, 64 * 64), rsrc((const float*)W.w2b, 64 * width * 3 / 2),
-          rsrc((const float*)W.w2c, 64 * width * 3 / 2), rsrc(W.w2r, 64 * width),
+          rsrc(W.w1p, 64 * 64), rsrc((const float*)W.w2b, 64 * width * 3 / 2), rsrc(W.w2r, 64 * width),
           rsrc((const float*)W.w2d, 64 * width * 3 / 2),
           rsrc((const float*)W.w2v, 64 * width * 3 / 2)};
 }
@@ -346,30 +297,6 @@ __device__ __forceinline__ void tp_acc(const float* x, const float* y, float w, 
   });
 #pragma unroll
   for (int k = 0; k < 2 * L3 + 1; ++k) acc[k] += w * t[k];
-}
-
-// tp_acc for two edges at once on packed f32 (v_pk_fma_f32): element 0 / 1 of
-// every pair is edge r = 2h / 2h + 1 of the lane group (E3GNN_FWD_PK)
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <int L1, int L2, int L3>
-__device__ __forceinline__ void tp_acc_pk(const f32x2* x, const f32x2* y, f32x2 w, f32x2* acc) {
-  using C = CG<L1, L2, L3>;
-  f32x2 t[2 * L3 + 1];
-#pragma unroll
-  for (int k = 0; k < 2 * L3 + 1; ++k) t[k] = f32x2{0.f, 0.f};
-  sfor<2 * L1 + 1>([&](auto i) {
-    sfor<2 * L2 + 1>([&](auto j) {
-      if constexpr (cg_pair<C, i, j>()) {
-        const f32x2 xy = x[i] * y[j];
-        sfor<C::n>([&](auto q) {
-          if constexpr (C::e[q].i == i && C::e[q].j == j)
-            t[C::e[q].k] = __builtin_elementwise_fma(f32x2{C::e[q].c, C::e[q].c}, xy, t[C::e[q].k]);
-        });
-      }
-    });
-  });
-#pragma unroll
-  for (int k = 0; k < 2 * L3 + 1; ++k) acc[k] = __builtin_elementwise_fma(w, t[k], acc[k]);
 }
 
 // The lane's four (edge or channel) slots r = 0..3 in lock-step: every CG
@@ -639,30 +566,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
               }
               phase();
               float acc[D3];
-              if constexpr (E3GNN_FWD_PK) {
-                // edge pairs (0, 1), (2, 3) of the lane group on packed f32
-                f32x2 accp[D3];
-#pragma unroll
-                for (int k = 0; k < D3; ++k) accp[k] = f32x2{0.f, 0.f};
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                  f32x2 xp[D1], yp[D2];
-#pragma unroll
-                  for (int i = 0; i < D1; ++i) xp[i] = f32x2{x[2 * h][i], x[2 * h + 1][i]};
-#pragma unroll
-                  for (int q = 0; q < D2; ++q)
-                    yp[q] = f32x2{ybuf[(4 * g + 2 * h) * 9 + yoff(p.l2) + q],
-                                  ybuf[(4 * g + 2 * h + 1) * 9 + yoff(p.l2) + q]};
-                  tp_acc_pk<p.l1, p.l2, p.l3>(xp, yp, f32x2{wv[2 * h], wv[2 * h + 1]}, accp);
-                }
-#pragma unroll
-                for (int k = 0; k < D3; ++k) acc[k] = accp[k][0] + accp[k][1];
-              } else {
 #pragma unroll
               for (int k = 0; k < D3; ++k) acc[k] = 0.f;
               // the lane's 4 edges in lock-step (padded edges have Y = 0)
               tp_acc4<p.l1, p.l2, p.l3>(&x[0][0], ybuf + 4 * g * 9 + yoff(p.l2), 9, wv, acc);
-              }
 #pragma unroll
               for (int k = 0; k < D3; ++k) {
                 float v = acc[k];
@@ -768,97 +675,6 @@ __device__ __forceinline__ float tp_bwd_xw(const float* x, const float* y, float
   return dwv;
 }
 
-// first CG entry of pair (I, J); first J of row I with an entry (-1: none)
-template <class C, int I, int J>
-__device__ __forceinline__ constexpr int cg_first_q() {
-  for (int q = 0; q < C::n; ++q)
-    if (C::e[q].i == I && C::e[q].j == J) return q;
-  return -1;
-}
-template <class C, int I, int D2>
-__device__ __forceinline__ constexpr int cg_first_j() {
-  for (int j = 0; j < D2; ++j)
-    for (int q = 0; q < C::n; ++q)
-      if (C::e[q].i == I && C::e[q].j == j) return j;
-  return -1;
-}
-// tp_bwd_xw of a lane's 4 channels on packed f32 (v_pk_fma_f32: two lanes of
-// work per VALU issue): channels (0, 1) and (2, 3) of the lane's block form the
-// pairs h = 0, 1.  The CG contraction t'_ij and the u_i / dE/dY products run
-// packed; the per-(i, channel) dE/dx, dE/dw and w x_i products stay scalar
-// (their operands are not pair-adjacent in the [channel][component] layout).
-// gl: the centre's dE/dagg of the block, [D3][4 channels] (LDS, staged so).
-template <class C, int J, int D1>
-__device__ __forceinline__ constexpr int cg_first_i() {
-  for (int i = 0; i < D1; ++i)
-    for (int q = 0; q < C::n; ++q)
-      if (C::e[q].i == i && C::e[q].j == J) return i;
-  return -1;
-}
-template <int L1, int L2, int L3, bool FW>
-__device__ __forceinline__ void tp_bwd_xw_pk(const float* x, const float* y, const f32x4 w,
-                                             const float* gl, float* dx, float* dy, float* dwr) {
-  using C = CG<L1, L2, L3>;
-  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
-  f32x2 gp[2][D3];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int k = 0; k < D3; ++k) gp[h][k] = f32x2{gl[4 * k + 2 * h], gl[4 * k + 2 * h + 1]};
-  f32x2 dyp[D2];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) dwr[r] = 0.f;
-  sfor<D1>([&](auto i) {
-    constexpr int J0 = cg_first_j<C, i, D2>();
-    if constexpr (J0 >= 0) {
-      f32x2 wx[2], u[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        wx[h] = f32x2{w[2 * h] * x[2 * h * D1 + i], w[2 * h + 1] * x[(2 * h + 1) * D1 + i]};
-      sfor<D2>([&](auto j) {
-        constexpr int Q0 = cg_first_q<C, i, j>();
-        if constexpr (Q0 >= 0) {
-          const f32x2 yj = f32x2{y[j], y[j]};
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            f32x2 tp = C::e[Q0].c * gp[h][C::e[Q0].k];
-            sfor<C::n>([&](auto q) {
-              if constexpr (q > Q0 && C::e[q].i == i && C::e[q].j == j)
-                tp = __builtin_elementwise_fma(f32x2{C::e[q].c, C::e[q].c}, gp[h][C::e[q].k], tp);
-            });
-            if constexpr (E3GNN_BWDX_PK == 2) {  // u scalar: no y splat pairs
-#pragma unroll
-              for (int e = 0; e < 2; ++e) {
-                if constexpr (j == J0) u[h][e] = tp[e] * y[j];
-                else u[h][e] += tp[e] * y[j];
-              }
-            } else if constexpr (j == J0) {
-              u[h] = tp * yj;
-            } else {
-              u[h] = __builtin_elementwise_fma(tp, yj, u[h]);
-            }
-            if constexpr (L2 > 0) {
-              if (h == 0 && cg_first_i<C, j, D1>() == (int)i) dyp[j] = tp * wx[h];
-              else dyp[j] = __builtin_elementwise_fma(tp, wx[h], dyp[j]);
-            }
-          }
-        }
-      });
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float ur = u[r >> 1][r & 1];
-        dx[r * D1 + i] += w[r] * ur;
-        if constexpr (FW) dwr[r] += x[r * D1 + i] * ur;
-      }
-    }
-  });
-  if constexpr (L2 > 0) {
-    sfor<D2>([&](auto j) {
-      if constexpr (cg_first_i<C, j, D1>() >= 0) dy[j] += dyp[j][0] + dyp[j][1];
-    });
-  }
-}
-
 // sum over the 16 lanes of a DPP row (fixed order; every lane gets the total)
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float x) {
@@ -880,24 +696,6 @@ __device__ __forceinline__ void load_gm(float* gmN, __amdgpu_buffer_rsrc_t Rg, i
   constexpr int D3 = 2 * L::P[PN].l3 + 1;
   ldv<4 * D3>(Rg, vg + 4 * g * D3 * 4, (L::P[PN].moff + 16 * jj * D3) * 4, gmN);
 }
-// issue the loads of the block after (I, jj, PI) in visiting order (if any)
-template <class L, int I, int PI>
-__device__ __forceinline__ void prefetch_gm(float* gmN, __amdgpu_buffer_rsrc_t Rg, int vg, int g,
-                                            int jj) {
-  constexpr int np = next_path_same_I<L>(PI);
-  if constexpr (np >= 0) {
-    load_gm<L, np>(gmN, Rg, vg, g, jj);
-  } else {
-    constexpr int f = first_path_of<L>(I);
-    constexpr int fn = first_path_after_I<L>(I);
-    if (jj + 1 < L::P[f].mul / 16) {
-      load_gm<L, f>(gmN, Rg, vg, g, jj + 1);
-    } else {
-      if constexpr (fn >= 0) load_gm<L, fn>(gmN, Rg, vg, g, 0);
-    }
-  }
-}
-
 // MLP chain backward of a 16-edge tile [e0, min(e0 + 16, end)) from dH2^T
 // (D[hidden 16 bh + 4g + r][edge slot c]): pre-activations recomputed, dA2,
 // dH1^T = W1 dA2^T, demb^T = W0 dA1^T, demb += (rows < 8)
@@ -948,31 +746,18 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
   }
 }
 
-// W2 pieces of the fused backward's dH2 product for block pair P, hidden block
-// bh (w2d order: [P][piece][bh][g][c][t] = piece of w2[16 bh + c][column of
-// element t of lane group g], MlpW::w2d)
-__device__ __forceinline__ void load_w2d(bf16x8 (&a)[3], __amdgpu_buffer_rsrc_t w2d, int lane, int P,
-                                         int bh) {
-#pragma unroll
-  for (int pc = 0; pc < 3; ++pc)
-    a[pc] = __builtin_bit_cast(
-        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2d, lane * 16, ((P * 3 + pc) * 4 + bh) * 1024, 0));
-}
-
 // B1: lane (g, c) = edge slot c of the tile x channels 4g..4g+3 of a 16-channel
 // block (transposed product w^T = W2^T H2^T: D[channel 4g+r][edge c]).  One
-// edge per lane keeps dE/dY in 8 registers; dE/dx[j] is summed over the 16
-// edge lanes of a row (DPP) once per block and accumulated in LDS.
-// MODE 0: one wave per NEIGHBOUR node over its incoming edges, dE/dx[j]
-// summed in LDS and written once.
-// MODE 1: one wave per fixed tile of 16 consecutive (CSR-order) edges -- the
-// centres' dE/dagg rows are then read in order (L2-resident) rather than
-// scattered -- and dE/dx is written per edge to dxc (summed per neighbour by
-// the transposed-CSR gather).
+// edge per lane keeps dE/dY in 8 registers.
+// MODE 0: one wave per NEIGHBOUR node over its incoming edges (transposed CSR),
+// dE/dx[j] summed over the 16 edge lanes of a row (DPP) once per block,
+// accumulated in LDS and written once (the last block).
 // MODE 2: one wave per CENTRE over its CSR edges in tiles of 16 (the forward
-// kernel's mapping), the centre's dE/dagg row (DM floats) staged in LDS once:
-// the 60 per-path-block dE/dagg reads of a middle block become LDS reads
-// instead of dependent global gathers; dE/dx per edge to dxc as in MODE 1.
+// kernel's mapping), the centre's dE/dagg row (DM floats) staged in LDS once;
+// dE/dx per edge to dxc (summed per neighbour by the transposed-CSR gather).
+// MODE 3: MODE 2 + dE/dw -> dH2 -> MLP chain -> dE/demb from the same registers.
+// The radial weights w of the NEXT visited block are formed (MFMA) before this
+// block's tensor product (VALU), so the matrix pipe works under the VALU stream.
 template <class L, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ? (L::DX == 128 ? E3GNN_BWDXW_WAVES_FIRST : E3GNN_BWDXW_WAVES) : E3GNN_BWDX_WAVES, MODE == 3 ? (L::DX == 128 ? E3GNN_BWDXW_WAVES_FIRST : E3GNN_BWDXW_WAVES) : E3GNN_BWDX_WAVES))) void k_conv_bwd_x(const int* __restrict__ src_ptr,
                                                     const int* __restrict__ src_perm,
@@ -987,75 +772,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
                                                     float* __restrict__ dxc, int n_edges,
                                                     const int* __restrict__ row_ptr, int r_begin,
                                                     int r_end, float* __restrict__ demb) {
-  constexpr bool EDGE = MODE != 0;  // per-edge dE/dx output (dxc)
-  constexpr bool CTR = MODE >= 2;   // one wave per centre, dE/dagg row in LDS
+  static_assert(MODE == 0 || MODE == 2 || MODE == 3, "backward modes 0, 2, 3");
+  constexpr bool EDGE = MODE != 0;  // per-edge dE/dx output (dxc), one wave per centre
   constexpr bool FW = MODE == 3;    // + dE/dw -> dH2 -> MLP chain -> dE/demb
-  // MODE 0: dE/dx[j] of the wave's node; MODE 2: dE/dagg row of its centre
-  __shared__ __attribute__((aligned(16))) float lds[4][MODE == 0 ? L::DX : (CTR ? L::DM : 1)];
+  // MODE 0: dE/dx[j] of the wave's node; MODE 2/3: dE/dagg row of its centre
+  __shared__ __attribute__((aligned(16))) float lds[4][MODE == 0 ? L::DX : L::DM];
   const int wid = threadIdx.x >> 6;
-  // wave index: node (MODE 0), 16-edge tile of [r_begin, r_end) (MODE 1), centre (MODE 2)
-  const int jn = __builtin_amdgcn_readfirstlane((MODE == 1 ? 0 : r_begin) + xcd_block() * 4 + wid);
-  if (MODE == 1 ? r_begin + jn * 16 >= r_end : jn >= r_end) return;
+  // wave index: node (MODE 0) or centre (MODE 2/3)
+  const int jn = __builtin_amdgcn_readfirstlane(r_begin + xcd_block() * 4 + wid);
+  if (jn >= r_end) return;
   float* dacc = lds[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
-  const int qb = MODE == 1 ? r_begin + jn * 16 : (CTR ? row_ptr[jn] : src_ptr[jn]);
-  const int qe = MODE == 1 ? min(qb + 16, r_end) : (CTR ? row_ptr[jn + 1] : src_ptr[jn + 1]);
-  if constexpr (CTR) {
+  const int qb = EDGE ? row_ptr[jn] : src_ptr[jn];
+  const int qe = EDGE ? row_ptr[jn + 1] : src_ptr[jn + 1];
+  if constexpr (EDGE) {
     // stage the centre's dE/dagg row: DM / 4 float4 per wave, all in flight
     const float4* src = reinterpret_cast<const float4*>(gagg + (int64_t)jn * L::DM);
-    if constexpr (E3GNN_BWDX_PK && !E3GNN_BWDX_GMPF) {
-      // packed tensor product (tp_bwd_xw_pk): every 4-channel x D3 group of a
-      // path segment stored [component][channel], so the channel pairs (0, 1)
-      // and (2, 3) of a component are aligned register pairs of one b128 read
-      sfor<L::NP>([&](auto pi) {
-        constexpr PathDef p = L::P[pi];
-        constexpr int D3 = 2 * p.l3 + 1, Q = 4 * D3;
-        for (int t4 = lane; t4 < p.mul * D3 / 4; t4 += 64) {
-          const float4 v = src[p.moff / 4 + t4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int t = 4 * t4 + e, quad = t / Q, within = t - quad * Q;
-            const int r = within / D3, k = within - r * D3;
-            dacc[p.moff + quad * Q + 4 * k + r] = v[e];
-          }
-        }
-      });
-    } else {
-      float4* dst = reinterpret_cast<float4*>(dacc);
-      for (int t = lane; t < L::DM / 4; t += 64) dst[t] = src[t];
-    }
+    float4* dst = reinterpret_cast<float4*>(dacc);
+    for (int t = lane; t < L::DM / 4; t += 64) dst[t] = src[t];
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
   }
   const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rx =
       EDGE ? rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4) : rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
-  // dE/dagg rows through a descriptor (32-bit lane offsets, scalar
-  // path/channel offsets).  EDGE: based at the tile's first centre -- 16
-  // consecutive CSR edges span at most 16 centres, so the offsets stay small
-  // at any system size; per neighbour node (last block, DM = 224): whole array
-  // (the host checks n_centers * 224 * 4 < 2^31)
-  const __amdgpu_buffer_rsrc_t RgAll = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
+  // MODE 0: the edges' centres' dE/dagg rows through a descriptor over the
+  // whole array (32-bit lane offsets; DM = 224, the host checks
+  // n_centers * 224 * 4 < 2^31); padded slots read past its end: 0
+  const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
   if constexpr (MODE == 0)
     for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
 
   for (int q0 = qb; q0 < qe; q0 += 16) {
     phase();
     Op3 wq;
-    if (!(FW && E3GNN_BWDXW_LEAN)) load_w2b(wq, R.w2b, lane, L::P[0].woff);
+    load_w2b(wq, R.w2b, lane, L::P[0].woff);
     // edge of slot c
     const int er = (q0 + col < qe) ? (EDGE ? q0 + col : src_perm[q0 + col]) : -1;
     // EDGE: the slot's gathered row (padded slots: row 0, w = 0 there)
     const int vx = EDGE ? (er >= 0 ? nbr[er] : 0) * L::DX * 4 : 0;
-    int cb = 0, nc = n_centers;  // centre rows [cb, cb + nc) under the descriptor
-    if constexpr (MODE == 1) {
-      cb = __builtin_amdgcn_readfirstlane(center[q0]);
-      nc = __builtin_amdgcn_readfirstlane(center[qe - 1]) - cb + 1;
-    }
-    const __amdgpu_buffer_rsrc_t Rg =
-        MODE == 1 ? rsrc_bytes(gagg + (int64_t)cb * L::DM, (int64_t)nc * L::DM * 4) : RgAll;
-    // padded slots read past the end of the descriptor: 0
-    const int vg = (er >= 0 ? (center[er] - cb) * L::DM : nc * L::DM) * 4;
+    const int vg = (er >= 0 ? center[er] * L::DM : n_centers * L::DM) * 4;
     float y[9];
 #pragma unroll
     for (int q = 0; q < 9; ++q) y[q] = er >= 0 ? Y[(int64_t)er * 9 + q] : 0.f;
@@ -1076,25 +832,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
     // MODE 3: dH2^T of the tile's edges (D[hidden 16 bh + 4g + r][edge c]),
     // accumulated over the visited blocks
     f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
-    constexpr bool DBF = FW && E3GNN_BWDXW_DH2BF;
-    int nb = 0;     // visited blocks of the tile (DBF: pairs (2P, 2P + 1))
-    // PIPE: w of the current block (formed during the previous one) and of the
+    int nb = 0;     // visited blocks of the tile
+    // w of the current block (formed during the previous one) and of the
     // next; wq then holds the operand of the block after the next (w2v: the
     // bf16 pieces in visiting order, block nb at column 16 nb)
-    constexpr bool PIPE = E3GNN_BWDX_PIPE && !E3GNN_BWDXW_LEAN;
     constexpr int NBLK = L::W / 16;
-    f32x4 wcur = zero4(), wnxt = zero4();
-    if constexpr (PIPE) {
-      wcur = w2_block<false>(hq, wq);
-      if (NBLK > 1) load_w2b(wq, R.w2v, lane, 16);
-    }
-    float dwp[4];   // DBF: dE/dw of the pair's first block
+    f32x4 wcur = w2_block<false>(hq, wq), wnxt = zero4();
+    if (NBLK > 1) load_w2b(wq, R.w2v, lane, 16);
     float dYa[9];  // dE/dY of edge c over this lane's channels (index 0 unused)
 #pragma unroll
     for (int q = 0; q < 9; ++q) dYa[q] = 0.f;
-    // dE/dagg operands run one path block ahead of their use (software pipeline)
-    float gmN[20];
-    if constexpr (E3GNN_BWDX_GMPF) load_gm<L, 0>(gmN, Rg, vg, g, 0);
 
     sfor<3>([&](auto I) {
       constexpr int MUL = iblock_mul<L, I>();
@@ -1112,19 +859,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
             if constexpr (p.l1 == I) {
               constexpr int D3 = 2 * p.l3 + 1;
               phase();
-              // dE/dagg of the edges' centres (loaded during the previous block);
-              // the next block's are issued now
-              constexpr bool PK = CTR && E3GNN_BWDX_PK && !E3GNN_BWDX_GMPF;
+              // dE/dagg of the edges' centres: the centre's row in LDS (4 D3
+              // contiguous floats per lane group), or gathered (MODE 0)
               float gm[4 * D3];
-              // PK: the block's 4 D3 values are read from LDS in pair order inside
-              const float* glb = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
-              if constexpr (PK) {
-              } else if constexpr (E3GNN_BWDX_GMPF) {
-#pragma unroll
-                for (int k = 0; k < 4 * D3; ++k) gm[k] = gmN[k];
-                prefetch_gm<L, I, pi>(gmN, Rg, vg, g, jj);
-              } else if constexpr (CTR) {
-                // the centre's row in LDS: 4 D3 contiguous floats per lane group
+              if constexpr (EDGE) {
                 const float* gl = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
 #pragma unroll
                 for (int k = 0; k < 4 * D3; ++k) gm[k] = gl[k];
@@ -1134,43 +872,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
               // MODE 3: W2 operands of this block's dH2 product, issued now and
               // consumed after the tensor product
               f32x4 bq[4];
-              if constexpr (FW && !DBF && !E3GNN_BWDXW_LEAN) load_w2q(bq, R.w2r, lane, p.woff + 16 * jj);
-              // DBF: the pair's W2 pieces (hidden block 0, or all four with
-              // E3GNN_BWDXW_DH2BF == 2), issued at its second block under its TP
-              bf16x8 pa[3];
-              bf16x8 pall[E3GNN_BWDXW_DH2BF == 2 ? 4 : 1][3];
-              if constexpr (DBF) {
-                if (nb & 1) {
-                  if constexpr (E3GNN_BWDXW_DH2BF == 2) {
-#pragma unroll
-                    for (int bh = 0; bh < 4; ++bh) load_w2d(pall[bh], R.w2d, lane, nb >> 1, bh);
-                  } else {
-                    load_w2d(pa, R.w2d, lane, nb >> 1, 0);
-                  }
-                }
-              }
+              if constexpr (FW) load_w2q(bq, R.w2r, lane, p.woff + 16 * jj);
               float dwr[4];
-              if constexpr (FW && E3GNN_BWDXW_LEAN) load_w2b(wq, R.w2b, lane, p.woff + 16 * jj);
               // w^T block: A = W2s[:, col0 + i]^T (w2p order), B = H2^T
-              f32x4 wv;
-              if constexpr (PIPE) {
-                wv = wcur;
-                if (nb + 1 < NBLK) wnxt = w2_block<false>(hq, wq);
-                if (nb + 2 < NBLK) load_w2b(wq, R.w2v, lane, 16 * (nb + 2));
-              } else {
-                wv = w2_block<false>(hq, wq);
-              }
-              if constexpr (!PIPE && !(FW && E3GNN_BWDXW_LEAN)) {
-                const int nc = next_block_col<L, I, pi>(jj);
-                if (nc >= 0) load_w2b(wq, R.w2b, lane, nc);
-              }
-              if constexpr (PK) {
-                phase();
-                tp_bwd_xw_pk<p.l1, p.l2, p.l3, FW>(x, y + yoff(p.l2), wv, glb, dx, dYa + yoff(p.l2),
-                                                   dwr);
-                pin<4 * D1>(dx);
-                pin<8>(dYa + 1);
-              } else
+              const f32x4 wv = wcur;
+              if (nb + 1 < NBLK) wnxt = w2_block<false>(hq, wq);
+              if (nb + 2 < NBLK) load_w2b(wq, R.w2v, lane, 16 * (nb + 2));
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 phase();
@@ -1193,61 +900,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
               }
               pin<4 * D1>(dx);
               pin<8>(dYa + 1);
-              if constexpr (DBF) {
-                if (nb & 1) {
-                  // dH2^T += W2[:, pair] dw^T, K = 32: element t of lane (g, c) is
-                  // channel 4g + t of the first block (t < 4) or 4g + t - 4 of the second
-                  bf16x8 d[3];
-#pragma unroll
-                  for (int t = 0; t < 8; ++t) {
-                    float v = t < 4 ? dwp[t] : dwr[t - 4];
-#pragma unroll
-                    for (int pc = 0; pc < 3; ++pc) {
-                      const __bf16 b = (__bf16)v;
-                      d[pc][t] = b;
-                      v -= (float)b;
-                    }
-                  }
-                  constexpr int PI_[6] = {2, 1, 0, 1, 0, 0}, PJ_[6] = {0, 1, 2, 0, 1, 0};
-                  if constexpr (E3GNN_BWDXW_DH2BF == 2) {
-#pragma unroll
-                    for (int bh = 0; bh < 4; ++bh)
-#pragma unroll
-                      for (int q = 0; q < 6; ++q)
-                        dh2[bh] = mfma16(pall[bh][PI_[q]], d[PJ_[q]], dh2[bh]);
-                  } else {
-#pragma unroll
-                  for (int bh = 0; bh < 4; ++bh) {
-                    bf16x8 pn[3];
-                    if (bh < 3) load_w2d(pn, R.w2d, lane, nb >> 1, bh + 1);
-#pragma unroll
-                    for (int q = 0; q < 6; ++q) dh2[bh] = mfma16(pa[PI_[q]], d[PJ_[q]], dh2[bh]);
-                    if (bh < 3) {
-#pragma unroll
-                      for (int pc = 0; pc < 3; ++pc) pa[pc] = pn[pc];
-                    }
-                  }
-                  }
-                } else {
-#pragma unroll
-                  for (int r = 0; r < 4; ++r) dwp[r] = dwr[r];
-                }
-                ++nb;
-              } else if constexpr (FW) {
+              if constexpr (FW) {
                 // dH2^T += W2[:, block] dw^T: k = lane group g, channel 4g + r
 #pragma unroll
-                for (int bh = 0; bh < 4; ++bh) {
-                  if constexpr (E3GNN_BWDXW_LEAN)
-                    bq[bh] = ldw4(R.w2r, ((lane >> 4) * 16 + (lane & 15)) * 16,
-                                  ((p.woff + 16 * jj) / 16 * 4 + bh) * 1024);
+                for (int bh = 0; bh < 4; ++bh)
 #pragma unroll
                   for (int r = 0; r < 4; ++r) dh2[bh] = mfma(bq[bh][r], dwr[r], dh2[bh]);
-                }
               }
-              if constexpr (PIPE) {
-                wcur = wnxt;
-                if constexpr (!DBF) ++nb;   // (DBF counts its pairs above)
-              }
+              wcur = wnxt;
+              ++nb;
             }
           });
           phase();
@@ -1308,12 +969,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
 constexpr int DWS = 20;       // row stride (16-byte aligned rows for b128 reads)
 constexpr int DWB = 16 * DWS;
 
-// dH2^T += W2[:, pair] dw^T over the block pair P (visited blocks 2P, 2P + 1 in
-// LDS buffers 0 and 1): K = 32 (lane groups 0-1: block 2P, 2-3: block 2P + 1)
-// v_mfma_f32_16x16x32_bf16 with both operands split in three bf16 pieces and the
-// six products with i + j <= 2 (see w2_block): 24 MFMAs x 16 cycles per pair
-// instead of 32 x 32 on v_mfma_f32_16x16x4_f32.
-// dH2^T += W2[:, block] dw^T on v_mfma_f32_16x16x4_f32 (E3GNN_BWDW_MODE 0;
+// dH2^T += W2[:, block] dw^T on v_mfma_f32_16x16x4_f32 (operands prefetched a block ahead;
 // w2q[col0/16][bh][g][c][s] = W2s[16 bh + c][col0 + 4s + g])
 __device__ __forceinline__ void mfma_dw(f32x4 (&dh2)[4], const f32x4 (&bq)[4], const float* dwb,
                                         int lane) {
@@ -1322,42 +978,6 @@ __device__ __forceinline__ void mfma_dw(f32x4 (&dh2)[4], const f32x4 (&bq)[4], c
   for (int bh = 0; bh < 4; ++bh)
 #pragma unroll
     for (int s = 0; s < 4; ++s) dh2[bh] = mfma(bq[bh][s], dwb[c * DWS + 4 * s + g], dh2[bh]);
-}
-
-struct PairW {
-  bf16x8 a[4][3];  // [bh][piece]
-};
-__device__ __forceinline__ void load_pair(PairW& w, __amdgpu_buffer_rsrc_t w2c, int P, int lane) {
-#pragma unroll
-  for (int bh = 0; bh < 4; ++bh)
-#pragma unroll
-    for (int pc = 0; pc < 3; ++pc)
-      w.a[bh][pc] = __builtin_bit_cast(
-          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2c, lane * 16, ((P * 3 + pc) * 4 + bh) * 1024, 0));
-}
-__device__ __forceinline__ void mfma_pair(f32x4 (&dh2)[4], const PairW& w, const float* dwb, int lane) {
-  const int g = lane >> 4, c = lane & 15;
-  const float* src = dwb + (g >> 1) * DWB + c * DWS + 8 * (g & 1);
-  bf16x8 d[3];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * h);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      float x = v[t];
-#pragma unroll
-      for (int pc = 0; pc < 3; ++pc) {
-        const __bf16 b = (__bf16)x;
-        d[pc][4 * h + t] = b;
-        x -= (float)b;
-      }
-    }
-  }
-  constexpr int I[6] = {2, 1, 0, 1, 0, 0}, J[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-  for (int bh = 0; bh < 4; ++bh)
-#pragma unroll
-    for (int q = 0; q < 6; ++q) dh2[bh] = mfma16(w.a[bh][I[q]], d[J[q]], dh2[bh]);
 }
 
 template <class L>
@@ -1397,9 +1017,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_
   for (int r = 0; r < 4; ++r) vh[r] = src[r] * L::DX * 4;
   f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
   int nb = 0;  // visited blocks; block b's dE/dw goes to LDS buffer b & 1
-  PairW pw;    // W2 operands of the pair (modes 1, 2)
-  f32x4 bq[4];  // W2 operands of the next block (mode 0)
-  if constexpr (E3GNN_BWDW_MODE == 0) load_w2q(bq, R.w2q, lane, L::P[0].woff);
+  f32x4 bq[4];  // W2 operands of the next block
+  load_w2q(bq, R.w2q, lane, L::P[0].woff);
 
   sfor<3>([&](auto I) {
     constexpr int MUL = iblock_mul<L, I>();
@@ -1424,19 +1043,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               ldv<D3>(Rg, vg[r] + col * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm[r]);
-            if constexpr (E3GNN_BWDW_MODE == 0) {
-              if (nb > 0) {
-                mfma_dw(dh2, bq, dwbuf + ((nb - 1) & 1) * DWB, lane);
-                load_w2q(bq, R.w2q, lane, p.woff + 16 * jj);
-              }
-            } else if constexpr (E3GNN_BWDW_MODE == 1) {
-              if (nb > 0 && (nb & 1) == 0) {
-                load_pair(pw, R.w2c, nb / 2 - 1, lane);
-                mfma_pair(dh2, pw, dwbuf, lane);
-              }
-            } else {
-              if (nb & 1) load_pair(pw, R.w2c, nb / 2, lane);
-              else if (nb > 0) mfma_pair(dh2, pw, dwbuf, lane);
+            if (nb > 0) {
+              mfma_dw(dh2, bq, dwbuf + ((nb - 1) & 1) * DWB, lane);
+              load_w2q(bq, R.w2q, lane, p.woff + 16 * jj);
             }
             phase();
             float* dwc = dwbuf + (nb & 1) * DWB;
@@ -1456,12 +1065,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_
   });
 
   phase();
-  if constexpr (E3GNN_BWDW_MODE == 0) {
-    mfma_dw(dh2, bq, dwbuf + ((nb - 1) & 1) * DWB, lane);  // last block
-  } else {
-    if constexpr (E3GNN_BWDW_MODE == 1) load_pair(pw, R.w2c, nb / 2 - 1, lane);
-    mfma_pair(dh2, pw, dwbuf, lane);  // last pair
-  }
+  mfma_dw(dh2, bq, dwbuf + ((nb - 1) & 1) * DWB, lane);  // last block
   // ---- MLP chain backward (pre-activations recomputed)
   phase();
   mlp_bwd_chain(R, emb, e0, end, lane, dh2, demb);
@@ -1885,11 +1489,6 @@ static hipError_t fwd_impl(const FusedArgs& a, hipStream_t s) {
                      a.Y, a.h, a.agg, a.W, a.c_begin, a.c_end, a.n_nodes, a.denom);
   return hipGetLastError();
 }
-// E3GNN_BWDX_MODE: 2 (default) per-centre tiles with the dE/dagg row in LDS,
-// 1 fixed 16-edge tiles with gathered dE/dagg (round-1 kernel)
-#ifndef E3GNN_BWDX_MODE
-#define E3GNN_BWDX_MODE 2
-#endif
 template <class L>
 static hipError_t bwd_x_impl(const FusedArgs& a, hipStream_t s) {
   if (a.n_nodes <= 0 || a.n_edges <= 0) return hipSuccess;
@@ -1901,20 +1500,13 @@ static hipError_t bwd_x_impl(const FusedArgs& a, hipStream_t s) {
                          a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
                          a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr, a.c_begin,
                          a.c_end, a.demb);
-    } else if (E3GNN_BWDX_MODE == 2) {
+    } else {   // dE/dx and dE/du only (the separate dE/dw kernel follows)
       const int nc = a.c_end - a.c_begin;
       if (nc <= 0) return hipSuccess;
       hipLaunchKernelGGL((k_conv_bwd_x<L, 2>), dim3((nc + 3) / 4), dim3(256), 0, s, a.src_ptr,
                          a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
                          a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr, a.c_begin,
                          a.c_end, a.demb);
-    } else {
-      const int tiles = (a.e_end - a.e_begin + 15) / 16;
-      if (tiles <= 0) return hipSuccess;
-      hipLaunchKernelGGL((k_conv_bwd_x<L, 1>), dim3((tiles + 3) / 4), dim3(256), 0, s, a.src_ptr,
-                         a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
-                         a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr, a.e_begin,
-                         a.e_end, a.demb);
     }
     return hipGetLastError();
   }

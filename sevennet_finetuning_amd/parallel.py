@@ -194,17 +194,21 @@ class Halo:
             o = torch.empty(out.shape, dtype=out.dtype)
             w = dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group,
                                        async_op=True)
-            return (w, o, out)
+            return [w, o, out]
         w = dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group,
                                    async_op=True)
-        return (w, None, out)
+        return [w, None, out]
 
     @staticmethod
     def _a2a_wait(h):
+        """Complete an all_to_all started by _a2a_start (idempotent)."""
+        if h[0] is None:
+            return
         w, o, out = h
         w.wait()
         if o is not None:
             out.copy_(o)
+        h[0] = None
 
     def forward_start(self, kind, t):
         """Ghost rows of buffer (kind, t) <- their owners' rows: pack + start."""
@@ -374,20 +378,26 @@ class ParallelE3GNN:
 
     def _exchange(self, start, finish, kind, t, timing):
         """Start an exchange (overlapped: the caller finishes it later).  With
-        ``timing`` (a dict) the exchange instead runs to completion on its own,
-        ranks aligned by a barrier and the device synchronised around it, and
-        its wall time is added to timing['exchange_s']."""
+        ``timing`` (a dict) the exchange's communication instead runs to
+        completion on its own (pack + all_to_all), ranks aligned by a barrier
+        and the device synchronised around it, and its wall time is added to
+        timing['exchange_s'].  Either way the caller's ``finish`` does the
+        unpack at the same point of the evaluation, so the result is the same
+        (a reverse exchange accumulates into rows that the second part of the
+        layer backward writes first)."""
         if timing is None:
             return start(kind, t)
         self._sync()
         if dist.is_initialized() and self.rg.world > 1:
             dist.barrier(group=self.group)
         t0 = time.perf_counter()
-        finish(start(kind, t))
+        h = start(kind, t)
+        if h is not None:
+            Halo._a2a_wait(h[4])
         self._sync()
         timing['exchange_s'] = timing.get('exchange_s', 0.0) + time.perf_counter() - t0
         timing['exchanges'] = timing.get('exchanges', 0) + 1
-        return None
+        return h
 
     def evaluate(self, timing=None):
         """One evaluation.  ``timing``: a dict to fill with the wall time of

@@ -653,23 +653,27 @@ class GraphedRehearsalStep:
         side.wait_stream(torch.cuda.current_stream())
         # warm-ups are local (no collectives: the other ranks may not be
         # capturing at this step) and rolled back
+        # (restored even if a warm-up raises: a rank left non-distributed
+        # would skip its all-reduces while its peers issue theirs)
         dist_flag, tr.distributed = tr.distributed, False
-        with torch.cuda.stream(side):
-            first = not tr.optimizer.state
-            if first:   # create the optimizer state, then undo the update
-                snap0 = tr.model.flat.detach().clone()
-                tr._rehearsal_body(sb, sm, graphs)
-                with torch.no_grad():
-                    tr.model.flat.copy_(snap0)
-                for s in tr.optimizer.state.values():
-                    for v in s.values():
-                        if torch.is_tensor(v):
-                            v.zero_()
-            snap = self._state()
-            for _ in range(2):
-                tr._rehearsal_body(sb, sm, graphs)
-            self._restore(snap)
-        tr.distributed = dist_flag
+        try:
+            with torch.cuda.stream(side):
+                first = not tr.optimizer.state
+                if first:   # create the optimizer state, then undo the update
+                    snap0 = tr.model.flat.detach().clone()
+                    tr._rehearsal_body(sb, sm, graphs)
+                    with torch.no_grad():
+                        tr.model.flat.copy_(snap0)
+                    for s in tr.optimizer.state.values():
+                        for v in s.values():
+                            if torch.is_tensor(v):
+                                v.zero_()
+                snap = self._state()
+                for _ in range(2):
+                    tr._rehearsal_body(sb, sm, graphs)
+                self._restore(snap)
+        finally:
+            tr.distributed = dist_flag
         torch.cuda.current_stream().wait_stream(side)
         if not tr.distributed:
             g = torch.cuda.CUDAGraph()
