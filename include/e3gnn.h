@@ -70,7 +70,12 @@ int e3gnn_abi_version(void);
 
 /* Load weights.bin + manifest.json (this build's deploy format; replaces the
  * TorchScript archive + _extra_files, deploy.py:34-51) onto HIP device
- * `device`.  Returns NULL on failure. */
+ * `device`.  Any E3_equivariant_model deployment (pair_e3gnn.cpp:294-386
+ * loads any deployed model): SevenNet-0's architecture runs on its
+ * specialised fused kernels, every other member of the nequip family (irreps
+ * with parity, lmax <= 2, XPLOR or polynomial cutoff, raw-vector SH, linear or
+ * `nequip` self-connection, any radial MLP) on the generic engine; both serve
+ * e3gnn_energy_forces and the segment API below.  Returns NULL on failure. */
 e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int device);
 void e3gnn_free(e3gnn_model* m);
 /* _extra_files metadata: num_species, cutoff, number of interaction layers,

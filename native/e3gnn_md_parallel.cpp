@@ -11,11 +11,14 @@
 // and the two results compared -- the compiled counterpart of the Python
 // driver's decomposition tests (parallel.py).
 //
-//   e3gnn_md_parallel <weights.bin> <manifest.json> <cells> <px> <py> <pz> [reps] [sigma_A]
+//   e3gnn_md_parallel <weights.bin> <manifest.json> <cells | structure file> <px> <py> <pz> [reps] [sigma_A]
 //
 // System: cells^3 Si diamond cells (a = 5.43 A, cells >= 3 so that the box is
 // wider than two cutoffs), positions displaced by N(0, sigma) (default 0.05 A,
-// fixed seed).  Prints one JSON line: atoms, ranks, ghosts, serial and
+// fixed seed) -- or any periodic structure (any deployed model, e.g. the
+// reference's HfO2 example) from a text file: n, the 9 cell numbers (rows =
+// lattice vectors), then n lines "symbol x y z"; its neighbour list is built
+// over all periodic images (triclinic cells).  Prints one JSON line: atoms, ranks, ghosts, serial and
 // decomposed energies, max |dF|, max |d virial|, and the device ms of one
 // decomposed evaluation (mean over `reps`).
 #include <hip/hip_runtime.h>
@@ -126,6 +129,43 @@ std::vector<Edge> neighbours(const std::vector<double>& x, double L, double rc) 
   return out;
 }
 
+// full periodic neighbour list of a general (triclinic) cell over all images
+// within the cutoff (edge vec = x_j + S cell - x_i, i == j allowed for S != 0),
+// centre-sorted, (j, S) order within a centre
+std::vector<Edge> neighbours_cell(const std::vector<double>& x, const double (&cell)[3][3], double rc) {
+  const int n = (int)x.size() / 3;
+  auto cross = [](const double* a, const double* b, double* c) {
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+  };
+  double c12[3], c20[3], c01[3];
+  cross(cell[1], cell[2], c12);
+  cross(cell[2], cell[0], c20);
+  cross(cell[0], cell[1], c01);
+  const double vol = std::fabs(cell[0][0] * c12[0] + cell[0][1] * c12[1] + cell[0][2] * c12[2]);
+  const double* cr[3] = {c12, c20, c01};
+  int nk[3];
+  for (int k = 0; k < 3; ++k) {
+    const double h = vol / std::sqrt(cr[k][0] * cr[k][0] + cr[k][1] * cr[k][1] + cr[k][2] * cr[k][2]);
+    nk[k] = (int)std::ceil(rc / h) + 1;
+  }
+  std::vector<Edge> out;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j)
+      for (int a = -nk[0]; a <= nk[0]; ++a)
+        for (int b = -nk[1]; b <= nk[1]; ++b)
+          for (int c = -nk[2]; c <= nk[2]; ++c) {
+            if (i == j && a == 0 && b == 0 && c == 0) continue;
+            double d[3];
+            for (int k = 0; k < 3; ++k)
+              d[k] = x[3 * j + k] + a * cell[0][k] + b * cell[1][k] + c * cell[2][k] - x[3 * i + k];
+            if (d[0] * d[0] + d[1] * d[1] + d[2] * d[2] < rc * rc)
+              out.push_back({i, j, {(float)d[0], (float)d[1], (float)d[2]}});
+          }
+  return out;
+}
+
 // one sub-domain: owned atoms (rows [0, n_local)), ghosts by (owner, id)
 struct Rank {
   std::vector<int> owned, ghosts;           // global ids
@@ -151,7 +191,9 @@ int main(int argc, char** argv) {
                  argv[0]);
     return 2;
   }
-  const int cells = std::atoi(argv[3]);
+  const std::string sys_arg = argv[3];
+  const bool from_file = sys_arg.find_first_not_of("0123456789") != std::string::npos;
+  const int cells = from_file ? 3 : std::atoi(argv[3]);
   const int grid[3] = {std::atoi(argv[4]), std::atoi(argv[5]), std::atoi(argv[6])};
   const int reps = argc > 7 ? std::atoi(argv[7]) : 3;
   const double sigma = argc > 8 ? std::atof(argv[8]) : 0.05;
@@ -160,8 +202,6 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "e3gnn_md_parallel: need cells >= 3 and a positive grid\n");
     return 2;
   }
-  const int si = species_index(argv[2], "Si");
-  if (si < 0) die("Si not in the manifest");
   e3gnn_model* model = e3gnn_load(argv[1], argv[2], 0);
   if (!model) die("e3gnn_load");
   int nsp = 0, nlayers = 0, comm = 0;
@@ -169,23 +209,49 @@ int main(int argc, char** argv) {
   if (e3gnn_model_info(model, &nsp, &cutoff, &nlayers, &comm)) die("e3gnn_model_info");
 
   // ---- the system
-  const double a0 = 5.43, L = cells * a0;
-  const double basis[8][3] = {{0, 0, 0},       {0, .5, .5},     {.5, 0, .5},     {.5, .5, 0},
-                              {.25, .25, .25}, {.25, .75, .75}, {.75, .25, .75}, {.75, .75, .25}};
-  const int n = 8 * cells * cells * cells;
-  std::vector<double> x(3 * n);
-  std::mt19937 rng(7);
-  std::normal_distribution<double> g(0.0, sigma);
-  int q = 0;
-  for (int i = 0; i < cells; ++i)
-    for (int j = 0; j < cells; ++j)
-      for (int k = 0; k < cells; ++k)
-        for (int b = 0; b < 8; ++b, ++q) {
-          const double p[3] = {(i + basis[b][0]) * a0, (j + basis[b][1]) * a0,
-                               (k + basis[b][2]) * a0};
-          for (int c = 0; c < 3; ++c) x[3 * q + c] = std::fmod(p[c] + g(rng) + L, L);
-        }
-  const std::vector<Edge> edges = neighbours(x, L, cutoff);
+  int n = 0;
+  std::vector<double> x;
+  std::vector<int32_t> species;
+  double cell[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+  std::vector<Edge> edges;
+  if (from_file) {
+    std::ifstream f(sys_arg);
+    if (!(f >> n) || n <= 0) die("structure file: atom count");
+    for (int a = 0; a < 3; ++a)
+      for (int k = 0; k < 3; ++k)
+        if (!(f >> cell[a][k])) die("structure file: cell");
+    x.resize(3 * (size_t)n);
+    species.resize(n);
+    for (int i = 0; i < n; ++i) {
+      std::string sym;
+      if (!(f >> sym >> x[3 * i] >> x[3 * i + 1] >> x[3 * i + 2])) die("structure file: atom line");
+      species[i] = species_index(argv[2], sym);
+      if (species[i] < 0) die(("species " + sym + " not in the manifest").c_str());
+    }
+    edges = neighbours_cell(x, cell, cutoff);
+  } else {
+    const int si = species_index(argv[2], "Si");
+    if (si < 0) die("Si not in the manifest");
+    const double a0 = 5.43, L = cells * a0;
+    const double basis[8][3] = {{0, 0, 0},       {0, .5, .5},     {.5, 0, .5},     {.5, .5, 0},
+                                {.25, .25, .25}, {.25, .75, .75}, {.75, .25, .75}, {.75, .75, .25}};
+    n = 8 * cells * cells * cells;
+    x.resize(3 * (size_t)n);
+    species.assign(n, si);
+    for (int k = 0; k < 3; ++k) cell[k][k] = L;
+    std::mt19937 rng(7);
+    std::normal_distribution<double> g(0.0, sigma);
+    int q = 0;
+    for (int i = 0; i < cells; ++i)
+      for (int j = 0; j < cells; ++j)
+        for (int k = 0; k < cells; ++k)
+          for (int b = 0; b < 8; ++b, ++q) {
+            const double p[3] = {(i + basis[b][0]) * a0, (j + basis[b][1]) * a0,
+                                 (k + basis[b][2]) * a0};
+            for (int c = 0; c < 3; ++c) x[3 * q + c] = std::fmod(p[c] + g(rng) + L, L);
+          }
+    edges = neighbours(x, L, cutoff);
+  }
   const int64_t E = (int64_t)edges.size();
 
   hipStream_t s;
@@ -195,7 +261,7 @@ int main(int argc, char** argv) {
   std::vector<float> f_ser(3 * n), vir_ser(6);
   float e_ser = 0.f;
   {
-    std::vector<int32_t> ty(n, si), c(E), nb(E);
+    std::vector<int32_t> ty = species, c(E), nb(E);
     std::vector<float> v(3 * E);
     for (int64_t e = 0; e < E; ++e) {
       c[e] = edges[e].i;
@@ -220,11 +286,31 @@ int main(int argc, char** argv) {
       HIPOK(hipFree(p));
   }
 
-  // ---- decomposition: owner = brick of the wrapped position
+  // ---- decomposition: owner = brick of the wrapped fractional position
+  double inv[3][3];  // frac = x inv (rows of `cell` are the lattice vectors)
+  {
+    const double(&m)[3][3] = cell;
+    const double det = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) -
+                       m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+                       m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+    inv[0][0] = (m[1][1] * m[2][2] - m[1][2] * m[2][1]) / det;
+    inv[0][1] = (m[0][2] * m[2][1] - m[0][1] * m[2][2]) / det;
+    inv[0][2] = (m[0][1] * m[1][2] - m[0][2] * m[1][1]) / det;
+    inv[1][0] = (m[1][2] * m[2][0] - m[1][0] * m[2][2]) / det;
+    inv[1][1] = (m[0][0] * m[2][2] - m[0][2] * m[2][0]) / det;
+    inv[1][2] = (m[0][2] * m[1][0] - m[0][0] * m[1][2]) / det;
+    inv[2][0] = (m[1][0] * m[2][1] - m[1][1] * m[2][0]) / det;
+    inv[2][1] = (m[0][1] * m[2][0] - m[0][0] * m[2][1]) / det;
+    inv[2][2] = (m[0][0] * m[1][1] - m[0][1] * m[1][0]) / det;
+  }
   std::vector<int> owner(n);
   for (int i = 0; i < n; ++i) {
     int b[3];
-    for (int k = 0; k < 3; ++k) b[k] = std::min(grid[k] - 1, (int)(x[3 * i + k] / L * grid[k]));
+    for (int k = 0; k < 3; ++k) {
+      double fr = x[3 * i] * inv[0][k] + x[3 * i + 1] * inv[1][k] + x[3 * i + 2] * inv[2][k];
+      fr -= std::floor(fr);
+      b[k] = std::min(grid[k] - 1, (int)(fr * grid[k]));
+    }
     owner[i] = (b[0] * grid[1] + b[1]) * grid[2] + b[2];
   }
   std::vector<Rank> R(nranks);
@@ -259,7 +345,9 @@ int main(int argc, char** argv) {
       rk.gend[p] = nl + (int)(hi - gh.begin());
     }
     ghosts_total += (int64_t)gh.size();
-    rk.type.assign(nl + gh.size(), si);
+    rk.type.resize(nl + gh.size());
+    for (size_t a = 0; a < rk.owned.size(); ++a) rk.type[a] = species[rk.owned[a]];
+    for (size_t a = 0; a < gh.size(); ++a) rk.type[nl + a] = species[gh[a].second];
     for (size_t a = 0; a < rk.owned.size(); ++a) {
       const int i = rk.owned[a];
       for (int e = begin_of[i]; e < begin_of[i + 1]; ++e) {

@@ -26,6 +26,8 @@
 #include "../../include/e3gnn.h"
 #include "cg_tables.h"
 #include "d3.h"
+#include "dbuf.h"
+#include "generic.h"
 #include "train_ops.h"
 #include "common.h"
 #include "fused.h"
@@ -99,47 +101,6 @@ Irreps merged(const Irreps& ir) {
   return out;
 }
 
-// ------------------------------------------------------------ device buffers
-struct DBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  DBuf() = default;
-  DBuf(const DBuf&) = delete;  // owns device memory: never copied
-  DBuf& operator=(const DBuf&) = delete;
-  DBuf(DBuf&& o) noexcept : p(o.p), cap(o.cap) {
-    o.p = nullptr;
-    o.cap = 0;
-  }
-  DBuf& operator=(DBuf&& o) noexcept {
-    std::swap(p, o.p);
-    std::swap(cap, o.cap);
-    return *this;
-  }
-  ~DBuf() {
-    if (p) (void)hipFree(p);
-  }
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) {
-      (void)hipFree(p);
-      p = nullptr;
-      cap = 0;
-    }
-    size_t b = bytes < 256 ? 256 : bytes;
-    hipError_t e = hipMalloc(&p, b);
-    if (e == hipSuccess) cap = b;
-    return e;
-  }
-  float* f() const { return (float*)p; }
-  int* i() const { return (int*)p; }
-};
-
-hipError_t upload(DBuf& b, const std::vector<float>& v) {
-  hipError_t e = b.ensure(v.size() * sizeof(float));
-  if (e != hipSuccess) return e;
-  return hipMemcpy(b.p, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice);
-}
-
 // bf16 round-to-nearest-even (finite inputs) and its exact widening
 uint16_t bf16_rne(float x) {
   uint32_t u;
@@ -199,8 +160,14 @@ struct e3gnn_model {
     DBuf w2b;            // 3-way bf16 split of w2 in 16x16x32 operand order (fused.h)
     DBuf w2d;            // the same for the fused backward's pairs (fused.h)
     DBuf w2v;            // w2b's column blocks in visiting order (fused.h)
+    DBuf w1b, w1tb, w0tb;  // layer-1 / chain-backward operands, w2b order (fused.h)
   };
   std::vector<Mlp> mlp;
+  // any other nequip-family deployment: the generic engine (generic.cpp)
+  GenModel* gen = nullptr;
+  ~e3gnn_model() {
+    if (gen) gen_free(gen);
+  }
 };
 
 namespace {
@@ -253,6 +220,7 @@ double tp_flops_per_edge(int kind) {
 
 struct e3gnn_ctx {
   e3gnn_model* m;
+  GenCtx* gen = nullptr;  // the generic engine's buffers (m->gen)
   int64_t n = 0, nl = 0, E = 0;
   // halo overlap: owned centres [0, n_int) have no ghost neighbour; their
   // edges are [0, e_int) (e3gnn_set_interior, effective at graph_set)
@@ -338,6 +306,7 @@ struct e3gnn_ctx {
     pending.clear();
   }
   ~e3gnn_ctx() {
+    if (gen) gen_ctx_free(gen);
     flush();
     for (auto e : evpool) (void)hipEventDestroy(e);
   }
@@ -627,9 +596,45 @@ MlpW mlp_ptrs(const e3gnn_model* m, int t) {
               mm.w1p.f(), mm.w2p.f(), mm.w2q.f(), mm.w2r.f(),
               static_cast<const uint16_t*>(mm.w2b.p),
               static_cast<const uint16_t*>(mm.w2d.p),
-              static_cast<const uint16_t*>(mm.w2v.p)};
+              static_cast<const uint16_t*>(mm.w2v.p),
+              static_cast<const uint16_t*>(mm.w1b.p),
+              static_cast<const uint16_t*>(mm.w1tb.p),
+              static_cast<const uint16_t*>(mm.w0tb.p)};
 }
 
+}  // namespace
+
+namespace {
+GenGraph gen_graph(e3gnn_ctx* c) {
+  return GenGraph{c->n, c->nl, c->E, c->type.i(), c->nbr.i(), c->vec.f(), c->row_ptr.i(),
+                  c->src_ptr.i(), c->src_perm.i(), c->err.i()};
+}
+
+// The SevenNet-0 architecture test (the same knobs as nn.sevennet0_kinds, plus
+// what the specialised kernels hard-code: 5 blocks, 8 Bessel functions, a
+// 64-64 radial MLP)
+bool is_sevennet0(const minijson::Value& man) {
+  if (man.has("is_parity") && man["is_parity"].boolean()) return false;
+  const int lmax = man.has("lmax_edge") ? (int)man["lmax_edge"].num()
+                                        : (man.has("lmax") ? (int)man["lmax"].num() : 2);
+  if (lmax != 2) return false;
+  if (man.has("sh_normalize") && !man["sh_normalize"].boolean()) return false;
+  if (man.has("self_connection_type") && man["self_connection_type"].str() != "linear") return false;
+  if (!man.has("cutoff_function") || man["cutoff_function"]["name"].str() != "XPLOR") return false;
+  if ((int)man["num_convolution_layer"].num() != 5) return false;
+  if (man.has("weight_nn_hidden_neurons")) {
+    const auto& h = man["weight_nn_hidden_neurons"].arr();
+    if (h.size() != 2 || (int)h[0].num() != 64 || (int)h[1].num() != 64) return false;
+  }
+  if (man.has("radial_basis") && man["radial_basis"].has("num") && (int)man["radial_basis"]["num"].num() != 8)
+    return false;
+  const auto& ir = man["irreps_manual"].arr();
+  const std::string mid = "128x0e+64x1e+32x2e";
+  if (ir.size() != 6 || ir[0].str() != "128x0e" || ir[5].str() != "128x0e") return false;
+  for (int t = 1; t < 5; ++t)
+    if (ir[t].str() != mid) return false;
+  return true;
+}
 }  // namespace
 
 extern "C" {
@@ -676,9 +681,19 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
   try {
     if (man["model_type"].str() != "E3_equivariant_model")
       throw std::runtime_error("unsupported model_type");
+    // SevenNet-0's architecture runs on the specialised kernels below; every
+    // other member of the family on the generic engine (generic.cpp)
+    if (!is_sevennet0(man)) {
+      m->gen = gen_load(man, flat);
+      m->nsp = gen_num_species(m->gen);
+      m->nlayer = gen_num_layers(m->gen);
+      m->cutoff = gen_cutoff(m->gen);
+      trace_point("load:generic");
+      (void)hipGetLastError();
+      return m.release();
+    }
     // the knobs this engine does not read must hold SevenNet-0's values (the
-    // same predicate as nn.sevennet0_kinds; every other architecture is served
-    // by the runtime-path-table model)
+    // same predicate as nn.sevennet0_kinds)
     if (man.has("sh_normalize") && !man["sh_normalize"].boolean())
       throw std::runtime_error("raw-vector spherical harmonics (sh_normalize false, sevenn < 0.9) "
                                "are not SevenNet-0's architecture");
@@ -850,20 +865,37 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
         // w2b (MlpW::w2b): w2 = p0 + p1 + p2 exactly (bf16 pieces, round to
         // nearest even); element t of lane (g, c) in k-half m of column block cb
         // is w2[16(2m + t/4) + 4g + t%4][16 cb + c]
-        std::vector<float> b2((size_t)W * 64 * 3 / 2);
-        uint16_t* b2h = reinterpret_cast<uint16_t*>(b2.data());
-        for (int cb = 0; cb < W / 16; ++cb)
-          for (int m2 = 0; m2 < 2; ++m2)
-            for (int g = 0; g < 4; ++g)
-              for (int c = 0; c < 16; ++c)
-                for (int t = 0; t < 8; ++t) {
-                  float v = a2[(size_t)(16 * (2 * m2 + t / 4) + 4 * g + t % 4) * W + 16 * cb + c];
-                  for (int pc = 0; pc < 3; ++pc) {
-                    const uint16_t hb = bf16_rne(v);
-                    b2h[((((size_t)cb * 3 + pc) * 2 + m2) * 64 + g * 16 + c) * 8 + t] = hb;
-                    v -= bf16_to_f32(hb);
+        auto bsplit = [](const std::vector<float>& a, int N) {
+          std::vector<float> o((size_t)N * 64 * 3 / 2);
+          uint16_t* oh = reinterpret_cast<uint16_t*>(o.data());
+          for (int cb = 0; cb < N / 16; ++cb)
+            for (int m2 = 0; m2 < 2; ++m2)
+              for (int g = 0; g < 4; ++g)
+                for (int c = 0; c < 16; ++c)
+                  for (int t = 0; t < 8; ++t) {
+                    float v = a[(size_t)(16 * (2 * m2 + t / 4) + 4 * g + t % 4) * N + 16 * cb + c];
+                    for (int pc = 0; pc < 3; ++pc) {
+                      const uint16_t hb = bf16_rne(v);
+                      oh[((((size_t)cb * 3 + pc) * 2 + m2) * 64 + g * 16 + c) * 8 + t] = hb;
+                      v -= bf16_to_f32(hb);
+                    }
                   }
-                }
+          return o;
+        };
+        const std::vector<float> b2 = bsplit(a2, W);
+        // the MLP's other products in the same order: W1 (64 x 64, in x out),
+        // W1^T, and W0^T (64 x 8) padded to 16 columns
+        {
+          const auto a0 = scaled(w0, 8, 64, s0, false);
+          std::vector<float> a1t((size_t)64 * 64), a0t((size_t)64 * 16, 0.f);
+          for (int i = 0; i < 64; ++i)
+            for (int j = 0; j < 64; ++j) a1t[(size_t)j * 64 + i] = a1[(size_t)i * 64 + j];
+          for (int n = 0; n < 8; ++n)
+            for (int k = 0; k < 64; ++k) a0t[(size_t)k * 16 + n] = a0[(size_t)n * 64 + k];
+          if (upload(mm.w1b, bsplit(a1, 64)) != hipSuccess || upload(mm.w1tb, bsplit(a1t, 64)) != hipSuccess ||
+              upload(mm.w0tb, bsplit(a0t, 16)) != hipSuccess)
+            throw std::runtime_error("upload mlp (w1b)");
+        }
         // the kernels' visiting order of the 16-column blocks (input irrep,
         // channel block, path): pairs of consecutive blocks
         const std::vector<int> cols = t == 0 ? bwd_w_block_cols<LayerFirst>()
@@ -924,7 +956,15 @@ int e3gnn_model_info(const e3gnn_model* m, int* num_species, float* cutoff, int*
   if (num_species) *num_species = m->nsp;
   if (cutoff) *cutoff = m->cutoff;
   if (num_layers) *num_layers = m->nlayer;
-  if (comm_size) *comm_size = irreps_dim(m->irreps[1]);
+  if (comm_size) {
+    if (m->gen) {  // the widest exchanged row (x[t] / dE/dx[t], t >= 1)
+      int d = 0;
+      for (int t = 1; t <= m->nlayer; ++t) d = std::max(d, gen_feature_dim(m->gen, t));
+      *comm_size = d;
+    } else {
+      *comm_size = irreps_dim(m->irreps[1]);
+    }
+  }
   return E3GNN_OK;
 }
 
@@ -935,6 +975,7 @@ e3gnn_ctx* e3gnn_ctx_create(e3gnn_model* m) {
   }
   auto c = new e3gnn_ctx();
   c->m = m;
+  if (m->gen) c->gen = gen_ctx_create(m->gen);
   const int L = m->nlayer;
   c->x.resize(L + 1);
   c->grad.resize(L + 1);
@@ -949,14 +990,17 @@ void e3gnn_ctx_free(e3gnn_ctx* c) { delete c; }
 
 int e3gnn_feature_dim(const e3gnn_ctx* c, int layer) {
   if (!c || layer < 0 || layer > c->m->nlayer) return -1;
+  if (c->m->gen) return gen_feature_dim(c->m->gen, layer);
   return irreps_dim(c->m->irreps[layer]);
 }
 float* e3gnn_feature_ptr(e3gnn_ctx* c, int layer) {
   if (!c || layer < 0 || layer > c->m->nlayer) return nullptr;
+  if (c->gen) return gen_x(c->gen, layer);
   return c->x[layer].f();
 }
 float* e3gnn_grad_ptr(e3gnn_ctx* c, int layer) {
   if (!c || layer < 0 || layer > c->m->nlayer) return nullptr;
+  if (c->gen) return gen_grad(c->gen, layer);
   return c->grad[layer].f();
 }
 
@@ -970,7 +1014,7 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   // the fused kernels gather node-feature rows through one 32-bit buffer
   // descriptor (n x 480 fp32 < 2 GiB); dE/dagg rows are addressed per edge tile
   // (any size), except on the per-neighbour dE/dx variant (E3GNN_BWD_X=node)
-  if ((n_local + n_ghost) * 480LL * 4 > 0x7fffffffLL)
+  if (!c->gen && (n_local + n_ghost) * 480LL * 4 > 0x7fffffffLL)
     return fail(E3GNN_ERR_ARG, "more than 1.1M atoms (owned + ghost) per device: shard the system");
   if (!c->bwd_edge && n_local * 3136LL * 4 > 0x7fffffffLL)
     return fail(E3GNN_ERR_ARG, "E3GNN_BWD_X=node supports at most 171k owned atoms per device");
@@ -998,47 +1042,49 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   HIPCHK(c->src_perm.ensure(E * 4));
   HIPCHK(c->cnt.ensure(n * 4));
   HIPCHK(c->err.ensure(4));
-  HIPCHK(c->Y.ensure(E * 9 * F));
-  HIPCHK(c->emb.ensure(E * 8 * F));
-  HIPCHK(c->dY.ensure(E * 9 * F));
-  HIPCHK(c->demb.ensure(E * 8 * F));
-  HIPCHK(c->fe.ensure(E * 3 * F));
-  HIPCHK(c->dgu.ensure(E * 3 * F));
-  const bool v1 = c->impl == 1;
-  c->graph_impl = c->impl;
-  if (v1) {
-    HIPCHK(c->H1.ensure(E * 64 * F));
-    HIPCHK(c->H2.ensure(E * 64 * F));
-  }
-  int maxW = 0, maxDM = 0;
-  for (int t = 0; t < m->nlayer; ++t) {
-    const int dx = irreps_dim(m->irreps[t]), dg = irreps_dim(m->gin[t]);
-    maxW = std::max(maxW, m->W[t]);
-    maxDM = std::max(maxDM, irreps_dim(m->mid[t]));
-    HIPCHK(c->x[t].ensure(std::max<int64_t>(n, 1) * dx * F));
-    HIPCHK(c->grad[t].ensure(std::max<int64_t>(n, 1) * dx * F));
-    HIPCHK(c->h[t].ensure(n * dx * F));
-    HIPCHK(c->y[t].ensure(nl * dg * F));
+  if (!c->gen) {
+    HIPCHK(c->Y.ensure(E * 9 * F));
+    HIPCHK(c->emb.ensure(E * 8 * F));
+    HIPCHK(c->dY.ensure(E * 9 * F));
+    HIPCHK(c->demb.ensure(E * 8 * F));
+    HIPCHK(c->fe.ensure(E * 3 * F));
+    HIPCHK(c->dgu.ensure(E * 3 * F));
+    const bool v1 = c->impl == 1;
+    c->graph_impl = c->impl;
     if (v1) {
-      HIPCHK(c->w[t].ensure(E * m->W[t] * F));
-      HIPCHK(c->a1[t].ensure(E * 64 * F));
-      HIPCHK(c->a2[t].ensure(E * 64 * F));
+      HIPCHK(c->H1.ensure(E * 64 * F));
+      HIPCHK(c->H2.ensure(E * 64 * F));
     }
-  }
-  const int dlast = irreps_dim(m->irreps[m->nlayer]);
-  HIPCHK(c->x[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
-  HIPCHK(c->grad[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
-  HIPCHK(c->agg.ensure(nl * maxDM * F));
-  if (v1) HIPCHK(c->dw.ensure(E * maxW * F));
-  c->graph_bwd_edge = c->bwd_edge;
-  if (v1 || c->bwd_edge) HIPCHK(c->dxc.ensure(E * 480 * F));
-  HIPCHK(c->dy.ensure(nl * 576 * F));
-  HIPCHK(c->dh.ensure(n * 480 * F));
-  HIPCHK(c->eat.ensure(std::max<int64_t>(nl, 1) * F));
-  HIPCHK(c->part.ensure((sum_blocks(nl) + 1) * F));
-  HIPCHK(c->vpart.ensure((edge_force_blocks(E) + 1) * 6 * F));
-  HIPCHK(c->scratch6.ensure(8 * F));
+    int maxW = 0, maxDM = 0;
+    for (int t = 0; t < m->nlayer; ++t) {
+      const int dx = irreps_dim(m->irreps[t]), dg = irreps_dim(m->gin[t]);
+      maxW = std::max(maxW, m->W[t]);
+      maxDM = std::max(maxDM, irreps_dim(m->mid[t]));
+      HIPCHK(c->x[t].ensure(std::max<int64_t>(n, 1) * dx * F));
+      HIPCHK(c->grad[t].ensure(std::max<int64_t>(n, 1) * dx * F));
+      HIPCHK(c->h[t].ensure(n * dx * F));
+      HIPCHK(c->y[t].ensure(nl * dg * F));
+      if (v1) {
+        HIPCHK(c->w[t].ensure(E * m->W[t] * F));
+        HIPCHK(c->a1[t].ensure(E * 64 * F));
+        HIPCHK(c->a2[t].ensure(E * 64 * F));
+      }
+    }
+    const int dlast = irreps_dim(m->irreps[m->nlayer]);
+    HIPCHK(c->x[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
+    HIPCHK(c->grad[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
+    HIPCHK(c->agg.ensure(nl * maxDM * F));
+    if (v1) HIPCHK(c->dw.ensure(E * maxW * F));
+    c->graph_bwd_edge = c->bwd_edge;
+    if (v1 || c->bwd_edge) HIPCHK(c->dxc.ensure(E * 480 * F));
+    HIPCHK(c->dy.ensure(nl * 576 * F));
+    HIPCHK(c->dh.ensure(n * 480 * F));
+    HIPCHK(c->eat.ensure(std::max<int64_t>(nl, 1) * F));
+    HIPCHK(c->part.ensure((sum_blocks(nl) + 1) * F));
+    HIPCHK(c->vpart.ensure((edge_force_blocks(E) + 1) * 6 * F));
+    HIPCHK(c->scratch6.ensure(8 * F));
 
+  }
   if (n > 0) HIPCHK(hipMemcpyAsync(c->type.p, type, n * 4, hipMemcpyDefault, s));
   if (E > 0) {
     HIPCHK(hipMemcpyAsync(c->center.p, edge_center, E * 4, hipMemcpyDefault, s));
@@ -1052,7 +1098,9 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
                               c->src_ptr.i(), c->src_perm.i(), c->cnt.i(), c->err.i(), s,
                               (int)c->n_int));
   }
-  {
+  if (c->gen) {
+    HIPCHK(gen_graph_set(c->gen, m->gen, gen_graph(c), s));
+  } else {
     Region r(c, s, C_EMBED_NODE, 0, (double)n * 128 * 4);
     HIPCHK(launch_embed((int)n, c->type.i(), m->nsp, m->embed.f(), c->x[0].f(), c->err.i(), s));
   }
@@ -1071,6 +1119,7 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
     if (err & 16) msg += " an interior centre (below n_interior) has a ghost neighbour;";
     return fail(E3GNN_ERR_GRAPH, msg);
   }
+  if (c->gen) return E3GNN_OK;  // (edge embedding done by gen_graph_set)
   {
     Region r(c, s, C_EMBED_EDGE, 0, (double)E * (12 + 68));
     HIPCHK(launch_edge_embed(E, c->vec.f(), m->coeffs.f(), m->cutoff, m->r_on, c->Y.f(),
@@ -1099,6 +1148,11 @@ int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
   if (part != 0 && part != 1) return fail(E3GNN_ERR_ARG, "part must be 0 or 1");
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
+  // generic engine: the whole layer after the halo of x[t] (part 1)
+  if (c->gen) {
+    if (part == 1) HIPCHK(gen_layer_forward(c->gen, m->gen, gen_graph(c), t, s));
+    return E3GNN_OK;
+  }
   const int64_t n = c->n, nl = c->nl, E = c->E;
   const int dx = irreps_dim(m->irreps[t]), dg = irreps_dim(m->gin[t]);
   const int dm = irreps_dim(m->mid[t]), W = m->W[t];
@@ -1259,6 +1313,11 @@ int e3gnn_readout(e3gnn_ctx* c, float* energy, float* atomic_energy, void* strea
   e3gnn_model* m = c->m;
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
+  if (c->gen) {
+    HIPCHK(gen_readout(c->gen, m->gen, gen_graph(c), energy, atomic_energy, s));
+    c->readout_done = 1;
+    return E3GNN_OK;
+  }
   const int64_t nl = c->nl;
   const int L = m->nlayer;
   {
@@ -1288,6 +1347,11 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
   if (!c->readout_done) return fail(E3GNN_ERR_ARG, "e3gnn_readout must precede the backward");
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
+  // generic engine: the whole layer before the reverse halo of dE/dx[t] (part 0)
+  if (c->gen) {
+    if (part == 0) HIPCHK(gen_layer_backward(c->gen, m->gen, gen_graph(c), t, s));
+    return E3GNN_OK;
+  }
   const int64_t n = c->n, nl = c->nl, E = c->E;
   const int dx = irreps_dim(m->irreps[t]), dg = irreps_dim(m->gin[t]);
   const int dm = irreps_dim(m->mid[t]), W = m->W[t];
@@ -1452,6 +1516,10 @@ int e3gnn_forces(e3gnn_ctx* c, float* forces, float* virial6, float* edge_grad, 
   e3gnn_model* m = c->m;
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
+  if (c->gen) {
+    HIPCHK(gen_forces(c->gen, m->gen, gen_graph(c), forces, virial6, edge_grad, s));
+    return E3GNN_OK;
+  }
   const int64_t n = c->n, nl = c->nl, E = c->E;
   {
     Region r(c, s, C_EDGE_FORCE, 0, (double)E * 4 * (3 + 9 + 8 + 3));
@@ -1683,6 +1751,12 @@ e3gnn_gtp* e3gnn_gtp_create(int n_paths, const int32_t* paths, int dx, int dy, i
 }
 
 void e3gnn_gtp_free(e3gnn_gtp* g) { delete g; }
+
+extern "C++" {  // internal accessor for the generic engine (generic.cpp)
+namespace e3gnn {
+const GtpTables* gtp_tables(const e3gnn_gtp* g) { return &g->T; }
+}  // namespace e3gnn
+}
 
 int e3gnn_gtp_dims(const e3gnn_gtp* g, int* dx, int* dy, int* dw, int* dm) {
   if (!g) return fail(E3GNN_ERR_ARG, "null gtp");

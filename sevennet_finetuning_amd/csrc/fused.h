@@ -26,6 +26,12 @@ struct MlpW {
   // w2b's column blocks in the kernels' visiting order (block k at column 16 k):
   // the software-pipelined loops fetch the operand of the block after next
   const uint16_t* w2v;
+  // the radial MLP's other bf16x6 products, in w2b's operand order: W1 (layer
+  // 1 forward, 64 columns), W1^T (dH1 = dA2 W1^T) and W0^T padded to 16 columns
+  // (demb = dA1 W0^T)
+  const uint16_t* w1b;
+  const uint16_t* w1tb;
+  const uint16_t* w0tb;
 };
 
 struct FusedArgs {

@@ -103,16 +103,17 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 // does not hoist hundreds of 64-bit addresses out of the centre loop (which it
 // did, and spilled).  Offsets outside the descriptor read 0 (padded rows).
 struct WRes {
-  __amdgpu_buffer_rsrc_t w0, w1, w2p, w2q, w1p, w2b, w2r, w2d, w2v;
+  __amdgpu_buffer_rsrc_t w0, w2p, w2q, w2b, w2r, w2d, w2v, w1b, w1tb, w0tb;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int nfloats) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
 }
 __device__ __forceinline__ WRes make_wres(const MlpW& W, int width) {
-  return {rsrc(W.w0, 8 * 64), rsrc(W.w1, 64 * 64), rsrc(W.w2p, 64 * width), rsrc(W.w2q, 64 * width),
-          rsrc(W.w1p, 64 * 64), rsrc((const float*)W.w2b, 64 * width * 3 / 2), rsrc(W.w2r, 64 * width),
+  return {rsrc(W.w0, 8 * 64), rsrc(W.w2p, 64 * width), rsrc(W.w2q, 64 * width),
+          rsrc((const float*)W.w2b, 64 * width * 3 / 2), rsrc(W.w2r, 64 * width),
           rsrc((const float*)W.w2d, 64 * width * 3 / 2),
-          rsrc((const float*)W.w2v, 64 * width * 3 / 2)};
+          rsrc((const float*)W.w2v, 64 * width * 3 / 2), rsrc((const float*)W.w1b, 64 * 64 * 3 / 2),
+          rsrc((const float*)W.w1tb, 64 * 64 * 3 / 2), rsrc((const float*)W.w0tb, 64 * 16 * 3 / 2)};
 }
 __device__ __forceinline__ float ldw(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
   // the builtin returns the raw 32 bits (an unsigned int): reinterpret, never convert
@@ -144,6 +145,19 @@ __device__ __forceinline__ void ldv(__amdgpu_buffer_rsrc_t r, int vbytes, int sb
 
 __device__ __forceinline__ void stw(float v, __amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vbytes, sbytes, 0);
+}
+// N contiguous floats to one lane offset (b128 pieces; 16-byte aligned);
+// offsets outside the descriptor are dropped
+template <int N>
+__device__ __forceinline__ void stv(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes, const float* v) {
+  static_assert(N % 4 == 0, "b128 pieces");
+#pragma unroll
+  for (int q = 0; q < N / 4; ++q) {
+    f32x4 t;
+    t[0] = v[4 * q], t[1] = v[4 * q + 1], t[2] = v[4 * q + 2], t[3] = v[4 * q + 3];
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, t), r,
+                                           vbytes, sbytes + 16 * q, 0);
+  }
 }
 // descriptor over [p, p + nbytes) (nbytes clamped to the 32-bit range)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_bytes(const void* p, int64_t nbytes) {
@@ -212,7 +226,11 @@ struct MlpT {
   f32x4 a1[4], a2[4];
 };
 
-// b[s] = emb[edge of slot (l&15)][4s + (l>>4)] (0 for padded slots)
+// b[s] = emb[edge of slot (l&15)][4s + (l>>4)]
+// Layer 0 (K = 8) on f32 MFMA; layer 1 (64 -> 64) on bf16x6 like w = H2 W2
+// (w2_block: act(a1) split in three bf16 pieces in its accumulator layout, W1
+// pre-split in the same operand order, MlpW::w1b): 48 MFMAs x 16 cycles
+// instead of 64 x 32 on v_mfma_f32_16x16x4_f32, f32-grade.
 __device__ __forceinline__ void mlp_chain(const WRes& R, const float (&b)[2], int lane, MlpT& m) {
   const int g = lane >> 4, c = lane & 15;
   const int v0 = (g * 64 + c) * 4;  // W0s[4s + g][16 bh + c]
@@ -223,21 +241,21 @@ __device__ __forceinline__ void mlp_chain(const WRes& R, const float (&b)[2], in
     for (int s = 0; s < 2; ++s) acc = mfma(ldw(R.w0, v0, (4 * s * 64 + 16 * bh) * 4), b[s], acc);
     m.a1[bh] = acc;
   }
-  const int v1 = (c * 64 + g * 16) * 4;  // w1p[16 bo + c][g][s] = W1s[KH(s) + 4g][16 bo + c]
+  Op3 hq;
+  {
+    f32x4 h1[4];
+#pragma unroll
+    for (int bh = 0; bh < 4; ++bh)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h1[bh][r] = act_fwd(m.a1[bh][r]);
+    split_h2(h1, hq);
+  }
 #pragma unroll
   for (int bo = 0; bo < 4; ++bo) {
     phase();
-    float a[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 v = ldw4(R.w1p, v1, (16 * bo * 64 + 4 * q) * 4);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) a[4 * q + t] = v[t];
-    }
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc = mfma(a[s], act_fwd(m.a1[s >> 2][s & 3]), acc);
-    m.a2[bo] = acc;
+    Op3 wq;
+    load_w2b(wq, R.w1b, lane, 16 * bo);
+    m.a2[bo] = w2_block<false>(hq, wq);
   }
 }
 
@@ -706,36 +724,36 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
   MlpT m;
   mlp_pre(R, emb, e0, end, lane, m);
 
-  f32x4 da2[4], dh1[4];
+  // dH1^T = W1 dA2^T and demb^T = W0 dA1^T on bf16x6 (operands W1^T and W0^T
+  // pre-split, MlpW::w1tb / w0tb; dA split in their accumulator layout)
+  f32x4 dh1[4];
+  {
+    f32x4 da2[4];
 #pragma unroll
-  for (int bb = 0; bb < 4; ++bb)
+    for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) da2[bb][r] = dh2[bb][r] * act_grad(m.a2[bb][r]);
-  // dH1^T = W1 dA2^T  (A[i = h_in][k = h_out] = W1s[h_in][h_out])
-  const int vb = (col * 64 + 4 * g) * 4;
+      for (int r = 0; r < 4; ++r) da2[bb][r] = dh2[bb][r] * act_grad(m.a2[bb][r]);
+    Op3 dq;
+    split_h2(da2, dq);
 #pragma unroll
-  for (int bi = 0; bi < 4; ++bi) {
-    phase();
-    float a[16];  // W1s[16 bi + c][16q + 4g + t]: 4 contiguous per q
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 v = ldw4(R.w1, vb, (16 * bi * 64 + 16 * q) * 4);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) a[4 * q + t] = v[t];
+    for (int bi = 0; bi < 4; ++bi) {
+      phase();
+      Op3 wq;
+      load_w2b(wq, R.w1tb, lane, 16 * bi);
+      dh1[bi] = w2_block<false>(dq, wq);
     }
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc = mfma(a[s], da2[s >> 2][s & 3], acc);
-    dh1[bi] = acc;
   }
-  // demb^T = W0 dA1^T (rows n < 8; lanes c >= 8 read 0 outside the descriptor)
-  f32x4 de = zero4();
+  f32x4 de;
+  {
+    f32x4 da1[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x4 a4 = ldw4(R.w0, vb, 16 * q * 4);
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-      de = mfma(a4[t], dh1[q][t] * act_grad(m.a1[q][t]), de);
+      for (int t = 0; t < 4; ++t) da1[q][t] = dh1[q][t] * act_grad(m.a1[q][t]);
+    Op3 dq, wq;
+    split_h2(da1, dq);
+    load_w2b(wq, R.w0tb, lane, 0);
+    de = w2_block<false>(dq, wq);   // rows 4g + r < 8: the embedding dims
   }
   {
     const int e = e0 + col;
@@ -1327,8 +1345,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     };
     float y[9];
     Op3 hq;
+    // neighbour rows (lanes without an edge read row 0: harmless, their y
+    // and w are 0); issued unconditionally, like every vector-memory op
+    // between two pair commits, so the commit's wait counts only the staging
+    // loads and leaves younger loads and stores in flight
+    load_group(std::integral_constant<int, first_I<L>()>{}, 0);
+    // per-edge dE/dx rows of this tile: lanes without an edge, inactive tiles
+    // and the first block (dxc == nullptr) store outside the descriptor
+    const int nrow = (act && dxc) ? min(16, end - q0) : 0;
+    const __amdgpu_buffer_rsrc_t Rd =
+        rsrc_bytes(dxc ? dxc + (int64_t)(act ? q0 : 0) * L::DX : gagg, (int64_t)nrow * L::DX * 4);
+    const int vd = col * L::DX * 4;
     if (act) {
-      load_group(std::integral_constant<int, first_I<L>()>{}, 0);
 #pragma unroll
       for (int q = 0; q < 9; ++q) y[q] = er >= 0 ? Y[(int64_t)er * 9 + q] : 0.f;
       float b[2];
@@ -1368,13 +1396,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
               x[i] = xpf[i];
               dx[i] = 0.f;
             }
-            if (act) {
-              if (jj + 1 < MUL / 16) {
-                load_group(I, jj + 1);
-              } else {
-                constexpr int IN = next_I<L>(I);
-                if constexpr (IN >= 0) load_group(std::integral_constant<int, IN>{}, 0);
-              }
+            if (jj + 1 < MUL / 16) {
+              load_group(I, jj + 1);
+            } else {
+              constexpr int IN = next_I<L>(I);
+              if constexpr (IN >= 0) load_group(std::integral_constant<int, IN>{}, 0);
             }
             sfor<L::NP>([&](auto pi) {
               constexpr PathDef p = L::P[pi];
@@ -1386,11 +1412,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                   commit();
                   issue((nb >> 1) + 1 < NPAIR ? (nb >> 1) + 1 : 0);
                   if (act) {
+                    __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
                     Op3 wq;
                     lds_op3(wq, img, lane);
                     wv0 = w2_block<false>(hq, wq);
                     lds_op3(wq, img + LS_BLK, lane);
                     wv1 = w2_block<false>(hq, wq);
+                    __builtin_amdgcn_s_setprio(0);
                   }
                 }
                 if (act) {
@@ -1405,7 +1433,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                   pin<4 * D1>(dx);
                   pin<8>(dYa + 1);
                   if constexpr (ODD) {
+                    __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
                     dh2_pair(dh2, dwp, dwr, img + LS_PAIR_W, lane);
+                    __builtin_amdgcn_s_setprio(0);
                   } else {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) dwp[r] = dwr[r];
@@ -1413,11 +1443,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 }
               }
             });
-            if (act && dxc && er >= 0) {   // per-edge dE/dx[nbr] (not needed for the first block)
-              float* o = dxc + (int64_t)er * L::DX + XOFF + (16 * jj + 4 * g) * D1;
-#pragma unroll
-              for (int i = 0; i < 4 * D1; ++i) o[i] = dx[i];
-            }
+            // per-edge dE/dx[nbr] (not needed for the first block)
+            stv<4 * D1>(Rd, vd + 4 * g * D1 * 4, (XOFF + 16 * jj * D1) * 4, dx);
           });
         }
       }

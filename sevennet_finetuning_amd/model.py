@@ -1,5 +1,6 @@
-"""SevenNet-0 energy/force model on the HIP path -- the Python mirror of the
-reference's model surface.
+"""Energy/force models on the HIP path -- the Python mirror of the reference's
+model surface (SevenNet-0 and, through the generic engine of the same library,
+any other deployment of the nequip family).
 
 Reference surface mirrored here:
 * ``AtomGraphSequential.forward(dict) -> dict`` (sevenn/nn/sequential.py:82-89)
@@ -299,12 +300,17 @@ class GenericE3GNNModel:
         return out
 
 
-def load_model(model_dir=os.path.join(ASSETS, 'sevennet0'), device=None):
-    """The engine for a deployment: the native SevenNet-0 engine (E3GNNModel)
-    for that architecture, GenericE3GNNModel for the rest of the family."""
+def load_model(model_dir=os.path.join(ASSETS, 'sevennet0'), device=None, engine='native'):
+    """The engine for a deployment (pair_e3gnn.cpp:294-386 loads any deployed
+    model): the native C-ABI engine (E3GNNModel -- SevenNet-0's specialised
+    kernels, or the generic engine of libe3gnn_hip.so for the rest of the
+    family); ``engine='torch'``: the trainable model in eval mode
+    (GenericE3GNNModel, autograd backward) for the non-SevenNet-0 ones."""
     from .nn import sevennet0_kinds
+    if engine not in ('native', 'torch'):
+        raise ValueError(f"engine must be 'native' or 'torch', got {engine!r}")
     with open(os.path.join(model_dir, 'manifest.json')) as f:
         man = json.load(f)
-    if sevennet0_kinds(man) is not None:
+    if engine == 'native' or sevennet0_kinds(man) is not None:
         return E3GNNModel(model_dir, device)
     return GenericE3GNNModel(model_dir, device)

@@ -1,4 +1,5 @@
 """Spawn targets of the multi-process decomposition tests (gloo, world_size > 1)."""
+import json
 import os
 import sys
 
@@ -19,9 +20,11 @@ def _init(rank, world, port):
     return dist
 
 
-def worker(rank, world, port, name, engine, out):
+def worker(rank, world, port, name, engine, out, model_dir=None, tile=None):
     """Evaluate system `name` decomposed over `world` ranks; rank 0 saves
-    the gathered energy / virial / forces / atomic energies to `out`."""
+    the gathered energy / virial / forces / atomic energies to `out`.
+    ``model_dir``: another deployment (HIP engine; its species list), ``tile``:
+    replicate the system's cell (nx, ny, nz) first."""
     import torch
     if engine == 'cpu':  # the ranks share the host's cores (no oversubscription)
         torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
@@ -29,8 +32,17 @@ def worker(rank, world, port, name, engine, out):
     from _systems import load_manifest_symbols, system
     from sevennet_finetuning_amd.parallel import (ParallelE3GNN, brick_grid, build_rank_graph,
                                                   gather_all)
-    pos, cell, types = system(name, load_manifest_symbols())
-    rg = build_rank_graph(pos, cell, types, 5.0, brick_grid(world), rank)
+    syms = load_manifest_symbols() if model_dir is None else \
+        json.load(open(os.path.join(model_dir, 'manifest.json')))['chemical_symbols']
+    pos, cell, types = system(name, syms)
+    if tile is not None:
+        from sevennet_finetuning_amd.structures import tile as tile_cells
+        n0 = len(pos)
+        pos, cell = tile_cells(pos, cell, tuple(tile))
+        types = np.tile(types, len(pos) // n0)
+    cutoff = 5.0 if model_dir is None else \
+        float(json.load(open(os.path.join(model_dir, 'manifest.json')))['cutoff'])
+    rg = build_rank_graph(pos, cell, types, cutoff, brick_grid(world), rank)
     if engine == 'cpu':
         from _segment_cpu import make_engine
         eng = make_engine(rg)
@@ -38,7 +50,8 @@ def worker(rank, world, port, name, engine, out):
         from sevennet_finetuning_amd.model import E3GNNModel
         from sevennet_finetuning_amd.parallel import HipSegmentEngine
         torch.cuda.set_device(0)
-        eng = HipSegmentEngine(E3GNNModel(device='cuda:0'))
+        eng = HipSegmentEngine(E3GNNModel(device='cuda:0') if model_dir is None else
+                               E3GNNModel(model_dir, device='cuda:0'))
     drv = ParallelE3GNN(eng)
     drv.set_graph(rg)
     # several evaluations of one neighbour list: the rank graph is uploaded
@@ -49,7 +62,7 @@ def worker(rank, world, port, name, engine, out):
     tm = {}
     res = drv.evaluate(timing=tm)
     same = first[0] == float(res['energy']) and torch.equal(first[1], res['forces'].detach().cpu())
-    timed_ok = tm.get('exchanges') == 9 and 0 < tm['exchange_s'] < tm['total_s']
+    timed_ok = tm.get("exchanges") == 2 * (eng.num_layers - 1) + 1 and 0 < tm["exchange_s"] < tm["total_s"]
     res = drv.evaluate()
     same = same and first[0] == float(res['energy']) and torch.equal(first[1],
                                                                      res['forces'].detach().cpu())

@@ -130,7 +130,7 @@ def _hfo2_oracle(pos, cell, types):
 @pytest.fixture(scope='module')
 def hfo2():
     from sevennet_finetuning_amd.model import GenericE3GNNModel, load_model
-    m = load_model(HFO2, device=DEV)
+    m = load_model(HFO2, device=DEV, engine='torch')
     assert isinstance(m, GenericE3GNNModel)
     assert isinstance(m.net.conv_backend, conv_ops.GenericHipConvBackend)
     return m
@@ -205,3 +205,63 @@ def test_generic_kernels_serve_sevennet0_like_the_specialised_ones():
     ea, eb = float(ra[KEY.PRED_TOTAL_ENERGY][0]), float(rb[KEY.PRED_TOTAL_ENERGY][0])
     assert abs(ea - eb) <= 2e-6 * abs(ea)
     assert float((ra[KEY.PRED_FORCE] - rb[KEY.PRED_FORCE]).abs().max()) <= 1e-4
+
+
+# ------------------------------------------------------------ native engine
+@pytest.fixture(scope='module')
+def hfo2_native():
+    from sevennet_finetuning_amd.model import E3GNNModel
+    return E3GNNModel(HFO2, device=DEV)
+
+
+def test_native_engine_serves_hfo2_example(hfo2_native, hfo2):
+    """e3gnn_load serves the HfO2 deployment on the generic C-ABI engine
+    (generic.cpp / generic.hip: dense e3nn linears, runtime-path-table
+    convolution, parity gate, FCTP self-connection, polynomial cutoff,
+    raw-vector SH, forward and hand-written backward) -- the reference's
+    pair_e3gnn.cpp:294-386 loads any deployed model.  res.dat against the fp64
+    oracle and the reference's frozen-model KAT (E, F[0]), against the
+    torch-side generic model (autograd backward), and bitwise repeatable."""
+    from sevennet_finetuning_amd.model import E3GNNModel, load_model
+    assert isinstance(load_model(HFO2, device=DEV), E3GNNModel)   # the default route
+    kat = json.load(open(f'{GOLD}/kat_reference.json'))['kats_hfo2_example']
+    d = np.load(f'{GOLD}/hfo2_resdat.npz')
+    types = np.array([hfo2_native.chemical_symbols.index(str(s)) for s in d['symbols']])
+    got = _run(hfo2_native, d['pos'], d['cell'], types)
+    ref = _hfo2_oracle(d['pos'], d['cell'], types)
+    assert abs(got['energy'] - float(ref['energy'])) <= 2e-6 * abs(float(ref['energy']))
+    assert np.abs(got['forces'] - ref['forces'].numpy()).max() <= 1e-4
+    assert np.abs(got['stress'] - ref['stress'].numpy()).max() <= 2e-6
+    assert abs(got['energy'] - kat['energy']) <= 2e-6 * abs(kat['energy'])
+    assert np.abs(got['forces'][0] - np.array(kat['force0'])).max() <= 1e-4
+    tm = _run(hfo2, d['pos'], d['cell'], types)
+    assert abs(got['energy'] - tm['energy']) <= 1e-6 * abs(tm['energy'])
+    assert np.abs(got['forces'] - tm['forces']).max() <= 2e-5
+    again = _run(hfo2_native, d['pos'], d['cell'], types)
+    assert again['energy'] == got['energy'] and np.array_equal(again['forces'], got['forces'])
+
+
+def test_native_engine_hfo2_decomposed_matches_serial(hfo2_native, tmp_path):
+    """The same deployment decomposed over two ranks (gloo, both on the box's
+    GPU) through the segment API and the halo exchanges (parallel.py, the
+    reference's e3gnn/parallel path): equal to the serial native evaluation."""
+    import socket
+
+    import torch.multiprocessing as mp
+    from _parallel_workers import worker
+    from sevennet_finetuning_amd.structures import tile
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / 'hfo2_2.npz')
+    mp.spawn(worker, args=(2, port, 'hfo2_resdat', 'hip', out, HFO2, (2, 2, 1)), nprocs=2, join=True)
+    got = np.load(out)
+    d = np.load(f'{GOLD}/hfo2_resdat.npz')
+    types = np.array([hfo2_native.chemical_symbols.index(str(s)) for s in d['symbols']])
+    pos4, cell4 = tile(d['pos'], d['cell'], (2, 2, 1))
+    one = _run(hfo2_native, pos4, cell4, np.tile(types, 4))
+    assert got['n_ghost'][0] > 0 and got['repeat_same'][0] and got['timed_ok'][0]
+    assert abs(float(got['energy']) - one['energy']) <= 2e-6 * abs(one['energy'])
+    assert np.abs(got['forces'] - one['forces']).max() <= 2e-5
+    vol = abs(np.linalg.det(cell4))
+    assert np.abs(got['virial'] / vol - one['stress']).max() <= 2e-6

@@ -102,3 +102,36 @@ def test_lammps_pair_core_matches_device_path(grid):
         assert out[k]['eatom_sum_rel'] < 1e-6, out
         assert out[k]['max_force'] < 1e-4, out
         assert out[k]['max_virial'] < 1e-3, out
+
+
+HFO2 = os.path.join(ROOT, 'sevennet_finetuning_amd', 'assets', 'hfo2_example')
+
+
+@pytest.mark.parametrize('grid', [(1, 1, 1), (2, 1, 1), (2, 2, 1)])
+def test_native_parallel_host_serves_hfo2_example(grid, tmp_path):
+    """Another architecture through the compiled e3gnn/parallel sequence: the
+    reference's HfO2 example deployment (odd parity, FCTP self-connection,
+    polynomial cutoff, raw-vector SH: the generic engine behind e3gnn_load)
+    on res.dat replicated 2x2x1 (triclinic), serial and on brick
+    sub-domains.  Serial energy = 4 x the reference's frozen-model KAT of
+    res.dat; decomposed = serial."""
+    from sevennet_finetuning_amd.structures import tile
+    assert os.path.exists(EXE_PAR), 'native/e3gnn_md_parallel not built (build_lib.build)'
+    d = np.load(os.path.join(ROOT, 'tests', 'golden', 'hfo2_resdat.npz'))
+    pos, cell = tile(d['pos'], d['cell'], (2, 2, 1))
+    syms = [str(s) for s in d['symbols']] * 4
+    path = tmp_path / 'hfo2_221.txt'
+    with open(path, 'w') as f:
+        f.write(f'{len(pos)}\n' + ' '.join(f'{v:.12f}' for v in cell.ravel()) + '\n')
+        for s, p in zip(syms, pos):
+            f.write(f'{s} {p[0]:.12f} {p[1]:.12f} {p[2]:.12f}\n')
+    r = subprocess.run([EXE_PAR, os.path.join(HFO2, 'weights.bin'), os.path.join(HFO2, 'manifest.json'),
+                        str(path), *map(str, grid), '2'], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    kat = json.load(open(os.path.join(ROOT, 'tests', 'golden', 'kat_reference.json')))['kats_hfo2_example']
+    assert out['n_atoms'] == 384 and out['ranks'] == int(np.prod(grid))
+    assert abs(out['energy_serial'] - 4 * kat['energy']) <= 2e-6 * abs(4 * kat['energy'])
+    assert out['energy_rel_diff'] < 1e-6
+    assert out['max_force_diff'] < 2e-5
+    assert out['max_virial_diff'] <= 1e-5 * max(1.0, out['max_virial'])

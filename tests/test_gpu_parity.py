@@ -253,7 +253,10 @@ def test_high_degree_centres(model):
     for i in range(1, len(pos)):
         if np.min(np.linalg.norm(pos[keep] - pos[i], axis=1)) > 1.1:
             keep.append(i)
-    pos = pos[keep]
+    # the model takes float32 positions: give the oracle the same (rounded)
+    # inputs -- at 1.1 A packings the forces reach 1e8 eV/A and a 1e-7 A input
+    # rounding alone moves them by ~1e-4 relative, which is not kernel error
+    pos = pos[keep].astype(np.float32).astype(np.float64)
     cell = np.eye(3) * 30.0
     types = np.full(len(pos), SYMS.index('Si'))
     from sevennet_finetuning_amd.neighbor import neighbor_list
