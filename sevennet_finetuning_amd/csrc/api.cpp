@@ -1394,8 +1394,9 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     // the last block (224 message channels) is faster per neighbour node
     a.edge_order = c->graph_bwd_edge && (kind != 2 || c->last_edge);
     a.dxc = (a.edge_order && t > 0) ? c->dxc.f() : nullptr;
-    // per-centre dE/dx kernel also does dE/dw (first and middle blocks)
-    a.fuse_w = a.edge_order && c->bwd_fuse;
+    // the dE/dx kernel also does dE/dw -> dE/demb: per centre (first and
+    // middle blocks) or per neighbour node (the last block)
+    a.fuse_w = c->bwd_fuse;
     a.scratch_dh = c->dh.f();
     a.dgu = c->dgu.f();
     a.demb = c->demb.f();

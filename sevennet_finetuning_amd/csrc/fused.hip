@@ -714,15 +714,20 @@ __device__ __forceinline__ void load_gm(float* gmN, __amdgpu_buffer_rsrc_t Rg, i
   constexpr int D3 = 2 * L::P[PN].l3 + 1;
   ldv<4 * D3>(Rg, vg + 4 * g * D3 * 4, (L::P[PN].moff + 16 * jj * D3) * 4, gmN);
 }
-// MLP chain backward of a 16-edge tile [e0, min(e0 + 16, end)) from dH2^T
-// (D[hidden 16 bh + 4g + r][edge slot c]): pre-activations recomputed, dA2,
-// dH1^T = W1 dA2^T, demb^T = W0 dA1^T, demb += (rows < 8)
-__device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __restrict__ emb, int e0,
-                                              int end, int lane, const f32x4 (&dh2)[4],
-                                              float* __restrict__ demb) {
-  const int g = lane >> 4, col = lane & 15;
+// MLP chain backward of a 16-edge tile from dH2^T (D[hidden 16 bh + 4g + r][edge
+// slot c]): pre-activations recomputed, dA2, dH1^T = W1 dA2^T, demb^T = W0 dA1^T,
+// demb += (rows < 8).  `er`: the edge of the lane's slot c (-1: padded slot).
+__device__ __forceinline__ void mlp_bwd_chain_ids(const WRes& R, const float* __restrict__ emb, int er,
+                                                  int lane, const f32x4 (&dh2)[4],
+                                                  float* __restrict__ demb) {
+  const int g = lane >> 4;
   MlpT m;
-  mlp_pre(R, emb, e0, end, lane, m);
+  {
+    float b[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) b[s] = er >= 0 ? emb[(int64_t)er * 8 + 4 * s + g] : 0.f;
+    mlp_chain(R, b, lane, m);
+  }
 
   // dH1^T = W1 dA2^T and demb^T = W0 dA1^T on bf16x6 (operands W1^T and W0^T
   // pre-split, MlpW::w1tb / w0tb; dA split in their accumulator layout)
@@ -755,13 +760,17 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
     load_w2b(wq, R.w0tb, lane, 0);
     de = w2_block<false>(dq, wq);   // rows 4g + r < 8: the embedding dims
   }
-  {
-    const int e = e0 + col;
-    if (g < 2 && e < end) {
+  if (g < 2 && er >= 0) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) demb[(int64_t)e * 8 + 4 * g + r] += de[r];
-    }
+    for (int r = 0; r < 4; ++r) demb[(int64_t)er * 8 + 4 * g + r] += de[r];
   }
+}
+// the same for the CSR edge tile [e0, min(e0 + 16, end))
+__device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __restrict__ emb, int e0,
+                                              int end, int lane, const f32x4 (&dh2)[4],
+                                              float* __restrict__ demb) {
+  const int e = e0 + (lane & 15);
+  mlp_bwd_chain_ids(R, emb, e < end ? e : -1, lane, dh2, demb);
 }
 
 // B1: lane (g, c) = edge slot c of the tile x channels 4g..4g+3 of a 16-channel
@@ -774,6 +783,8 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
 // kernel's mapping), the centre's dE/dagg row (DM floats) staged in LDS once;
 // dE/dx per edge to dxc (summed per neighbour by the transposed-CSR gather).
 // MODE 3: MODE 2 + dE/dw -> dH2 -> MLP chain -> dE/demb from the same registers.
+// MODE 4: MODE 0 + dE/dw -> dH2 -> MLP chain -> dE/demb (the last block: every
+// edge is visited once, by the wave of its neighbour, whose own row is x).
 // The radial weights w of the NEXT visited block are formed (MFMA) before this
 // block's tensor product (VALU), so the matrix pipe works under the VALU stream.
 template <class L, int MODE>
@@ -790,11 +801,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
                                                     float* __restrict__ dxc, int n_edges,
                                                     const int* __restrict__ row_ptr, int r_begin,
                                                     int r_end, float* __restrict__ demb) {
-  static_assert(MODE == 0 || MODE == 2 || MODE == 3, "backward modes 0, 2, 3");
-  constexpr bool EDGE = MODE != 0;  // per-edge dE/dx output (dxc), one wave per centre
-  constexpr bool FW = MODE == 3;    // + dE/dw -> dH2 -> MLP chain -> dE/demb
-  // MODE 0: dE/dx[j] of the wave's node; MODE 2/3: dE/dagg row of its centre
-  __shared__ __attribute__((aligned(16))) float lds[4][MODE == 0 ? L::DX : L::DM];
+  static_assert(MODE == 0 || MODE == 2 || MODE == 3 || MODE == 4, "backward modes 0, 2, 3, 4");
+  constexpr bool EDGE = MODE == 2 || MODE == 3;  // per-edge dE/dx output (dxc), one wave per centre
+  constexpr bool FW = MODE == 3 || MODE == 4;    // + dE/dw -> dH2 -> MLP chain -> dE/demb
+  // MODE 0/4: dE/dx[j] of the wave's node; MODE 2/3: dE/dagg row of its centre
+  __shared__ __attribute__((aligned(16))) float lds[4][EDGE ? L::DM : L::DX];
   const int wid = threadIdx.x >> 6;
   // wave index: node (MODE 0) or centre (MODE 2/3)
   const int jn = __builtin_amdgcn_readfirstlane(r_begin + xcd_block() * 4 + wid);
@@ -818,7 +829,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
   // whole array (32-bit lane offsets; DM = 224, the host checks
   // n_centers * 224 * 4 < 2^31); padded slots read past its end: 0
   const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
-  if constexpr (MODE == 0)
+  if constexpr (!EDGE)
     for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
 
   for (int q0 = qb; q0 < qe; q0 += 16) {
@@ -972,10 +983,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
     }
     if constexpr (FW) {
       phase();
-      mlp_bwd_chain(R, emb, q0, qe, lane, dh2, demb);
+      mlp_bwd_chain_ids(R, emb, er, lane, dh2, demb);
     }
   }
-  if constexpr (MODE == 0) {
+  if constexpr (!EDGE) {
     phase();
     __builtin_amdgcn_s_waitcnt(0);
     float* dhj = dh + (int64_t)jn * L::DX;
@@ -1537,14 +1548,21 @@ static hipError_t bwd_x_impl(const FusedArgs& a, hipStream_t s) {
     }
     return hipGetLastError();
   }
-  // per neighbour node over [node_begin, node_end); first block: dE/dx of the
-  // embedding is not needed (scratch sink), only dE/du
+  // per neighbour node over [node_begin, node_end) (fuse_w: + dE/dw -> dE/demb
+  // of its incoming edges); first block: dE/dx of the embedding is not needed
+  // (scratch sink), only dE/du
   const int nn = a.node_end - a.node_begin;
   if (nn <= 0) return hipSuccess;
-  hipLaunchKernelGGL((k_conv_bwd_x<L, 0>), dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr,
-                     a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W,
-                     a.dh ? a.dh : a.scratch_dh, a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc,
-                     a.n_edges, a.row_ptr, a.node_begin, a.node_end, a.demb);
+  if (a.fuse_w)
+    hipLaunchKernelGGL((k_conv_bwd_x<L, 4>), dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr,
+                       a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W,
+                       a.dh ? a.dh : a.scratch_dh, a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc,
+                       a.n_edges, a.row_ptr, a.node_begin, a.node_end, a.demb);
+  else
+    hipLaunchKernelGGL((k_conv_bwd_x<L, 0>), dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr,
+                       a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W,
+                       a.dh ? a.dh : a.scratch_dh, a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc,
+                       a.n_edges, a.row_ptr, a.node_begin, a.node_end, a.demb);
   return hipGetLastError();
 }
 template <class L>
