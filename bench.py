@@ -119,10 +119,12 @@ def device_nl_timing(box, device, reps=5):
 def rocprof_name(cls):
     """Kernel symbol (as rocprofv3 prints it) of a fused timing class."""
     kinds = {'first': 'LayerFirst', 'mid': 'LayerMid', 'last': 'LayerLast'}
-    if '.' in cls:  # template prefix (k_conv_bwd_x has a second, int argument)
+    if '.' in cls:  # template prefix
         k, kind = cls.split('.')
-        if k == 'conv_bwd_x' and kind != 'last' and os.environ.get('E3GNN_CONV') != 'wave':
-            k = 'conv_bwd_ls'   # first / middle blocks: the lock-step kernel
+        if k == 'conv_bwd_x':
+            # first / middle blocks: the lock-step kernel; the last block: one
+            # wave per neighbour node
+            k = 'conv_bwd_nbr' if kind == 'last' else 'conv_bwd_ls'
         return f'k_{k}<e3gnn::{kinds[kind]}'
     return cls
 

@@ -187,8 +187,7 @@ const char* kClassNames[] = {"graph_build", "edge_embed",  "node_linear", "radia
                              "atom_force",  "embed",
                              // fused kernels, one class per kernel and block kind
                              "conv_fwd.first", "conv_fwd.mid", "conv_fwd.last",
-                             "conv_bwd_x.first", "conv_bwd_x.mid", "conv_bwd_x.last",
-                             "conv_bwd_w.first", "conv_bwd_w.mid", "conv_bwd_w.last"};
+                             "conv_bwd_x.first", "conv_bwd_x.mid", "conv_bwd_x.last"};
 enum Cls {
   C_GRAPH,
   C_EMBED_EDGE,
@@ -206,8 +205,7 @@ enum Cls {
   C_EMBED_NODE,
   C_CONV_FWD,             // + kind (0 first, 1 mid, 2 last)
   C_CONV_BWD_X = C_CONV_FWD + 3,
-  C_CONV_BWD_W = C_CONV_BWD_X + 3,
-  C_NCLS = C_CONV_BWD_W + 3
+  C_NCLS = C_CONV_BWD_X + 3
 };
 static_assert(sizeof(kClassNames) / sizeof(kClassNames[0]) == C_NCLS, "class names");
 
@@ -228,39 +226,9 @@ struct e3gnn_ctx {
   // graph
   DBuf type, center, nbr, vec, row_ptr, src_ptr, src_perm, cnt, err;
   DBuf Y, emb, dY, dgu, demb, fe;
-  // fused dE/dx kernel over CSR edge tiles + per-edge buffer + gather (1,
-  // default) or one wave per neighbour node writing dh directly (0;
-  // E3GNN_BWD_X=node)
-  int bwd_edge = [] {
-    const char* v = std::getenv("E3GNN_BWD_X");
-    return (v && std::string(v) == "node") ? 0 : 1;
-  }();
-  int graph_bwd_edge = 1;
-  // per-centre dE/dx kernel also computes dE/dw -> dH2 -> dE/demb (one
-  // backward launch per block; 1, default) or a separate dE/dw kernel over
-  // edge tiles (0; E3GNN_BWD_FUSE=0)
-  int bwd_fuse = [] {
-    const char* v = std::getenv("E3GNN_BWD_FUSE");
-    return (v && std::string(v) == "0") ? 0 : 1;
-  }();
   // node linears on k_nodelin (node-aligned tiles, si2 + sc in one problem,
   // gate in the epilogue; 1, default) or the grouped k_gemm + k_gate kernels
   // (0; E3GNN_NODELIN=0)
-  // the last block's backward in edge order with the fused dE/dw too (1) or
-  // per neighbour node + a separate dE/dw kernel (0, default; E3GNN_LAST_EDGE=1)
-  int last_edge = [] {
-    const char* v = std::getenv("E3GNN_LAST_EDGE");
-    return (v && std::string(v) == "1") ? 1 : 0;
-  }();
-  // lock-step convolution kernels (4 centres per workgroup, W2 operands staged
-  // per block pair in LDS, dH2 on bf16x6; 1) or the per-wave kernels (0;
-  // E3GNN_CONV=wave)
-  int conv_ls = [] {
-    const char* v = std::getenv("E3GNN_CONV");
-    if (!v) return 2;
-    const std::string m(v);
-    return m == "ls" ? 3 : (m == "wave" ? 0 : (m == "lsf" ? 1 : 2));
-  }();
   int nodelin = [] {
     const char* v = std::getenv("E3GNN_NODELIN");
     return (v && std::string(v) == "0") ? 0 : 1;
@@ -1012,12 +980,10 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   if (n_local + n_ghost > (1LL << 30) || n_edges > (1LL << 31) - 1)
     return fail(E3GNN_ERR_ARG, "graph too large for int32 indices");
   // the fused kernels gather node-feature rows through one 32-bit buffer
-  // descriptor (n x 480 fp32 < 2 GiB); dE/dagg rows are addressed per edge tile
-  // (any size), except on the per-neighbour dE/dx variant (E3GNN_BWD_X=node)
+  // descriptor (n x 480 fp32 < 2 GiB; the last block's dE/dagg rows, nl x 224,
+  // fit whenever these do)
   if (!c->gen && (n_local + n_ghost) * 480LL * 4 > 0x7fffffffLL)
     return fail(E3GNN_ERR_ARG, "more than 1.1M atoms (owned + ghost) per device: shard the system");
-  if (!c->bwd_edge && n_local * 3136LL * 4 > 0x7fffffffLL)
-    return fail(E3GNN_ERR_ARG, "E3GNN_BWD_X=node supports at most 171k owned atoms per device");
   if ((n_local + n_ghost > 0 && !type) || (n_edges > 0 && (!edge_center || !edge_nbr || !edge_vec)))
     return fail(E3GNN_ERR_ARG, "null input array");
   e3gnn_model* m = c->m;
@@ -1075,8 +1041,7 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
     HIPCHK(c->grad[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
     HIPCHK(c->agg.ensure(nl * maxDM * F));
     if (v1) HIPCHK(c->dw.ensure(E * maxW * F));
-    c->graph_bwd_edge = c->bwd_edge;
-    if (v1 || c->bwd_edge) HIPCHK(c->dxc.ensure(E * 480 * F));
+    HIPCHK(c->dxc.ensure(E * 480 * F));
     HIPCHK(c->dy.ensure(nl * 576 * F));
     HIPCHK(c->dh.ensure(n * 480 * F));
     HIPCHK(c->eat.ensure(std::max<int64_t>(nl, 1) * F));
@@ -1179,7 +1144,7 @@ int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     a.denom = m->denom[t];
     a.c_begin = (int)c0;
     a.c_end = (int)c1;
-    HIPCHK((c->conv_ls & 1) ? launch_conv_fwd_ls(kind, a, s) : launch_conv_fwd(kind, a, s));
+    HIPCHK(launch_conv_fwd(kind, a, s));
     return E3GNN_OK;
   };
   if (part == 0) {
@@ -1374,9 +1339,9 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
         HIPCHK(launch_gemm(lin_bwd(*m->si2[t], c->dy.f(), dg, c->agg.f(), dm, nl, 0), s));
     }
   }
-  // per-edge dE/dx + transposed-CSR gather (edge-ordered kernels) or dE/dx
-  // written per neighbour node (the last block)
-  const bool gather = !fused || (c->graph_bwd_edge && (!last || c->last_edge));
+  // first / middle blocks: per-edge dE/dx (dxc) + transposed-CSR gather; the
+  // last block (224 message channels) writes dE/dx per neighbour node
+  const bool gather = !fused || !last;
   if (fused) {
     FusedArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -1390,14 +1355,8 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     a.n_edges = (int)E;
     a.src_ptr = c->src_ptr.i();
     a.src_perm = c->src_perm.i();
-    a.dh = t > 0 ? c->dh.f() : nullptr;
-    // the last block (224 message channels) is faster per neighbour node
-    a.edge_order = c->graph_bwd_edge && (kind != 2 || c->last_edge);
-    a.dxc = (a.edge_order && t > 0) ? c->dxc.f() : nullptr;
-    // the dE/dx kernel also does dE/dw -> dE/demb: per centre (first and
-    // middle blocks) or per neighbour node (the last block)
-    a.fuse_w = c->bwd_fuse;
-    a.scratch_dh = c->dh.f();
+    a.dh = c->dh.f();  // the last block writes its dE/dx rows here
+    a.dxc = (!last && t > 0) ? c->dxc.f() : nullptr;
     a.dgu = c->dgu.f();
     a.demb = c->demb.f();
     a.W = mlp_ptrs(m, t);
@@ -1406,31 +1365,25 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     // part 0: boundary centres / their edges / ghost neighbour nodes
     a.c_begin = (int)(part == 0 ? n_int : 0);
     a.c_end = (int)(part == 0 ? nl : n_int);
-    a.e_begin = (int)(part == 0 ? e_int : 0);
-    a.e_end = (int)(part == 0 ? E : e_int);
     a.node_begin = (int)(part == 0 ? nl : 0);
     a.node_end = (int)(part == 0 ? n : nl);
-    const double ef = (double)(a.e_end - a.e_begin);
-    // algorithmic FLOP (the forward radial MLP the dE/dx kernel recomputes is
-    // not counted): dE/dx + dE/dY = 2 x TP; dE/dw = TP, dH2 = dw W2^T, MLP chain
-    // empty ranges launch nothing (and are not counted as launches)
-    const bool any_x = a.edge_order ? a.c_end > a.c_begin : a.node_end > a.node_begin;
-    if (any_x) {
-      // fused (a.fuse_w): + dE/dw = TP, dH2 = dw W2^T and the MLP chain backward
-      const double xf = 2.0 * tp_flops_per_edge(kind) +
-                        (a.fuse_w ? tp_flops_per_edge(kind) + 2.0 * (64 * W + 64 * 64 + 8 * 64) : 0.0);
-      Region r(c, s, C_CONV_BWD_X + kind, xf * ef,
-               ef * 4 * (8 + 9 + 2 + 3 + (a.fuse_w ? 8 : 0)) + (a.c_end - a.c_begin) * 4.0 * dm);
-      if ((c->conv_ls & 2) && a.edge_order && a.fuse_w)
-        HIPCHK(launch_conv_bwd_ls(kind, a, s));
-      else
-        HIPCHK(launch_conv_bwd_x(kind, a, s));
+    double ef = (double)(part == 0 ? E - e_int : e_int);
+    if (last && c->timing && a.node_end > a.node_begin) {
+      // the last block's launch covers the edges of its neighbour-node range
+      int32_t q[2];
+      HIPCHK(hipMemcpyAsync(&q[0], a.src_ptr + a.node_begin, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(&q[1], a.src_ptr + a.node_end, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      ef = (double)(q[1] - q[0]);
     }
-    if (ef > 0 && !a.fuse_w) {
-      Region r(c, s, C_CONV_BWD_W + kind,
-               tp_flops_per_edge(kind) * ef + 2.0 * ef * (64 * W + 64 * 64 + 8 * 64),
-               ef * 4 * (8 + 9 + 2 + 8 + dx));
-      HIPCHK(launch_conv_bwd_w(kind, a, s));
+    // empty ranges launch nothing (and are not counted as launches)
+    if (last ? a.node_end > a.node_begin : a.c_end > a.c_begin) {
+      // algorithmic FLOP (the forward radial MLP the kernel recomputes is not
+      // counted): dE/dx + dE/dY = 2 x TP; dE/dw = TP, dH2 = dw W2^T, MLP chain
+      const double xf = 3.0 * tp_flops_per_edge(kind) + 2.0 * (64 * W + 64 * 64 + 8 * 64);
+      Region r(c, s, C_CONV_BWD_X + kind, xf * ef,
+               ef * 4 * (8 + 9 + 2 + 3 + 8) + (a.c_end - a.c_begin) * 4.0 * dm);
+      HIPCHK(last ? launch_conv_bwd_nbr_last(a, s) : launch_conv_bwd_ls(kind, a, s));
     }
   } else {
   {

@@ -45,11 +45,8 @@ struct FusedArgs {
   const float* gagg;  // bwd in  [n_centers, DM] (dE/dagg / denominator)
   const int* src_ptr;  // [n_nodes + 1] transposed CSR (edges by edge_index[1])
   const int* src_perm; // [E]
-  float* dh;           // bwd out [n_nodes, DX]: dE/dx of the gathered features (nullable)
-  float* scratch_dh;   // [n_nodes, DX] sink used when dh is null
-  float* dxc;          // [E, DX] per-edge dE/dx (edge-ordered dE/dx kernel; nullable)
-  int edge_order;      // dE/dx kernel over CSR edge tiles (writes dxc) vs per neighbour
-  int fuse_w;          // per-centre dE/dx kernel also does dE/dw -> dE/demb (no bwd_w launch)
+  float* dh;           // bwd out [n_nodes, DX]: dE/dx of the gathered features (last block)
+  float* dxc;          // [E, DX] per-edge dE/dx (first / middle blocks; null: not stored)
   float* dgu;         // bwd in/out [E, 3]  dE/du accumulated over layers
   float* demb;        // bwd in/out [E, 8]  dE/demb accumulated over layers
   MlpW W;
@@ -58,19 +55,18 @@ struct FusedArgs {
   int n_nodes;
   float denom;
   // work range of one launch (halo overlap splits a layer into parts):
-  // centres [c_begin, c_end) (forward, per-centre dE/dx), edges [e_begin,
-  // e_end) (dE/dw, edge tiles), neighbour nodes [node_begin, node_end)
-  // (per-node dE/dx); the host sets them to the whole graph by default
-  int c_begin, c_end, e_begin, e_end, node_begin, node_end;
+  // centres [c_begin, c_end) (forward, first / middle backward), neighbour
+  // nodes [node_begin, node_end) (last backward)
+  int c_begin, c_end, node_begin, node_end;
 };
 
 hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s);
-// lock-step kernels: 4 centres per workgroup, W2 operands staged per block pair
-// in LDS, dH2 on bf16x6 (fused.hip); the backward writes dxc (first / middle blocks)
-hipError_t launch_conv_fwd_ls(int kind, const FusedArgs& a, hipStream_t s);
+// backward of a first / middle block: the lock-step kernel (4 centres per
+// workgroup, W2 operands staged per block pair in LDS, dH2 on bf16x6), per-edge
+// dE/dx to dxc, dE/du, dE/dw -> dE/demb
 hipError_t launch_conv_bwd_ls(int kind, const FusedArgs& a, hipStream_t s);
-hipError_t launch_conv_bwd(int kind, const FusedArgs& a, hipStream_t s);  // = _x then _w
-hipError_t launch_conv_bwd_x(int kind, const FusedArgs& a, hipStream_t s);  // dE/dx, dE/du
-hipError_t launch_conv_bwd_w(int kind, const FusedArgs& a, hipStream_t s);  // dE/dw -> dE/demb
+// backward of the last block, one wave per neighbour node: dE/dx to dh, dE/du,
+// dE/dw -> dE/demb
+hipError_t launch_conv_bwd_nbr_last(const FusedArgs& a, hipStream_t s);
 
 }  // namespace e3gnn

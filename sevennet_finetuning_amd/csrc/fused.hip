@@ -41,23 +41,9 @@
 #ifndef E3GNN_FWD_WAVES
 #define E3GNN_FWD_WAVES 3
 #endif
-#ifndef E3GNN_BWDW_WAVES
-#define E3GNN_BWDW_WAVES 4
-#endif
-#ifndef E3GNN_BWDX_WAVES
-#define E3GNN_BWDX_WAVES 3
-#endif
-// the fused dE/dx + dE/dw kernel (MODE 3) holds dH2 accumulators and the
-// block's W2 operands on top: 2 waves/SIMD without spills
-#ifndef E3GNN_BWDXW_WAVES
-#define E3GNN_BWDXW_WAVES 2
-#endif
-// ... of the first block (x = 128x0e: 169 VGPRs at 2 waves, one over the
-// 3-wave budget; at 3 waves it spills 18 and measured 3.42 -> 3.34 ms, within
-// box noise of the whole step, so 2)
-#ifndef E3GNN_BWDXW_WAVES_FIRST
-#define E3GNN_BWDXW_WAVES_FIRST 2
-#endif
+// the per-neighbour backward of the last block (k_conv_bwd_nbr): 159 VGPRs
+constexpr int BWD_NBR_WAVES = 3;
+
 namespace e3gnn {
 namespace {
 
@@ -269,24 +255,6 @@ __device__ __forceinline__ void mlp_pre(const WRes& R, const float* __restrict__
   mlp_chain(R, b, lane, m);
 }
 
-// w[:, col0:col0+16] of the tile: lane (g, c) reg r = w[edge 4g+r][channel col0+c]
-__device__ __forceinline__ f32x4 mlp_w_block(const f32x4 (&h2)[4], __amdgpu_buffer_rsrc_t w2,
-                                             int W, int col0, int lane) {
-  const int g = lane >> 4, c = lane & 15;
-  float b[16];
-  const int v = (c * 64 + g * 16) * 4;  // w2p[col0 + c][g][s] = W2s[KH(s) + 4g][col0 + c]
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const f32x4 t4 = ldw4(w2, v, (col0 * 64 + 4 * q) * 4);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) b[4 * q + t] = t4[t];
-  }
-  f32x4 acc = zero4();
-#pragma unroll
-  for (int s = 0; s < 16; ++s) acc = mfma(h2[s >> 2][s & 3], b[s], acc);
-  return acc;
-}
-
 // ---------------------------------------------------------------- TP pieces
 // CG entries grouped by (i, j): each pair's partial sum over k is formed and
 // consumed at once (short live ranges, one product per pair)
@@ -295,26 +263,6 @@ __device__ __forceinline__ constexpr bool cg_pair() {
   for (int q = 0; q < C::n; ++q)
     if (C::e[q].i == I && C::e[q].j == J) return true;
   return false;
-}
-
-template <int L1, int L2, int L3>
-__device__ __forceinline__ void tp_acc(const float* x, const float* y, float w, float* acc) {
-  using C = CG<L1, L2, L3>;
-  float t[2 * L3 + 1];
-#pragma unroll
-  for (int k = 0; k < 2 * L3 + 1; ++k) t[k] = 0.f;
-  sfor<2 * L1 + 1>([&](auto i) {
-    sfor<2 * L2 + 1>([&](auto j) {
-      if constexpr (cg_pair<C, i, j>()) {
-        const float xy = x[i] * y[j];
-        sfor<C::n>([&](auto q) {
-          if constexpr (C::e[q].i == i && C::e[q].j == j) t[C::e[q].k] += C::e[q].c * xy;
-        });
-      }
-    });
-  });
-#pragma unroll
-  for (int k = 0; k < 2 * L3 + 1; ++k) acc[k] += w * t[k];
 }
 
 // The lane's four (edge or channel) slots r = 0..3 in lock-step: every CG
@@ -436,12 +384,6 @@ __device__ __forceinline__ int next_block_col(int jj) {
     if (jj + 1 < L::P[f].mul / 16) return L::P[f].woff + 16 * (jj + 1);
     return fn >= 0 ? L::P[fn].woff : -1;
   }
-}
-// 16 k-values of W2[:, col0 + c] for lane group g (w2p order): 4 x b128
-__device__ __forceinline__ void load_w2p(f32x4 (&b)[4], __amdgpu_buffer_rsrc_t w2p, int lane, int col0) {
-  const int v = ((lane & 15) * 64 + (lane >> 4) * 16) * 4;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) b[q] = ldw4(w2p, v, (col0 * 64 + 4 * q) * 4);
 }
 // w2q blocks of column block col0 (bwd_w dH2 operand): 4 x b128
 __device__ __forceinline__ void load_w2q(f32x4 (&b)[4], __amdgpu_buffer_rsrc_t w2q, int lane, int col0) {
@@ -615,55 +557,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
 }
 
 // ---------------------------------------------------------------- backward
-// Two kernels (one fused kernel held ~250 VGPRs: 1 wave/SIMD):
-//  B1 k_conv_bwd_x:  one wave per NEIGHBOUR node j over its incoming edges
-//      (transposed CSR src_ptr/src_perm, ascending edge id, tiles of 16):
-//      recompute w (MFMA), dE/dx[j] = sum_e TP^T_x(Y_e, w_e, g_ctr(e)) summed in
-//      registers/LDS and written once (no per-edge E x 480 buffer, no gather
-//      pass), and dE/du per edge.
-//  B2 k_conv_bwd_w:  one wave per fixed tile of 16 consecutive edges:
-//      dE/dw = TP^T_w(x_src, Y, g_ctr) (needs no w) -> LDS transpose ->
-//      dH2^T = W2 dw^T (MFMA) -> MLP chain backward -> dE/demb.
-// Each per-edge output is written by exactly one wave per layer (deterministic).
-// In: gagg = dE/dagg / denom (row of the edge's centre).
-
-template <int L1, int L2, int L3>
-__device__ __forceinline__ void tp_bwd_x(const float* x, const float* y, float w, const float* gm,
-                                         float* dx, float* dy) {
-  using C = CG<L1, L2, L3>;
-  float gw[2 * L3 + 1];
-#pragma unroll
-  for (int k = 0; k < 2 * L3 + 1; ++k) gw[k] = gm[k] * w;
-  sfor<2 * L1 + 1>([&](auto i) {
-    sfor<2 * L2 + 1>([&](auto j) {
-      if constexpr (cg_pair<C, i, j>()) {
-        float t = 0.f;  // sum_k C_ijk g_k w
-        sfor<C::n>([&](auto q) {
-          if constexpr (C::e[q].i == i && C::e[q].j == j) t += C::e[q].c * gw[C::e[q].k];
-        });
-        dx[i] += t * y[j];
-        dy[j] += t * x[i];
-      }
-    });
-  });
-}
-template <int L1, int L2, int L3>
-__device__ __forceinline__ float tp_bwd_w(const float* x, const float* y, const float* gm) {
-  using C = CG<L1, L2, L3>;
-  float dwv = 0.f;
-  sfor<2 * L1 + 1>([&](auto i) {
-    sfor<2 * L2 + 1>([&](auto j) {
-      if constexpr (cg_pair<C, i, j>()) {
-        float t = 0.f;
-        sfor<C::n>([&](auto q) {
-          if constexpr (C::e[q].i == i && C::e[q].j == j) t += C::e[q].c * gm[C::e[q].k];
-        });
-        dwv += t * (x[i] * y[j]);
-      }
-    });
-  });
-  return dwv;
-}
 // tp_bwd_x and dE/dw of the same (edge, channel) in one pass: with
 // t'_ij = sum_k C_ijk g_k and u_i = sum_j t'_ij y_j,
 //   dE/dx_i += w u_i,  dE/dy_j += t'_ij (w x_i),  dE/dw = sum_i x_i u_i
@@ -773,73 +666,43 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
   mlp_bwd_chain_ids(R, emb, e < end ? e : -1, lane, dh2, demb);
 }
 
-// B1: lane (g, c) = edge slot c of the tile x channels 4g..4g+3 of a 16-channel
-// block (transposed product w^T = W2^T H2^T: D[channel 4g+r][edge c]).  One
-// edge per lane keeps dE/dY in 8 registers.
-// MODE 0: one wave per NEIGHBOUR node over its incoming edges (transposed CSR),
-// dE/dx[j] summed over the 16 edge lanes of a row (DPP) once per block,
-// accumulated in LDS and written once (the last block).
-// MODE 2: one wave per CENTRE over its CSR edges in tiles of 16 (the forward
-// kernel's mapping), the centre's dE/dagg row (DM floats) staged in LDS once;
-// dE/dx per edge to dxc (summed per neighbour by the transposed-CSR gather).
-// MODE 3: MODE 2 + dE/dw -> dH2 -> MLP chain -> dE/demb from the same registers.
-// MODE 4: MODE 0 + dE/dw -> dH2 -> MLP chain -> dE/demb (the last block: every
-// edge is visited once, by the wave of its neighbour, whose own row is x).
-// The radial weights w of the NEXT visited block are formed (MFMA) before this
-// block's tensor product (VALU), so the matrix pipe works under the VALU stream.
-template <class L, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ? (L::DX == 128 ? E3GNN_BWDXW_WAVES_FIRST : E3GNN_BWDXW_WAVES) : E3GNN_BWDX_WAVES, MODE == 3 ? (L::DX == 128 ? E3GNN_BWDXW_WAVES_FIRST : E3GNN_BWDXW_WAVES) : E3GNN_BWDX_WAVES))) void k_conv_bwd_x(const int* __restrict__ src_ptr,
-                                                    const int* __restrict__ src_perm,
-                                                    const int* __restrict__ center,
-                                                    const float* __restrict__ emb,
-                                                    const float* __restrict__ Y,
-                                                    const float* __restrict__ h,
-                                                    const float* __restrict__ gagg, MlpW W,
-                                                    float* __restrict__ dh,
-                                                    float* __restrict__ dgu, int n_nodes,
-                                                    int n_centers, const int* __restrict__ nbr,
-                                                    float* __restrict__ dxc, int n_edges,
-                                                    const int* __restrict__ row_ptr, int r_begin,
-                                                    int r_end, float* __restrict__ demb) {
-  static_assert(MODE == 0 || MODE == 2 || MODE == 3 || MODE == 4, "backward modes 0, 2, 3, 4");
-  constexpr bool EDGE = MODE == 2 || MODE == 3;  // per-edge dE/dx output (dxc), one wave per centre
-  constexpr bool FW = MODE == 3 || MODE == 4;    // + dE/dw -> dH2 -> MLP chain -> dE/demb
-  // MODE 0/4: dE/dx[j] of the wave's node; MODE 2/3: dE/dagg row of its centre
-  __shared__ __attribute__((aligned(16))) float lds[4][EDGE ? L::DM : L::DX];
+// Backward of the last block (224 message channels), one wave per NEIGHBOUR
+// node j over its incoming edges (transposed CSR src_ptr / src_perm, ascending
+// edge id, tiles of 16): lane (g, c) = edge slot c x channels 4g..4g+3 of a
+// 16-channel block (transposed product w^T = W2^T H2^T: D[channel 4g+r][edge
+// c]); x = h[j] (one row), the edges' centres' dE/dagg gathered per block
+// (DM = 224 floats a row).  dE/dx[j] is summed over the tile's 16 edge lanes
+// (DPP) once per block, accumulated in LDS and written once (no per-edge
+// buffer, no gather pass); per edge: dE/dY -> dE/du, and dE/dw -> dH2^T = W2
+// dw^T (f32 MFMA) -> MLP chain -> dE/demb.  Every edge is visited once (by its
+// neighbour's wave): deterministic.  The radial weights w of the NEXT visited
+// block are formed (MFMA) before this block's tensor product (VALU).
+template <class L>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BWD_NBR_WAVES, BWD_NBR_WAVES))) void k_conv_bwd_nbr(
+    const int* __restrict__ src_ptr, const int* __restrict__ src_perm, const int* __restrict__ center,
+    const float* __restrict__ emb, const float* __restrict__ Y, const float* __restrict__ h,
+    const float* __restrict__ gagg, MlpW W, float* __restrict__ dh, float* __restrict__ dgu, int n_centers,
+    int r_begin, int r_end, float* __restrict__ demb) {
+  __shared__ __attribute__((aligned(16))) float lds[4][L::DX];
   const int wid = threadIdx.x >> 6;
-  // wave index: node (MODE 0) or centre (MODE 2/3)
   const int jn = __builtin_amdgcn_readfirstlane(r_begin + xcd_block() * 4 + wid);
   if (jn >= r_end) return;
   float* dacc = lds[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
-  const int qb = EDGE ? row_ptr[jn] : src_ptr[jn];
-  const int qe = EDGE ? row_ptr[jn + 1] : src_ptr[jn + 1];
-  if constexpr (EDGE) {
-    // stage the centre's dE/dagg row: DM / 4 float4 per wave, all in flight
-    const float4* src = reinterpret_cast<const float4*>(gagg + (int64_t)jn * L::DM);
-    float4* dst = reinterpret_cast<float4*>(dacc);
-    for (int t = lane; t < L::DM / 4; t += 64) dst[t] = src[t];
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-  }
+  const int qb = src_ptr[jn], qe = src_ptr[jn + 1];
   const WRes R = make_wres(W, L::W);
-  const __amdgpu_buffer_rsrc_t Rx =
-      EDGE ? rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4) : rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
-  // MODE 0: the edges' centres' dE/dagg rows through a descriptor over the
-  // whole array (32-bit lane offsets; DM = 224, the host checks
-  // n_centers * 224 * 4 < 2^31); padded slots read past its end: 0
+  const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
+  // the edges' centres' dE/dagg rows through a descriptor over the whole array
+  // (32-bit lane offsets; the host checks n_centers * DM * 4 < 2^31); padded
+  // slots read past its end: 0
   const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
-  if constexpr (!EDGE)
-    for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
+  for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
 
   for (int q0 = qb; q0 < qe; q0 += 16) {
     phase();
     Op3 wq;
     load_w2b(wq, R.w2b, lane, L::P[0].woff);
-    // edge of slot c
-    const int er = (q0 + col < qe) ? (EDGE ? q0 + col : src_perm[q0 + col]) : -1;
-    // EDGE: the slot's gathered row (padded slots: row 0, w = 0 there)
-    const int vx = EDGE ? (er >= 0 ? nbr[er] : 0) * L::DX * 4 : 0;
+    const int er = (q0 + col < qe) ? src_perm[q0 + col] : -1;   // edge of slot c
     const int vg = (er >= 0 ? center[er] * L::DM : n_centers * L::DM) * 4;
     float y[9];
 #pragma unroll
@@ -858,8 +721,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
         for (int r = 0; r < 4; ++r) h2[bb][r] = act_fwd(m.a2[bb][r]);
       split_h2(h2, hq);
     }
-    // MODE 3: dH2^T of the tile's edges (D[hidden 16 bh + 4g + r][edge c]),
-    // accumulated over the visited blocks
+    // dH2^T of the tile's edges (D[hidden 16 bh + 4g + r][edge c]), accumulated
+    // over the visited blocks
     f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
     int nb = 0;     // visited blocks of the tile
     // w of the current block (formed during the previous one) and of the
@@ -880,7 +743,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
         for (int jj = 0; jj < MUL / 16; ++jj) {
           float x[4 * D1], dx[4 * D1];
           phase();
-          ldv<4 * D1>(Rx, vx + 4 * g * D1 * 4, (XOFF + 16 * jj * D1) * 4, x);
+          ldv<4 * D1>(Rx, 4 * g * D1 * 4, (XOFF + 16 * jj * D1) * 4, x);
 #pragma unroll
           for (int i = 0; i < 4 * D1; ++i) dx[i] = 0.f;
           sfor<L::NP>([&](auto pi) {
@@ -888,22 +751,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
             if constexpr (p.l1 == I) {
               constexpr int D3 = 2 * p.l3 + 1;
               phase();
-              // dE/dagg of the edges' centres: the centre's row in LDS (4 D3
-              // contiguous floats per lane group), or gathered (MODE 0)
               float gm[4 * D3];
-              if constexpr (EDGE) {
-                const float* gl = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
-#pragma unroll
-                for (int k = 0; k < 4 * D3; ++k) gm[k] = gl[k];
-              } else {
-                load_gm<L, pi>(gm, Rg, vg, g, jj);
-              }
-              // MODE 3: W2 operands of this block's dH2 product, issued now and
-              // consumed after the tensor product
+              load_gm<L, pi>(gm, Rg, vg, g, jj);
+              // W2 operands of this block's dH2 product, issued now and consumed
+              // after the tensor product
               f32x4 bq[4];
-              if constexpr (FW) load_w2q(bq, R.w2r, lane, p.woff + 16 * jj);
+              load_w2q(bq, R.w2r, lane, p.woff + 16 * jj);
               float dwr[4];
-              // w^T block: A = W2s[:, col0 + i]^T (w2p order), B = H2^T
               const f32x4 wv = wcur;
               if (nb + 1 < NBLK) wnxt = w2_block<false>(hq, wq);
               if (nb + 2 < NBLK) load_w2b(wq, R.w2v, lane, 16 * (nb + 2));
@@ -913,13 +767,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
                 float dy[2 * p.l2 + 1];
 #pragma unroll
                 for (int q = 0; q < 2 * p.l2 + 1; ++q) dy[q] = 0.f;
-                // padded slots: w = 0 and g = 0 (MODE 3: y = 0, so dE/dw = 0)
-                if constexpr (FW)
-                  dwr[r] = tp_bwd_xw<p.l1, p.l2, p.l3>(x + r * D1, y + yoff(p.l2), wv[r],
-                                                       gm + r * D3, dx + r * D1, dy);
-                else
-                  tp_bwd_x<p.l1, p.l2, p.l3>(x + r * D1, y + yoff(p.l2), wv[r], gm + r * D3,
-                                             dx + r * D1, dy);
+                // padded slots: w = 0, g = 0 and y = 0 (so dE/dw = 0)
+                dwr[r] = tp_bwd_xw<p.l1, p.l2, p.l3>(x + r * D1, y + yoff(p.l2), wv[r], gm + r * D3,
+                                                     dx + r * D1, dy);
                 if constexpr (p.l2 > 0) {
 #pragma unroll
                   for (int q = 0; q < 2 * p.l2 + 1; ++q) dYa[yoff(p.l2) + q] += dy[q];
@@ -929,31 +779,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
               }
               pin<4 * D1>(dx);
               pin<8>(dYa + 1);
-              if constexpr (FW) {
-                // dH2^T += W2[:, block] dw^T: k = lane group g, channel 4g + r
+              // dH2^T += W2[:, block] dw^T: k = lane group g, channel 4g + r
 #pragma unroll
-                for (int bh = 0; bh < 4; ++bh)
+              for (int bh = 0; bh < 4; ++bh)
 #pragma unroll
-                  for (int r = 0; r < 4; ++r) dh2[bh] = mfma(bq[bh][r], dwr[r], dh2[bh]);
-              }
+                for (int r = 0; r < 4; ++r) dh2[bh] = mfma(bq[bh][r], dwr[r], dh2[bh]);
               wcur = wnxt;
               ++nb;
             }
           });
           phase();
-          if constexpr (EDGE) {  // per-edge dE/dx[nbr] (not needed for the first block)
-            if (dxc && er >= 0) {
-              float* o = dxc + (int64_t)er * L::DX + XOFF + (16 * jj + 4 * g) * D1;
+          // sum over the tile's 16 edges (row lanes), lane c == 0 accumulates
 #pragma unroll
-              for (int i = 0; i < 4 * D1; ++i) o[i] = dx[i];
-            }
-          } else {
-            // sum over the tile's 16 edges (row lanes), lane c == 0 accumulates
-#pragma unroll
-            for (int i = 0; i < 4 * D1; ++i) {
-              const float v = row_sum16(dx[i]);
-              if (col == 0) dacc[XOFF + (16 * jj + 4 * g) * D1 + i] += v;
-            }
+          for (int i = 0; i < 4 * D1; ++i) {
+            const float v = row_sum16(dx[i]);
+            if (col == 0) dacc[XOFF + (16 * jj + 4 * g) * D1 + i] += v;
           }
         }
       }
@@ -963,11 +803,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
     // dE/dY of edge c: sum over the 4 lane groups, then dE/du through the SH
     // polynomials (serial_code.py:50-70)
 #pragma unroll
-    for (int q = 1; q < 9; ++q) {
-      float v = dYa[q];
-      v = sum_rows4(v);
-      dYa[q] = v;
-    }
+    for (int q = 1; q < 9; ++q) dYa[q] = sum_rows4(dYa[q]);
     if (g == 0 && er >= 0) {
       const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f, c15 = s3 * s5;
       const float is3 = 0.57735026918962576f;  // 1 / sqrt(3)
@@ -981,123 +817,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ?
       o[1] += gy;
       o[2] += gz;
     }
-    if constexpr (FW) {
-      phase();
-      mlp_bwd_chain_ids(R, emb, er, lane, dh2, demb);
-    }
-  }
-  if constexpr (!EDGE) {
     phase();
-    __builtin_amdgcn_s_waitcnt(0);
-    float* dhj = dh + (int64_t)jn * L::DX;
-    for (int t = lane; t < L::DX; t += 64) dhj[t] = dacc[t];
+    mlp_bwd_chain_ids(R, emb, er, lane, dh2, demb);
   }
-}
-
-// dE/dw of one visited 16-channel block in LDS: [edge slot][DWS]
-constexpr int DWS = 20;       // row stride (16-byte aligned rows for b128 reads)
-constexpr int DWB = 16 * DWS;
-
-// dH2^T += W2[:, block] dw^T on v_mfma_f32_16x16x4_f32 (operands prefetched a block ahead;
-// w2q[col0/16][bh][g][c][s] = W2s[16 bh + c][col0 + 4s + g])
-__device__ __forceinline__ void mfma_dw(f32x4 (&dh2)[4], const f32x4 (&bq)[4], const float* dwb,
-                                        int lane) {
-  const int g = lane >> 4, c = lane & 15;
-#pragma unroll
-  for (int bh = 0; bh < 4; ++bh)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) dh2[bh] = mfma(bq[bh][s], dwb[c * DWS + 4 * s + g], dh2[bh]);
-}
-
-template <class L>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_BWDW_WAVES, E3GNN_BWDW_WAVES))) void k_conv_bwd_w(const int* __restrict__ center,
-                                                    const int* __restrict__ nbr,
-                                                    const float* __restrict__ emb,
-                                                    const float* __restrict__ Y,
-                                                    const float* __restrict__ h,
-                                                    const float* __restrict__ gagg, MlpW W,
-                                                    float* __restrict__ demb, int e_begin,
-                                                    int e_end, int n_nodes, int n_centers) {
-  // per wave: two dw transpose tiles [16 slots][DWS] + Y of the tile [16][9]
-  __shared__ __attribute__((aligned(16))) float lds[4][2 * DWB + 160];
-  const int wid = threadIdx.x >> 6;
-  const int e0 = __builtin_amdgcn_readfirstlane(e_begin + (xcd_block() * 4 + wid) * 16);
-  if (e0 >= e_end) return;
-  const int end = e_end;
-  float* dwbuf = lds[wid];
-  float* ybuf = lds[wid] + 2 * DWB;
-  const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
-  const WRes R = make_wres(W, L::W);
-  int src[4], vg[4];
-  load_tile_edges(nbr, Y, e0, end, lane, src, ybuf);
-  // dE/dagg rows of the tile's centres [cb, cb + nc): descriptor based at the
-  // first one (16 consecutive CSR edges: small offsets at any system size)
-  const int cb = __builtin_amdgcn_readfirstlane(center[e0]);
-  const int nc = __builtin_amdgcn_readfirstlane(center[min(e0 + 16, end) - 1]) - cb + 1;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int e = e0 + 4 * g + r;
-    vg[r] = (e < end ? (center[e] - cb) * L::DM : nc * L::DM) * 4;  // padded: reads 0
-  }
-  const __amdgpu_buffer_rsrc_t Rh = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
-  const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg + (int64_t)cb * L::DM, (int64_t)nc * L::DM * 4);
-  int vh[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) vh[r] = src[r] * L::DX * 4;
-  f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
-  int nb = 0;  // visited blocks; block b's dE/dw goes to LDS buffer b & 1
-  f32x4 bq[4];  // W2 operands of the next block
-  load_w2q(bq, R.w2q, lane, L::P[0].woff);
-
-  sfor<3>([&](auto I) {
-    constexpr int MUL = iblock_mul<L, I>();
-    if constexpr (MUL > 0) {
-      constexpr int D1 = 2 * I + 1;
-      constexpr int XOFF = iblock_xoff<L, I>();
-      for (int jj = 0; jj < MUL / 16; ++jj) {
-        const int u = 16 * jj + col;
-        float x[4][D1];
-        phase();
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          ldv<D1>(Rh, vh[r] + col * D1 * 4, (XOFF + 16 * jj * D1) * 4, x[r]);
-        sfor<L::NP>([&](auto pi) {
-          constexpr PathDef p = L::P[pi];
-          if constexpr (p.l1 == I) {
-            constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
-            phase();
-            // software pipeline: this block's dE/dagg gathers are issued, then the
-            // MFMAs of the previous (complete) block pair run while they are in flight
-            float gm[4][D3];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              ldv<D3>(Rg, vg[r] + col * D3 * 4, (p.moff + 16 * jj * D3) * 4, gm[r]);
-            if (nb > 0) {
-              mfma_dw(dh2, bq, dwbuf + ((nb - 1) & 1) * DWB, lane);
-              load_w2q(bq, R.w2q, lane, p.woff + 16 * jj);
-            }
-            phase();
-            float* dwc = dwbuf + (nb & 1) * DWB;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float* yr = ybuf + (4 * g + r) * 9;
-              float y[D2];
-#pragma unroll
-              for (int q = 0; q < D2; ++q) y[q] = yr[yoff(p.l2) + q];
-              dwc[(4 * g + r) * DWS + col] = tp_bwd_w<p.l1, p.l2, p.l3>(x[r], y, gm[r]);
-            }
-            ++nb;
-          }
-        });
-      }
-    }
-  });
-
   phase();
-  mfma_dw(dh2, bq, dwbuf + ((nb - 1) & 1) * DWB, lane);  // last block
-  // ---- MLP chain backward (pre-activations recomputed)
-  phase();
-  mlp_bwd_chain(R, emb, e0, end, lane, dh2, demb);
+  __builtin_amdgcn_s_waitcnt(0);
+  float* dhj = dh + (int64_t)jn * L::DX;
+  for (int t = lane; t < L::DX; t += 64) dhj[t] = dacc[t];
 }
 
 // ================================================================ lock-step kernels
@@ -1164,139 +890,6 @@ __device__ __forceinline__ int ls_tiles(const int* __restrict__ row_ptr, int cb,
     }
   }
   return __builtin_amdgcn_readfirstlane(T);
-}
-
-// Forward: agg[c] = sum_e TP(h[nbr e], Y_e, w_e) / denom (IrrepsConvolution.forward,
-// convolution.py:104-123); the centre's message sum over its tiles stays in LDS.
-// Per block pair: both blocks' w = H2 W2 (bf16x6) are formed at the pair start,
-// so the second block's MFMAs run under the first block's tensor product; the
-// neighbour rows of the next channel group are loaded under the current one.
-template <class L>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_fwd_ls(
-    const int* __restrict__ row_ptr, const int* __restrict__ nbr, const float* __restrict__ emb,
-    const float* __restrict__ Y, const float* __restrict__ h, float* __restrict__ agg, MlpW W,
-    int c_begin, int c_end, int n_nodes, float denom) {
-  constexpr int NBLK = L::W / 16, NPAIR = NBLK / 2;
-  static_assert(NBLK % 2 == 0, "weight blocks come in pairs");
-  constexpr int NST = LS_PAIR_W / 16 / 256;  // b128 staging chunks per thread
-  // [4 agg rows | 4 x Y of the tile (16 x 9, padded to 160) | pair image]
-  __shared__ __attribute__((aligned(16))) float smem[4 * L::DM + 4 * 160 + LS_PAIR_W / 4];
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, g = lane >> 4, col = lane & 15;
-  const int cb = c_begin + blockIdx.x * 4;
-  const int c = cb + wid;
-  const bool valid = c < c_end;
-  const int beg = valid ? row_ptr[c] : 0, end = valid ? row_ptr[c + 1] : 0;
-  const int ntile = valid ? max(1, (end - beg + 15) >> 4) : 0;
-  const int T = ls_tiles(row_ptr, cb, c_end, true);
-  float* acl = smem + wid * L::DM;
-  float* ybuf = smem + 4 * L::DM + wid * 160;
-  char* img = reinterpret_cast<char*>(smem + 4 * L::DM + 4 * 160);
-  const WRes R = make_wres(W, L::W);
-  const __amdgpu_buffer_rsrc_t Rh = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
-  const float rden = 1.0f / denom;
-  f32x4 st[NST];
-  auto issue = [&](int P) {
-#pragma unroll
-    for (int i = 0; i < NST; ++i) st[i] = ldw4(R.w2v, (tid + 256 * i) * 16, P * LS_PAIR_W);
-  };
-  auto commit = [&]() {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < NST; ++i) *reinterpret_cast<f32x4*>(img + (tid + 256 * i) * 16) = st[i];
-    __syncthreads();
-  };
-  issue(0);
-  for (int t = 0; t < T; ++t) {
-    const bool act = t < ntile;   // wave-uniform
-    const bool first_tile = t == 0;
-    const int e0 = beg + 16 * t;
-    int src[4];
-    float xpf[20];   // neighbour rows of the next channel group (4 edges x D1)
-    auto load_group = [&](auto Iq, int jq) {
-      constexpr int D1q = 2 * Iq + 1;
-      constexpr int XOq = iblock_xoff<L, Iq>();
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        ldv<D1q>(Rh, (src[r] * L::DX + col * D1q) * 4, (XOq + 16 * jq * D1q) * 4, xpf + r * D1q);
-    };
-    Op3 hq;
-    if (act) {
-      load_tile_edges(nbr, Y, e0, end, lane, src, ybuf);
-      load_group(std::integral_constant<int, first_I<L>()>{}, 0);
-      MlpT m;
-      mlp_pre(R, emb, e0, end, lane, m);
-      f32x4 h2[4];
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h2[b][r] = act_fwd(m.a2[b][r]);
-      split_h2(h2, hq);
-    }
-    int nb = 0;
-    f32x4 wv0 = zero4(), wv1 = zero4();   // w of the pair's two blocks
-    sfor<3>([&](auto I) {
-      constexpr int MUL = iblock_mul<L, I>();
-      if constexpr (MUL > 0) {
-        constexpr int D1 = 2 * I + 1;
-        for (int j = 0; j < MUL / 16; ++j) {
-          float x[4][D1];
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int i = 0; i < D1; ++i) x[r][i] = xpf[r * D1 + i];
-          if (act) {
-            if (j + 1 < MUL / 16) {
-              load_group(I, j + 1);
-            } else {
-              constexpr int IN = next_I<L>(I);
-              if constexpr (IN >= 0) load_group(std::integral_constant<int, IN>{}, 0);
-            }
-          }
-          sfor<L::NP>([&](auto pi) {
-            constexpr PathDef p = L::P[pi];
-            if constexpr (p.l1 == I) {
-              constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
-              if ((nb & 1) == 0) {   // pair start: stage it, fetch the next one
-                commit();
-                issue((nb >> 1) + 1 < NPAIR ? (nb >> 1) + 1 : 0);
-                if (act) {
-                  Op3 wq;
-                  lds_op3(wq, img, lane);
-                  wv0 = w2_block<true>(hq, wq);
-                  lds_op3(wq, img + LS_BLK, lane);
-                  wv1 = w2_block<true>(hq, wq);
-                }
-              }
-              if (act) {
-                const f32x4 wv = (nb & 1) ? wv1 : wv0;
-                float acc[D3];
-#pragma unroll
-                for (int k = 0; k < D3; ++k) acc[k] = 0.f;
-                // padded edges: Y = 0
-                tp_acc4<p.l1, p.l2, p.l3>(&x[0][0], ybuf + 4 * g * 9 + yoff(p.l2), 9, wv, acc);
-#pragma unroll
-                for (int k = 0; k < D3; ++k) {
-                  const float v = sum_rows4(acc[k]) * rden;
-                  if (g == 0) {
-                    float* a = acl + p.moff + (16 * j + col) * D3 + k;
-                    *a = first_tile ? v : *a + v;
-                  }
-                }
-              }
-              ++nb;
-            }
-          });
-        }
-      }
-    });
-  }
-  if (valid) {
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-    const float4* s4 = reinterpret_cast<const float4*>(acl);
-    float4* d4 = reinterpret_cast<float4*>(agg + (int64_t)c * L::DM);
-    for (int k = lane; k < L::DM / 4; k += 64) d4[k] = s4[k];
-  }
 }
 
 // Backward of a first / middle block (per-edge dE/dx to dxc, summed per
@@ -1485,21 +1078,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 }  // namespace
 
-hipError_t launch_conv_fwd_ls(int kind, const FusedArgs& a, hipStream_t s) {
-  const int nc = a.c_end - a.c_begin;
-  if (nc <= 0) return hipSuccess;
-  const dim3 grid((nc + 3) / 4), block(256);
-  switch (kind) {
-    case 0: hipLaunchKernelGGL(k_conv_fwd_ls<LayerFirst>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb, a.Y,
-                               a.h, a.agg, a.W, a.c_begin, a.c_end, a.n_nodes, a.denom); break;
-    case 1: hipLaunchKernelGGL(k_conv_fwd_ls<LayerMid>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb, a.Y,
-                               a.h, a.agg, a.W, a.c_begin, a.c_end, a.n_nodes, a.denom); break;
-    default: hipLaunchKernelGGL(k_conv_fwd_ls<LayerLast>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb,
-                                a.Y, a.h, a.agg, a.W, a.c_begin, a.c_end, a.n_nodes, a.denom); break;
-  }
-  return hipGetLastError();
-}
-
 hipError_t launch_conv_bwd_ls(int kind, const FusedArgs& a, hipStream_t s) {
   const int nc = a.c_end - a.c_begin;
   if (nc <= 0 || a.n_nodes <= 0) return hipSuccess;
@@ -1511,10 +1089,7 @@ hipError_t launch_conv_bwd_ls(int kind, const FusedArgs& a, hipStream_t s) {
     case 1: hipLaunchKernelGGL(k_conv_bwd_ls<LayerMid>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb, a.Y,
                                a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb, a.c_begin, a.c_end, a.n_nodes);
       break;
-    default: hipLaunchKernelGGL(k_conv_bwd_ls<LayerLast>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb,
-                                a.Y, a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb, a.c_begin, a.c_end,
-                                a.n_nodes);
-      break;
+    default: return hipErrorInvalidValue;  // the last block: launch_conv_bwd_nbr_last
   }
   return hipGetLastError();
 }
@@ -1527,53 +1102,6 @@ static hipError_t fwd_impl(const FusedArgs& a, hipStream_t s) {
                      a.Y, a.h, a.agg, a.W, a.c_begin, a.c_end, a.n_nodes, a.denom);
   return hipGetLastError();
 }
-template <class L>
-static hipError_t bwd_x_impl(const FusedArgs& a, hipStream_t s) {
-  if (a.n_nodes <= 0 || a.n_edges <= 0) return hipSuccess;
-  if (a.edge_order) {  // per-edge dE/dx (caller gathers)
-    if (a.fuse_w) {  // dE/dx, dE/du and dE/dw -> dE/demb in one pass
-      const int nc = a.c_end - a.c_begin;
-      if (nc <= 0) return hipSuccess;
-      hipLaunchKernelGGL((k_conv_bwd_x<L, 3>), dim3((nc + 3) / 4), dim3(256), 0, s, a.src_ptr,
-                         a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
-                         a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr, a.c_begin,
-                         a.c_end, a.demb);
-    } else {   // dE/dx and dE/du only (the separate dE/dw kernel follows)
-      const int nc = a.c_end - a.c_begin;
-      if (nc <= 0) return hipSuccess;
-      hipLaunchKernelGGL((k_conv_bwd_x<L, 2>), dim3((nc + 3) / 4), dim3(256), 0, s, a.src_ptr,
-                         a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu,
-                         a.n_nodes, a.n_centers, a.nbr, a.dxc, a.n_edges, a.row_ptr, a.c_begin,
-                         a.c_end, a.demb);
-    }
-    return hipGetLastError();
-  }
-  // per neighbour node over [node_begin, node_end) (fuse_w: + dE/dw -> dE/demb
-  // of its incoming edges); first block: dE/dx of the embedding is not needed
-  // (scratch sink), only dE/du
-  const int nn = a.node_end - a.node_begin;
-  if (nn <= 0) return hipSuccess;
-  if (a.fuse_w)
-    hipLaunchKernelGGL((k_conv_bwd_x<L, 4>), dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr,
-                       a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W,
-                       a.dh ? a.dh : a.scratch_dh, a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc,
-                       a.n_edges, a.row_ptr, a.node_begin, a.node_end, a.demb);
-  else
-    hipLaunchKernelGGL((k_conv_bwd_x<L, 0>), dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr,
-                       a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W,
-                       a.dh ? a.dh : a.scratch_dh, a.dgu, a.n_nodes, a.n_centers, a.nbr, a.dxc,
-                       a.n_edges, a.row_ptr, a.node_begin, a.node_end, a.demb);
-  return hipGetLastError();
-}
-template <class L>
-static hipError_t bwd_w_impl(const FusedArgs& a, hipStream_t s) {
-  const int tiles = (a.e_end - a.e_begin + 15) / 16;  // edge range of this launch
-  if (a.n_nodes <= 0 || tiles <= 0 || a.fuse_w) return hipSuccess;  // fused: done in bwd_x
-  hipLaunchKernelGGL(k_conv_bwd_w<L>, dim3((tiles + 3) / 4), dim3(256), 0, s, a.center, a.nbr,
-                     a.emb, a.Y, a.h, a.gagg, a.W, a.demb, a.e_begin, a.e_end, a.n_nodes,
-                     a.n_centers);
-  return hipGetLastError();
-}
 
 hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s) {
   switch (kind) {
@@ -1582,23 +1110,13 @@ hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s) {
     default: return fwd_impl<LayerLast>(a, s);
   }
 }
-hipError_t launch_conv_bwd_x(int kind, const FusedArgs& a, hipStream_t s) {
-  switch (kind) {
-    case 0: return bwd_x_impl<LayerFirst>(a, s);
-    case 1: return bwd_x_impl<LayerMid>(a, s);
-    default: return bwd_x_impl<LayerLast>(a, s);
-  }
-}
-hipError_t launch_conv_bwd_w(int kind, const FusedArgs& a, hipStream_t s) {
-  switch (kind) {
-    case 0: return bwd_w_impl<LayerFirst>(a, s);
-    case 1: return bwd_w_impl<LayerMid>(a, s);
-    default: return bwd_w_impl<LayerLast>(a, s);
-  }
-}
-hipError_t launch_conv_bwd(int kind, const FusedArgs& a, hipStream_t s) {
-  const hipError_t e = launch_conv_bwd_x(kind, a, s);
-  return e != hipSuccess ? e : launch_conv_bwd_w(kind, a, s);
+hipError_t launch_conv_bwd_nbr_last(const FusedArgs& a, hipStream_t s) {
+  const int nn = a.node_end - a.node_begin;
+  if (nn <= 0 || a.n_nodes <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_conv_bwd_nbr<LayerLast>, dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr,
+                     a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu, a.n_centers,
+                     a.node_begin, a.node_end, a.demb);
+  return hipGetLastError();
 }
 
 }  // namespace e3gnn

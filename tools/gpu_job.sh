@@ -28,17 +28,12 @@ for s in "$@"; do
     benchnl) step benchnl 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     benchq) step bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10 ;;
     benchf) step benchf 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
-    benchnofuse) step benchnofuse 600 env E3GNN_BWD_FUSE=0 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
-    benchsplit) step benchsplit 600 env E3GNN_BWD=split python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchmorton) step benchmorton 600 env E3GNN_BENCH_ORDER=morton python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchmorton_*) v=${s#benchmorton_}; step benchmorton_$v 600 env E3GNN_BENCH_ORDER=morton E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     t_*) t=${s#t_}; step t_$t 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k $t ;;
-    benchn) step benchn 600 env E3GNN_BWD_X=node python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
-    testsn) step testsn 600 env E3GNN_BWD_X=node python -m pytest tests/test_gpu_parity.py -q -x ;;
     bench10k) step bench10k 300 python bench.py --cells 11 --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --profile-only --no-parity-check ;;
     proftrace) step proftrace 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/proftrace -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
-    benchlastedge) step benchlastedge 600 env E3GNN_LAST_EDGE=1 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     bench2gloo) step bench2gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --same-device --no-cpu-baseline ;;
     traingraph) step traingraph 600 python -u -m pytest tests/test_gpu_train.py -x -v --timeout 300 --timeout-method thread -k "graph" ;;
     highdeg) step highdeg 300 python tools/diag_highdeg.py && step highdeg0 300 env E3GNN_NODELIN=0 python tools/diag_highdeg.py ;;
@@ -71,13 +66,7 @@ for s in "$@"; do
     testsv_*) v=${s#testsv_}; step tests_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -m pytest tests -m gpu -x -q ;;
     diagewc) step diagewc 400 python tools/diag_ewc_interleave.py ;;
     bench2self) step bench2self 600 python bench.py --gpus 2 --same-device --steps 2 --warmup 1 --cells 11 --no-cpu-baseline ;;
-    parityls) step parityls 600 env E3GNN_CONV=ls python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
-    benchls) step benchls 600 env E3GNN_CONV=ls python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
-    benchlsb) step benchlsb 600 env E3GNN_CONV=lsb python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     paritydef) step paritydef 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
-    profls) step profls 600 env E3GNN_CONV=ls rocprofv3 --kernel-trace --stats -d gpurun_out/profls -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --profile-only --no-parity-check ;;
-    pmcsqls) step pmcsqls 600 env E3GNN_CONV=ls rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES --kernel-trace --output-format csv -d gpurun_out/pmc_sqls -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
-    pmcsq2ls) step pmcsq2ls 600 env E3GNN_CONV=ls rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM_RD SQ_INSTS_VALU_MFMA_MOPS_F32 --kernel-trace --output-format csv -d gpurun_out/pmc_sq2ls -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
     reduce) step reduce 300 python tools/diag_graph_reduce.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
