@@ -265,73 +265,146 @@ __device__ __forceinline__ constexpr bool cg_pair() {
   return false;
 }
 
-// The lane's four (edge or channel) slots r = 0..3 in lock-step: every CG
-// product is issued for the four slots back to back, so the dependency chains
-// of the contraction run four-wide (the per-slot form serialises them).
-// Forward: acc[k] += sum_r w[r] sum_ij C_ijk x[r][i] y[r][j]; y[r] = the slot's
-// SH block (stride ys between slots).
+// The lane's four edge slots r = 0..3 in lock-step (the dependency chains of
+// the contraction run four-wide).  Forward:
+//   acc[k] += sum_ij C_ijk s_ij,  s_ij = sum_r w[r] x[r][i] y[r][j]
+// (4 per (i, j) pair + 1 per CG entry; forming sum_ij C_ijk x y per slot first
+// and weighting at the end costs 4 per CG entry); y[r] = the slot's SH block
+// (stride ys between slots).
 template <int L1, int L2, int L3>
 __device__ __forceinline__ void tp_acc4(const float* x, const float* y, int ys, const f32x4 w,
                                         float* acc) {
   using C = CG<L1, L2, L3>;
-  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
+  constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1;
   float yv[4][D2];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int q = 0; q < D2; ++q) yv[r][q] = y[r * ys + q];
-  float t[4][D3];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int k = 0; k < D3; ++k) t[r][k] = 0.f;
   sfor<D1>([&](auto i) {
+    float wx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wx[r] = w[r] * x[r * D1 + i];
     sfor<D2>([&](auto j) {
       if constexpr (cg_pair<C, i, j>()) {
-        float xy[4];
+        float sv = wx[0] * yv[0][j];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xy[r] = x[r * D1 + i] * yv[r][j];
+        for (int r = 1; r < 4; ++r) sv += wx[r] * yv[r][j];
         sfor<C::n>([&](auto q) {
-          if constexpr (C::e[q].i == i && C::e[q].j == j) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) t[r][C::e[q].k] += C::e[q].c * xy[r];
-          }
+          if constexpr (C::e[q].i == i && C::e[q].j == j) acc[C::e[q].k] += C::e[q].c * sv;
         });
       }
     });
   });
-#pragma unroll
-  for (int k = 0; k < D3; ++k) acc[k] += (w[0] * t[0][k] + w[1] * t[1][k]) + (w[2] * t[2][k] + w[3] * t[3][k]);
 }
 
-// Backward, the lane's 4 channels r of one edge: with t'_rij = sum_k C_ijk
-// g[r][k] and u_ri = sum_j t'_rij y_j,
-//   dx[r][i] += w[r] u_ri,  dy_j += sum_r t'_rij w[r] x[r][i],  dw[r] = sum_i x[r][i] u_ri
+// Backward, the lane's 4 channels r of one edge:
+//   u_ri = sum_jk C_ijk y_j g[r][k],  dx[r][i] += w[r] u_ri,  dw[r] = sum_i x[r][i] u_ri,
+//   dy_j += sum_ik C_ijk sum_r w[r] x[r][i] g[r][k]
+// Two contraction orders, chosen per path at compile time by VALU count:
+//  * by (i, j): t'_rij = sum_k C_ijk g[r][k] (4 per CG entry: g is per channel),
+//    u_ri += t'_rij y_j, dy_j += sum_r t'_rij w[r] x[r][i] (4 + 4 per (i, j) pair);
+//  * by (i, k): ytilde_ik = sum_j C_ijk y_j (1 per CG entry: y is per edge, the
+//    same for the lane's 4 channels), u_ri += ytilde_ik g[r][k] and
+//    m_ik = sum_r w[r] x[r][i] g[r][k] (4 + 4 per (i, k) pair), dy_j += C_ijk m_ik
+//    (1 per CG entry).  For the paths with many CG entries per output (l >= 1
+//    on all three legs) this is ~25 % fewer VALU instructions.
+template <class C, int I, int K>
+__device__ __forceinline__ constexpr bool cg_ik() {
+  for (int q = 0; q < C::n; ++q)
+    if (C::e[q].i == I && C::e[q].k == K) return true;
+  return false;
+}
+template <class C>
+constexpr int cg_count_pairs(bool by_ik) {
+  int n = 0;
+  for (int q = 0; q < C::n; ++q) {
+    bool first = true;
+    for (int p = 0; p < q; ++p)
+      if (C::e[p].i == C::e[q].i && (by_ik ? C::e[p].k == C::e[q].k : C::e[p].j == C::e[q].j)) first = false;
+    n += first;
+  }
+  return n;
+}
+// CG entries that cost an instruction in the (i, j) order (a pair's only entry
+// with coefficient 1 is a register alias)
+template <class C>
+constexpr int cg_cost_ij_entries() {
+  int n = 0;
+  for (int q = 0; q < C::n; ++q) {
+    int cnt = 0;
+    for (int p = 0; p < C::n; ++p) cnt += C::e[p].i == C::e[q].i && C::e[p].j == C::e[q].j;
+    n += !(cnt == 1 && C::e[q].c == 1.0f);
+  }
+  return n;
+}
+template <int L1, int L2, int L3>
+constexpr bool tp_bwd_by_ik() {
+  using C = CG<L1, L2, L3>;
+  const int P = cg_count_pairs<C>(false), Q = cg_count_pairs<C>(true);
+  const int ij = 4 * (cg_cost_ij_entries<C>() + P) + (L2 > 0 ? 4 * P : 0);
+  const int ik = C::n + 4 * Q + (L2 > 0 ? 4 * Q + C::n : 0);
+  return ik < ij;
+}
+
 template <int L1, int L2, int L3>
 __device__ __forceinline__ void tp_bwd_xw4(const float* x, const float* y, const f32x4 w,
                                            const float* gm, float* dx, float* dy, float* dw) {
   using C = CG<L1, L2, L3>;
   constexpr int D1 = 2 * L1 + 1, D2 = 2 * L2 + 1, D3 = 2 * L3 + 1;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) dw[r] = 0.f;
+  for (int r = 0; r < 4; ++r) dw[r] = -0.f;
+  // ytilde depends on the edge only: without this opaque copy LLVM hoists
+  // every path's ytilde out of the channel-group loop (74 live values for
+  // l1 = 2: spills)
+  float yl[D2];
+  if constexpr (tp_bwd_by_ik<L1, L2, L3>()) {
+#pragma unroll
+    for (int q = 0; q < D2; ++q) yl[q] = y[q];
+    pin<D2>(yl);
+  }
   sfor<D1>([&](auto i) {
-    float u[4] = {0.f, 0.f, 0.f, 0.f}, wx[4];
+    float u[4] = {-0.f, -0.f, -0.f, -0.f}, wx[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) wx[r] = w[r] * x[r * D1 + i];
-    sfor<D2>([&](auto j) {
-      if constexpr (cg_pair<C, i, j>()) {
-        float tp[4] = {0.f, 0.f, 0.f, 0.f};
-        sfor<C::n>([&](auto q) {
-          if constexpr (C::e[q].i == i && C::e[q].j == j) {
+    if constexpr (tp_bwd_by_ik<L1, L2, L3>()) {
+      sfor<D3>([&](auto k) {
+        if constexpr (cg_ik<C, i, k>()) {
+          float yt = -0.f;
+          sfor<C::n>([&](auto q) {
+            if constexpr (C::e[q].i == i && C::e[q].k == k) yt += C::e[q].c * yl[C::e[q].j];
+          });
 #pragma unroll
-            for (int r = 0; r < 4; ++r) tp[r] += C::e[q].c * gm[r * D3 + C::e[q].k];
+          for (int r = 0; r < 4; ++r) u[r] += yt * gm[r * D3 + k];
+          if constexpr (L2 > 0) {
+            float m = wx[0] * gm[k];
+#pragma unroll
+            for (int r = 1; r < 4; ++r) m += wx[r] * gm[r * D3 + k];
+            sfor<C::n>([&](auto q) {
+              if constexpr (C::e[q].i == i && C::e[q].k == k) dy[C::e[q].j] += C::e[q].c * m;
+            });
           }
-        });
+        }
+      });
+    } else {
+      sfor<D2>([&](auto j) {
+        if constexpr (cg_pair<C, i, j>()) {
+          float tp[4] = {-0.f, -0.f, -0.f, -0.f};
+          sfor<C::n>([&](auto q) {
+            if constexpr (C::e[q].i == i && C::e[q].j == j) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) u[r] += tp[r] * y[j];
-        if constexpr (L2 > 0) dy[j] += (tp[0] * wx[0] + tp[1] * wx[1]) + (tp[2] * wx[2] + tp[3] * wx[3]);
-      }
-    });
+              for (int r = 0; r < 4; ++r) tp[r] += C::e[q].c * gm[r * D3 + C::e[q].k];
+            }
+          });
+#pragma unroll
+          for (int r = 0; r < 4; ++r) u[r] += tp[r] * y[j];
+          if constexpr (L2 > 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dy[j] += tp[r] * wx[r];
+          }
+        }
+      });
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       dx[r * D1 + i] += w[r] * u[r];
@@ -527,7 +600,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
               phase();
               float acc[D3];
 #pragma unroll
-              for (int k = 0; k < D3; ++k) acc[k] = 0.f;
+              for (int k = 0; k < D3; ++k) acc[k] = -0.f;
               // the lane's 4 edges in lock-step (padded edges have Y = 0)
               tp_acc4<p.l1, p.l2, p.l3>(&x[0][0], ybuf + 4 * g * 9 + yoff(p.l2), 9, wv, acc);
 #pragma unroll
@@ -566,13 +639,13 @@ template <int L1, int L2, int L3>
 __device__ __forceinline__ float tp_bwd_xw(const float* x, const float* y, float w, const float* gm,
                                            float* dx, float* dy) {
   using C = CG<L1, L2, L3>;
-  float dwv = 0.f;
+  float dwv = -0.f;
   sfor<2 * L1 + 1>([&](auto i) {
-    float ui = 0.f;
+    float ui = -0.f;
     const float wx = w * x[i];
     sfor<2 * L2 + 1>([&](auto j) {
       if constexpr (cg_pair<C, i, j>()) {
-        float tp = 0.f;
+        float tp = -0.f;
         sfor<C::n>([&](auto q) {
           if constexpr (C::e[q].i == i && C::e[q].j == j) tp += C::e[q].c * gm[C::e[q].k];
         });
