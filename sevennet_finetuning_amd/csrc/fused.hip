@@ -1107,7 +1107,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                   float dwr[4];
                   // padded slots: y = 0, so dE/dx = dE/dw = 0 there
                   tp_bwd_xw4<p.l1, p.l2, p.l3>(x, y + yoff(p.l2), wv, gm, dx, dYa + yoff(p.l2), dwr);
-                  pin<4 * D1>(dx);
+                  if constexpr (!std::is_same<L, LayerFirst>::value) pin<4 * D1>(dx);
                   pin<8>(dYa + 1);
                   if constexpr (ODD) {
                     __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
@@ -1120,8 +1120,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 }
               }
             });
-            // per-edge dE/dx[nbr] (not needed for the first block)
-            stv<4 * D1>(Rd, vd + 4 * g * D1 * 4, (XOFF + 16 * jj * D1) * 4, dx);
+            // per-edge dE/dx[nbr]; the first block's inputs are the species
+            // embedding, whose gradient no output needs: no stores at all (a
+            // store to an empty descriptor still costs its issue and its
+            // trip through the texture unit), and dx itself is dead code there
+            if constexpr (!std::is_same<L, LayerFirst>::value)
+              stv<4 * D1>(Rd, vd + 4 * g * D1 * 4, (XOFF + 16 * jj * D1) * 4, dx);
           });
         }
       }
