@@ -9,24 +9,22 @@
 // blocks) never touch HBM: f32 MFMA produces them directly in the registers the
 // tensor product reads.
 //
-// Mapping: one wave = one centre, its CSR edges in tiles of 16.
+// Mapping: one wave = one centre (forward, first / middle backward) or one
+// neighbour node (last backward), its edges in tiles of 16 edge slots.
 //   * v_mfma_f32_16x16x4_f32: A lane l = A[i=l&15][k=l>>4], B lane l =
 //     B[k=l>>4][j=l&15], D lane l reg r = D[4(l>>4)+r][l&15].  Lane group
 //     g = l>>4, column c = l&15.
 //   * The MLP runs transposed (H^T = W^T emb^T: rows = hidden units, columns =
 //     edge slots), so every product's accumulator is the k-operand of the next
-//     one (k-step s of a 64-deep product covers hidden unit 16(s>>2)+4g+(s&3)
-//     in lane group g; the weight operand uses the same permuted k).
-//   * w = H2 W2[:, 16-column block]: lane (g, c) holds w[edge 4g+r][channel c]
-//     in register r -- 4 consecutive edges x 1 channel per lane.  The tensor
-//     product runs on that layout: the forward sums the centre's message over
-//     registers and the 4 lane groups; the backward produces dE/dw (-> 1 KB LDS
-//     transpose -> dH2^T = W2 dw^T), dE/dx (accumulated over the paths of an
-//     input irrep in registers, stored once per edge) and dE/du (12 registers,
-//     reduced over the 16 channel lanes once per tile).  The MLP chain backward
-//     (dA2, dH1, dA1, demb) stays in accumulators.
-//   * ~120 VGPRs, 4 waves/SIMD; weights via buffer descriptors (scalar k
-//     offsets, one VGPR of lane offset).
+//     one; the 64 -> W layer (90 % of the MLP FLOPs) on bf16x6 MFMA (below).
+//   * Forward: w = H2 W2[:, 16-column block], lane (g, c) holds w[edge 4g+r]
+//     [channel c]; two tiles per pass share every W2 operand block; the
+//     message is summed over registers and the 4 lane groups into the
+//     centre's row in LDS.  Backward (lock-step, 4 centres per workgroup, W2
+//     pieces staged per block pair in LDS): w^T recomputed, lane (g, c) =
+//     edge c x channels 4g..4g+3; dE/dx per edge, dE/dY -> dE/du, dE/dw ->
+//     dH2 (bf16x6 over the pair) -> MLP chain -> dE/demb.
+//   * Weights via buffer descriptors (scalar k offsets, one VGPR of lane offset).
 // Deterministic: no atomics; every sum has a fixed order.
 #include "cg_tables.h"
 #include "common.h"
@@ -35,12 +33,6 @@
 
 #include <type_traits>
 
-// waves per SIMD the register allocation targets (unified VGPR+AGPR file:
-// 4 waves <= 128 registers, 3 <= 168); without the hint the compiler parks
-// MFMA accumulators in AGPRs and lands just above a boundary
-#ifndef E3GNN_FWD_WAVES
-#define E3GNN_FWD_WAVES 3
-#endif
 // the per-neighbour backward of the last block (k_conv_bwd_nbr): 159 VGPRs
 constexpr int BWD_NBR_WAVES = 3;
 
@@ -518,23 +510,29 @@ __device__ __forceinline__ void load_tile_edges(const int* __restrict__ nbr,
 }
 
 // ---------------------------------------------------------------- forward
-// agg[c] = sum_e TP(h[nbr e], Y_e, w_e) / denom; the first tile stores, later ones add.
+// agg[c] = sum_e TP(h[nbr e], Y_e, w_e) / denom.
+// Two 16-edge tiles of the centre per pass: every W2 operand block
+// (6 KB per lane set, from L2) feeds both tiles' w = H2 W2 products, halving
+// the operand stream that dominates the one-tile kernel, and the two tiles'
+// messages are summed in registers before the LDS accumulation.
+// waves per SIMD the register allocation targets (unified VGPR+AGPR file:
+// 3 waves <= 168 registers, 2 <= 256; without the hint the compiler parks
+// MFMA accumulators in AGPRs and lands just above a boundary): the first
+// block (128 input channels) fits three, the others two
 template <class L>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_WAVES, E3GNN_FWD_WAVES))) void k_conv_fwd(const int* __restrict__ row_ptr,
-                                                  const int* __restrict__ nbr,
-                                                  const float* __restrict__ emb,
-                                                  const float* __restrict__ Y,
-                                                  const float* __restrict__ h,
-                                                  float* __restrict__ agg, MlpW W, int c_begin,
-                                                  int c_end, int n_nodes, float denom) {
-  __shared__ float lds[4][160];
-  // the centre's message sum over its tiles stays in LDS (first tile stores,
-  // later tiles add: no global read-back), one coalesced copy out at the end
+struct Fwd2Waves {
+  static constexpr int v = std::is_same<L, LayerFirst>::value ? 3 : 2;
+};
+template <class L>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Fwd2Waves<L>::v, Fwd2Waves<L>::v))) void k_conv_fwd(
+    const int* __restrict__ row_ptr, const int* __restrict__ nbr, const float* __restrict__ emb,
+    const float* __restrict__ Y, const float* __restrict__ h, float* __restrict__ agg, MlpW W, int c_begin,
+    int c_end, int n_nodes, float denom) {
+  __shared__ float lds[4][2][160];
   __shared__ __attribute__((aligned(16))) float aggl[4][L::DM];
   const int wid = threadIdx.x >> 6;
   const int c = __builtin_amdgcn_readfirstlane(c_begin + xcd_block() * 4 + wid);
   if (c >= c_end) return;
-  float* ybuf = lds[wid];
   float* acl = aggl[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
   const int beg = row_ptr[c], end = row_ptr[c + 1];
@@ -542,45 +540,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
   const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rh = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
   const float rden = 1.0f / denom;
-  for (int e0 = beg; e0 < end || e0 == beg; e0 += 16) {
+  for (int e0 = beg; e0 < end || e0 == beg; e0 += 32) {
     const bool first_tile = e0 == beg;
-    int src[4];
+    const bool two = e0 + 16 < end;   // wave-uniform: the second tile has edges
+    int src[2][4];
     Op3 wq;
     load_w2b(wq, R.w2b, lane, L::P[0].woff);
-    load_tile_edges(nbr, Y, e0, end, lane, src, ybuf);
-    // neighbour rows of the next channel group (4 edges x D1), loaded under the
-    // current group's work
+#pragma unroll
+    for (int u = 0; u < 2; ++u) load_tile_edges(nbr, Y, e0 + 16 * u, end, lane, src[u], lds[wid][u]);
+    // tile 0's neighbour rows of the next channel group are prefetched under
+    // the current group; tile 1's are loaded at the group start (consumed
+    // after tile 0's first product: their latency hides there)
     float xpf[20];
-    auto load_group = [&](auto Iq, int jq) {
+    auto load_rows = [&](auto Iq, int jq, int u, float* dst) {
       constexpr int D1q = 2 * Iq + 1;
       constexpr int XOq = iblock_xoff<L, Iq>();
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        ldv<D1q>(Rh, (src[r] * L::DX + col * D1q) * 4, (XOq + 16 * jq * D1q) * 4, xpf + r * D1q);
+        ldv<D1q>(Rh, (src[u][r] * L::DX + col * D1q) * 4, (XOq + 16 * jq * D1q) * 4, dst + r * D1q);
     };
+    auto load_group = [&](auto Iq, int jq) { load_rows(Iq, jq, 0, xpf); };
     load_group(std::integral_constant<int, first_I<L>()>{}, 0);
-    Op3 hq;
-    {
+    Op3 hq[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
       MlpT m;
-      mlp_pre(R, emb, e0, end, lane, m);
+      mlp_pre(R, emb, e0 + 16 * u, end, lane, m);
       f32x4 h2[4];
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) h2[b][r] = act_fwd(m.a2[b][r]);
-      split_h2(h2, hq);
+      split_h2(h2, hq[u]);
     }
     sfor<3>([&](auto I) {
       constexpr int MUL = iblock_mul<L, I>();
       if constexpr (MUL > 0) {
         constexpr int D1 = 2 * I + 1;
         for (int j = 0; j < MUL / 16; ++j) {
-          float x[4][D1];
+          float x[2][4 * D1];
           phase();
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int i = 0; i < D1; ++i) x[r][i] = xpf[r * D1 + i];
+          for (int i = 0; i < 4 * D1; ++i) x[0][i] = xpf[i];
+          load_rows(I, j, 1, x[1]);
           if (j + 1 < MUL / 16) {
             load_group(I, j + 1);
           } else {
@@ -590,9 +593,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
           sfor<L::NP>([&](auto pi) {
             constexpr PathDef p = L::P[pi];
             if constexpr (p.l1 == I) {
-              constexpr int D2 = 2 * p.l2 + 1, D3 = 2 * p.l3 + 1;
+              constexpr int D3 = 2 * p.l3 + 1;
               phase();
-              const f32x4 wv = w2_block<true>(hq, wq);
+              const f32x4 wv0 = w2_block<true>(hq[0], wq);
+              const f32x4 wv1 = two ? w2_block<true>(hq[1], wq) : zero4();
               {  // operands of the next block load under this block's tensor product
                 const int nc = next_block_col<L, I, pi>(j);
                 if (nc >= 0) load_w2b(wq, R.w2b, lane, nc);
@@ -601,8 +605,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_FWD_W
               float acc[D3];
 #pragma unroll
               for (int k = 0; k < D3; ++k) acc[k] = -0.f;
-              // the lane's 4 edges in lock-step (padded edges have Y = 0)
-              tp_acc4<p.l1, p.l2, p.l3>(&x[0][0], ybuf + 4 * g * 9 + yoff(p.l2), 9, wv, acc);
+              // the lane's 4 edges of each tile (padded edges have Y = 0)
+              tp_acc4<p.l1, p.l2, p.l3>(x[0], lds[wid][0] + 4 * g * 9 + yoff(p.l2), 9, wv0, acc);
+              if (two) tp_acc4<p.l1, p.l2, p.l3>(x[1], lds[wid][1] + 4 * g * 9 + yoff(p.l2), 9, wv1, acc);
 #pragma unroll
               for (int k = 0; k < D3; ++k) {
                 float v = acc[k];
