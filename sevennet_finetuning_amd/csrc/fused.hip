@@ -33,8 +33,6 @@
 
 #include <type_traits>
 
-// the per-neighbour backward of the last block (k_conv_bwd_nbr): 159 VGPRs
-constexpr int BWD_NBR_WAVES = 3;
 
 namespace e3gnn {
 namespace {
@@ -755,8 +753,12 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
 // dw^T (f32 MFMA) -> MLP chain -> dE/demb.  Every edge is visited once (by its
 // neighbour's wave): deterministic.  The radial weights w of the NEXT visited
 // block are formed (MFMA) before this block's tensor product (VALU).
+// Two 16-edge tiles of the node per pass (28 incoming edges on average: one
+// pass per node): every W2 operand block (w recompute and dH2) feeds both
+// tiles, and dE/dx[j] of both tiles is summed in registers before the
+// per-block DPP row sum.  The second tile is skipped when it has no edge.
 template <class L>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BWD_NBR_WAVES, BWD_NBR_WAVES))) void k_conv_bwd_nbr(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_bwd_nbr(
     const int* __restrict__ src_ptr, const int* __restrict__ src_perm, const int* __restrict__ center,
     const float* __restrict__ emb, const float* __restrict__ Y, const float* __restrict__ h,
     const float* __restrict__ gagg, MlpW W, float* __restrict__ dh, float* __restrict__ dgu, int n_centers,
@@ -770,26 +772,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BWD_NBR_WAV
   const int qb = src_ptr[jn], qe = src_ptr[jn + 1];
   const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
-  // the edges' centres' dE/dagg rows through a descriptor over the whole array
-  // (32-bit lane offsets; the host checks n_centers * DM * 4 < 2^31); padded
-  // slots read past its end: 0
   const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
   for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
 
-  for (int q0 = qb; q0 < qe; q0 += 16) {
+  for (int q0 = qb; q0 < qe; q0 += 32) {
+    const bool two = q0 + 16 < qe;   // wave-uniform
     phase();
     Op3 wq;
     load_w2b(wq, R.w2b, lane, L::P[0].woff);
-    const int er = (q0 + col < qe) ? src_perm[q0 + col] : -1;   // edge of slot c
-    const int vg = (er >= 0 ? center[er] * L::DM : n_centers * L::DM) * 4;
-    float y[9];
+    int er[2], vg[2];
+    float y[2][9];
+    Op3 hq[2];
 #pragma unroll
-    for (int q = 0; q < 9; ++q) y[q] = er >= 0 ? Y[(int64_t)er * 9 + q] : 0.f;
-    Op3 hq;
-    {
+    for (int u = 0; u < 2; ++u) {
+      const int q = q0 + 16 * u + col;
+      er[u] = q < qe ? src_perm[q] : -1;   // edge of slot c
+      vg[u] = (er[u] >= 0 ? center[er[u]] * L::DM : n_centers * L::DM) * 4;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) y[u][k] = er[u] >= 0 ? Y[(int64_t)er[u] * 9 + k] : 0.f;
+      if (u == 1 && !two) continue;
       float b[2];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) b[s] = er >= 0 ? emb[(int64_t)er * 8 + 4 * s + g] : 0.f;
+      for (int k = 0; k < 2; ++k) b[k] = er[u] >= 0 ? emb[(int64_t)er[u] * 8 + 4 * k + g] : 0.f;
       MlpT m;
       mlp_chain(R, b, lane, m);
       f32x4 h2[4];
@@ -797,21 +801,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BWD_NBR_WAV
       for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) h2[bb][r] = act_fwd(m.a2[bb][r]);
-      split_h2(h2, hq);
+      split_h2(h2, hq[u]);
     }
-    // dH2^T of the tile's edges (D[hidden 16 bh + 4g + r][edge c]), accumulated
-    // over the visited blocks
-    f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
-    int nb = 0;     // visited blocks of the tile
-    // w of the current block (formed during the previous one) and of the
-    // next; wq then holds the operand of the block after the next (w2v: the
-    // bf16 pieces in visiting order, block nb at column 16 nb)
-    constexpr int NBLK = L::W / 16;
-    f32x4 wcur = w2_block<false>(hq, wq), wnxt = zero4();
-    if (NBLK > 1) load_w2b(wq, R.w2v, lane, 16);
-    float dYa[9];  // dE/dY of edge c over this lane's channels (index 0 unused)
+    f32x4 dh2[2][4];
 #pragma unroll
-    for (int q = 0; q < 9; ++q) dYa[q] = 0.f;
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) dh2[u][bb] = zero4();
+    int nb = 0;
+    constexpr int NBLK = L::W / 16;
+    f32x4 wcur[2], wnxt[2] = {zero4(), zero4()};
+    wcur[0] = w2_block<false>(hq[0], wq);
+    wcur[1] = two ? w2_block<false>(hq[1], wq) : zero4();
+    if (NBLK > 1) load_w2b(wq, R.w2v, lane, 16);
+    float dYa[2][9];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) dYa[u][k] = 0.f;
 
     sfor<3>([&](auto I) {
       constexpr int MUL = iblock_mul<L, I>();
@@ -823,51 +830,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BWD_NBR_WAV
           phase();
           ldv<4 * D1>(Rx, 4 * g * D1 * 4, (XOFF + 16 * jj * D1) * 4, x);
 #pragma unroll
-          for (int i = 0; i < 4 * D1; ++i) dx[i] = 0.f;
+          for (int i = 0; i < 4 * D1; ++i) dx[i] = -0.f;
           sfor<L::NP>([&](auto pi) {
             constexpr PathDef p = L::P[pi];
             if constexpr (p.l1 == I) {
               constexpr int D3 = 2 * p.l3 + 1;
               phase();
-              float gm[4 * D3];
-              load_gm<L, pi>(gm, Rg, vg, g, jj);
-              // W2 operands of this block's dH2 product, issued now and consumed
-              // after the tensor product
+              float gm[2][4 * D3];
+              load_gm<L, pi>(gm[0], Rg, vg[0], g, jj);
+              load_gm<L, pi>(gm[1], Rg, vg[1], g, jj);
               f32x4 bq[4];
               load_w2q(bq, R.w2r, lane, p.woff + 16 * jj);
-              float dwr[4];
-              const f32x4 wv = wcur;
-              if (nb + 1 < NBLK) wnxt = w2_block<false>(hq, wq);
+              f32x4 wv[2] = {wcur[0], wcur[1]};
+              if (nb + 1 < NBLK) {
+                wnxt[0] = w2_block<false>(hq[0], wq);
+                wnxt[1] = two ? w2_block<false>(hq[1], wq) : zero4();
+              }
               if (nb + 2 < NBLK) load_w2b(wq, R.w2v, lane, 16 * (nb + 2));
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                phase();
-                float dy[2 * p.l2 + 1];
+              for (int u = 0; u < 2; ++u) {
+                if (u == 1 && !two) break;
+                float dwr[4];
 #pragma unroll
-                for (int q = 0; q < 2 * p.l2 + 1; ++q) dy[q] = 0.f;
-                // padded slots: w = 0, g = 0 and y = 0 (so dE/dw = 0)
-                dwr[r] = tp_bwd_xw<p.l1, p.l2, p.l3>(x + r * D1, y + yoff(p.l2), wv[r], gm + r * D3,
-                                                     dx + r * D1, dy);
-                if constexpr (p.l2 > 0) {
+                for (int r = 0; r < 4; ++r) {
+                  phase();
+                  float dy[2 * p.l2 + 1];
 #pragma unroll
-                  for (int q = 0; q < 2 * p.l2 + 1; ++q) dYa[yoff(p.l2) + q] += dy[q];
+                  for (int q = 0; q < 2 * p.l2 + 1; ++q) dy[q] = 0.f;
+                  // padded slots: w = 0, g = 0 and y = 0 (so dE/dw = 0)
+                  dwr[r] = tp_bwd_xw<p.l1, p.l2, p.l3>(x + r * D1, y[u] + yoff(p.l2), wv[u][r], gm[u] + r * D3,
+                                                       dx + r * D1, dy);
+                  if constexpr (p.l2 > 0) {
+#pragma unroll
+                    for (int q = 0; q < 2 * p.l2 + 1; ++q) dYa[u][yoff(p.l2) + q] += dy[q];
+                  }
+                  pin<D1>(dx + r * D1);
+                  pin<8>(dYa[u] + 1);
                 }
-                pin<D1>(dx + r * D1);
-                pin<8>(dYa + 1);
+                // dH2^T += W2[:, block] dw^T: k = lane group g, channel 4g + r
+#pragma unroll
+                for (int bh = 0; bh < 4; ++bh)
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) dh2[u][bh] = mfma(bq[bh][r], dwr[r], dh2[u][bh]);
               }
               pin<4 * D1>(dx);
-              pin<8>(dYa + 1);
-              // dH2^T += W2[:, block] dw^T: k = lane group g, channel 4g + r
-#pragma unroll
-              for (int bh = 0; bh < 4; ++bh)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) dh2[bh] = mfma(bq[bh][r], dwr[r], dh2[bh]);
-              wcur = wnxt;
+              wcur[0] = wnxt[0];
+              wcur[1] = wnxt[1];
               ++nb;
             }
           });
           phase();
-          // sum over the tile's 16 edges (row lanes), lane c == 0 accumulates
+          // both tiles' edges summed per lane already: one row sum over the 16
+          // edge lanes, lane c == 0 accumulates the node's row
 #pragma unroll
           for (int i = 0; i < 4 * D1; ++i) {
             const float v = row_sum16(dx[i]);
@@ -877,26 +891,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BWD_NBR_WAV
       }
     });
 
-    phase();
-    // dE/dY of edge c: sum over the 4 lane groups, then dE/du through the SH
-    // polynomials (serial_code.py:50-70)
 #pragma unroll
-    for (int q = 1; q < 9; ++q) dYa[q] = sum_rows4(dYa[q]);
-    if (g == 0 && er >= 0) {
-      const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f, c15 = s3 * s5;
-      const float is3 = 0.57735026918962576f;  // 1 / sqrt(3)
-      const float ux = y[1] * is3, uy = y[2] * is3, uz = y[3] * is3;
-      const float* d = dYa + 1;  // d[0..2] = dE/dY_1, d[3..7] = dE/dY_2
-      const float gx = s3 * d[0] + c15 * (uz * d[3] + uy * d[4]) - s5 * ux * d[5] - c15 * ux * d[7];
-      const float gy = s3 * d[1] + c15 * (ux * d[4] + uz * d[6]) + 2.f * s5 * uy * d[5];
-      const float gz = s3 * d[2] + c15 * (ux * d[3] + uy * d[6]) - s5 * uz * d[5] + c15 * uz * d[7];
-      float* o = dgu + (int64_t)er * 3;
-      o[0] += gx;
-      o[1] += gy;
-      o[2] += gz;
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      phase();
+      // dE/dY of edge c: sum over the 4 lane groups, then dE/du through the SH
+      // polynomials (serial_code.py:50-70)
+      float d[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) d[q] = sum_rows4(dYa[u][q + 1]);
+      if (g == 0 && er[u] >= 0) {
+        const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f, c15 = s3 * s5;
+        const float is3 = 0.57735026918962576f;  // 1 / sqrt(3)
+        const float ux = y[u][1] * is3, uy = y[u][2] * is3, uz = y[u][3] * is3;
+        const float gx = s3 * d[0] + c15 * (uz * d[3] + uy * d[4]) - s5 * ux * d[5] - c15 * ux * d[7];
+        const float gy = s3 * d[1] + c15 * (ux * d[4] + uz * d[6]) + 2.f * s5 * uy * d[5];
+        const float gz = s3 * d[2] + c15 * (ux * d[3] + uy * d[6]) - s5 * uz * d[5] + c15 * uz * d[7];
+        float* o = dgu + (int64_t)er[u] * 3;
+        o[0] += gx;
+        o[1] += gy;
+        o[2] += gz;
+      }
+      phase();
+      mlp_bwd_chain_ids(R, emb, er[u], lane, dh2[u], demb);
     }
-    phase();
-    mlp_bwd_chain_ids(R, emb, er, lane, dh2, demb);
   }
   phase();
   __builtin_amdgcn_s_waitcnt(0);
