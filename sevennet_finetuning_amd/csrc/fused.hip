@@ -931,7 +931,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // operand crosses the L2 -> CU path once per 4 tiles instead of once per tile
 // and needs no per-wave prefetch registers.  The backward's dH2 = dw W2^T runs
 // on bf16x6 MFMA over the pair (K = 32 channels): 24 x 16 MFMA cycles instead of
-// 2 x 16 x 32 on f32 MFMA.  Two workgroups per CU (LDS), 2 waves per SIMD.
+// 2 x 16 x 32 on f32 MFMA.  Middle blocks: two workgroups per CU (LDS), 2 waves
+// per SIMD; the first block: 3 waves per SIMD.
 constexpr int LS_BLK = 6144;            // bytes of one w2v column block (3 pieces x 2 halves x 1 KB)
 constexpr int LS_PAIR_W = 2 * LS_BLK;   // the pair's two w-recompute operand blocks
 constexpr int LS_PAIR_D = 12288;        // the pair's dH2 operand (w2d: 3 pieces x 4 bh x 1 KB)
@@ -993,8 +994,16 @@ __device__ __forceinline__ int ls_tiles(const int* __restrict__ row_ptr, int cb,
 // chain -> dE/demb), the centre's dE/dagg row staged in LDS once.  Same pair
 // structure as the forward (both blocks' w formed at the pair start, next
 // group's neighbour rows prefetched); dH2 of the pair on bf16x6 at its end.
+// waves per SIMD: the first block (128 input channels, 1,152 message channels:
+// 42 KB of LDS per workgroup) runs three (168 VGPRs with a few spills
+// measured 2.57 -> 2.27 ms against two), the middle blocks two (244 VGPRs;
+// their 75 KB of LDS allows no more)
 template <class L>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_bwd_ls(
+struct BwdLsWaves {
+  static constexpr int v = std::is_same<L, LayerFirst>::value ? 3 : 2;
+};
+template <class L>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdLsWaves<L>::v, BwdLsWaves<L>::v))) void k_conv_bwd_ls(
     const int* __restrict__ row_ptr, const int* __restrict__ nbr, const float* __restrict__ emb,
     const float* __restrict__ Y, const float* __restrict__ h, const float* __restrict__ gagg, MlpW W,
     float* __restrict__ dxc, float* __restrict__ dgu, float* __restrict__ demb, int c_begin,
