@@ -309,6 +309,39 @@ def check_world(args, world):
                            f'--nproc-per-node {args.gpus}')
 
 
+def box_plan(args, world):
+    """(cells, brick grid, total cells per axis) of the evaluated box: one
+    cells^3 box at N = 1 and with --strong, N bricks of cells^3 (weak scaling)
+    otherwise.  8 atoms per conventional Si cell."""
+    from sevennet_finetuning_amd.parallel import brick_grid
+    cells = args.cells or (46 if args.strong else 23)
+    grid = tuple(brick_grid(world)) if world > 1 else (1, 1, 1)
+    total = (cells,) * 3 if (args.strong or world == 1) else tuple(cells * g for g in grid)
+    return cells, grid, total
+
+
+def describe(n_total, world, cells, strong, grid=(1, 1, 1)):
+    """(metric, workload) of a bench line, naming the box actually evaluated:
+    BASELINE.json's metric is quoted on the 100k-atom box per GPU; a weak
+    multi-rank run evaluates world x that box, a strong run one box split over
+    the ranks (46^3 cells = 778,688 atoms: config 4, the 800k box)."""
+    base = 'atoms/sec energy+force, SevenNet-0 lmax=2'
+    g = 'x'.join(str(v) for v in grid)
+    if world == 1:
+        metric = f'{base}, {n_total:,}-atom box @1 GPU'
+        work = f'SevenNet-0 energy+force+virial, {n_total:,}-atom periodic Si box ({cells}^3 cells), 1 GPU'
+    elif strong:
+        metric = f'{base}, {n_total:,}-atom box split over {world} GPUs (strong scaling)'
+        work = (f'SevenNet-0 energy+force+virial, one {n_total:,}-atom periodic Si box ({cells}^3 cells) '
+                f'domain-decomposed {g} over {world} GPUs, halo exchange per layer')
+    else:
+        per = n_total // world
+        metric = f'{base}, {per:,}-atom box per GPU = {n_total:,}-atom box @{world} GPUs (weak scaling)'
+        work = (f'SevenNet-0 energy+force+virial, {n_total:,}-atom periodic Si box ({world} bricks of '
+                f'{cells}^3 cells, {g}) over {world} GPUs, halo exchange per layer')
+    return metric, work
+
+
 def main():
     args = parse()
     rc = maybe_launch(args, sys.argv[1:])
@@ -332,7 +365,7 @@ def main():
 
     from sevennet_finetuning_amd.model import E3GNNModel
     model = E3GNNModel(device=device)
-    cells = args.cells or (46 if args.strong else 23)
+    cells, grid, total = box_plan(args, world)
     scaling = 'strong' if args.strong else 'weak'
     parity = None
     if world == 1:
@@ -351,10 +384,8 @@ def main():
         # brick of cells^3 per rank; strong -- one cells^3 box split over the
         # ranks; halo exchange per layer over RCCL
         from sevennet_finetuning_amd.parallel import (HipSegmentEngine, ParallelE3GNN,
-                                                      brick_grid, build_rank_graph)
+                                                      build_rank_graph)
         from sevennet_finetuning_amd.structures import si_diamond
-        grid = brick_grid(world)
-        total = (cells,) * 3 if args.strong else tuple(cells * g for g in grid)
         pos, cell = si_diamond(total, sigma=0.05)
         n = len(pos)
         rg = build_rank_graph(pos, cell, np.full(n, 69), 5.0, grid, rank)
@@ -446,16 +477,15 @@ def main():
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_cells)
 
     if rank == 0:
+        metric, workload = describe(n, world, cells, args.strong, grid)
         line = {
-            'metric': 'atoms/sec energy+force, SevenNet-0 lmax=2, 100k-atom box',
+            'metric': metric,
             'value': round(value, 2), 'unit': 'atoms/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
             'higher_is_better': True, 'scaling': scaling, 'vs_baseline': None, 'dtype': 'f32',
             'data': 'synthetic Si diamond box, default_rng(0) 0.05 A displacements; '
                     'SevenNet-0 weights (reference opt_params_sevenn.pt)',
-            'config': {'workload': f'SevenNet-0 energy+force+virial, {n}-atom periodic Si box '
-                                   f'({cells}^3 cells{"" if args.strong else " per rank"}), '
-                                   f'{E} edges on rank 0',
+            'config': {'workload': workload, 'total_atoms': n, 'scaling': scaling,
                        'atoms_per_rank': n_rank, 'edges_per_rank': E,
                        'parallelism': parallelism},
             'energy': energy,

@@ -6,10 +6,11 @@
    pack_/unpack_forward_init (:750-801), pack_/unpack_{forward,reverse}_comm_gnn
    (:803-933).  The graph build, the per-layer segment calls and the force /
    virial / eatom scatter are e3gnn_pair::ParallelStep (native/pair_e3gnn_core.cpp);
-   this file keeps the CommBrick side: the per-swap row index maps the
-   reference builds in its "false" preprocessing forward_comm, and the packing
-   of the rows into / out of the MPI buffers with the library's halo kernels
-   (device buffers with GPU-aware MPI, host-staged otherwise).
+   the per-swap row maps of the "false" preprocessing forward_comm and their
+   reverse dedup are e3gnn_pair::CommMaps (tested under an in-process CommBrick
+   emulation, native/e3gnn_pair_check.cpp); this file only maps the CommBrick
+   hooks onto them and moves the rows into / out of the MPI buffers (device
+   buffers with GPU-aware MPI, host-staged otherwise).
 ------------------------------------------------------------------------- */
 
 #include "pair_e3gnn_parallel.h"
@@ -31,7 +32,6 @@
 
 #include <cstdlib>
 #include <cstring>
-#include <set>
 #include <stdexcept>
 
 using namespace LAMMPS_NS;
@@ -69,9 +69,7 @@ PairE3GNNParallel::PairE3GNNParallel(LAMMPS *lmp) : Pair(lmp)
 
 PairE3GNNParallel::~PairE3GNNParallel()
 {
-  for (int p = 0; p < 6; p++)
-    for (int32_t *q : {d_pack_fwd[p], d_unpack_fwd[p], d_unpack_rev[p]})
-      if (q) (void) hipFree(q);
+  maps.reset();
   if (d_stage) (void) hipFree(d_stage);
   if (allocated) {
     memory->destroy(setflag);
@@ -123,73 +121,25 @@ void PairE3GNNParallel::compute(int eflag, int vflag)
 }
 
 // ---------------------------------------------------------------- comm maps
+// the "false" forward communication: CommBrick calls the *_init hooks per
+// swap, e3gnn_pair::CommMaps keeps the row maps and their dedup (:703-748)
 void PairE3GNNParallel::comm_preprocess()
 {
-  for (int p = 0; p < 6; p++) {
-    idx_pack_fwd[p].clear();
-    idx_unpack_fwd[p].clear();
-    idx_unpack_rev[p].clear();
-  }
+  maps->begin();
   comm_preprocess_done = false;
-  // the "false" forward communication: CommBrick calls the *_init hooks per swap
   dynamic_cast<CommBrick *>(comm)->forward_comm(this);
-  // reverse accumulation rows: a graph row sent more than once (to several
-  // swaps) is accumulated once, the other copies go to the trash row (:712-733)
-  std::set<int> already_met;
-  const int G = step->graph_size(), trash = step->trash_row();
-  for (int p = 0; p < 6; p++) {
-    for (int32_t r : idx_pack_fwd[p]) {
-      if (r < G) {
-        if (already_met.count(r)) idx_unpack_rev[p].push_back(trash);
-        else {
-          idx_unpack_rev[p].push_back(r);
-          already_met.insert(r);
-        }
-      } else {
-        idx_unpack_rev[p].push_back(r);
-      }
-    }
-    std::vector<int32_t> *h[3] = {&idx_pack_fwd[p], &idx_unpack_fwd[p], &idx_unpack_rev[p]};
-    int32_t **d[3] = {&d_pack_fwd[p], &d_unpack_fwd[p], &d_unpack_rev[p]};
-    for (int k = 0; k < 3; k++) {
-      const int64_t n = (int64_t) h[k]->size();
-      if (n > cap_idx[p][k]) {
-        if (*d[k]) (void) hipFree(*d[k]);
-        cap_idx[p][k] = n + n / 4 + 64;
-        if (hipMalloc(d[k], cap_idx[p][k] * 4) != hipSuccess) error->one(FLERR, "e3gnn/parallel: hipMalloc");
-      }
-      if (n && hipMemcpy(*d[k], h[k]->data(), n * 4, hipMemcpyHostToDevice) != hipSuccess)
-        error->one(FLERR, "e3gnn/parallel: hipMemcpy");
-    }
-  }
+  if (maps->finish()) error->one(FLERR, "e3gnn/parallel: " + maps->error());
   comm_preprocess_done = true;
 }
 
-// rows of the atoms CommBrick sends in swap `comm_phase`: their graph rows, or
-// an extra row for an atom this rank only relays (:750-779; the reference keys
-// a new extra row by the loop counter, here by the atom index it stands for)
 void PairE3GNNParallel::pack_forward_init(int n, int *list_send, int comm_phase)
 {
-  auto &idx = idx_pack_fwd[comm_phase];
-  idx.reserve(n);
-  for (int i = 0; i < n; i++) {
-    const int a = list_send[i];
-    int r = step->graph_row(a);
-    if (r < 0) r = step->extra_row(a);
-    idx.push_back(r);
-  }
+  if (maps->pack_forward_init(n, list_send, comm_phase)) error->one(FLERR, maps->error());
 }
 
-// rows of the ghost atoms [first, first + n) received in swap `comm_phase` (:781-801)
 void PairE3GNNParallel::unpack_forward_init(int n, int first, int comm_phase)
 {
-  auto &idx = idx_unpack_fwd[comm_phase];
-  idx.reserve(n);
-  for (int i = first; i < first + n; i++) {
-    int r = step->graph_row(i);
-    if (r < 0) r = step->extra_row(i);
-    idx.push_back(r);
-  }
+  if (maps->unpack_forward_init(n, first, comm_phase)) error->one(FLERR, maps->error());
 }
 
 int PairE3GNNParallel::host_stage(int64_t floats)
@@ -202,68 +152,54 @@ int PairE3GNNParallel::host_stage(int64_t floats)
   return 0;
 }
 
-// pack rows `idx` of the comm rows into buf (device buffer with GPU-aware MPI,
-// else through the device staging buffer to the host buffer)
-static int pack_rows(e3gnn_pair::ParallelStep &s, const int32_t *d_idx, int64_t n, float *buf,
-                     bool device_buf, float *stage)
+// the row copies run on device buffers: the MPI buffer itself with GPU-aware
+// MPI, else the device staging buffer copied to / from the host buffer
+int PairE3GNNParallel::gnn_copy(int which, float *buf, int comm_phase)
 {
-  float *dst = device_buf ? buf : stage;
-  if (s.pack(d_idx, n, dst)) return 1;
-  if (!device_buf)
-    return hipMemcpyAsync(buf, stage, n * s.comm_dim() * 4, hipMemcpyDeviceToHost,
-                          (hipStream_t) s.stream()) != hipSuccess ||
-        hipStreamSynchronize((hipStream_t) s.stream()) != hipSuccess;
-  return hipStreamSynchronize((hipStream_t) s.stream()) != hipSuccess;
-}
-
-static int unpack_rows(e3gnn_pair::ParallelStep &s, const int32_t *d_idx, int64_t n, float *buf,
-                       bool device_buf, float *stage, bool accumulate)
-{
-  const float *src = buf;
-  if (!device_buf) {
-    if (hipMemcpyAsync(stage, buf, n * s.comm_dim() * 4, hipMemcpyHostToDevice,
-                       (hipStream_t) s.stream()) != hipSuccess)
-      return 1;
-    src = stage;
+  const bool to_buf = which == 0 || which == 2;
+  const int64_t n = (which == 0 || which == 3) ? maps->nsend(comm_phase) : maps->nrecv(comm_phase);
+  const int64_t floats = n * step->comm_dim();
+  if (!n) return 0;
+  hipStream_t s = (hipStream_t) step->stream();
+  float *dev = buf;
+  if (!use_cuda_mpi) {
+    if (host_stage(floats)) error->one(FLERR, "e3gnn/parallel: staging");
+    dev = d_stage;
+    if (!to_buf && hipMemcpyAsync(dev, buf, floats * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+      error->one(FLERR, "e3gnn/parallel: hipMemcpy");
   }
-  if (s.unpack(d_idx, n, src, accumulate)) return 1;
-  return hipStreamSynchronize((hipStream_t) s.stream()) != hipSuccess;
+  int64_t rc = 0;
+  switch (which) {
+    case 0: rc = maps->pack_forward(comm_phase, dev); break;
+    case 1: rc = maps->unpack_forward(comm_phase, dev); break;
+    case 2: rc = maps->pack_reverse(comm_phase, dev); break;
+    default: rc = maps->unpack_reverse(comm_phase, dev); break;
+  }
+  if (rc < 0) error->one(FLERR, "e3gnn/parallel: " + step->error());
+  if (!use_cuda_mpi && to_buf && hipMemcpyAsync(buf, dev, floats * 4, hipMemcpyDeviceToHost, s) != hipSuccess)
+    error->one(FLERR, "e3gnn/parallel: hipMemcpy");
+  if (hipStreamSynchronize(s) != hipSuccess) error->one(FLERR, "e3gnn/parallel: hipStreamSynchronize");
+  return (int) floats;
 }
 
 int PairE3GNNParallel::pack_forward_comm_gnn(float *buf, int comm_phase)
 {
-  const int64_t n = (int64_t) idx_pack_fwd[comm_phase].size();
-  if (!use_cuda_mpi && host_stage(n * step->comm_dim())) error->one(FLERR, "e3gnn/parallel: staging");
-  if (n && pack_rows(*step, d_pack_fwd[comm_phase], n, buf, use_cuda_mpi, d_stage))
-    error->one(FLERR, "e3gnn/parallel: pack_forward_comm_gnn: " + step->error());
-  return (int) (n * step->comm_dim());
+  return gnn_copy(0, buf, comm_phase);
 }
 
 void PairE3GNNParallel::unpack_forward_comm_gnn(float *buf, int comm_phase)
 {
-  const int64_t n = (int64_t) idx_unpack_fwd[comm_phase].size();
-  if (!use_cuda_mpi && host_stage(n * step->comm_dim())) error->one(FLERR, "e3gnn/parallel: staging");
-  if (n && unpack_rows(*step, d_unpack_fwd[comm_phase], n, buf, use_cuda_mpi, d_stage, false))
-    error->one(FLERR, "e3gnn/parallel: unpack_forward_comm_gnn: " + step->error());
+  gnn_copy(1, buf, comm_phase);
 }
 
 int PairE3GNNParallel::pack_reverse_comm_gnn(float *buf, int comm_phase)
 {
-  // the rows received in the forward go back to the swap's sender (:873-900)
-  const int64_t n = (int64_t) idx_unpack_fwd[comm_phase].size();
-  if (!use_cuda_mpi && host_stage(n * step->comm_dim())) error->one(FLERR, "e3gnn/parallel: staging");
-  if (n && pack_rows(*step, d_unpack_fwd[comm_phase], n, buf, use_cuda_mpi, d_stage))
-    error->one(FLERR, "e3gnn/parallel: pack_reverse_comm_gnn: " + step->error());
-  return (int) (n * step->comm_dim());
+  return gnn_copy(2, buf, comm_phase);
 }
 
 void PairE3GNNParallel::unpack_reverse_comm_gnn(float *buf, int comm_phase)
 {
-  // accumulated into the rows packed in the forward (duplicates: trash row), :902-933
-  const int64_t n = (int64_t) idx_unpack_rev[comm_phase].size();
-  if (!use_cuda_mpi && host_stage(n * step->comm_dim())) error->one(FLERR, "e3gnn/parallel: staging");
-  if (n && unpack_rows(*step, d_unpack_rev[comm_phase], n, buf, use_cuda_mpi, d_stage, true))
-    error->one(FLERR, "e3gnn/parallel: unpack_reverse_comm_gnn: " + step->error());
+  gnn_copy(3, buf, comm_phase);
 }
 
 // ---------------------------------------------------------------- setup
@@ -299,6 +235,7 @@ void PairE3GNNParallel::coeff(int narg, char **arg)
     model.reset(new e3gnn_pair::Model(arg[3], device));
     species = model->type_map(elements);
     step.reset(new e3gnn_pair::ParallelStep(*model));
+    maps.reset(new e3gnn_pair::CommMaps(*step));
   } catch (const std::exception &e) {
     error->all(FLERR, std::string("e3gnn/parallel: ") + e.what());
   }
@@ -325,7 +262,9 @@ double PairE3GNNParallel::init_one(int, int) { return cutoff; }
 // ---------------------------------------------------------------- device buffers
 DeviceBuffManager &DeviceBuffManager::getInstance()
 {
-  static DeviceBuffManager instance;
+  // one per thread: one rank per process in LAMMPS, one per thread in the
+  // in-process CommBrick emulation of native/e3gnn_pair_check
+  static thread_local DeviceBuffManager instance;
   return instance;
 }
 

@@ -34,6 +34,7 @@ PairStyle(e3gnn/parallel, PairE3GNNParallel)
 namespace e3gnn_pair {
 class Model;
 class ParallelStep;
+class CommMaps;
 }  // namespace e3gnn_pair
 
 namespace LAMMPS_NS {
@@ -60,6 +61,8 @@ class PairE3GNNParallel : public Pair {
   bool use_cuda_mpi_();
   bool is_comm_preprocess_done();
 
+  // the per-swap row maps of the last compute (counters for tests and logs)
+  const e3gnn_pair::CommMaps *comm_maps() const { return maps.get(); }
   bool print_info = false;
   int world_rank = 0;
 
@@ -75,11 +78,8 @@ class PairE3GNNParallel : public Pair {
   std::unique_ptr<e3gnn_pair::ParallelStep> step;
   std::vector<int> species;
   std::vector<int64_t> tag64;
-  // per swap (<= 6): rows packed in the forward, rows written by it, rows the
-  // reverse accumulates into (first occurrence of a row, the rest to the trash row)
-  std::vector<int32_t> idx_pack_fwd[6], idx_unpack_fwd[6], idx_unpack_rev[6];
-  int32_t *d_pack_fwd[6] = {}, *d_unpack_fwd[6] = {}, *d_unpack_rev[6] = {};
-  int64_t cap_idx[6][3] = {};
+  std::unique_ptr<e3gnn_pair::CommMaps> maps;   // per-swap row maps (comm_preprocess)
+  int gnn_copy(int which, float *buf, int comm_phase);
   float *d_stage = nullptr;    // device staging when MPI takes host buffers
   int64_t stage_cap = 0;
 };

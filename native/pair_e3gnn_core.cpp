@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <fstream>
 #include <sstream>
@@ -250,11 +251,14 @@ int ParallelStep::build(const NeighborView& nv, const std::vector<int>& map, int
   const double rc2 = model_.cutoff() * model_.cutoff();
   nlocal_ = nl;
   tag_ = nv.tag;
+  ntotal_ = (int64_t)nv.nlocal + nv.nghost;
   tag_to_row_.assign(natoms + 1, -1);
-  i_to_row_.assign(nv.nlocal + nv.nghost, -1);
+  tag_to_extra_.assign(natoms + 1, -1);
+  i_to_row_.assign(ntotal_, -1);
   row_to_i_.clear();
   type_.clear();
-  extra_.clear();
+  nextra_ = 0;
+  ntrash_ = 0;
   auto type_of = [&](int i, int32_t& out) {
     const int ty = nv.type[i];
     if (ty < 1 || ty >= (int)map.size() || map[ty] < 0) return false;
@@ -321,21 +325,21 @@ int ParallelStep::build(const NeighborView& nv, const std::vector<int>& map, int
 }
 
 int ParallelStep::graph_row(int idx) const {
-  if (idx < 0 || idx >= (int)i_to_row_.size()) return -1;
+  if (idx < 0 || idx >= ntotal_) return -1;
   const int64_t tg = tag_[idx];
   return (tg >= 1 && tg < (int64_t)tag_to_row_.size()) ? tag_to_row_[tg] : -1;
 }
 
 int ParallelStep::extra_row(int idx) {
-  for (auto& e : extra_)
-    if (e.first == idx) return e.second;
-  const int r = graph_size() + (int)extra_.size();
-  extra_.push_back({idx, r});
-  return r;
+  if (idx < 0 || idx >= ntotal_) return -1;
+  const int64_t tg = tag_[idx];
+  if (tg < 1 || tg >= (int64_t)tag_to_extra_.size()) return -1;
+  if (tag_to_extra_[tg] < 0) tag_to_extra_[tg] = graph_size() + nextra_++;
+  return tag_to_extra_[tg];
 }
 
 int ParallelStep::grow_comm(int rows, int dim) {
-  const int need = rows * dim;
+  const int64_t need = (int64_t)rows * dim;
   if (need > comm_cap_) {
     if (comm_) CORE_HIP(hipFree(comm_));
     comm_cap_ = need + need / 4 + 1024;
@@ -347,8 +351,8 @@ int ParallelStep::grow_comm(int rows, int dim) {
 }
 
 int ParallelStep::load_rows(float* src, int dim, int rows) {
-  // x_comm = cat(graph rows, zeros for the extra rows and the trash row)
-  const int total = graph_size() + (int)extra_.size() + 1;
+  // x_comm = cat(graph rows, zeros for the extra, zero and trash rows)
+  const int total = comm_row_count();
   if (int rc = grow_comm(total, dim)) return rc;
   hipStream_t s = (hipStream_t)stream_;
   CORE_HIP(hipMemcpyAsync(comm_, src, (size_t)rows * dim * 4, hipMemcpyDeviceToDevice, s));
@@ -438,6 +442,177 @@ int ParallelStep::compute(Exchange& ex, double** f, double* eatom, PairOut& out)
   out.energy += sc[0];
   add_virial(out.virial, sc + 1);
   return E3GNN_OK;
+}
+
+// ------------------------------------------------------------------ CommMaps
+CommMaps::~CommMaps() {
+  for (auto& ph : d_)
+    for (int32_t* q : ph)
+      if (q) (void)hipFree(q);
+}
+
+void CommMaps::begin() {
+  for (int p = 0; p < kPhases; ++p) {
+    send_[p].clear();
+    recv_[p].clear();
+    fwd_dst_[p].clear();
+    rev_src_[p].clear();
+    rev_dst_[p].clear();
+    send_is_ghost_[p].clear();
+  }
+  st_ = Stats();
+  ready_ = false;
+}
+
+// rows of the atoms CommBrick sends in swap `phase`: local atoms and ghosts
+// received in earlier swaps (pair_e3gnn_parallel.cpp:750-779)
+int CommMaps::pack_forward_init(int n, const int* list_send, int phase) {
+  if (phase < 0 || phase >= kPhases) {
+    err_ = "PairE3GNNParallel: Cell size is too small. Please use a single GPU or replicate the cell.";
+    return E3GNN_ERR_ARG;
+  }
+  auto& idx = send_[phase];
+  idx.reserve(idx.size() + n);
+  for (int k = 0; k < n; ++k) {
+    const int a = list_send[k];
+    const int r = s_.row_of(a);
+    if (r < 0) {
+      err_ = "pack_forward_init: atom without a tag";
+      return E3GNN_ERR_ARG;
+    }
+    idx.push_back(r);
+    send_is_ghost_[phase].push_back(a >= s_.nlocal() ? 1 : 0);
+  }
+  return E3GNN_OK;
+}
+
+// rows of the ghosts [first, first + n) received in swap `phase` (:781-801)
+int CommMaps::unpack_forward_init(int n, int first, int phase) {
+  if (phase < 0 || phase >= kPhases) {
+    err_ = "PairE3GNNParallel: Cell size is too small. Please use a single GPU or replicate the cell.";
+    return E3GNN_ERR_ARG;
+  }
+  auto& idx = recv_[phase];
+  idx.reserve(idx.size() + n);
+  for (int a = first; a < first + n; ++a) {
+    const int r = s_.row_of(a);
+    if (r < 0) {
+      err_ = "unpack_forward_init: atom without a tag";
+      return E3GNN_ERR_ARG;
+    }
+    idx.push_back(r);
+  }
+  return E3GNN_OK;
+}
+
+int CommMaps::finish() {
+  const int zero = s_.zero_row();
+  const int nlocal = (int)s_.nlocal();
+  // rows already returned by an earlier reception (receiver side) and rows
+  // already accumulated in this swap (sender side); sized after every extra
+  // row is known (finish runs after the last *_init hook)
+  std::vector<char> returned(zero, 0);
+  std::vector<int> seen_in_phase(zero, -1);
+  int ntrash = 0;
+  for (int p = 0; p < kPhases; ++p) {
+    const auto& rv = recv_[p];
+    const auto& sd = send_[p];
+    if (rv.empty() && sd.empty()) continue;
+    ++st_.swaps;
+    // forward unpack: unique destinations; a repeat of a row within the swap,
+    // or a reception of one of this rank's own atoms, goes to a trash row
+    int tf = 0;
+    fwd_dst_[p].resize(rv.size());
+    rev_src_[p].resize(rv.size());
+    for (size_t k = 0; k < rv.size(); ++k) {
+      const int r = rv[k];
+      if (r < nlocal || seen_in_phase[r] == 2 * p) {
+        fwd_dst_[p][k] = -1 - tf++;   // resolved below, once the zero row is fixed
+        ++st_.trash_forward;
+      } else {
+        fwd_dst_[p][k] = r;
+        seen_in_phase[r] = 2 * p;
+      }
+      // reverse pack: the row's value once over all receptions, zero otherwise
+      if (r >= nlocal && !returned[r]) {
+        rev_src_[p][k] = r;
+        returned[r] = 1;
+      } else {
+        rev_src_[p][k] = zero;
+        ++st_.zero_sends;
+      }
+    }
+    // reverse unpack (accumulate): unique destinations within the swap
+    int tr = 0;
+    rev_dst_[p].resize(sd.size());
+    for (size_t k = 0; k < sd.size(); ++k) {
+      const int r = sd[k];
+      if (seen_in_phase[r] == 2 * p + 1) {
+        rev_dst_[p][k] = -1 - tr++;
+        ++st_.trash_reverse;
+      } else {
+        rev_dst_[p][k] = r;
+        seen_in_phase[r] = 2 * p + 1;
+      }
+      st_.sent += 1;
+      st_.relayed += send_is_ghost_[p][k];
+    }
+    ntrash = std::max(ntrash, std::max(tf, tr));
+  }
+  s_.set_trash_rows(ntrash);
+  st_.extra_rows = s_.extra_rows();
+  for (int p = 0; p < kPhases; ++p) {
+    for (auto* v : {&fwd_dst_[p], &rev_dst_[p]})
+      for (auto& r : *v)
+        if (r < 0) r = s_.trash_row(-1 - r);
+    const std::vector<int32_t>* h[4] = {&send_[p], &fwd_dst_[p], &rev_src_[p], &rev_dst_[p]};
+    for (int k = 0; k < 4; ++k) {
+      const int64_t n = (int64_t)h[k]->size();
+      if (n > cap_[p][k]) {
+        if (d_[p][k]) (void)hipFree(d_[p][k]);
+        d_[p][k] = nullptr;
+        cap_[p][k] = n + n / 4 + 64;
+        if (hipMalloc(&d_[p][k], cap_[p][k] * 4) != hipSuccess) {
+          err_ = "CommMaps: hipMalloc";
+          return E3GNN_ERR_HIP;
+        }
+      }
+      if (n && hipMemcpy(d_[p][k], h[k]->data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        err_ = "CommMaps: hipMemcpy";
+        return E3GNN_ERR_HIP;
+      }
+    }
+  }
+  ready_ = true;
+  return E3GNN_OK;
+}
+
+// pack_forward_comm_gnn (:803-839): rows of the sent atoms -> buf
+int64_t CommMaps::pack_forward(int p, float* buf) {
+  const int64_t n = nsend(p);
+  if (s_.pack(d_[p][0], n, buf)) return -1;
+  return n * s_.comm_dim();
+}
+
+// unpack_forward_comm_gnn (:841-871): buf -> rows of the received ghosts
+int64_t CommMaps::unpack_forward(int p, const float* buf) {
+  const int64_t n = nrecv(p);
+  if (s_.unpack(d_[p][1], n, buf, false)) return -1;
+  return n * s_.comm_dim();
+}
+
+// pack_reverse_comm_gnn (:873-900): the received ghosts' rows go back
+int64_t CommMaps::pack_reverse(int p, float* buf) {
+  const int64_t n = nrecv(p);
+  if (s_.pack(d_[p][2], n, buf)) return -1;
+  return n * s_.comm_dim();
+}
+
+// unpack_reverse_comm_gnn (:902-933): accumulated into the sent atoms' rows
+int64_t CommMaps::unpack_reverse(int p, const float* buf) {
+  const int64_t n = nsend(p);
+  if (s_.unpack(d_[p][3], n, buf, true)) return -1;
+  return n * s_.comm_dim();
 }
 
 }  // namespace e3gnn_pair

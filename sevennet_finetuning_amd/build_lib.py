@@ -75,7 +75,10 @@ NATIVE = os.path.join(os.path.dirname(HERE), 'native')
 
 NATIVE_HOSTS = ('e3gnn_md', 'e3gnn_md_parallel', 'e3gnn_pair_check')
 # extra translation units of a host (the LAMMPS pair-style core)
-NATIVE_EXTRA = {'e3gnn_pair_check': ['pair_e3gnn_core.cpp']}
+NATIVE_EXTRA = {'e3gnn_pair_check': ['pair_e3gnn_core.cpp', 'lammps/pair_e3gnn_hip.cpp',
+                                     'lammps/pair_e3gnn_parallel_hip.cpp', 'lammps_mock/mini_lammps.cpp']}
+# e3gnn_pair_check compiles the LAMMPS adaptors against the mini-LAMMPS scaffold
+NATIVE_INCLUDES = {'e3gnn_pair_check': ['.', 'lammps_mock', 'lammps']}
 
 
 def build_native(lib=LIB, verbose=False, only_stale=False):
@@ -86,13 +89,14 @@ def build_native(lib=LIB, verbose=False, only_stale=False):
     exes = []
     for name in NATIVE_HOSTS:
         srcs = [os.path.join(NATIVE, f) for f in [name + '.cpp'] + NATIVE_EXTRA.get(name, [])]
-        hdrs = [os.path.join(NATIVE, f) for f in os.listdir(NATIVE) if f.endswith('.h')]
+        incs = [os.path.join(NATIVE, d) for d in NATIVE_INCLUDES.get(name, [])]
+        hdrs = [os.path.join(d, f) for d in [NATIVE, *incs] for f in os.listdir(d) if f.endswith('.h')]
         exe = os.path.join(NATIVE, name)
         exes.append(exe)
         if (only_stale and os.path.exists(exe) and os.path.getmtime(exe) >=
                 max([os.path.getmtime(f) for f in srcs + hdrs] + [os.path.getmtime(lib)])):
             continue
-        cmd = [HIPCC, '-O2', '-std=c++17', f'-I{INCLUDE}', *srcs, '-o', exe,
+        cmd = [HIPCC, '-O2', '-std=c++17', f'-I{INCLUDE}', *[f'-I{d}' for d in incs], *srcs, '-o', exe,
                f'-L{os.path.dirname(lib)}', '-le3gnn_hip', '-lpthread',
                "-Wl,-rpath,$ORIGIN/../sevennet_finetuning_amd"]
         if verbose:

@@ -449,12 +449,15 @@ def checkpoint_of(model):
     """The reference checkpoint layout of a model: state dict + config."""
     sd = {n: model.flat[o:o + k].detach().cpu().clone().view(shape)
           for n, (o, k, shape) in model.slices.items()}
-    # the user-level keys, '_normalize_sph' included (model_from_checkpoint
-    # reads its absence as a pre-0.9 checkpoint); the keys resolve_config
-    # derives are recomputed on load
+    # the user-level keys plus the two underscore keys that change the
+    # architecture: '_normalize_sph' (model_from_checkpoint reads its absence as
+    # a pre-0.9 checkpoint) and '_conv_irreps_manual' (the convolution built on
+    # irreps_manual, the sevenn 0.8.6 layout); the keys resolve_config derives
+    # are recomputed on load
     derived = ('_irreps', '_lmax_edge', '_lmax_node', '_conv_denominator')
+    kept = ('_normalize_sph', '_conv_irreps_manual')
     cfg = {k: v for k, v in getattr(model, 'config', {}).items()
-           if (not k.startswith('_') or k == '_normalize_sph') and k not in derived}
+           if (not k.startswith('_') or k in kept) and k not in derived}
     if not cfg:
         raise ValueError('model has no config (build it with build_E3_equivariant_model)')
     return {'model_state_dict': sd, 'config': cfg}

@@ -90,3 +90,23 @@ def test_bench_gpus_2_without_launcher():
     assert sum(x['owned'] for x in d['ranks']) == 2 * 8 * 6 ** 3   # weak: 6^3 cells per rank
     assert all(x['ghosts'] > 0 and x['exchange_ms'] > 0 for x in d['ranks'])
     assert d['exchanges_per_step'] == 9   # 4 forward, 4 reverse, 1 ghost-force reverse
+
+
+@pytest.mark.parametrize('argv,world,n_total,needle', [
+    ([], 1, 97336, '97,336-atom box @1 GPU'),
+    (['--gpus', '8'], 8, 778688, '97,336-atom box per GPU = 778,688-atom box @8 GPUs (weak scaling)'),
+    (['--gpus', '8', '--strong'], 8, 778688, '778,688-atom box split over 8 GPUs (strong scaling)'),
+    (['--strong'], 1, 778688, '778,688-atom box @1 GPU'),
+])
+def test_bench_line_names_the_evaluated_box(argv, world, n_total, needle):
+    """The metric / workload of a bench line name the box actually evaluated:
+    a weak --gpus 8 line is the 778,688-atom box (config 4), so is --strong."""
+    import numpy as np
+    args = _args(argv)
+    cells, grid, total = bench.box_plan(args, world)
+    assert 8 * int(np.prod(total)) == n_total
+    assert (grid == (2, 2, 2)) == (world == 8)
+    metric, work = bench.describe(n_total, world, cells, args.strong, grid)
+    assert metric.startswith('atoms/sec energy+force, SevenNet-0 lmax=2, ')
+    assert needle in metric, metric
+    assert f'{n_total:,}-atom' in work

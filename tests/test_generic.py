@@ -69,3 +69,28 @@ def test_sevennet0_kinds_selected_for_sevennet0_only():
     assert [b['kind'] for b in h.blocks] == [0, 1, 2, 3]
     pos, cell, types = system('si_rng0_1x1x1', syms)
     assert len(pos) == 8
+
+
+def test_gate_layout_matches_hand_derived_e3nn_gate():
+    """nn._gate_irreps against e3nn's Gate layout derived by hand
+    (equivariant_gate.py:30-51 builds Gate(scalars, gates, gated); e3nn's
+    _Sortcut simplifies each group, stable-sorts the concatenation by the Irrep
+    tuple (l, p) -- p = -1 before +1 -- and simplifies again):
+      '4x0e+4x0o+4x1e': gates '4x0e' ('0e' is among the scalars);
+        pieces [4x0e | 4x0o | gates 4x0e | 4x1e] sort to 0o(1), 0e(0), 0e(2), 1e(3)
+        -> irreps_in 4x0o+8x0e+4x1e, offsets 4, 0, 8, 12, not the natural order;
+      '4x0o+4x1e': gates '4x0o' (no '0e') -> 8x0o+4x1e, offsets 0, 4, 8, natural."""
+    from sevennet_finetuning_amd.nn import _gate_irreps
+    simp, scal, gated, (gate_p, offs, natural) = _gate_irreps([(4, 0, 1), (4, 0, -1), (4, 1, 1)])
+    assert simp == [(4, 0, -1), (8, 0, 1), (4, 1, 1)]
+    assert scal == [(4, 0, 1), (4, 0, -1)] and gated == [(4, 1, 1)]
+    assert gate_p == 1 and offs == [4, 0, 8, 12] and natural is False
+    simp, scal, gated, (gate_p, offs, natural) = _gate_irreps([(4, 0, -1), (4, 1, 1)])
+    assert simp == [(8, 0, -1), (4, 1, 1)]
+    assert gate_p == -1 and offs == [0, 4, 8] and natural is True
+    # the oracle's restatement gives the same hand-derived layout
+    from oracle.nequip_ref import gate_irreps
+    ir, _, _, gp, offs = gate_irreps([(4, 0, 1), (4, 0, -1), (4, 1, 1)])
+    assert [tuple(t) for t in ir] == [(4, 0, -1), (8, 0, 1), (4, 1, 1)] and gp == 1 and offs == [4, 0, 8, 12]
+    ir, _, _, gp, offs = gate_irreps([(4, 0, -1), (4, 1, 1)])
+    assert [tuple(t) for t in ir] == [(8, 0, -1), (4, 1, 1)] and gp == -1 and offs == [0, 4, 8]

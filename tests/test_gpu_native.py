@@ -80,31 +80,100 @@ def test_native_parallel_host_matches_serial(grid):
 
 
 EXE_PAIR = os.path.join(ROOT, 'native', 'e3gnn_pair_check')
+HFO2 = os.path.join(ROOT, 'sevennet_finetuning_amd', 'assets', 'hfo2_example')
+KATS = json.load(open(os.path.join(ROOT, 'tests', 'golden', 'kat_reference.json')))
 
 
-@pytest.mark.parametrize('grid', [(1, 1, 1), (2, 1, 1), (2, 2, 1)])
-def test_lammps_pair_core_matches_device_path(grid):
-    """The LAMMPS pair-style core (native/pair_e3gnn_core.cpp, what
-    native/lammps/pair_e3gnn_hip.cpp and pair_e3gnn_parallel_hip.cpp call) on
-    LAMMPS-shaped inputs -- scrambled atom indices and tags, periodic-image
-    ghosts carrying their owner's tag, full neighbour lists with a skin and
-    NEIGHMASK bits -- serial (pair_e3gnn.cpp:72-275) and on brick sub-domains
-    with threaded ranks and halo exchanges (pair_e3gnn_parallel.cpp:207-933),
-    against the device neighbour list + e3gnn_energy_forces of the same box."""
+def _write_structure(path, pos, cell, syms):
+    with open(path, 'w') as f:
+        f.write(f'{len(pos)}\n' + ' '.join(f'{v:.12f}' for v in np.asarray(cell).ravel()) + '\n')
+        for s, p in zip(syms, pos):
+            f.write(f'{s} {p[0]:.12f} {p[1]:.12f} {p[2]:.12f}\n')
+
+
+def _pair_check(model_dir, path, grid, *extra):
     assert os.path.exists(EXE_PAIR), 'native/e3gnn_pair_check not built (build_lib.build)'
-    r = subprocess.run([EXE_PAIR, ASSET, '4', *map(str, grid), '3'], capture_output=True,
+    r = subprocess.run([EXE_PAIR, model_dir, str(path), *map(str, grid), '3', *extra], capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr
-    out = json.loads(r.stdout.strip().splitlines()[-1])
-    assert out['n_atoms'] == 512 and out['ranks'] == int(np.prod(grid))
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _check_pair_run(out, grid, kat_energy, n_atoms):
+    """Both pair styles against the reference KAT, the library's own
+    evaluation and each other; the CommBrick machinery actually exercised."""
+    assert out['n_atoms'] == n_atoms and out['ranks'] == int(np.prod(grid))
     for k in ('serial', 'parallel'):
+        # the reference's frozen-model energy of this structure (SURVEY 8c)
+        assert abs(out[k]['energy'] - kat_energy) <= 2e-6 * abs(kat_energy), out
         assert out[k]['energy_rel'] < 1e-6, out
         assert out[k]['eatom_sum_rel'] < 1e-6, out
         assert out[k]['max_force'] < 1e-4, out
-        assert out[k]['max_virial'] < 1e-3, out
+        assert out[k]['max_virial'] <= 1e-5 * max(1.0, out['max_virial_ref']), out
+        assert out[k]['repeat_bitwise'], out
+    # decomposed = serial (fp32 summation order only)
+    assert out['parallel']['vs_serial_energy_rel'] < 1e-6, out
+    assert out['parallel']['vs_serial_max_force'] < 1e-4, out
+    c = out['comm']
+    split = sum(g > 1 for g in grid)
+    if split == 0:
+        assert c['swaps'] == 0 and c['sent'] == 0, c   # six self swaps, nothing exchanged
+    else:
+        assert c['swaps'] == 2 * split * int(np.prod(grid)), c
+        assert c['extra_rows'] > 0, c     # received ghosts outside the graph (cutoff < ghost cutoff)
+        assert c['zero_sends'] > 0, c     # one atom received by one rank in both swaps of a dimension
+    if split >= 2:
+        assert c['relayed'] > 0, c        # corner atoms forwarded in a later dimension
+        assert c['trash_forward'] > 0 and c['trash_reverse'] > 0, c   # images relayed in one swap
 
 
-HFO2 = os.path.join(ROOT, 'sevennet_finetuning_amd', 'assets', 'hfo2_example')
+PAIR_GRIDS = [(1, 1, 1), (2, 1, 1), (2, 2, 1), (2, 2, 2)]
+
+
+@pytest.mark.parametrize('grid', PAIR_GRIDS)
+def test_lammps_pair_styles_si_kat(grid, tmp_path):
+    """The LAMMPS adaptors (native/lammps/pair_e3gnn_hip.cpp and
+    pair_e3gnn_parallel_hip.cpp, compiled as they are) inside the mini-LAMMPS
+    scaffold: LAMMPS-shaped atoms (scrambled tags and indices), CommBrick's
+    borders() swaps (self swaps, corner relays), full lists with a skin and
+    NEIGHMASK bits, the reference's patched forward_comm / reverse_comm of the
+    pair (comm_brick.cpp:1057-1120) and LAMMPS' newton-on force reverse comm.
+    Displaced Si 3x3x3 (216 atoms) against the reference's KAT -1158.691895 eV."""
+    from _systems import system, load_manifest_symbols
+    pos, cell, _ = system('si_rng0_3x3x3', load_manifest_symbols())
+    path = tmp_path / 'si333.txt'
+    _write_structure(path, pos, cell, ['Si'] * len(pos))
+    kat = next(k for k in KATS['kats'] if k['name'] == 'si_rng0_3x3x3')
+    out = _pair_check(ASSET, path, grid)
+    _check_pair_run(out, grid, kat['energy'], 216)
+
+
+def test_lammps_pair_parallel_gpu_aware_buffers(tmp_path):
+    """pair_e3gnn_parallel.cpp's use_cuda_mpi branch: device MPI buffers from
+    DeviceBuffManager, rows packed straight into them (no host staging)."""
+    from _systems import system, load_manifest_symbols
+    pos, cell, _ = system('si_rng0_3x3x3', load_manifest_symbols())
+    path = tmp_path / 'si333.txt'
+    _write_structure(path, pos, cell, ['Si'] * len(pos))
+    kat = next(k for k in KATS['kats'] if k['name'] == 'si_rng0_3x3x3')
+    out = _pair_check(ASSET, path, (2, 2, 2), '--gpu-aware')
+    _check_pair_run(out, (2, 2, 2), kat['energy'], 216)
+
+
+@pytest.mark.parametrize('grid', PAIR_GRIDS)
+def test_lammps_pair_styles_hfo2_kat(grid, tmp_path):
+    """The same on the reference's HfO2 example deployment (generic engine,
+    triclinic cell: CommBrick in lamda coordinates) on res.dat x 2x2x1:
+    energy = 4 x the reference's frozen-model KAT."""
+    from sevennet_finetuning_amd.structures import tile
+    d = np.load(os.path.join(ROOT, 'tests', 'golden', 'hfo2_resdat.npz'))
+    pos, cell = tile(d['pos'], d['cell'], (2, 2, 1))
+    path = tmp_path / 'hfo2_221.txt'
+    _write_structure(path, pos, cell, [str(s) for s in d['symbols']] * 4)
+    out = _pair_check(HFO2, path, grid)
+    _check_pair_run(out, grid, 4 * KATS['kats_hfo2_example']['energy'], 384)
+
+
 
 
 @pytest.mark.parametrize('grid', [(1, 1, 1), (2, 1, 1), (2, 2, 1)])

@@ -219,6 +219,44 @@ def test_checkpoint_keeps_normalize_sph_and_loads_old_names(monkeypatch):
     assert torch.equal(m2.flat, m.flat)
 
 
+def _hfo2_config():
+    import os
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        'sevennet_finetuning_amd', 'assets', 'hfo2_example')
+    ref = json.load(open(os.path.join(root, 'manifest.json')))
+    return {'chemical_species': 'Hf O', 'cutoff': 4.0, 'channel': 4, 'lmax': 1, 'is_parity': True,
+            'num_convolution_layer': 4, 'irreps_manual': ref['irreps_manual'],
+            'self_connection_type': 'nequip', 'conv_denominator': ref['conv_denominator'][0],
+            '_normalize_sph': False, '_conv_irreps_manual': True,
+            'cutoff_function': {'cutoff_function_name': 'poly_cut', 'poly_cut_p_value': 6}}
+
+
+def test_checkpoint_round_trip_keeps_conv_irreps_manual(monkeypatch):
+    """The sevenn 0.8.6 layout (convolution on irreps_manual) survives
+    checkpoint_of -> model_from_checkpoint: without '_conv_irreps_manual' the
+    rebuilt last block's radial weight shrinks (40 -> 8) and loading fails."""
+    from _conv_cpu import GenericCpuConvBackend
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+
+    def build_cpu(config, device='cuda', **kw):
+        cfg = mb.resolve_config(dict(config))
+        man = mb.model_manifest(cfg)
+        m = SevenNetTrainable(device='cpu', conv_backend=GenericCpuConvBackend(), manifest=man,
+                              weights=mb.init_weights(man, cfg, 11))
+        m.config = cfg
+        return m
+    m = build_cpu(_hfo2_config())
+    with torch.no_grad():
+        m.flat.add_(torch.randn_like(m.flat) * 1e-3)
+    ck = mb.checkpoint_of(m)
+    assert ck['config']['_conv_irreps_manual'] is True and ck['config']['_normalize_sph'] is False
+    monkeypatch.setattr(mb, 'build_E3_equivariant_model', build_cpu)
+    m2, cfg2 = mb.model_from_checkpoint(ck, device='cpu')
+    assert cfg2['_conv_irreps_manual'] is True
+    assert [(n, k) for n, (_, k, _) in m2.slices.items()] == [(n, k) for n, (_, k, _) in m.slices.items()]
+    assert torch.equal(m2.flat, m.flat)
+
+
 def test_routing_uses_one_predicate():
     """model.load_model, model_build's family label and the trainable
     model's kernel choice agree (nn.sevennet0_kinds)."""

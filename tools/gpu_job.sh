@@ -62,6 +62,9 @@ for s in "$@"; do
     listc) step listc 120 rocprofv3 -L ;;
     pmcsq) step pmcsq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES --kernel-trace --output-format csv -d gpurun_out/pmc_sq -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
     pmcsq2) step pmcsq2 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace --output-format csv -d gpurun_out/pmc_sq2 -o run -- python bench.py --cells 11 --steps 1 --warmup 1 --profile-only ;;
+    pmcsqf) step pmcsqf 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_BUSY_CYCLES --kernel-trace --output-format csv -d gpurun_out/pmc_sqf -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
+    pmcsq2f) step pmcsq2f 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace --output-format csv -d gpurun_out/pmc_sq2f -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
+    pmcsq3f) step pmcsq3f 600 rocprofv3 --pmc SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_WR SQ_WAIT_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS --kernel-trace --output-format csv -d gpurun_out/pmc_sq3f -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     proftracev_*) v=${s#proftracev_}; step proftrace_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so rocprofv3 --kernel-trace --output-format csv -d gpurun_out/proftrace_$v -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     benchv_*) v=${s#benchv_}; step bench_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     testsv_*) v=${s#testsv_}; step tests_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -m pytest tests -m gpu -x -q ;;
