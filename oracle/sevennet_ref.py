@@ -219,11 +219,39 @@ class SevenNet0Ref:
         agg = agg.index_add(0, edge_dst, msg)
         return agg / self.t(f'{pre}.denominator')[0], mid
 
-    def energy(self, pos, types, edge_index, shift, cell, with_stress=True, trace=None):
+    def _convolution_chunked(self, t, x, emb, sh, edge_src, edge_dst, irreps_x, lmax_out, chunk):
+        """convolution() over edge chunks, each under activation checkpointing:
+        the same sum (added chunk by chunk), with the per-edge intermediates of
+        one chunk alive at a time (fp64 autograd on ~10^6 edges otherwise holds
+        tens of GB)."""
+        from torch.utils.checkpoint import checkpoint
+        agg, mid = None, None
+        for a in range(0, emb.shape[0], chunk):
+            b = min(a + chunk, emb.shape[0])
+
+            def part(xx, ee, ss, _a=a, _b=b):
+                return self.convolution(t, xx, ee, ss, edge_src[_a:_b], edge_dst[_a:_b],
+                                        irreps_x, lmax_out)[0]
+            c = checkpoint(part, x, emb[a:b], sh[a:b], use_reentrant=False)
+            agg = c if agg is None else agg + c
+        mid = conv_instructions(irreps_x, lmax_out)[1]
+        if agg is None:
+            dim = sum(m * (2 * l + 1) for m, l in mid)
+            agg = torch.zeros(x.shape[0], dim, dtype=self.dtype)
+        return agg, mid
+
+    def energy(self, pos, types, edge_index, shift, cell, with_stress=True, trace=None,
+               layer_edges=None, edge_chunk=None):
         """Returns dict with E (scalar), atomic_energy [N], and the autograd
         graph inputs so forces/stress can be taken (force_output.py:74-130).
         ``trace``: optional list receiving the node features after each
-        interaction block (layer-wise known answers for the HIP kernels)."""
+        interaction block (layer-wise known answers for the HIP kernels).
+        ``layer_edges``: optional per-block index tensors of the edges whose
+        messages block t computes (the rest contribute nothing): an open-cluster
+        evaluation then spends block t only on the centres whose features later
+        blocks still need (the receptive field shrinks by one cutoff a block).
+        ``edge_chunk``: evaluate each convolution in checkpointed edge chunks
+        (same values, bounded memory)."""
         dt = self.dtype
         pos = pos.to(dt)
         cell = cell.to(dt)
@@ -249,7 +277,13 @@ class SevenNet0Ref:
             sc = e3nn_linear(x, irr_x, gin, self.p[f'{t}_self_connection_intro.linear.weight'])
             h = e3nn_linear(x, irr_x, irr_x, self.p[f'{t}_self_interaction_1.linear.weight'])
             # convolution uses edge_index[1] as source, [0] as target (convolution.py:111-113)
-            agg, mid = self.convolution(t, h, emb, sh, dst, src, irr_x, 0 if last else 2)
+            k = layer_edges[t] if layer_edges is not None else slice(None)
+            if edge_chunk:
+                agg, mid = self._convolution_chunked(t, h, emb[k], sh[k], dst[k], src[k], irr_x,
+                                                     0 if last else 2, edge_chunk)
+            else:
+                agg, mid = self.convolution(t, h, emb[k], sh[k], dst[k], src[k], irr_x,
+                                            0 if last else 2)
             y = e3nn_linear(agg, mid, gin, self.p[f'{t}_self_interaction_2.linear.weight']) + sc
             x = self.gate(y, irr_out)
             if trace is not None:

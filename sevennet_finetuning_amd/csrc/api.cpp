@@ -145,6 +145,7 @@ struct e3gnn_model {
   int device = 0;
   int nsp = 0, nlayer = 0;
   float cutoff = 5.f, r_on = 4.5f;
+  int raw_sh = 0;   // SH of the raw edge vector (sh_normalize false: checkpoints before sevenn 0.9)
   std::vector<Irreps> irreps;  // irreps_manual per layer boundary (merged)
   std::vector<Irreps> gin, mid;
   std::vector<int> W;          // radial weight numel per layer
@@ -586,7 +587,6 @@ bool is_sevennet0(const minijson::Value& man) {
   const int lmax = man.has("lmax_edge") ? (int)man["lmax_edge"].num()
                                         : (man.has("lmax") ? (int)man["lmax"].num() : 2);
   if (lmax != 2) return false;
-  if (man.has("sh_normalize") && !man["sh_normalize"].boolean()) return false;
   if (man.has("self_connection_type") && man["self_connection_type"].str() != "linear") return false;
   if (!man.has("cutoff_function") || man["cutoff_function"]["name"].str() != "XPLOR") return false;
   if ((int)man["num_convolution_layer"].num() != 5) return false;
@@ -662,9 +662,9 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
     }
     // the knobs this engine does not read must hold SevenNet-0's values (the
     // same predicate as nn.sevennet0_kinds)
-    if (man.has("sh_normalize") && !man["sh_normalize"].boolean())
-      throw std::runtime_error("raw-vector spherical harmonics (sh_normalize false, sevenn < 0.9) "
-                               "are not SevenNet-0's architecture");
+    // sh_normalize false (checkpoints before sevenn 0.9, util.py:130-146): the
+    // same kernels, the SH polynomials of the raw vector (node.hip)
+    m->raw_sh = man.has("sh_normalize") && !man["sh_normalize"].boolean() ? 1 : 0;
     if (man.has("is_parity") && man["is_parity"].boolean())
       throw std::runtime_error("odd-parity filters are not SevenNet-0's architecture");
     if (man.has("self_connection_type") && man["self_connection_type"].str() != "linear")
@@ -1087,7 +1087,7 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   if (c->gen) return E3GNN_OK;  // (edge embedding done by gen_graph_set)
   {
     Region r(c, s, C_EMBED_EDGE, 0, (double)E * (12 + 68));
-    HIPCHK(launch_edge_embed(E, c->vec.f(), m->coeffs.f(), m->cutoff, m->r_on, c->Y.f(),
+    HIPCHK(launch_edge_embed(E, c->vec.f(), m->coeffs.f(), m->cutoff, m->r_on, m->raw_sh, c->Y.f(),
                              c->emb.f(), s));
   }
   if (E > 0) {
@@ -1477,7 +1477,7 @@ int e3gnn_forces(e3gnn_ctx* c, float* forces, float* virial6, float* edge_grad, 
   const int64_t n = c->n, nl = c->nl, E = c->E;
   {
     Region r(c, s, C_EDGE_FORCE, 0, (double)E * 4 * (3 + 9 + 8 + 3));
-    HIPCHK(launch_edge_force(E, c->vec.f(), m->coeffs.f(), m->cutoff, m->r_on, c->dY.f(),
+    HIPCHK(launch_edge_force(E, c->vec.f(), m->coeffs.f(), m->cutoff, m->r_on, m->raw_sh, c->dY.f(),
                              c->dgu.f(), c->demb.f(), c->fe.f(), c->vpart.f(), s));
     HIPCHK(launch_final_sum(edge_force_blocks(E), 6, c->vpart.f(),
                             virial6 ? virial6 : c->scratch6.f(), s));

@@ -5,10 +5,10 @@
 
 namespace e3gnn {
 hipError_t launch_edge_embed(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
-                             float* Y, float* emb, hipStream_t s);
+                             int raw_sh, float* Y, float* emb, hipStream_t s);
 int edge_force_blocks(int64_t E);
 hipError_t launch_edge_force(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
-                             const float* dY, const float* dgu, const float* demb, float* fe,
+                             int raw_sh, const float* dY, const float* dgu, const float* demb, float* fe,
                              float* vir_part, hipStream_t s);
 hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, const int* src_ptr,
                              const int* src_perm, const float* fe, float* F, hipStream_t s);

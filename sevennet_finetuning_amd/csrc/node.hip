@@ -16,14 +16,17 @@ inline int nblk(int64_t n, int t = TPB) { return (int)((n + t - 1) / t); }
 // EdgeEmbedding.forward (sevenn/nn/edge_embedding.py:220-230): r = |r_ij|,
 // BesselBasis (:114-116) B_n = (2/rc) sin(c_n r) / r with trainable c_n,
 // XPLORCutoff (:163-173), SphericalEncoding (:177-198; e3nn SH lmax 2,
-// normalize=True, 'component'; polynomial of serial_code.py:50-70).
+// 'component'; polynomial of serial_code.py:50-70) of the unit vector
+// (normalize=True) or, for checkpoints before sevenn 0.9 (`_normalize_sph`
+// absent, util.py:130-146), of the raw vector: Y_l(r) = |r|^l Y_l(r/|r|).
 __global__ void k_edge_embed(int64_t E, const float* __restrict__ vec, const float* __restrict__ coeffs,
-                             float rc, float ron, float* __restrict__ Y, float* __restrict__ emb) {
+                             float rc, float ron, int raw_sh, float* __restrict__ Y,
+                             float* __restrict__ emb) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E) return;
   const float vx = vec[3 * e], vy = vec[3 * e + 1], vz = vec[3 * e + 2];
   const float r = sqrtf(vx * vx + vy * vy + vz * vz);
-  const float x = vx / r, y = vy / r, z = vz / r;
+  const float x = raw_sh ? vx : vx / r, y = raw_sh ? vy : vy / r, z = raw_sh ? vz : vz / r;
   const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f;
   float* yo = Y + 9 * e;
   yo[0] = 1.f;
@@ -48,9 +51,12 @@ __global__ void k_edge_embed(int64_t E, const float* __restrict__ vec, const flo
 
 // dE/dr_ij from the accumulated dE/dY (all layers) and dE/demb (all layers):
 // the chain rule of the two functions above (force_output.py:83-130 obtains
-// the same through autograd).  Also writes per-block virial partials.
+// the same through autograd).  Also writes per-block virial partials.  With
+// raw_sh the SH polynomials take the raw vector: their gradient (and dgu, which
+// the fused kernels form from Y_1 / sqrt 3 = the SH argument) is dE/dr_ij
+// directly, without the unit-vector projection.
 __global__ void k_edge_force(int64_t E, const float* __restrict__ vec, const float* __restrict__ coeffs,
-                             float rc, float ron, const float* __restrict__ dY,
+                             float rc, float ron, int raw_sh, const float* __restrict__ dY,
                              const float* __restrict__ dgu, const float* __restrict__ demb,
                              float* __restrict__ fe, float* __restrict__ vir_part) {
   __shared__ float red[6][TPB];
@@ -59,10 +65,11 @@ __global__ void k_edge_force(int64_t E, const float* __restrict__ vec, const flo
   if (e < E) {
     const float vx = vec[3 * e], vy = vec[3 * e + 1], vz = vec[3 * e + 2];
     const float r = sqrtf(vx * vx + vy * vy + vz * vz);
-    const float x = vx / r, y = vy / r, z = vz / r;
+    const float ux = vx / r, uy = vy / r, uz = vz / r;
+    const float x = raw_sh ? vx : ux, y = raw_sh ? vy : uy, z = raw_sh ? vz : uz;
     const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f;
     const float* g = dY + 9 * e;
-    // gradient w.r.t. the unit vector u
+    // gradient w.r.t. the SH argument (unit vector u, or r_ij itself)
     float gx = s3 * g[1], gy = s3 * g[2], gz = s3 * g[3];
     const float c = s5 * s3;
     gx += c * (z * g[4] + y * g[5]) - s5 * x * g[6] - c * x * g[8];
@@ -73,8 +80,13 @@ __global__ void k_edge_force(int64_t E, const float* __restrict__ vec, const flo
       gy += dgu[3 * e + 1];
       gz += dgu[3 * e + 2];
     }
-    const float dot = gx * x + gy * y + gz * z;
-    float fx = (gx - dot * x) / r, fy = (gy - dot * y) / r, fz = (gz - dot * z) / r;
+    float fx = gx, fy = gy, fz = gz;
+    if (!raw_sh) {
+      const float dot = gx * ux + gy * uy + gz * uz;
+      fx = (gx - dot * ux) / r;
+      fy = (gy - dot * uy) / r;
+      fz = (gz - dot * uz) / r;
+    }
     // radial part
     float env = 1.f, denv = 0.f;
     if (r >= ron) {
@@ -93,9 +105,9 @@ __global__ void k_edge_force(int64_t E, const float* __restrict__ vec, const flo
       const float db = (2.f / rc) * (cn * cs * r - sn) / (r * r);
       dr += ge[n] * (db * env + b * denv);
     }
-    fx += dr * x;
-    fy += dr * y;
-    fz += dr * z;
+    fx += dr * ux;
+    fy += dr * uy;
+    fz += dr * uz;
     fe[3 * e] = fx;
     fe[3 * e + 1] = fy;
     fe[3 * e + 2] = fz;
@@ -453,15 +465,15 @@ __global__ void k_unpack(int64_t n, int dim, const int* __restrict__ idx, const 
   } while (0)
 
 hipError_t launch_edge_embed(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
-                             float* Y, float* emb, hipStream_t s) {
-  LAUNCH(k_edge_embed, nblk(E), E, vec, coeffs, rc, ron, Y, emb);
+                             int raw_sh, float* Y, float* emb, hipStream_t s) {
+  LAUNCH(k_edge_embed, nblk(E), E, vec, coeffs, rc, ron, raw_sh, Y, emb);
   return hipGetLastError();
 }
 int edge_force_blocks(int64_t E) { return nblk(E); }
 hipError_t launch_edge_force(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
-                             const float* dY, const float* dgu, const float* demb, float* fe,
+                             int raw_sh, const float* dY, const float* dgu, const float* demb, float* fe,
                              float* vir_part, hipStream_t s) {
-  LAUNCH(k_edge_force, nblk(E), E, vec, coeffs, rc, ron, dY, dgu, demb, fe, vir_part);
+  LAUNCH(k_edge_force, nblk(E), E, vec, coeffs, rc, ron, raw_sh, dY, dgu, demb, fe, vir_part);
   return hipGetLastError();
 }
 hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, const int* src_ptr,

@@ -290,7 +290,8 @@ def _sh_map(lmax, device, dtype):
 def sevennet0_kinds(manifest, conv_only=False):
     """THE test for SevenNet-0's architecture, shared by every router
     (model.load_model and model_build's family label; e3gnn_load checks the
-    same knobs): even-parity lmax-2 filters on normalised edge vectors, the
+    same knobs): even-parity lmax-2 filters (SH of the unit vector, or of the
+    raw vector for pre-0.9 checkpoints: one flag of the edge kernels), the
     XPLOR cutoff, a linear self-connection and exactly
     128x0e -> 4 x (128x0e+64x1e+32x2e) -> 128x0e.  Returns the kernel kind of
     every block (0 first, 1 middle, 2 last; csrc/tp.h) or None.
@@ -301,8 +302,7 @@ def sevennet0_kinds(manifest, conv_only=False):
     if man.get('is_parity', False) or int(man.get('lmax_edge', man.get('lmax', 2))) != 2:
         return None
     cf = man.get('cutoff_function', {}) or {}
-    if not conv_only and (not bool(man.get('sh_normalize', True)) or
-                          man.get('self_connection_type', 'linear') != 'linear' or
+    if not conv_only and (man.get('self_connection_type', 'linear') != 'linear' or
                           cf.get('name', 'XPLOR') != 'XPLOR'):
         return None
     irreps = [parse_irreps(s) for s in man['irreps_manual']]

@@ -12,9 +12,11 @@ the quantities):
 * the fused kernels against the independent unfused v1 kernels on the bench
   box (random per-atom displacements, every atom's environment distinct);
 * bitwise run-to-run determinism on the bench box;
-* direct oracle parity inside the random full-size boxes: an atom's energy
-  depends only on atoms within 5 cutoffs (25 A, ~3,500 atoms), so the fp64
-  oracle evaluates that open cluster and must reproduce the HIP value.
+* direct oracle parity inside the random full-size boxes: a chosen atom's
+  per-edge dE/dr_ij, force and atomic energy depend only on atoms within 10
+  cutoffs (50 A), so the fp64 oracle evaluates that open cluster (block by
+  block, only the centres later blocks still need) and must reproduce the
+  HIP values.
 """
 import numpy as np
 import pytest
@@ -128,47 +130,88 @@ def test_bitwise_determinism_at_97k(model, bench_box):
     assert np.array_equal(a['stress'], b['stress'])
 
 
-def _cluster_atomic_energy(pos, cell, types, centre, cutoff, n_layers):
-    """fp64 oracle atomic energy of ``centre`` from the open cluster of every
-    atom image within n_layers * cutoff of it.  E_i depends only on atoms
-    within that radius (each interaction block reaches one cutoff further,
-    nn/convolution.py message passing; the readout after the last block is
-    per atom), so the cluster value is the periodic box's value exactly."""
-    from oracle.neighbor import neighbor_list
+def _cluster_oracle(pos, cell, types, centre, cutoff, n_layers, with_force=True):
+    """fp64 oracle on the open cluster that determines, exactly, (a) dE/dr_ij of
+    every edge of ``centre``, (b) the force on ``centre`` and (c) the atomic
+    energies of every atom within n_layers * rc of it.
+
+    Receptive fields (nn/convolution.py message passing, one cutoff per block;
+    readout per atom): E_k depends on the position of ``centre`` only for k
+    within L*rc (L = 5 blocks: 25 A), so E_S with S = B(L*rc) has dE_S/dx_c =
+    dE/dx_c and dE_S/dr_e = dE/dr_e for the centre's edges.  x_L(k) for k in S
+    needs block L's messages at centres in B(L*rc), x_{t}(k) for k in B(R) needs
+    block t's messages at centres in B(R + rc): block t (0-based) computes
+    messages only at centres within (2L - 1 - t)*rc = 45, 40, 35, 30, 25 A, and
+    the cluster holds every atom within 2*L*rc = 50 A (their one-hot
+    embeddings).  Per-block edge subsets keep the oracle at ~1.4M edge
+    evaluations instead of a full 26k-atom cluster five times.
+    ``with_force`` False: only (a) and (c) -- S = B((L-1)*rc), every radius one
+    cutoff smaller (45 A cluster, ~0.9M edge evaluations)."""
+    from scipy.spatial import cKDTree
     from oracle.sevennet_ref import SevenNet0Ref
-    r = n_layers * cutoff + 0.25
+    L = n_layers
+    top = 2 * L if with_force else 2 * L - 1     # cluster radius in cutoffs
+    s_r = L if with_force else L - 1             # radius of the energy set S
     d = pos - pos[centre]
     f = d @ np.linalg.inv(cell)
-    f -= np.round(f)                       # minimum image: the box is > 2r wide
+    f -= np.round(f)                       # minimum image: the box is > 2 x 50 A wide
     d = f @ cell
-    sel = np.nonzero((d * d).sum(1) <= r * r)[0]
-    box = np.eye(3) * (4 * r + 10)
-    cp = d[sel] + box[0, 0] / 2
-    ei, sh = neighbor_list(cp, box, cutoff, pbc=(False, False, False))
+    r = np.sqrt((d * d).sum(1))
+    sel = np.nonzero(r <= top * cutoff)[0]
+    cp, rs = d[sel], r[sel]
+    c0 = int(np.nonzero(sel == centre)[0][0])
+    pairs = cKDTree(cp).query_pairs(cutoff, output_type='ndarray')
+    dv = cp[pairs[:, 1]] - cp[pairs[:, 0]]
+    pairs = pairs[np.sqrt((dv * dv).sum(1)) < cutoff]
+    ei = np.concatenate([pairs, pairs[:, ::-1]]).T
+    layer_edges = [torch.as_tensor(np.nonzero(rs[ei[0]] < (top - 1 - t) * cutoff)[0])
+                   for t in range(L)]
     ref = SevenNet0Ref(dtype=torch.float64)
-    with torch.no_grad():
-        out = ref.energy(torch.tensor(cp), torch.tensor(types[sel]), torch.tensor(ei),
-                         torch.tensor(sh), torch.tensor(box), False)
-    return float(out['atomic_energy'][int(np.nonzero(sel == centre)[0][0])]), len(sel)
+    posd = torch.tensor(cp, requires_grad=True)
+    box = np.eye(3) * (8 * L * cutoff)
+    out = ref.energy(posd, torch.tensor(types[sel]), torch.tensor(ei), torch.zeros(ei.shape[1], 3,
+                     dtype=torch.float64), torch.tensor(box), False, layer_edges=layer_edges,
+                     edge_chunk=16384)
+    in_s = torch.as_tensor(rs < s_r * cutoff)
+    e_s = out['atomic_energy'][in_s].sum()
+    g_vec, g_pos = torch.autograd.grad(e_s, [out['edge_vec'], posd])
+    ce = np.nonzero(ei[0] == c0)[0]
+    return {'nbr': sel[ei[1][ce]], 'edge_grad': g_vec[ce].numpy(),
+            'force': -g_pos[c0].numpy() if with_force else None,
+            'atomic_energy': float(out['atomic_energy'][c0].detach()), 'n_cluster': len(sel),
+            'n_edge_evals': int(sum(len(k) for k in layer_edges))}
 
 
-@pytest.mark.parametrize('cells,centres', [(23, (0, 48611)), (46, (500001,))],
+@pytest.mark.parametrize('cells,centre,with_force', [(23, 48611, True), (46, 500001, False)],
                          ids=['97k', '778k'])
-def test_atomic_energies_at_full_size_vs_oracle(model, cells, centres):
+def test_edge_gradients_and_force_at_full_size_vs_oracle(model, cells, centre, with_force):
     """Direct oracle parity INSIDE the full-size random boxes (config 3 and
-    config 4's atom count, every atom's environment distinct): the HIP
-    atomic energies of chosen atoms equal the fp64 oracle's on the open
-    cluster that determines them (~3,500 atoms each)."""
+    config 4's atom count, every atom's environment distinct): for a chosen
+    atom, the HIP per-edge dE/dr_ij of all its edges (edge_grad, what
+    ForceStressOutputFromEdge differentiates, force_output.py:158-215), its
+    force and its atomic energy equal the fp64 oracle's on the open cluster
+    that determines them exactly (50 A, ~26k atoms; see _cluster_oracle).  At
+    778k the force is left out (45 A cluster) to bound the oracle's time."""
     from sevennet_finetuning_amd.structures import si_diamond
     from sevennet_finetuning_amd.neighbor import DeviceNeighborList
     pos, cell = si_diamond((cells,) * 3, sigma=0.05)
     types = np.full(len(pos), SI)
     dev = model.device
     c, nb, _, vec = DeviceNeighborList(dev)(pos, cell, model.cutoff)
-    out = model.energy_forces(torch.as_tensor(types, dtype=torch.int32, device=dev), c, nb, vec)
-    eat = out['atomic_energy'].cpu().numpy()
+    out = model.energy_forces(torch.as_tensor(types, dtype=torch.int32, device=dev), c, nb, vec,
+                              want_edge_grad=True)
+    mine = torch.nonzero(c == centre).flatten()
+    nbr = nb[mine].cpu().numpy()
+    g_hip = out['edge_grad'][mine].cpu().numpy()
+    f_hip = out['forces'][centre].cpu().numpy()
+    e_hip = float(out['atomic_energy'][centre])
     del c, nb, vec, out
-    for i in centres:
-        e_ref, n = _cluster_atomic_energy(pos, cell, types, i, model.cutoff, 5)
-        assert n > 3000
-        assert abs(eat[i] - e_ref) <= 2e-5, (i, eat[i], e_ref)
+    ref = _cluster_oracle(pos, cell, types, centre, model.cutoff, 5, with_force)
+    assert ref['n_cluster'] > (20000 if with_force else 15000)
+    assert sorted(nbr.tolist()) == sorted(ref['nbr'].tolist())   # one image per neighbour here
+    order = {j: k for k, j in enumerate(ref['nbr'].tolist())}
+    g_ref = ref['edge_grad'][[order[j] for j in nbr.tolist()]]
+    assert np.abs(g_hip - g_ref).max() <= F_TOL, np.abs(g_hip - g_ref).max()
+    if with_force:
+        assert np.abs(f_hip - ref['force']).max() <= F_TOL, (f_hip, ref['force'])
+    assert abs(e_hip - ref['atomic_energy']) <= 2e-5, (e_hip, ref['atomic_energy'])

@@ -170,10 +170,10 @@ def test_old_checkpoint_config_is_patched():
     assert 'train_avg_num_neigh' not in p and 'poly_cut_p_value' not in p['cutoff_function']
     man = mb.model_manifest(mb.resolve_config(p))
     assert man['sh_normalize'] is False
-    # not SevenNet-0's architecture any more: routed to the family model
-    assert man['family'] == 'nequip'
+    # still SevenNet-0's architecture: the specialised kernels with raw-vector SH
+    assert man['family'] == 'sevennet0'
     from sevennet_finetuning_amd.nn import sevennet0_kinds
-    assert sevennet0_kinds(man) is None and sevennet0_kinds(man, conv_only=True) is not None
+    assert sevennet0_kinds(man) == sevennet0_kinds(man, conv_only=True) == [0, 1, 1, 1, 2]
     c2 = ft_config()
     c2.pop('conv_denominator')
     assert mb._patch_old_config(c2)['conv_denominator'] == 0.0
@@ -262,7 +262,9 @@ def test_routing_uses_one_predicate():
     model's kernel choice agree (nn.sevennet0_kinds)."""
     from sevennet_finetuning_amd.nn import sevennet0_kinds
     assert sevennet0_kinds(MAN) == [0, 1, 1, 1, 2]
-    for change in ({'sh_normalize': False}, {'is_parity': True},
+    # raw-vector SH (pre-0.9 checkpoints) is one flag of the edge kernels
+    assert sevennet0_kinds(dict(MAN, sh_normalize=False)) == [0, 1, 1, 1, 2]
+    for change in ({'is_parity': True},
                    {'self_connection_type': 'nequip'}, {'lmax_edge': 1},
                    {'cutoff_function': {'name': 'poly_cut', 'p': 6.0}}):
         man = dict(MAN, **change)
