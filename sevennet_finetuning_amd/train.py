@@ -202,8 +202,8 @@ def _sum_two_level(v):
     flat buffer is PyTorch's multi-block global reduction, whose semaphores
     are re-zeroed by a hipMemsetAsync before each launch; captured in a HIP
     graph (the graphed rehearsal step) it returned wrong sums on replays that
-    other work ran between (tools/diag_graph_reduce.py, tools/
-    diag_ewc_interleave.py: the reported EWC loss, never the gradients, which
+    other work ran between (the diagnostic scripts of
+    round 3, in git history: the reported EWC loss, never the gradients, which
     _FlatEWC.backward forms element-wise)."""
     m = v.numel() // 1024 * 1024
     s = v[:m].view(-1, 1024).sum(1).sum() if m else v.new_zeros(())

@@ -296,7 +296,7 @@ def test_graphed_step_replays_of_equal_shapes_equal_eager():
 
 def test_graphed_ewc_step_interleaved_with_eager_trainer():
     """An eager and a graphed EWC trainer stepped alternately in one process
-    (tools/diag_ewc_interleave.py): every step's losses and the final
+    (round 3 diagnostic, git history): every step's losses and the final
     parameters equal.  Round 2 shipped this broken: the graphed trainer's
     REPORTED loss came back ~800 (parameters right) once other work ran
     between its replays -- the EWC term's torch.sum over the 842k-entry flat

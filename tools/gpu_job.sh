@@ -36,7 +36,6 @@ for s in "$@"; do
     proftrace) step proftrace 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/proftrace -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     bench2gloo) step bench2gloo 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --same-device --no-cpu-baseline ;;
     traingraph) step traingraph 600 python -u -m pytest tests/test_gpu_train.py -x -v --timeout 300 --timeout-method thread -k "graph" ;;
-    highdeg) step highdeg 300 python tools/diag_highdeg.py && step highdeg0 300 env E3GNN_NODELIN=0 python tools/diag_highdeg.py ;;
     proftrain) step proftrain 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_train -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 && mkdir -p gpurun_out/prof_train && cp /tmp/prof_train/*/*stats* /tmp/prof_train/*stats* gpurun_out/prof_train/ 2>/dev/null; ls gpurun_out/prof_train ;;
     traintests) step traintests 400 python -m pytest tests/test_gpu_train.py -x -q --timeout 200 --timeout-method thread ;;
     benchtrain) step benchtrain 300 python bench_train.py --steps 10 --warmup 3 ;;
@@ -68,10 +67,8 @@ for s in "$@"; do
     proftracev_*) v=${s#proftracev_}; step proftrace_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so rocprofv3 --kernel-trace --output-format csv -d gpurun_out/proftrace_$v -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     benchv_*) v=${s#benchv_}; step bench_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     testsv_*) v=${s#testsv_}; step tests_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -m pytest tests -m gpu -x -q ;;
-    diagewc) step diagewc 400 python tools/diag_ewc_interleave.py ;;
     bench2self) step bench2self 600 python bench.py --gpus 2 --same-device --steps 2 --warmup 1 --cells 11 --no-cpu-baseline ;;
     paritydef) step paritydef 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
-    reduce) step reduce 300 python tools/diag_graph_reduce.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
