@@ -58,7 +58,7 @@ def cpu_baseline(batches, cfg, seconds):
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get('OMP_NUM_THREADS', '16')))
     torch.set_num_threads(threads)
     model = SevenNetTrainable(device='cpu', conv_backend=CpuConvBackend())
-    c = dict(cfg, device='cpu', is_ddp=False, hip_graph=False)
+    c = dict(cfg, device='cpu', is_ddp=False, hip_graph=False, explicit_grad=False)
     c['continue'] = dict(cfg['continue'],
                          fisher_information={k: v.cpu() for k, v in
                                              cfg['continue']['fisher_information'].items()},
@@ -89,6 +89,9 @@ def main():
     ap.add_argument('--eager', action='store_true',
                     help='no HIP-graph capture of the step (always eager for N > 1)')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    ap.add_argument('--autograd', action='store_true',
+                    help='the loss gradient by autograd double backward instead of the '
+                         'hand-scheduled derivatives (train_explicit.py)')
     args = ap.parse_args()
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -108,7 +111,7 @@ def main():
            'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
            'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
            'scheduler_param': {'gamma': 0.99}, 'is_ddp': world > 1, 'device': device,
-           'hip_graph': not args.eager,
+           'hip_graph': not args.eager, 'explicit_grad': not args.autograd,
            'continue': {'fisher_information': fisher, 'opt_params': opt, 'ewc_lambda': 1e5}}
     tr = train.Trainer(model, cfg)
     n_b = 4
@@ -159,7 +162,8 @@ def main():
                                    'Adam, grad all-reduce',
                        'atoms_per_rank_step': atoms_per_step, 'edges_per_batch': edges,
                        'parallelism': f'dp{world}',
-                       'hip_graph': bool(tr.hip_graph)},
+                       'hip_graph': bool(tr.hip_graph),
+                       'explicit_grad': tr.explicit is not None},
             'atoms_per_s': round(atoms_per_step * world * args.steps / dt, 1),
             'loss': float(loss), 'mem_loss': float(mloss), 'cpu_baseline': cpu}), flush=True)
     if world > 1:

@@ -26,6 +26,7 @@
  *     (training: convolution.py:104-123, trainer.py:155-222)         _forward / _backward
  *   e3nn normalize2mom(silu) and its derivatives (training)          e3gnn_act
  *   EquivariantGate / e3nn Gate and its derivatives (training)       e3gnn_gate
+ *   second-order fine-tune derivatives, hand-scheduled (training)   e3gnn_act_dual, e3gnn_gate_dual
  *   LAMMPS pair_style d3 settings/coeff, compute/update             e3gnn_d3_create /
  *     (pair_d3.cu:265-767, :2003-2056)                               e3gnn_d3_compute
  *   error->all(FLERR, msg)                                           return code +
@@ -221,6 +222,20 @@ int e3gnn_act(int op, int64_t n, const float* x, const float* g, const float* gg
  * n_groups (<= 2), then per group: offset_in, offset_out, mul, 2l+1. */
 int e3gnn_gate(int op, int64_t n, const int32_t* dims, const float* y, const float* go,
                const float* q, float* out0, float* out1, float scale, void* stream);
+
+/* The hand-scheduled fine-tune derivatives (train_explicit.py: a tangent
+ * forward along dL/dforces and one reverse sweep replace the double backward
+ * of ForceStressOutputFromEdge, force_output.py:158-215, under the trainer's
+ * loss.backward(), trainer.py:155-222).  e3gnn_act_dual: the reverse of
+ * (y(x), y'(x) xd): og = g y'(x) + gd y''(x) xd, ogd = gd y'(x). */
+int e3gnn_act_dual(int64_t n, const float* x, const float* xd, const float* g, const float* gd,
+                   float* og, float* ogd, float scale, void* stream);
+
+/* Gate of e3gnn_gate, tangent and dual reverse: op 0 out0 = J(y) yd; op 1
+ * out0 = J(y)^T xb + d/dy <xdb, J(y) yd>, out1 = J(y)^T xdb. */
+int e3gnn_gate_dual(int op, int64_t n, const int32_t* dims, const float* y, const float* yd,
+                    const float* xb, const float* xdb, float* out0, float* out1, float scale,
+                    void* stream);
 
 /* ---- device neighbour list (the graph build in front of the hot path) ----
  * Replaces ASE primitive_neighbor_list('ijDS', pbc, cell, pos, cutoff,

@@ -55,6 +55,8 @@ SIGNATURES = {
                                     _vp, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_act': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_f, _vp]),
     'e3gnn_gate': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_f, _vp]),
+    'e3gnn_act_dual': (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_f, _vp]),
+    'e3gnn_gate_dual': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_f, _vp]),
     'e3gnn_d3_create': (_vp, [_c_int, _c_int, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_d3_free': (None, [_vp]),
     'e3gnn_d3_compute': (_c_int, [_vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -367,6 +367,24 @@ class _GateBackward(torch.autograd.Function):
         return dyy, dgo, None, None, None
 
 
+def _act_dual_call(lib, x, xd, g, gd, og, ogd, scale):
+    """e3gnn_act_dual: reverse of (act(x), act'(x) xd) (train_explicit.py)"""
+    c = lambda t: t.contiguous()   # noqa: E731
+    x, xd, g, gd = c(x), c(xd), c(g), c(gd)
+    _lib.check(lib.e3gnn_act_dual(x.numel(), x.data_ptr(), xd.data_ptr(), g.data_ptr(),
+                                  gd.data_ptr(), og.data_ptr(), ogd.data_ptr(), ctypes.c_float(scale),
+                                  torch.cuda.current_stream(x.device).cuda_stream))
+
+
+def _gate_dual_call(lib, op, dims, y, yd, xb=None, xdb=None, out0=None, out1=None, scale=1.0):
+    """e3gnn_gate_dual: op 0 out0 = J yd; op 1 out0 = J^T xb + d/dy <xdb, J yd>,
+    out1 = J^T xdb (train_explicit.py)"""
+    p = lambda t: t.contiguous().data_ptr() if t is not None else None  # noqa: E731
+    _lib.check(lib.e3gnn_gate_dual(op, y.shape[0], dims.ctypes.data, p(y), p(yd), p(xb), p(xdb),
+                                   p(out0), p(out1), ctypes.c_float(scale),
+                                   torch.cuda.current_stream(y.device).cuda_stream))
+
+
 def gate_dims(scal, gated):
     """dims vector of e3gnn_gate for Gate irreps (scalars, gated (mul, l))."""
     import numpy as np

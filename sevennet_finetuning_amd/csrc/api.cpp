@@ -1774,6 +1774,26 @@ int e3gnn_gate(int op, int64_t n, const int32_t* dims, const float* y, const flo
   return E3GNN_OK;
 }
 
+int e3gnn_act_dual(int64_t n, const float* x, const float* xd, const float* g, const float* gd,
+                   float* og, float* ogd, float scale, void* stream) {
+  if (n < 0) return fail(E3GNN_ERR_ARG, "negative size");
+  if (n > 0 && (!x || !xd || !g || !gd || !og || !ogd)) return fail(E3GNN_ERR_ARG, "null act operand");
+  HIPCHK(launch_act_dual(n, x, xd, g, gd, og, ogd, scale, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_gate_dual(int op, int64_t n, const int32_t* dims, const float* y, const float* yd,
+                    const float* xb, const float* xdb, float* out0, float* out1, float scale,
+                    void* stream) {
+  if (op < 0 || op > 1) return fail(E3GNN_ERR_ARG, "gate_dual op must be 0 or 1");
+  if (n < 0 || !dims) return fail(E3GNN_ERR_ARG, "bad gate arguments");
+  if (dims[4] < 0 || dims[4] > 2) return fail(E3GNN_ERR_ARG, "at most two gated irreps");
+  if (n > 0 && (!y || !yd || !out0 || (op == 1 && (!xb || !xdb || !out1))))
+    return fail(E3GNN_ERR_ARG, "null gate operand");
+  HIPCHK(launch_gate_dual(op, n, dims, y, yd, xb, xdb, out0, out1, scale, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
 // ------------------------------------------------------------ neighbour list
 struct e3gnn_nlist {
   int device = 0;

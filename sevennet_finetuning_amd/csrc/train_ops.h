@@ -13,4 +13,12 @@ hipError_t launch_act(int op, int64_t n, const float* x, const float* g, const f
 // dims: ns, ng, din, dout, ngroups, then per group (<= 2): off_in, off_out, mul, 2l+1
 hipError_t launch_gate(int op, int64_t n, const int* dims, const float* y, const float* go,
                        const float* q, float* out0, float* out1, float c, hipStream_t s);
+// reverse of (phi(x), phi'(x) x'): og = g phi' + gd phi'' x', ogd = gd phi'
+hipError_t launch_act_dual(int64_t n, const float* x, const float* xd, const float* g,
+                           const float* gd, float* og, float* ogd, float c, hipStream_t s);
+// gate tangent (op 0: out0 = J y') and the reverse of (G(y), J y') (op 1:
+// out0 = J^T xb + d/dy <xdb, J y'>, out1 = J^T xdb)
+hipError_t launch_gate_dual(int op, int64_t n, const int* dims, const float* y, const float* yd,
+                            const float* xb, const float* xdb, float* out0, float* out1, float c,
+                            hipStream_t s);
 }  // namespace e3gnn

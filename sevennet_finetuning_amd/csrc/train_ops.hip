@@ -39,7 +39,29 @@ __global__ void k_act_bwd2(int64_t n, const float* __restrict__ x, const float* 
   if (dg) dg[i] = a * s * (1.0f + v * (1.0f - s));
 }
 
+// reverse of the pair (phi(x), phi'(x) x') of the hand-scheduled fine-tune
+// derivatives (train_explicit.py): og = g phi'(x) + gd phi''(x) x', ogd = gd phi'(x)
+__global__ void k_act_dual(int64_t n, const float* __restrict__ x, const float* __restrict__ xd,
+                           const float* __restrict__ g, const float* __restrict__ gd,
+                           float* __restrict__ og, float* __restrict__ ogd, float c) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = x[i], s = sig(v);
+  const float d1 = c * s * (1.0f + v * (1.0f - s));
+  const float d2 = c * s * (1.0f - s) * (2.0f + v * (1.0f - 2.0f * s));
+  og[i] = g[i] * d1 + gd[i] * d2 * xd[i];
+  ogd[i] = gd[i] * d1;
+}
+
 }  // namespace
+
+hipError_t launch_act_dual(int64_t n, const float* x, const float* xd, const float* g,
+                           const float* gd, float* og, float* ogd, float c, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_act_dual, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, x, xd, g,
+                     gd, og, ogd, c);
+  return hipGetLastError();
+}
 
 hipError_t launch_act(int op, int64_t n, const float* x, const float* g, const float* gg,
                       float* out0, float* out1, float c, hipStream_t s) {
@@ -171,7 +193,101 @@ __global__ void k_gate_bwd2(int64_t n, GateDims D, const float* __restrict__ y,
   if (dyy) dyy[r * D.din + t] = qg * sgb * d2 + sqb * d1;
 }
 
+// tangent (JVP) of the gate: o' = J(y) y'
+__global__ void k_gate_jvp(int64_t n, GateDims D, const float* __restrict__ y,
+                           const float* __restrict__ yd, float* __restrict__ od, float c) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = D.ns + D.ng;
+  if (tid >= n * per) return;
+  const int64_t r = tid / per;
+  const int t = (int)(tid - r * per);
+  const float* yr = y + r * D.din;
+  const float* ydr = yd + r * D.din;
+  float* orow = od + r * D.dout;
+  float a, d1, d2;
+  act3(yr[t], c, a, d1, d2);
+  if (t < D.ns) {
+    orow[t] = d1 * ydr[t];
+    return;
+  }
+  int grp, k;
+  gate_of(D, t - D.ns, grp, k);
+  const float gd = d1 * ydr[t];
+  const int w = D.gdim[grp];
+  for (int m = 0; m < w; ++m) {
+    const int ii = D.goff_in[grp] + k * w + m, oo = D.goff_out[grp] + k * w + m;
+    orow[oo] = gd * yr[ii] + a * ydr[ii];
+  }
+}
+
+// reverse of (o, o') = (G(y), J(y) y') for the output cotangents (xb, xdb):
+// yb = J^T xb + d/dy <xdb, J(y) y'>,  ydb = J^T xdb
+__global__ void k_gate_dual(int64_t n, GateDims D, const float* __restrict__ y,
+                            const float* __restrict__ yd, const float* __restrict__ xb,
+                            const float* __restrict__ xdb, float* __restrict__ yb,
+                            float* __restrict__ ydb, float c) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = D.ns + D.ng;
+  if (tid >= n * per) return;
+  const int64_t r = tid / per;
+  const int t = (int)(tid - r * per);
+  const float* yr = y + r * D.din;
+  const float* ydr = yd + r * D.din;
+  const float* xr = xb + r * D.dout;
+  const float* xdr = xdb + r * D.dout;
+  float* br = yb + r * D.din;
+  float* bdr = ydb + r * D.din;
+  float a, d1, d2;
+  act3(yr[t], c, a, d1, d2);
+  if (t < D.ns) {
+    br[t] = xr[t] * d1 + xdr[t] * d2 * ydr[t];
+    bdr[t] = xdr[t] * d1;
+    return;
+  }
+  int grp, k;
+  gate_of(D, t - D.ns, grp, k);
+  const float gdot = ydr[t];
+  const int w = D.gdim[grp];
+  float sxb = 0.f, sxdb = 0.f, sxdbd = 0.f;
+  for (int m = 0; m < w; ++m) {
+    const int ii = D.goff_in[grp] + k * w + m, oo = D.goff_out[grp] + k * w + m;
+    const float b = yr[ii], bd = ydr[ii], x0 = xr[oo], x1 = xdr[oo];
+    sxb = fmaf(x0, b, sxb);
+    sxdb = fmaf(x1, b, sxdb);
+    sxdbd = fmaf(x1, bd, sxdbd);
+    br[ii] = a * x0 + x1 * d1 * gdot;
+    bdr[ii] = a * x1;
+  }
+  br[t] = d1 * sxb + d2 * gdot * sxdb + d1 * sxdbd;
+  bdr[t] = d1 * sxdb;
+}
+
 }  // namespace
+
+hipError_t launch_gate_dual(int op, int64_t n, const int* dims, const float* y, const float* yd,
+                            const float* xb, const float* xdb, float* out0, float* out1, float c,
+                            hipStream_t s) {
+  GateDims D{};
+  D.ns = dims[0];
+  D.ng = dims[1];
+  D.din = dims[2];
+  D.dout = dims[3];
+  D.ngrp = dims[4];
+  for (int g = 0; g < 2; ++g) {
+    D.goff_in[g] = dims[5 + 4 * g];
+    D.goff_out[g] = dims[6 + 4 * g];
+    D.gmul[g] = dims[7 + 4 * g];
+    D.gdim[g] = dims[8 + 4 * g];
+  }
+  const int64_t total = n * (D.ns + D.ng);
+  if (total <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  if (op == 0)
+    hipLaunchKernelGGL(k_gate_jvp, grid, block, 0, s, n, D, y, yd, out0, c);
+  else
+    hipLaunchKernelGGL(k_gate_dual, grid, block, 0, s, n, D, y, yd, xb, xdb, out0, out1, c);
+  return hipGetLastError();
+}
 
 hipError_t launch_gate(int op, int64_t n, const int* dims, const float* y, const float* go,
                        const float* q, float* out0, float* out1, float c, hipStream_t s) {

@@ -40,6 +40,10 @@ PER_ATOM_ENERGY = 'per_atom_energy'
 IS_DDP, LOCAL_RANK = 'is_ddp', 'local_rank'
 HIP_GRAPH = 'hip_graph'
 BLAS = 'blas'
+# EXPLICIT_GRAD (this build, default on where it applies): the loss gradient by
+# the hand-scheduled derivatives of train_explicit.py instead of autograd's
+# double backward (same values; a few hundred launches per batch, not thousands)
+EXPLICIT_GRAD = 'explicit_grad'
 
 
 # ------------------------------------------------------------------ losses
@@ -477,6 +481,11 @@ class Trainer:
                 # graphed step's side-stream warm-up or capture
                 loss_def._flat_terms(self.model)
             loss_def.static = self.hip_graph
+        self.explicit = None
+        if bool(config.get(EXPLICIT_GRAD, True)) and hasattr(self.model, 'blocks'):
+            from . import train_explicit
+            if train_explicit.supported(self.model):
+                self.explicit = train_explicit.ExplicitStep(self.model)
         self._graphed = GraphedRehearsalStep(self, config.get('hip_graph_max', 16)) \
             if self.hip_graph else None
 
@@ -495,6 +504,27 @@ class Trainer:
         if self.distributed:
             self.all_reduce_grad()
 
+    def loss_backward(self, batch, graph=None, reduce=True):
+        """Forward, loss, and its parameter gradient accumulated into the
+        model's gradient buffer (+ the data-parallel average when ``reduce``):
+        loss.backward() through the model's autograd graph, or the explicit
+        derivatives (train_explicit.py) -- the loss itself is the same
+        autograd expression on (E, F, S) either way."""
+        if self.explicit is None:
+            output = self.model(batch, graph=graph)
+            loss = self.total_loss(output)
+            loss.backward()
+        else:
+            output = self.explicit.forward(batch, graph)
+            loss = self.total_loss(output)
+            loss.backward()          # cotangents of E, F, S (+ the flat EWC term)
+            S = output.get(KEY.PRED_STRESS)
+            self.explicit.backward(output[KEY.PRED_TOTAL_ENERGY].grad, output[KEY.PRED_FORCE].grad,
+                                   S.grad if S is not None else None)
+        if reduce and self.distributed:
+            self.all_reduce_grad()
+        return loss, output
+
     def all_reduce_grad(self):
         """DDP's gradient average (one all-reduce of the flat gradient buffer)."""
         import torch.distributed as dist
@@ -505,9 +535,7 @@ class Trainer:
     def train_step(self, batch):
         """One optimizer step of Trainer.run_one_epoch (trainer.py:55-68)."""
         self.zero_grad()
-        output = self.model(batch)
-        loss = self.total_loss(output)
-        self.backward(loss)
+        loss, output = self.loss_backward(batch)
         self.optimizer.step()
         return loss.detach(), output
 
@@ -521,13 +549,9 @@ class Trainer:
 
     def _rehearsal_body(self, batch, batch_mem, graphs=(None, None)):
         self.zero_grad()
-        output = self.model(batch, graph=graphs[0])
-        loss = self.total_loss(output)
-        self.backward(loss)
+        loss, _ = self.loss_backward(batch, graphs[0])
         self.optimizer.step()
-        memout = self.model(batch_mem, graph=graphs[1])
-        mem_loss = self.total_loss(memout)
-        self.backward(mem_loss)
+        mem_loss, _ = self.loss_backward(batch_mem, graphs[1])
         self.optimizer.step()
         return loss.detach(), mem_loss.detach()
 
@@ -683,13 +707,11 @@ class GraphedRehearsalStep:
         segs = [torch.cuda.CUDAGraph() for _ in range(3)]
         with torch.cuda.graph(segs[0]):
             tr.zero_grad()
-            loss = tr.total_loss(tr.model(sb, graph=graphs[0]))
-            loss.backward()
+            loss, _ = tr.loss_backward(sb, graphs[0], reduce=False)
         pool = segs[0].pool()
         with torch.cuda.graph(segs[1], pool=pool):
             tr.optimizer.step()
-            mloss = tr.total_loss(tr.model(sm, graph=graphs[1]))
-            mloss.backward()
+            mloss, _ = tr.loss_backward(sm, graphs[1], reduce=False)
         with torch.cuda.graph(segs[2], pool=pool):
             tr.optimizer.step()
         return {'g': segs, 'b': sb, 'm': sm, 'graphs': graphs,

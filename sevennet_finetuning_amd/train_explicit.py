@@ -1,0 +1,627 @@
+"""Hand-scheduled derivatives of the fine-tune step (SURVEY.md §8f row 1,
+BASELINE config 5) -- no autograd graph over the model.
+
+The reference trains with a force loss: ``ForceStressOutputFromEdge`` takes
+F = -dE/dr with ``create_graph=True`` (force_output.py:158-215) and the
+trainer back-propagates the loss through that graph (trainer.py:155-222), a
+second-order derivative that PyTorch's autograd expands into thousands of
+small kernels (the step is launch-bound at the reference's batch sizes).
+Here the same gradient is written out by hand:
+
+  1. primal forward, intermediates kept (SevenNetTrainable.forward's math);
+  2. first reverse (seed dE/d atomic = 1): f_e = dE/dr_e per edge, then
+     forces F and stress S from the edges, as the reference does;
+  3. the loss on (E, F, S) as leaves (the reference's loss definitions,
+     autograd over a few small tensors) gives cE = dL/dE, cF, cS, hence the
+     per-edge cotangent v_e = dL/df_e;
+  4. since  dL/dtheta = sum_g cE_g dE_g/dtheta + d/dtheta <v, dE/dr>  and
+     <v, dE/dr> is the directional derivative of E along v, a TANGENT forward
+     along v (every activation q gets q' = dq/d eps, r -> r + eps v) followed
+     by ONE reverse sweep over the primal+tangent pairs, seeded with cE on E
+     and 1 on E', gives the parameter gradient (reverse-over-forward).
+
+Every bilinear piece has a closed form: linears (e3nn Linear as dense
+matrices, y' = x' W), the scaled-SiLU chain (phi, phi', phi''), the gate
+(J y', J^T x, and the second-order term d/dy <x'bar, J(y) y'>), the edge
+basis / spherical harmonics, and the convolution agg = C(h, Y, w), which is
+trilinear: its tangent is C(h', Y, w) + C(h, Y', w) + C(h, Y, w') and its
+dual reverse four conv backward launches (ExplicitStep.backward).  The conv
+launches are the library's (e3gnn_conv_forward / _backward), the element-wise
+pieces the HIP kernels of train_ops.hip on the GPU (torch on the CPU, where
+the tests compare this module in float64 with autograd of the trainable
+model).
+
+Scope: SevenNet-0's architecture (nn.sevennet0_kinds, linear
+self-connection, XPLOR cutoff, normalised or raw SH, silu gates); other
+members of the family keep the autograd path.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _keys as KEY
+from . import conv_ops
+
+
+def supported(model):
+    """True when the explicit derivatives cover this trainable model."""
+    from .nn import sevennet0_kinds
+    if sevennet0_kinds(model.manifest, conv_only=True) is None:
+        return False
+    if model.sc_type != 'linear' or model.cut.get('name', 'XPLOR') != 'XPLOR':
+        return False
+    if model.lmax_edge != 2 or model.filter_parity != 1:
+        return False
+    for blk in model.blocks:
+        _, scal, gated, (gate_p, _, natural) = blk['gate']
+        if not natural or gate_p != 1 or any(t[2] != 1 for t in scal) or len(gated) > 2:
+            return False
+    return True
+
+
+# ------------------------------------------------------------------ primitives
+class _Prims:
+    """Element-wise primitives: the HIP kernels of train_ops.hip for float32
+    device tensors, torch formulas otherwise (CPU tests, float64)."""
+
+    def __init__(self, model):
+        self.c = float(model.silu_norm)
+        self.lib = model._act_lib() if model.flat.is_cuda else None
+
+    def _hip(self, x):
+        return self.lib is not None and x.is_cuda and x.dtype == torch.float32
+
+    # scaled SiLU: phi = c x s, phi' = c s (1 + x (1 - s)), phi'' = c s (1 - s) (2 + x (1 - 2 s))
+    def _d(self, x):
+        s = torch.sigmoid(x)
+        d1 = self.c * s * (1 + x * (1 - s))
+        d2 = self.c * s * (1 - s) * (2 + x * (1 - 2 * s))
+        return d1, d2
+
+    def act(self, x):
+        if self._hip(x):
+            y = torch.empty_like(x)
+            conv_ops._act_call(self.lib, 0, x, out0=y, scale=self.c)
+            return y
+        return self.c * x * torch.sigmoid(x)
+
+    def act_jvp(self, x, xd):
+        """phi'(x) x'"""
+        if self._hip(x):
+            y = torch.empty_like(x)
+            conv_ops._act_call(self.lib, 1, x, g=xd.contiguous(), out0=y, scale=self.c)
+            return y
+        return self._d(x)[0] * xd
+
+    def act_dual(self, x, xd, g, gd):
+        """reverse of (phi(x), phi'(x) x'): (g phi' + g' phi'' x', g' phi')"""
+        if self._hip(x):
+            o0, o1 = torch.empty_like(x), torch.empty_like(x)
+            conv_ops._act_dual_call(self.lib, x, xd, g, gd, o0, o1, self.c)
+            return o0, o1
+        d1, d2 = self._d(x)
+        return g * d1 + gd * d2 * xd, gd * d1
+
+
+class _Gate:
+    """e3nn Gate of a block in the natural layout [s | g | gated_k], silu
+    (scaled) on scalars and gates: x = [phi(s) | phi(g_k) b_k]."""
+
+    def __init__(self, gate_irreps, prims):
+        _, scal, gated, _ = gate_irreps
+        self.ns = sum(t[0] for t in scal)
+        self.ng = sum(t[0] for t in gated)
+        self.gated = [(t[0], 2 * t[1] + 1) for t in gated]
+        self.p = prims
+        self.dims = conv_ops.gate_dims([t[:2] for t in scal], [t[:2] for t in gated]) if self.ng \
+            else None
+
+    def _split(self, y):
+        s = y[:, :self.ns]
+        g = y[:, self.ns:self.ns + self.ng]
+        blks, off = [], self.ns + self.ng
+        for m, d in self.gated:
+            blks.append(y[:, off:off + m * d].reshape(-1, m, d))
+            off += m * d
+        return s, g, blks
+
+    def _gsplit(self, g):
+        return g.split([m for m, _ in self.gated], dim=1) if len(self.gated) > 1 else (g,)
+
+    def _xsplit(self, x):
+        # output row [s | blocks]
+        out, off = [x[:, :self.ns]], self.ns
+        for m, d in self.gated:
+            out.append(x[:, off:off + m * d].reshape(-1, m, d))
+            off += m * d
+        return out
+
+    def fwd(self, y):
+        p = self.p
+        if not self.ng:
+            return p.act(y)
+        if p._hip(y):
+            o = torch.empty(y.shape[0], int(self.dims[3]), device=y.device)
+            conv_ops._gate_call(p.lib, 0, self.dims, y.contiguous(), out0=o, scale=p.c)
+            return o
+        s, g, blks = self._split(y)
+        ga = self._gsplit(p.act(g))
+        outs = [p.act(s)] + [(a.unsqueeze(-1) * b).reshape(y.shape[0], -1) for a, b in zip(ga, blks)]
+        return torch.cat(outs, 1)
+
+    def vjp(self, y, xb):
+        """J^T x-bar"""
+        p = self.p
+        if not self.ng:
+            return p.act_jvp(y, xb)
+        if p._hip(y):
+            o = torch.empty_like(y)
+            conv_ops._gate_call(p.lib, 1, self.dims, y.contiguous(), go=xb.contiguous(), out0=o,
+                                scale=p.c)
+            return o
+        s, g, blks = self._split(y)
+        xs = self._xsplit(xb)
+        d1g = p._d(g)[0]
+        ga = self._gsplit(p.act(g))
+        gds = self._gsplit(d1g)
+        out = [p.act_jvp(s, xs[0])]
+        gbar = [gd * (xk * b).sum(-1) for gd, xk, b in zip(gds, xs[1:], blks)]
+        out += gbar
+        out += [(a.unsqueeze(-1) * xk).reshape(y.shape[0], -1) for a, xk in zip(ga, xs[1:])]
+        return torch.cat(out, 1)
+
+    def jvp(self, y, yd):
+        """J y'"""
+        p = self.p
+        if not self.ng:
+            return p.act_jvp(y, yd)
+        if p._hip(y):
+            o = torch.empty(y.shape[0], int(self.dims[3]), device=y.device)
+            conv_ops._gate_dual_call(p.lib, 0, self.dims, y, yd, out0=o, scale=p.c)
+            return o
+        s, g, blks = self._split(y)
+        sd, gd, bds = self._split(yd)
+        ga = self._gsplit(p.act(g))
+        gjv = self._gsplit(p.act_jvp(g, gd))
+        outs = [p.act_jvp(s, sd)]
+        for a, aj, b, bd in zip(ga, gjv, blks, bds):
+            outs.append((aj.unsqueeze(-1) * b + a.unsqueeze(-1) * bd).reshape(y.shape[0], -1))
+        return torch.cat(outs, 1)
+
+    def dual_vjp(self, y, yd, xb, xbd):
+        """reverse of (x, x') = (G(y), J(y) y'):
+        y-bar = J^T x-bar + d/dy <x'-bar, J(y) y'>,  y'-bar = J^T x'-bar"""
+        p = self.p
+        if not self.ng:
+            return p.act_dual(y, yd, xb, xbd)
+        if p._hip(y):
+            yb, ydb = torch.empty_like(y), torch.empty_like(y)
+            conv_ops._gate_dual_call(p.lib, 1, self.dims, y, yd, xb, xbd, out0=yb, out1=ydb,
+                                     scale=p.c)
+            return yb, ydb
+        yb = self.vjp(y, xb)
+        ydb = self.vjp(y, xbd)
+        # second-order term
+        s, g, blks = self._split(y)
+        sd, gd, bds = self._split(yd)
+        xs = self._xsplit(xbd)
+        d1s, d2s = p._d(s)
+        d1g, d2g = p._d(g)
+        out = [xs[0] * d2s * sd]
+        d1gs, d2gs, gds = self._gsplit(d1g), self._gsplit(d2g), self._gsplit(gd)
+        gpart, bpart = [], []
+        for d1, d2, gdk, xk, b, bd in zip(d1gs, d2gs, gds, xs[1:], blks, bds):
+            gpart.append(d2 * gdk * (xk * b).sum(-1) + d1 * (xk * bd).sum(-1))
+            bpart.append((xk * (d1 * gdk).unsqueeze(-1)).reshape(y.shape[0], -1))
+        h = torch.cat(out + gpart + bpart, 1)
+        return yb + h, ydb
+
+
+# ------------------------------------------------------------------ edge geometry
+class _Geometry:
+    """r, u, Y = SH(u) (e3nn 'component', lmax 2, of the unit or raw vector;
+    nn.spherical_harmonics) and emb = Bessel(r) * XPLOR(r) (nn._edge_basis),
+    with the tangent along a direction v and the transposes the reverse
+    sweeps need."""
+
+    def __init__(self, model):
+        from .nn import _sh_map
+        self.rc = float(model.cutoff)
+        self.ron = float(model.r_on)
+        self.normalize = bool(model.sh_normalize)
+        self._map = lambda dev, dt: _sh_map(2, dev, dt)   # noqa: E731
+
+    def _env(self, r):
+        rc2, ron2 = self.rc * self.rc, self.ron * self.ron
+        d3 = (rc2 - ron2) ** 3
+        s = torch.clamp(r * r, min=ron2)
+        env = (rc2 - s) ** 2 * (2.0 * s + (rc2 - 3.0 * ron2)) / d3
+        # d env / dr = 6 (rc2 - s)(ron2 - s) / d3 * ds/dr, ds/dr = 2r above r_on, 0 below
+        denv = torch.where(r * r > ron2, 12.0 * r * (rc2 - s) * (ron2 - s) / d3, torch.zeros_like(r))
+        return env, denv
+
+    def forward(self, vec, coeffs):
+        r = torch.linalg.norm(vec, dim=-1)
+        u = vec / r.unsqueeze(-1) if self.normalize else vec
+        mono = torch.cat([torch.ones_like(u[:, :1]), u, (u.unsqueeze(-1) * u.unsqueeze(-2)).reshape(-1, 9)], 1)
+        Y = mono @ self._map(vec.device, vec.dtype)
+        env, denv = self._env(r)
+        cr = coeffs * r.unsqueeze(-1)
+        sn, cs = torch.sin(cr), torch.cos(cr)
+        k = 2.0 / self.rc
+        ur = r.unsqueeze(-1)
+        b = k * sn / ur
+        emb = b * env.unsqueeze(-1)
+        # d emb / dr
+        db = k * (coeffs * cs * ur - sn) / (ur * ur)
+        demb = db * env.unsqueeze(-1) + b * denv.unsqueeze(-1)
+        return {'r': r, 'u': u, 'Y': Y, 'emb': emb, 'demb': demb, 'env': env, 'denv': denv,
+                'sn': sn, 'cs': cs}
+
+    def sh_vjp_u(self, G, u):
+        """dE/du from dE/dY"""
+        gm = G @ self._map(G.device, G.dtype).t()          # E x 13 (monomials)
+        q = gm[:, 4:].reshape(-1, 3, 3)
+        return gm[:, 1:4] + ((q + q.transpose(1, 2)) @ u.unsqueeze(-1)).squeeze(-1)
+
+    def vjp(self, g, Yb, embb):
+        """dE/dvec from dE/dY and dE/demb"""
+        u, r = g['u'], g['r']
+        ub = self.sh_vjp_u(Yb, u)
+        rb = (embb * g['demb']).sum(-1)
+        if self.normalize:
+            uhat = u
+            vb = (ub - uhat * (uhat * ub).sum(-1, keepdim=True)) / r.unsqueeze(-1)
+        else:
+            uhat = u / r.unsqueeze(-1)
+            vb = ub
+        return vb + uhat * rb.unsqueeze(-1)
+
+    def jvp(self, g, v):
+        """(Y', emb') along the direction v"""
+        u, r = g['u'], g['r']
+        uhat = u if self.normalize else u / r.unsqueeze(-1)
+        rd = (uhat * v).sum(-1)
+        ud = (v - uhat * rd.unsqueeze(-1)) / r.unsqueeze(-1) if self.normalize else v
+        quad = (ud.unsqueeze(-1) * u.unsqueeze(-2) + u.unsqueeze(-1) * ud.unsqueeze(-2)).reshape(-1, 9)
+        mono = torch.cat([torch.zeros_like(u[:, :1]), ud, quad], 1)
+        Yd = mono @ self._map(v.device, v.dtype)
+        embd = g['demb'] * rd.unsqueeze(-1)
+        return Yd, embd, rd
+
+    def coeff_grad(self, g, embb, embdb, rd, coeffs):
+        """d/dc of <emb-bar, emb> + <emb'-bar, emb'>"""
+        k = 2.0 / self.rc
+        env, denv = g['env'].unsqueeze(-1), g['denv'].unsqueeze(-1)
+        sn, cs = g['sn'], g['cs']
+        de_dc = k * cs * env
+        ddr_dc = k * (-coeffs * sn * env + cs * denv)
+        return (embb * de_dc + embdb * ddr_dc * rd.unsqueeze(-1)).sum(0)
+
+
+# ------------------------------------------------------------------ dense linears
+class _DenseBank:
+    """Every e3nn Linear of the model as a dense (din x dout) matrix in ONE
+    buffer, built from the flat parameters with one gather / scale / scatter
+    (nn._Linear's dense form), and the map back: flat_grad[u] += alpha *
+    sum over the 2l+1 copies of u of the dense gradient (a padded gather and a
+    row sum -- no atomics, deterministic)."""
+
+    def __init__(self, model, entries):
+        # entries: (key, _Linear, parameter name)
+        self.model = model
+        self.views = {}
+        pos, src, scl, self.shapes = [], [], [], {}
+        off = 0
+        upos, usrc, uscl = [], [], []
+        for key, lin, pname in entries:
+            din, dout = lin.in_off[-1], lin.out_off[-1]
+            poff = model.slices[pname][0]
+            woff = 0
+            for i, j in lin.ins:
+                mi = lin.irreps_in[i][0]
+                mo, d = lin.irreps_out[j][0], 2 * lin.irreps_in[i][1] + 1
+                u, v, m = np.meshgrid(np.arange(mi), np.arange(mo), np.arange(d), indexing='ij')
+                p = off + (lin.in_off[i] + u * d + m) * dout + lin.out_off[j] + v * d + m
+                pos.append(p.ravel())
+                src.append((poff + woff + u * mo + v).ravel())
+                scl.append(np.full(u.size, lin.alpha[j]))
+                # reverse map: flat element (u, v) <- its d dense positions
+                pr = p.reshape(mi * mo, d)
+                pad = np.full((mi * mo, 5), -1, dtype=np.int64)
+                pad[:, :d] = pr
+                upos.append(pad)
+                usrc.append(poff + woff + np.arange(mi * mo))
+                uscl.append(np.full(mi * mo, lin.alpha[j]))
+                woff += mi * mo
+            self.shapes[key] = (off, din, dout)
+            off += din * dout
+        self.total = off
+        dev, dt = model.flat.device, model.flat.dtype
+        self.pos = torch.as_tensor(np.concatenate(pos), device=dev)
+        self.src = torch.as_tensor(np.concatenate(src), device=dev)
+        self.scl = torch.as_tensor(np.concatenate(scl), device=dev, dtype=dt)
+        up = np.concatenate(upos)
+        up[up < 0] = off                    # the zero slot after the buffer
+        self.upos = torch.as_tensor(up, device=dev)
+        self.usrc = torch.as_tensor(np.concatenate(usrc), device=dev)
+        self.uscl = torch.as_tensor(np.concatenate(uscl), device=dev, dtype=dt)
+        self.buf = torch.zeros(off, device=dev, dtype=dt)
+        self.gbuf = torch.zeros(off + 1, device=dev, dtype=dt)
+
+    def build(self):
+        flat = self.model.flat.detach()
+        self.buf.index_put_((self.pos,), flat[self.src] * self.scl)
+        return {k: self.buf[o:o + a * b].view(a, b) for k, (o, a, b) in self.shapes.items()}
+
+    def grads(self):
+        self.gbuf.zero_()
+        return {k: self.gbuf[o:o + a * b].view(a, b) for k, (o, a, b) in self.shapes.items()}
+
+    def flush(self, flat_grad):
+        vals = self.gbuf[self.upos].sum(1) * self.uscl
+        flat_grad.index_add_(0, self.usrc, vals)
+
+
+# ------------------------------------------------------------------ the step
+class ExplicitStep:
+    """Forces, stress and the loss gradient of one batch for a trainable
+    SevenNet-0 (nn.SevenNetTrainable), accumulating dL/dtheta into
+    model.flat_grad.  See the module docstring."""
+
+    def __init__(self, model):
+        if not supported(model):
+            raise ValueError('the explicit fine-tune derivatives cover SevenNet-0\'s architecture only')
+        self.m = model
+        self.p = _Prims(model)
+        self.geo = _Geometry(model)
+        self.gates = [_Gate(b['gate'], self.p) for b in model.blocks]
+        ent = []
+        for t, blk in enumerate(model.blocks):
+            ent += [(f'sc{t}', blk['sc'], f'{t}_self_connection_intro.linear.weight'),
+                    (f'si1{t}', blk['si1'], f'{t}_self_interaction_1.linear.weight'),
+                    (f'si2{t}', blk['si2'], f'{t}_self_interaction_2.linear.weight')]
+        ent += [('r1', model.readout1, 'reduce_input_to_hidden.linear.weight'),
+                ('r2', model.readout2, 'reduce_hidden_to_energy.linear.weight')]
+        self.bank = _DenseBank(model, ent)
+
+    def _P(self, name):
+        return self.m.param(name)
+
+    def _G(self, name):
+        """the gradient view of a parameter (a slice of flat_grad), or None when frozen"""
+        p = self.m.param(name)
+        if not p.requires_grad:
+            return None
+        off, n, shape = self.m.slices[name]
+        return self.m.flat_grad[off:off + n].view(shape)
+
+    # ---------------------------------------------------------------- 1 + 2
+    def forward(self, data, graph=None):
+        """Primal forward and first reverse.  Returns the model's output dict
+        (energy per graph, forces, stress) -- the loss's inputs."""
+        m = self.m
+        dev = m.flat.device
+        types = data[KEY.NODE_FEATURE].to(dev).long()
+        n = int(types.shape[0])
+        ei = data[KEY.EDGE_IDX].to(dev).long()
+        vec = data[KEY.EDGE_VEC].to(dev, m.dtype).detach()
+        batch = data[KEY.BATCH].to(dev).long() if KEY.BATCH in data else \
+            torch.zeros(n, dtype=torch.long, device=dev)
+        nb = int(data[KEY.NUM_ATOMS].numel()) if KEY.NUM_ATOMS in data else 1
+        center, nbr = ei[0], ei[1]
+        perm = None
+        if graph is None:
+            if center.numel() > 1 and bool((center[1:] < center[:-1]).any()):
+                perm = torch.argsort(center, stable=True)
+                center, nbr = center[perm], nbr[perm]
+            graph = conv_ops.ConvGraph(n, center, nbr, m.conv_backend)
+        vec_k = vec[perm] if perm is not None else vec
+        S = self.S = {'n': n, 'nb': nb, 'types': types, 'batch': batch, 'center': center,
+                      'nbr': nbr, 'graph': graph, 'vec': vec_k}
+        coeffs = self._P('edge_embedding.basis_function.coeffs').detach()
+        g = self.geo.forward(vec_k, coeffs)
+        S['geo'] = g
+        D = S['D'] = self.bank.build()
+        P = lambda name: self._P(name).detach()   # noqa: E731
+        x = P('onehot_to_feature_x.linear.weight').view(m.nsp, -1)[types] / math.sqrt(m.nsp)
+        blocks = []
+        be = m.conv_backend
+        for t, blk in enumerate(m.blocks):
+            pre = f'{t}_convolution'
+            b = {'x': x}
+            sc = x @ D[f'sc{t}']
+            h = x @ D[f'si1{t}']
+            w0 = P(f'{pre}.weight_nn.layer0.weight')
+            w1 = P(f'{pre}.weight_nn.layer1.weight')
+            w2 = P(f'{pre}.weight_nn.layer2.weight')
+            W0 = w0 / math.sqrt(w0.shape[0])
+            W1 = w1 / math.sqrt(w1.shape[0])
+            W2 = w2 / math.sqrt(w2.shape[0])
+            a1 = g['emb'] @ W0
+            h1 = self.p.act(a1)
+            a2 = h1 @ W1
+            h2 = self.p.act(a2)
+            w = h2 @ W2
+            den = P(f'{pre}.denominator')
+            agg = be.forward(blk['kind'], graph, h, g['Y'], w)
+            aggs = agg / den
+            y = torch.addmm(sc, aggs, D[f'si2{t}'])
+            b.update(h=h, a1=a1, h1=h1, a2=a2, h2=h2, w=w, W=(W0, W1, W2), den=den, aggs=aggs, y=y)
+            x = self.gates[t].fwd(y)
+            blocks.append(b)
+        S['blocks'] = blocks
+        S['xL'] = x
+        hid = x @ D['r1']
+        e = (hid @ D['r2'])[:, 0]
+        scale = P('rescale_atomic_energy.scale')[types]
+        atomic = e * scale + P('rescale_atomic_energy.shift')[types]
+        S.update(hid=hid, e=e, scale=scale)
+        energy = torch.zeros(nb, device=dev, dtype=atomic.dtype).index_add(0, batch, atomic)
+
+        # ---- first reverse: dE/dr per edge (seed dE/d atomic = 1)
+        xb = (scale.unsqueeze(-1) * D['r2'][:, 0].unsqueeze(0)) @ D['r1'].t()
+        Yb = torch.zeros_like(g['Y'])
+        embb = torch.zeros_like(g['emb'])
+        for t in range(len(blocks) - 1, -1, -1):
+            b, blk = blocks[t], m.blocks[t]
+            yb = self.gates[t].vjp(b['y'], xb)
+            ab = (yb @ D[f'si2{t}'].t()) / b['den']
+            hb, dY, wb = be.backward(blk['kind'], graph, b['h'], g['Y'], b['w'], ab, need_h=t > 0)
+            Yb += dY
+            W0, W1, W2 = b['W']
+            h1b = self.p.act_jvp(b['a2'], wb @ W2.t())
+            a1b = self.p.act_jvp(b['a1'], h1b @ W1.t())
+            embb += a1b @ W0.t()
+            if t > 0:
+                xb = torch.addmm(hb @ D[f'si1{t}'].t(), yb, D[f'sc{t}'].t())
+        fij = self.geo.vjp(g, Yb, embb)                    # dE/dr_e, centre-sorted order
+        S['fij'] = fij
+        force = torch.zeros(n, 3, device=dev, dtype=fij.dtype).index_add(
+            0, torch.cat([center, nbr]), torch.cat([fij, -fij]))
+        voigt = vec_k.repeat(1, 2) * torch.cat([fij, fij.roll(-1, dims=1)], dim=1)
+        s_graph = torch.zeros(nb, 6, device=dev, dtype=fij.dtype).index_add(0, batch[nbr], voigt)
+        out = dict(data)
+        out[KEY.ATOMIC_ENERGY] = atomic.unsqueeze(-1)
+        out[KEY.PRED_TOTAL_ENERGY] = energy.requires_grad_(True)
+        out[KEY.PRED_FORCE] = force.requires_grad_(True)
+        if KEY.CELL_VOLUME in data:
+            vol = data[KEY.CELL_VOLUME].to(dev, m.dtype).view(-1)
+            S['vol'] = vol
+            out[KEY.PRED_STRESS] = (torch.neg(s_graph) / vol.unsqueeze(-1)).detach().requires_grad_(True)
+        self.out = out
+        return out
+
+    # ---------------------------------------------------------------- 4
+    def backward(self, cE, cF, cS=None):
+        """Accumulate dL/dtheta into model.flat_grad from the loss cotangents
+        of the energies (per graph), forces and stress (per graph, or None)."""
+        m, S = self.m, self.S
+        D, g = S['D'], S['geo']
+        types, batch, center, nbr = S['types'], S['batch'], S['center'], S['nbr']
+        be, graph = m.conv_backend, S['graph']
+        dt = m.dtype
+        cE = cE.to(dt) if cE is not None else torch.zeros(S['nb'], device=types.device, dtype=dt)
+        cF = cF.to(dt) if cF is not None else torch.zeros(S['n'], 3, device=types.device, dtype=dt)
+        # v_e = dL/df_e: forces F_i = sum_{centre i} f_e - sum_{nbr i} f_e, stress from the edges
+        v = cF[center] - cF[nbr]
+        if cS is not None:
+            vol = S['vol']
+            c = cS.to(dt)[batch[nbr]] / vol[batch[nbr]].unsqueeze(-1)
+            r = S['vec']
+            v = v - torch.stack([c[:, 0] * r[:, 0] + c[:, 5] * r[:, 2],
+                                 c[:, 1] * r[:, 1] + c[:, 3] * r[:, 0],
+                                 c[:, 2] * r[:, 2] + c[:, 4] * r[:, 1]], 1)
+        # ---- tangent forward along v
+        Yd, embd, rd = self.geo.jvp(g, v)
+        blocks = S['blocks']
+        xd = None
+        for t, blk in enumerate(m.blocks):
+            b = blocks[t]
+            W0, W1, W2 = b['W']
+            a1d = embd @ W0
+            h1d = self.p.act_jvp(b['a1'], a1d)
+            a2d = h1d @ W1
+            h2d = self.p.act_jvp(b['a2'], a2d)
+            wd = h2d @ W2
+            aggd = be.forward(blk['kind'], graph, b['h'], Yd, b['w']) + \
+                be.forward(blk['kind'], graph, b['h'], g['Y'], wd)
+            hd = None
+            if xd is not None:
+                hd = xd @ D[f'si1{t}']
+                aggd = aggd + be.forward(blk['kind'], graph, hd, g['Y'], b['w'])
+            aggsd = aggd / b['den']
+            yd = aggsd @ D[f'si2{t}']
+            if xd is not None:
+                yd = torch.addmm(yd, xd, D[f'sc{t}'])
+            b.update(a1d=a1d, h1d=h1d, a2d=a2d, h2d=h2d, wd=wd, hd=hd, aggsd=aggsd, yd=yd, xd=xd)
+            xd = self.gates[t].jvp(b['y'], yd)
+        hidd = xd @ D['r1']
+        ed = (hidd @ D['r2'])[:, 0]
+
+        # ---- one reverse sweep over (primal, tangent); seeds cE on E, 1 on E'
+        G = self.bank.grads()
+        scale = S['scale']
+        atb = cE[batch]                       # d L / d atomic
+        eb = atb * scale
+        edb = scale                           # seed 1 on sum of atomic'
+        gsc = self._G('rescale_atomic_energy.scale')
+        if gsc is not None:
+            gsc.index_add_(0, types, atb * S['e'] + ed)
+        gsh = self._G('rescale_atomic_energy.shift')
+        if gsh is not None:
+            gsh.index_add_(0, types, atb)
+        hid = S['hid']
+        G['r2'].addmm_(hid.t(), eb.unsqueeze(-1)).addmm_(hidd.t(), edb.unsqueeze(-1))
+        r2 = D['r2'][:, 0].unsqueeze(0)
+        hidb = eb.unsqueeze(-1) * r2
+        hiddb = edb.unsqueeze(-1) * r2
+        G['r1'].addmm_(S['xL'].t(), hidb).addmm_(xd.t(), hiddb)
+        xb = hidb @ D['r1'].t()
+        xdb = hiddb @ D['r1'].t()
+        embb = torch.zeros_like(g['emb'])
+        embdb = torch.zeros_like(g['emb'])
+        for t in range(len(blocks) - 1, -1, -1):
+            b, blk = blocks[t], m.blocks[t]
+            k = blk['kind']
+            pre = f'{t}_convolution'
+            yb, ydb = self.gates[t].dual_vjp(b['y'], b['yd'], xb, xdb)
+            G[f'si2{t}'].addmm_(b['aggs'].t(), yb).addmm_(b['aggsd'].t(), ydb)
+            aggsb = yb @ D[f'si2{t}'].t()
+            aggsdb = ydb @ D[f'si2{t}'].t()
+            gden = self._G(f'{pre}.denominator')
+            if gden is not None:
+                gden.sub_(((aggsb * b['aggs']).sum() + (aggsdb * b['aggsd']).sum()) / b['den'])
+            ab = aggsb / b['den']
+            adb = aggsdb / b['den']
+            h, w, Y = b['h'], b['w'], g['Y']
+            # trilinear agg = C(h, Y, w): B(h', Y', w'; c) = (B_h(Y', w'), B_Y(h', w'), B_w(h', Y'))
+            hb, _, wb = be.backward(k, graph, h, Y, w, ab)                  # B_h(Y,w;a), B_w(h,Y;a)
+            t_h, _, t_w = be.backward(k, graph, h, Yd, w, adb)              # B_h(Y',w), B_w(h,Y')
+            hb, wb = hb + t_h, wb + t_w
+            t_h, _, wdb = be.backward(k, graph, h, Y, b['wd'], adb)         # B_h(Y,w'), B_w(h,Y) = w'-bar
+            hb = hb + t_h
+            hdb = None
+            if b['hd'] is not None:
+                hdb, _, t_w = be.backward(k, graph, b['hd'], Y, w, adb)    # B_h(Y,w) = h'-bar, B_w(h',Y)
+                wb = wb + t_w
+            # radial MLP
+            W0, W1, W2 = b['W']
+            gw2 = self._G(f'{pre}.weight_nn.layer2.weight')
+            s2 = 1.0 / math.sqrt(W2.shape[0])
+            if gw2 is not None:
+                gw2.addmm_(b['h2'].t(), wb, alpha=s2).addmm_(b['h2d'].t(), wdb, alpha=s2)
+            h2b, h2db = wb @ W2.t(), wdb @ W2.t()
+            a2b, a2db = self.p.act_dual(b['a2'], b['a2d'], h2b, h2db)
+            gw1 = self._G(f'{pre}.weight_nn.layer1.weight')
+            s1 = 1.0 / math.sqrt(W1.shape[0])
+            if gw1 is not None:
+                gw1.addmm_(b['h1'].t(), a2b, alpha=s1).addmm_(b['h1d'].t(), a2db, alpha=s1)
+            h1b, h1db = a2b @ W1.t(), a2db @ W1.t()
+            a1b, a1db = self.p.act_dual(b['a1'], b['a1d'], h1b, h1db)
+            gw0 = self._G(f'{pre}.weight_nn.layer0.weight')
+            s0 = 1.0 / math.sqrt(W0.shape[0])
+            if gw0 is not None:
+                gw0.addmm_(g['emb'].t(), a1b, alpha=s0).addmm_(embd.t(), a1db, alpha=s0)
+            embb += a1b @ W0.t()
+            embdb += a1db @ W0.t()
+            # self-interaction 1 and self-connection (sc-bar = y-bar)
+            x = b['x']
+            G[f'si1{t}'].addmm_(x.t(), hb)
+            G[f'sc{t}'].addmm_(x.t(), yb)
+            if b['xd'] is not None:
+                G[f'si1{t}'].addmm_(b['xd'].t(), hdb)
+                G[f'sc{t}'].addmm_(b['xd'].t(), ydb)
+            xb = torch.addmm(hb @ D[f'si1{t}'].t(), yb, D[f'sc{t}'].t())
+            xdb = torch.addmm(hdb @ D[f'si1{t}'].t(), ydb, D[f'sc{t}'].t()) \
+                if hdb is not None else None
+        # embedding (x0 = W[types] / sqrt(nsp)) and the radial basis coefficients
+        gemb = self._G('onehot_to_feature_x.linear.weight')
+        if gemb is not None:
+            gemb.view(m.nsp, -1).index_add_(0, types, xb / math.sqrt(m.nsp))
+        gco = self._G('edge_embedding.basis_function.coeffs')
+        if gco is not None:
+            coeffs = self._P('edge_embedding.basis_function.coeffs').detach()
+            gco.add_(self.geo.coeff_grad(g, embb, embdb, rd, coeffs))
+        self.bank.flush(m.flat_grad)

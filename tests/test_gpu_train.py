@@ -160,6 +160,81 @@ def test_force_loss_parameter_gradients_vs_fp64(models):
         assert float((g32[off:off + n] - ref).norm() / ref.norm()) < 1e-3, name
 
 
+def test_explicit_step_gradients_vs_fp64(models):
+    """The hand-scheduled derivatives (train_explicit.py: first reverse for
+    the forces, tangent forward along dL/dF, one reverse sweep) on the HIP
+    kernels -- the Trainer's default path -- against float64 autograd of the
+    same loss; plus the dual act / gate kernels against their torch forms."""
+    from sevennet_finetuning_amd.train_explicit import ExplicitStep, _Gate, _Prims
+    m32, m64 = models
+    cfg = {'loss': 'huber', 'loss_param': {'delta': 0.01}, 'force_loss_weight': 1.0,
+           'stress_loss_weight': 1e-2, 'is_train_stress': True,
+           'continue': {'fisher_information': False, 'opt_params': False}}
+    fns = train.get_loss_functions_from_config(cfg)
+    gs = _batch([8, 9])
+    step = ExplicitStep(m32)
+    m32.zero_grad()
+    out = step.forward(train.collate(gs, device=DEV, dtype=torch.float32))
+    loss = sum(f.get_loss(out, m32) * w for f, w in fns)
+    loss.backward()
+    step.backward(out[KEY.PRED_TOTAL_ENERGY].grad, out[KEY.PRED_FORCE].grad,
+                  out[KEY.PRED_STRESS].grad)
+    g32 = m32.flat_grad.detach().cpu().double().clone()
+    m64.train(True)
+    m64.zero_grad()
+    o64 = m64(train.collate(gs, dtype=torch.float64))
+    sum(f.get_loss(o64, m64) * w for f, w in fns).backward()
+    m64.train(False)
+    g64 = m64.flat_grad.detach().clone()
+    assert float((out[KEY.PRED_FORCE].detach().cpu().double() - o64[KEY.PRED_FORCE]).abs().max()) < 1e-4
+    assert float((g32 - g64).norm() / g64.norm()) < 1e-4
+    for name, (off, n, _) in m64.slices.items():
+        ref = g64[off:off + n]
+        if float(ref.abs().max()) == 0.0:
+            assert float(g32[off:off + n].abs().max()) == 0.0, name
+            continue
+        assert float((g32[off:off + n] - ref).norm() / ref.norm()) < 1e-3, name
+    # the dual kernels against the torch forms of the same module
+    torch.manual_seed(0)
+    p = _Prims(m32)
+    x, xd, g, gd = (torch.randn(1000, device=DEV) for _ in range(4))
+    a0, a1 = p.act_dual(x, xd, g, gd)
+    d1, d2 = p._d(x)
+    assert torch.allclose(a0, g * d1 + gd * d2 * xd, atol=1e-5) and torch.allclose(a1, gd * d1, atol=1e-5)
+    gate = _Gate(m32.blocks[1]['gate'], p)
+    y, yd = torch.randn(50, 576, device=DEV), torch.randn(50, 576, device=DEV)
+    xb, xdb = torch.randn(50, 480, device=DEV), torch.randn(50, 480, device=DEV)
+    lib, gate.p.lib = gate.p.lib, None          # torch forms
+    ref_jvp, ref_dual = gate.jvp(y, yd), gate.dual_vjp(y, yd, xb, xdb)
+    gate.p.lib = lib
+    assert torch.allclose(gate.jvp(y, yd), ref_jvp, atol=1e-5)
+    got = gate.dual_vjp(y, yd, xb, xdb)
+    assert torch.allclose(got[0], ref_dual[0], atol=1e-4) and torch.allclose(got[1], ref_dual[1], atol=1e-5)
+
+
+def test_explicit_and_autograd_trainers_take_the_same_step(models):
+    """Trainer with explicit_grad (default) and with autograd: one rehearsal
+    step (SGD: the update is the gradient) from the same parameters makes the
+    same parameter change."""
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    cfg = {'loss': 'mse', 'force_loss_weight': 0.5, 'stress_loss_weight': 1e-3,
+           'is_train_stress': True, 'optimizer': 'sgd', 'optim_param': {'lr': 1e-3},
+           'scheduler': 'exponentiallr', 'scheduler_param': {'gamma': 0.99},
+           'continue': {'fisher_information': False, 'opt_params': False}}
+    b = train.collate(_batch([11, 12]), device=DEV, dtype=torch.float32)
+    mem = train.collate(_batch([13]), device=DEV, dtype=torch.float32)
+    deltas = []
+    for explicit in (True, False):
+        m = SevenNetTrainable(device=DEV)
+        before = m.flat.detach().clone()
+        tr = train.Trainer(m, dict(cfg, explicit_grad=explicit))
+        assert (tr.explicit is not None) == explicit
+        tr.rehearsal_step(b, mem)
+        deltas.append((m.flat.detach() - before).double())
+    assert float(deltas[1].norm()) > 0
+    assert float((deltas[0] - deltas[1]).norm() / deltas[1].norm()) < 1e-4
+
+
 def test_rehearsal_ewc_steps_reduce_loss(models):
     """A few rehearsal+EWC Adam steps (the reference's FT_w_reEWC recipe,
     Huber delta 0.01) on fixed batches lower the data loss of both batches,

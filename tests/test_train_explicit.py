@@ -1,0 +1,110 @@
+"""The hand-scheduled fine-tune derivatives (train_explicit.py) against
+autograd of the trainable model, float64 on the CPU (conv op: the oracle's
+tensor product, _conv_cpu.py).
+
+The explicit step computes forces / stress by a first reverse and the
+parameter gradient of the loss (energy + force + stress terms, the
+second-order derivative of force_output.py:158-215 under trainer.py:155-222)
+by a tangent forward along dL/df and one reverse sweep; autograd of
+nn.SevenNetTrainable (itself pinned against the fp64 oracle in
+test_train.py) differentiates the same loss with create_graph.  Every
+trainable parameter (incl. shift/scale, denominators, Bessel coefficients)
+must agree to float64 round-off."""
+import numpy as np
+import pytest
+import torch
+
+from _conv_cpu import CpuConvBackend
+from _systems import load_manifest_symbols
+from sevennet_finetuning_amd import _keys as KEY
+from sevennet_finetuning_amd import train
+from sevennet_finetuning_amd.nn import SevenNetTrainable
+from sevennet_finetuning_amd.structures import diamond_primitive, mixed_symbols
+
+SYMS = load_manifest_symbols()
+
+
+@pytest.fixture(scope='module')
+def model():
+    return SevenNetTrainable(device='cpu', conv_backend=CpuConvBackend(), dtype=torch.float64,
+                             train_shift_scale=True, train_denominator=True)
+
+
+def _batch(seeds=(0, 1), cells=(2, 2, 1)):
+    gs = []
+    for s in seeds:
+        pos, cell = diamond_primitive(cells, sigma=0.08, seed=s)
+        types = np.array([SYMS.index(x) for x in mixed_symbols(len(pos), seed=s + 1)])
+        rng = np.random.default_rng(50 + s)
+        gs.append(train.labeled_graph(pos, cell, types, 5.0, energy=-4.0 * len(pos),
+                                      force=rng.normal(size=(len(pos), 3)),
+                                      stress=rng.normal(size=6) * 1e-2))
+    return train.collate(gs, dtype=torch.float64)
+
+
+def _losses(kind):
+    cfg = {'loss': kind, 'force_loss_weight': 0.7, 'stress_loss_weight': 0.05,
+           'is_train_stress': True, 'continue': {'fisher_information': False, 'opt_params': False}}
+    if kind == 'huber':
+        cfg['loss_param'] = {'delta': 0.05}
+    return train.get_loss_functions_from_config(cfg)
+
+
+def _autograd(model, batch, fns):
+    model.train(True)
+    model.zero_grad()
+    out = model(batch)
+    loss = sum(f.get_loss(out, model) * w for f, w in fns)
+    loss.backward()
+    model.train(False)
+    return out, float(loss), model.flat_grad.clone()
+
+
+def _explicit(model, batch, fns):
+    from sevennet_finetuning_amd.train_explicit import ExplicitStep
+    step = ExplicitStep(model)
+    model.zero_grad()
+    out = step.forward(batch)
+    loss = sum(f.get_loss(out, model) * w for f, w in fns)
+    leaves = [out[KEY.PRED_TOTAL_ENERGY], out[KEY.PRED_FORCE], out[KEY.PRED_STRESS]]
+    cE, cF, cS = torch.autograd.grad(loss, leaves, allow_unused=True)
+    step.backward(cE, cF, cS)
+    return out, float(loss), model.flat_grad.clone()
+
+
+@pytest.mark.parametrize('kind', ['mse', 'huber'])
+def test_explicit_gradient_equals_autograd(model, kind):
+    batch = _batch()
+    fns = _losses(kind)
+    oa, la, ga = _autograd(model, batch, fns)
+    oe, le, ge = _explicit(model, batch, fns)
+    for k in (KEY.PRED_TOTAL_ENERGY, KEY.PRED_FORCE, KEY.PRED_STRESS):
+        assert torch.allclose(oe[k].detach(), oa[k].detach(), rtol=1e-11, atol=1e-12), k
+    assert abs(le - la) <= 1e-11 * abs(la)
+    scale = ga.abs().max()
+    bad = {}
+    for name, (off, n, _) in model.slices.items():
+        d = (ge[off:off + n] - ga[off:off + n]).abs().max()
+        if d > 1e-9 * scale:
+            bad[name] = (float(d), float(ga[off:off + n].abs().max()))
+    assert not bad, bad
+    assert float(ga.abs().sum()) > 0
+
+
+def test_explicit_gradient_unsorted_edges_and_frozen_parameters():
+    """Edges not centre-sorted (the step sorts them as the model does) and the
+    default trainability (shift/scale and denominators frozen)."""
+    m = SevenNetTrainable(device='cpu', conv_backend=CpuConvBackend(), dtype=torch.float64)
+    batch = _batch(seeds=(3,))
+    perm = torch.randperm(batch[KEY.EDGE_IDX].shape[1], generator=torch.Generator().manual_seed(0))
+    for k in (KEY.EDGE_IDX,):
+        batch[k] = batch[k][:, perm]
+    for k in (KEY.EDGE_VEC, KEY.CELL_SHIFT):
+        if k in batch:
+            batch[k] = batch[k][perm]
+    fns = _losses('mse')
+    _, _, ga = _autograd(m, batch, fns)
+    _, _, ge = _explicit(m, batch, fns)
+    assert torch.allclose(ge, ga, rtol=1e-9, atol=1e-9 * float(ga.abs().max()))
+    off, n, _ = m.slices['rescale_atomic_energy.scale']
+    assert float(ge[off:off + n].abs().max()) == 0.0

@@ -41,6 +41,9 @@ for s in "$@"; do
     benchtrain) step benchtrain 300 python bench_train.py --steps 10 --warmup 3 ;;
     benchtrain2) step benchtrain2 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchtrainblk) step benchtrainblk 300 env E3GNN_TRAIN_DENSE_LINEAR=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    benchtrainag) step benchtrainag 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline --autograd ;;
+    proftrainx) step proftrainx 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trainx -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    fullsize2) step fullsize2 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 600 --timeout-method thread -k edge_gradients ;;
     benchtraineager) step benchtraineager 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline --eager ;;
     benchd3) step benchd3 300 python bench_d3.py ;;
     profd3) step profd3 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_d3 -o run --output-format csv -- python bench_d3.py --no-cpu-baseline && mkdir -p gpurun_out/prof_d3 && cp /tmp/prof_d3/*/*stats* /tmp/prof_d3/*stats* gpurun_out/prof_d3/ 2>/dev/null; ls gpurun_out/prof_d3 ;;
