@@ -99,7 +99,7 @@ def _pair_check(model_dir, path, grid, *extra):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def _check_pair_run(out, grid, kat_energy, n_atoms):
+def _check_pair_run(out, grid, kat_energy, n_atoms, thin=True):
     """Both pair styles against the reference KAT, the library's own
     evaluation and each other; the CommBrick machinery actually exercised."""
     assert out['n_atoms'] == n_atoms and out['ranks'] == int(np.prod(grid))
@@ -121,10 +121,12 @@ def _check_pair_run(out, grid, kat_energy, n_atoms):
     else:
         assert c['swaps'] == 2 * split * int(np.prod(grid)), c
         assert c['extra_rows'] > 0, c     # received ghosts outside the graph (cutoff < ghost cutoff)
-        assert c['zero_sends'] > 0, c     # one atom received by one rank in both swaps of a dimension
+        if thin:   # bricks narrower than two ghost cutoffs: an atom sent in both swaps of a dimension
+            assert c['zero_sends'] > 0, c
     if split >= 2:
         assert c['relayed'] > 0, c        # corner atoms forwarded in a later dimension
-        assert c['trash_forward'] > 0 and c['trash_reverse'] > 0, c   # images relayed in one swap
+        if thin:   # two images of one atom relayed in one swap
+            assert c['trash_forward'] > 0 and c['trash_reverse'] > 0, c
 
 
 PAIR_GRIDS = [(1, 1, 1), (2, 1, 1), (2, 2, 1), (2, 2, 2)]
@@ -171,7 +173,8 @@ def test_lammps_pair_styles_hfo2_kat(grid, tmp_path):
     path = tmp_path / 'hfo2_221.txt'
     _write_structure(path, pos, cell, [str(s) for s in d['symbols']] * 4)
     out = _pair_check(HFO2, path, grid)
-    _check_pair_run(out, grid, 4 * KATS['kats_hfo2_example']['energy'], 384)
+    # bricks of ~10 A = two ghost cutoffs (4 + 1 A): no atom is sent both ways
+    _check_pair_run(out, grid, 4 * KATS['kats_hfo2_example']['energy'], 384, thin=False)
 
 
 
