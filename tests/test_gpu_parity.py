@@ -324,11 +324,30 @@ def raw_sh_dir(tmp_path_factory):
     import shutil
     src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                        'sevennet_finetuning_amd', 'assets', 'sevennet0')
+    from sevennet_finetuning_amd.nn import conv_instructions, parse_irreps
     d = tmp_path_factory.mktemp('sevennet0_raw_sh')
-    shutil.copy(os.path.join(src, 'weights.bin'), d / 'weights.bin')
     man = json.load(open(os.path.join(src, 'manifest.json')))
     man['sh_normalize'] = False
     json.dump(man, open(d / 'manifest.json', 'w'))
+    # SevenNet-0's weights with the radial weights of every l2 = 1, 2 path
+    # divided by r0^l2 (r0 = 3.5 A, a typical neighbour distance): Y_l(r) =
+    # |r|^l Y_l(r/|r|), so the messages keep the trained model's magnitude and
+    # the outputs stay physical (forces of a few eV/A) -- what a checkpoint
+    # trained on raw-vector SH looks like
+    flat = np.fromfile(os.path.join(src, 'weights.bin'), dtype='<f4').copy()
+    tens = {t['name']: t for t in man['tensors']}
+    irr = [parse_irreps(x) for x in man['irreps_manual']]
+    r0 = 3.5
+    for t in range(int(man['num_convolution_layer'])):
+        ins, _, _ = conv_instructions(irr[t], 2, 1, irr[t + 1])
+        w2 = tens[f'{t}_convolution.weight_nn.layer2.weight']
+        W = flat[w2['offset']:w2['offset'] + w2['numel']].reshape(w2['shape'])
+        col = 0
+        for (_, l2, _, _, mul) in ins:
+            W[:, col:col + mul] /= r0 ** l2
+            col += mul
+        assert col == W.shape[1]
+    flat.tofile(d / 'weights.bin')
     return str(d)
 
 
@@ -355,12 +374,8 @@ def test_raw_vector_sh_on_the_fused_kernels(raw_sh_dir, model, name):
     ref = ref_m(torch.tensor(pos), torch.tensor(types), torch.tensor(ei), torch.tensor(sh),
                 torch.tensor(cell))
     assert abs(got['energy'] - float(ref['energy'])) <= E_RTOL * abs(float(ref['energy']))
-    # SevenNet-0's weights on raw-vector SH (|Y_2| ~ r^2 larger) give forces of
-    # ~100 eV/A: the north-star 1e-4 eV/A bar is applied relative to that scale
-    f_ref, s_ref = ref['forces'].numpy(), ref['stress'].numpy()
-    fscale = max(1.0, float(np.abs(f_ref).max()))
-    assert np.abs(got['forces'] - f_ref).max() <= F_TOL * fscale
-    assert np.abs(got['stress'] - s_ref).max() <= S_TOL * max(1.0, float(np.abs(s_ref).max()) / 1e-2)
+    assert np.abs(got['forces'] - ref['forces'].numpy()).max() <= F_TOL
+    assert np.abs(got['stress'] - ref['stress'].numpy()).max() <= S_TOL
     # the flag matters: the normalised model gives another energy
     norm = run(model, pos, cell, types)
     assert abs(norm['energy'] - got['energy']) > 1e-3
