@@ -101,17 +101,20 @@ class HipConvBackend:
                 raise _lib.E3GNNError(f'conv kind {kind}: {name} must be float32 {shape} on '
                                       f'the GPU, got {t.dtype} {tuple(t.shape)} on {t.device}')
 
-    def forward(self, kind, g, h, Y, w):
+    def forward(self, kind, g, h, Y, w, out=None):
         self._check(kind, g, h, Y, w)
         h, Y, w = h.contiguous(), Y.contiguous(), w.contiguous()
-        agg = torch.empty(g.n_nodes, self.dims[kind][2], device=h.device)
+        agg = _out(out, (g.n_nodes, self.dims[kind][2]), h.device)
         a = g.aux
         _lib.check(self.lib.e3gnn_conv_forward(
             kind, g.n_nodes, a['row_ptr'].data_ptr(), a['nbr'].data_ptr(), h.data_ptr(),
             Y.data_ptr(), w.data_ptr(), agg.data_ptr(), self._stream(h)))
         return agg
 
-    def backward(self, kind, g, h, Y, w, gagg, need_h=True):
+    def backward(self, kind, g, h, Y, w, gagg, need_h=True, dh_out=None, dw_out=None):
+        """(dh, dY, dw); ``dh_out`` / ``dw_out``: contiguous float32 buffers
+        of the right shape to write dh / dw into (the explicit fine-tune
+        derivatives stack primal and tangent rows)"""
         self._check(kind, g, h, Y, w)
         dx, dwd, dm = self.dims[kind]
         h, Y, w = h.contiguous(), Y.contiguous(), w.contiguous()
@@ -121,8 +124,8 @@ class HipConvBackend:
         dev = h.device
         E = g.n_edges
         dY = torch.empty(E, 9, device=dev)
-        dw = torch.empty(E, dwd, device=dev)
-        dh = torch.empty(g.n_nodes, dx, device=dev) if need_h else None
+        dw = _out(dw_out, (E, dwd), dev)
+        dh = _out(dh_out, (g.n_nodes, dx), dev) if need_h else None
         dxc = torch.empty(E, dx, device=dev) if need_h and E else None
         a = g.aux
         _lib.check(self.lib.e3gnn_conv_backward(
@@ -132,6 +135,16 @@ class HipConvBackend:
             dY.data_ptr(), dw.data_ptr(), dxc.data_ptr() if dxc is not None else None,
             self._stream(h)))
         return dh, dY, dw
+
+
+def _out(buf, shape, device):
+    """a caller's output buffer (checked), or a new one"""
+    if buf is None:
+        return torch.empty(*shape, device=device)
+    if tuple(buf.shape) != tuple(shape) or buf.dtype != torch.float32 or not buf.is_contiguous():
+        raise _lib.E3GNNError(f'output buffer must be contiguous float32 {tuple(shape)}, got '
+                              f'{buf.dtype} {tuple(buf.shape)}')
+    return buf
 
 
 class GenericHipConvBackend(HipConvBackend):

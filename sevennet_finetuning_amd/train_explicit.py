@@ -79,29 +79,53 @@ class _Prims:
         d2 = self.c * s * (1 - s) * (2 + x * (1 - 2 * s))
         return d1, d2
 
-    def act(self, x):
+    def act(self, x, out=None):
         if self._hip(x):
-            y = torch.empty_like(x)
+            y = torch.empty_like(x) if out is None else out
             conv_ops._act_call(self.lib, 0, x, out0=y, scale=self.c)
             return y
-        return self.c * x * torch.sigmoid(x)
+        return _put(out, self.c * x * torch.sigmoid(x))
 
-    def act_jvp(self, x, xd):
+    def act_jvp(self, x, xd, out=None):
         """phi'(x) x'"""
         if self._hip(x):
-            y = torch.empty_like(x)
+            y = torch.empty_like(x) if out is None else out
             conv_ops._act_call(self.lib, 1, x, g=xd.contiguous(), out0=y, scale=self.c)
             return y
-        return self._d(x)[0] * xd
+        return _put(out, self._d(x)[0] * xd)
 
-    def act_dual(self, x, xd, g, gd):
+    def act_dual(self, x, xd, g, gd, out0=None, out1=None):
         """reverse of (phi(x), phi'(x) x'): (g phi' + g' phi'' x', g' phi')"""
         if self._hip(x):
-            o0, o1 = torch.empty_like(x), torch.empty_like(x)
+            o0 = torch.empty_like(x) if out0 is None else out0
+            o1 = torch.empty_like(x) if out1 is None else out1
             conv_ops._act_dual_call(self.lib, x, xd, g, gd, o0, o1, self.c)
             return o0, o1
         d1, d2 = self._d(x)
-        return g * d1 + gd * d2 * xd, gd * d1
+        return _put(out0, g * d1 + gd * d2 * xd), _put(out1, gd * d1)
+
+
+def _put(out, v):
+    if out is None:
+        return v
+    out.copy_(v)
+    return out
+
+
+def _wgrad(G, A, B, alpha=1.0):
+    """G += alpha A^T B for a tall K (edges) and a small output: split over
+    K-chunks as one batched GEMM and a sum (a single GEMM with K = 24k rows
+    and a 64 x 64 output runs on 4 workgroups)"""
+    K = A.shape[0]
+    if K < 2048 or A.shape[1] * B.shape[1] > (1 << 17):
+        G.addmm_(A.t(), B, alpha=alpha)
+        return
+    S = next((s for s in range(K // 384, 7, -1) if K % s == 0), 1)
+    if S <= 1:
+        G.addmm_(A.t(), B, alpha=alpha)
+        return
+    part = torch.bmm(A.view(S, K // S, -1).transpose(1, 2), B.view(S, K // S, -1))
+    G.add_(part.sum(0), alpha=alpha)
 
 
 class _Gate:
@@ -137,18 +161,18 @@ class _Gate:
             off += m * d
         return out
 
-    def fwd(self, y):
+    def fwd(self, y, out=None):
         p = self.p
         if not self.ng:
-            return p.act(y)
+            return p.act(y, out)
         if p._hip(y):
-            o = torch.empty(y.shape[0], int(self.dims[3]), device=y.device)
+            o = torch.empty(y.shape[0], int(self.dims[3]), device=y.device) if out is None else out
             conv_ops._gate_call(p.lib, 0, self.dims, y.contiguous(), out0=o, scale=p.c)
             return o
         s, g, blks = self._split(y)
         ga = self._gsplit(p.act(g))
         outs = [p.act(s)] + [(a.unsqueeze(-1) * b).reshape(y.shape[0], -1) for a, b in zip(ga, blks)]
-        return torch.cat(outs, 1)
+        return _put(out, torch.cat(outs, 1))
 
     def vjp(self, y, xb):
         """J^T x-bar"""
@@ -171,13 +195,13 @@ class _Gate:
         out += [(a.unsqueeze(-1) * xk).reshape(y.shape[0], -1) for a, xk in zip(ga, xs[1:])]
         return torch.cat(out, 1)
 
-    def jvp(self, y, yd):
+    def jvp(self, y, yd, out=None):
         """J y'"""
         p = self.p
         if not self.ng:
-            return p.act_jvp(y, yd)
+            return p.act_jvp(y, yd, out)
         if p._hip(y):
-            o = torch.empty(y.shape[0], int(self.dims[3]), device=y.device)
+            o = torch.empty(y.shape[0], int(self.dims[3]), device=y.device) if out is None else out
             conv_ops._gate_dual_call(p.lib, 0, self.dims, y, yd, out0=o, scale=p.c)
             return o
         s, g, blks = self._split(y)
@@ -187,16 +211,17 @@ class _Gate:
         outs = [p.act_jvp(s, sd)]
         for a, aj, b, bd in zip(ga, gjv, blks, bds):
             outs.append((aj.unsqueeze(-1) * b + a.unsqueeze(-1) * bd).reshape(y.shape[0], -1))
-        return torch.cat(outs, 1)
+        return _put(out, torch.cat(outs, 1))
 
-    def dual_vjp(self, y, yd, xb, xbd):
+    def dual_vjp(self, y, yd, xb, xbd, out0=None, out1=None):
         """reverse of (x, x') = (G(y), J(y) y'):
         y-bar = J^T x-bar + d/dy <x'-bar, J(y) y'>,  y'-bar = J^T x'-bar"""
         p = self.p
         if not self.ng:
-            return p.act_dual(y, yd, xb, xbd)
+            return p.act_dual(y, yd, xb, xbd, out0, out1)
         if p._hip(y):
-            yb, ydb = torch.empty_like(y), torch.empty_like(y)
+            yb = torch.empty_like(y) if out0 is None else out0
+            ydb = torch.empty_like(y) if out1 is None else out1
             conv_ops._gate_dual_call(p.lib, 1, self.dims, y, yd, xb, xbd, out0=yb, out1=ydb,
                                      scale=p.c)
             return yb, ydb
@@ -215,7 +240,7 @@ class _Gate:
             gpart.append(d2 * gdk * (xk * b).sum(-1) + d1 * (xk * bd).sum(-1))
             bpart.append((xk * (d1 * gdk).unsqueeze(-1)).reshape(y.shape[0], -1))
         h = torch.cat(out + gpart + bpart, 1)
-        return yb + h, ydb
+        return _put(out0, yb + h), _put(out1, ydb)
 
 
 # ------------------------------------------------------------------ edge geometry
@@ -400,13 +425,20 @@ class ExplicitStep:
     # ---------------------------------------------------------------- 1 + 2
     def forward(self, data, graph=None):
         """Primal forward and first reverse.  Returns the model's output dict
-        (energy per graph, forces, stress) -- the loss's inputs."""
+        (energy per graph, forces, stress) -- the loss's inputs.
+
+        Activations live in STACKED buffers, primal rows first and their
+        tangents (filled by backward()) after them -- [emb; emb'], [a1; a1'],
+        [h1; h1'], ..., [x; x'], [agg/den; agg'/den], [y; y'] -- so the reverse
+        sweep forms each weight gradient x^T y-bar + x'^T y'-bar and each input
+        gradient [y-bar; y'-bar] W^T as ONE GEMM."""
         m = self.m
         dev = m.flat.device
+        dt = m.dtype
         types = data[KEY.NODE_FEATURE].to(dev).long()
         n = int(types.shape[0])
         ei = data[KEY.EDGE_IDX].to(dev).long()
-        vec = data[KEY.EDGE_VEC].to(dev, m.dtype).detach()
+        vec = data[KEY.EDGE_VEC].to(dev, dt).detach()
         batch = data[KEY.BATCH].to(dev).long() if KEY.BATCH in data else \
             torch.zeros(n, dtype=torch.long, device=dev)
         nb = int(data[KEY.NUM_ATOMS].numel()) if KEY.NUM_ATOMS in data else 1
@@ -418,42 +450,57 @@ class ExplicitStep:
                 center, nbr = center[perm], nbr[perm]
             graph = conv_ops.ConvGraph(n, center, nbr, m.conv_backend)
         vec_k = vec[perm] if perm is not None else vec
-        S = self.S = {'n': n, 'nb': nb, 'types': types, 'batch': batch, 'center': center,
+        E = int(vec_k.shape[0])
+        S = self.S = {'n': n, 'E': E, 'nb': nb, 'types': types, 'batch': batch, 'center': center,
                       'nbr': nbr, 'graph': graph, 'vec': vec_k}
         coeffs = self._P('edge_embedding.basis_function.coeffs').detach()
         g = self.geo.forward(vec_k, coeffs)
         S['geo'] = g
+        EMB = torch.empty(2 * E, 8, device=dev, dtype=dt)
+        EMB[:E].copy_(g['emb'])
+        S['EMB'] = EMB
         D = S['D'] = self.bank.build()
         P = lambda name: self._P(name).detach()   # noqa: E731
-        x = P('onehot_to_feature_x.linear.weight').view(m.nsp, -1)[types] / math.sqrt(m.nsp)
+        emb_w = P('onehot_to_feature_x.linear.weight').view(m.nsp, -1)
+        X = torch.empty(2 * n, emb_w.shape[1], device=dev, dtype=dt)
+        torch.mul(emb_w[types], 1.0 / math.sqrt(m.nsp), out=X[:n])
+        X[n:].zero_()                          # x0 does not depend on the edge vectors
         blocks = []
         be = m.conv_backend
+        new = lambda *shape: torch.empty(*shape, device=dev, dtype=dt)   # noqa: E731
         for t, blk in enumerate(m.blocks):
             pre = f'{t}_convolution'
-            b = {'x': x}
+            W0 = P(f'{pre}.weight_nn.layer0.weight')
+            W1 = P(f'{pre}.weight_nn.layer1.weight')
+            W2 = P(f'{pre}.weight_nn.layer2.weight')
+            W0, W1, W2 = (W0 / math.sqrt(W0.shape[0]), W1 / math.sqrt(W1.shape[0]),
+                          W2 / math.sqrt(W2.shape[0]))
+            x = X[:n]
             sc = x @ D[f'sc{t}']
-            h = x @ D[f'si1{t}']
-            w0 = P(f'{pre}.weight_nn.layer0.weight')
-            w1 = P(f'{pre}.weight_nn.layer1.weight')
-            w2 = P(f'{pre}.weight_nn.layer2.weight')
-            W0 = w0 / math.sqrt(w0.shape[0])
-            W1 = w1 / math.sqrt(w1.shape[0])
-            W2 = w2 / math.sqrt(w2.shape[0])
-            a1 = g['emb'] @ W0
-            h1 = self.p.act(a1)
-            a2 = h1 @ W1
-            h2 = self.p.act(a2)
-            w = h2 @ W2
+            H = new(2 * n, D[f'si1{t}'].shape[1])
+            torch.mm(x, D[f'si1{t}'], out=H[:n])
+            A1, H1 = new(2 * E, W0.shape[1]), new(2 * E, W0.shape[1])
+            A2, H2 = new(2 * E, W1.shape[1]), new(2 * E, W1.shape[1])
+            WT = new(2 * E, W2.shape[1])
+            torch.mm(EMB[:E], W0, out=A1[:E])
+            self.p.act(A1[:E], out=H1[:E])
+            torch.mm(H1[:E], W1, out=A2[:E])
+            self.p.act(A2[:E], out=H2[:E])
+            torch.mm(H2[:E], W2, out=WT[:E])
             den = P(f'{pre}.denominator')
-            agg = be.forward(blk['kind'], graph, h, g['Y'], w)
-            aggs = agg / den
-            y = torch.addmm(sc, aggs, D[f'si2{t}'])
-            b.update(h=h, a1=a1, h1=h1, a2=a2, h2=h2, w=w, W=(W0, W1, W2), den=den, aggs=aggs, y=y)
-            x = self.gates[t].fwd(y)
-            blocks.append(b)
+            agg = be.forward(blk['kind'], graph, H[:n], g['Y'], WT[:E])
+            AGG = new(2 * n, agg.shape[1])
+            torch.div(agg, den, out=AGG[:n])
+            Yg = new(2 * n, D[f'si2{t}'].shape[1])
+            torch.addmm(sc, AGG[:n], D[f'si2{t}'], out=Yg[:n])
+            Xn = new(2 * n, self.gates[t].dims[3] if self.gates[t].ng else Yg.shape[1])
+            self.gates[t].fwd(Yg[:n], out=Xn[:n])
+            blocks.append({'X': X, 'H': H, 'A1': A1, 'H1': H1, 'A2': A2, 'H2': H2, 'WT': WT,
+                           'W': (W0, W1, W2), 'den': den, 'AGG': AGG, 'Y': Yg})
+            X = Xn
         S['blocks'] = blocks
-        S['xL'] = x
-        hid = x @ D['r1']
+        S['XL'] = X
+        hid = X[:n] @ D['r1']
         e = (hid @ D['r2'])[:, 0]
         scale = P('rescale_atomic_energy.scale')[types]
         atomic = e * scale + P('rescale_atomic_energy.shift')[types]
@@ -466,14 +513,15 @@ class ExplicitStep:
         embb = torch.zeros_like(g['emb'])
         for t in range(len(blocks) - 1, -1, -1):
             b, blk = blocks[t], m.blocks[t]
-            yb = self.gates[t].vjp(b['y'], xb)
+            yb = self.gates[t].vjp(b['Y'][:n], xb)
             ab = (yb @ D[f'si2{t}'].t()) / b['den']
-            hb, dY, wb = be.backward(blk['kind'], graph, b['h'], g['Y'], b['w'], ab, need_h=t > 0)
+            hb, dY, wb = be.backward(blk['kind'], graph, b['H'][:n], g['Y'], b['WT'][:E], ab,
+                                     need_h=t > 0)
             Yb += dY
             W0, W1, W2 = b['W']
-            h1b = self.p.act_jvp(b['a2'], wb @ W2.t())
-            a1b = self.p.act_jvp(b['a1'], h1b @ W1.t())
-            embb += a1b @ W0.t()
+            a2b = self.p.act_jvp(b['A2'][:E], wb @ W2.t())
+            a1b = self.p.act_jvp(b['A1'][:E], a2b @ W1.t())
+            embb.addmm_(a1b, W0.t())
             if t > 0:
                 xb = torch.addmm(hb @ D[f'si1{t}'].t(), yb, D[f'sc{t}'].t())
         fij = self.geo.vjp(g, Yb, embb)                    # dE/dr_e, centre-sorted order
@@ -499,11 +547,13 @@ class ExplicitStep:
         of the energies (per graph), forces and stress (per graph, or None)."""
         m, S = self.m, self.S
         D, g = S['D'], S['geo']
+        n, E = S['n'], S['E']
         types, batch, center, nbr = S['types'], S['batch'], S['center'], S['nbr']
         be, graph = m.conv_backend, S['graph']
         dt = m.dtype
-        cE = cE.to(dt) if cE is not None else torch.zeros(S['nb'], device=types.device, dtype=dt)
-        cF = cF.to(dt) if cF is not None else torch.zeros(S['n'], 3, device=types.device, dtype=dt)
+        dev = types.device
+        cE = cE.to(dt) if cE is not None else torch.zeros(S['nb'], device=dev, dtype=dt)
+        cF = cF.to(dt) if cF is not None else torch.zeros(n, 3, device=dev, dtype=dt)
         # v_e = dL/df_e: forces F_i = sum_{centre i} f_e - sum_{nbr i} f_e, stress from the edges
         v = cF[center] - cF[nbr]
         if cS is not None:
@@ -513,115 +563,118 @@ class ExplicitStep:
             v = v - torch.stack([c[:, 0] * r[:, 0] + c[:, 5] * r[:, 2],
                                  c[:, 1] * r[:, 1] + c[:, 3] * r[:, 0],
                                  c[:, 2] * r[:, 2] + c[:, 4] * r[:, 1]], 1)
-        # ---- tangent forward along v
+        # ---- tangent forward along v (second halves of the stacked buffers)
         Yd, embd, rd = self.geo.jvp(g, v)
+        EMB = S['EMB']
+        EMB[E:].copy_(embd)
         blocks = S['blocks']
-        xd = None
+        Y = g['Y']
         for t, blk in enumerate(m.blocks):
             b = blocks[t]
+            k = blk['kind']
             W0, W1, W2 = b['W']
-            a1d = embd @ W0
-            h1d = self.p.act_jvp(b['a1'], a1d)
-            a2d = h1d @ W1
-            h2d = self.p.act_jvp(b['a2'], a2d)
-            wd = h2d @ W2
-            aggd = be.forward(blk['kind'], graph, b['h'], Yd, b['w']) + \
-                be.forward(blk['kind'], graph, b['h'], g['Y'], wd)
-            hd = None
-            if xd is not None:
-                hd = xd @ D[f'si1{t}']
-                aggd = aggd + be.forward(blk['kind'], graph, hd, g['Y'], b['w'])
-            aggsd = aggd / b['den']
-            yd = aggsd @ D[f'si2{t}']
-            if xd is not None:
-                yd = torch.addmm(yd, xd, D[f'sc{t}'])
-            b.update(a1d=a1d, h1d=h1d, a2d=a2d, h2d=h2d, wd=wd, hd=hd, aggsd=aggsd, yd=yd, xd=xd)
-            xd = self.gates[t].jvp(b['y'], yd)
-        hidd = xd @ D['r1']
+            A1, H1, A2, H2, WT = b['A1'], b['H1'], b['A2'], b['H2'], b['WT']
+            torch.mm(EMB[E:], W0, out=A1[E:])
+            self.p.act_jvp(A1[:E], A1[E:], out=H1[E:])
+            torch.mm(H1[E:], W1, out=A2[E:])
+            self.p.act_jvp(A2[:E], A2[E:], out=H2[E:])
+            torch.mm(H2[E:], W2, out=WT[E:])
+            h, w = b['H'][:n], WT[:E]
+            aggd = be.forward(k, graph, h, Yd, w)
+            aggd += be.forward(k, graph, h, Y, WT[E:])
+            X = b['X']
+            if t > 0:
+                torch.mm(X[n:], D[f'si1{t}'], out=b['H'][n:])
+                aggd += be.forward(k, graph, b['H'][n:], Y, w)
+            AGG, Yg = b['AGG'], b['Y']
+            torch.div(aggd, b['den'], out=AGG[n:])
+            if t > 0:
+                torch.addmm(X[n:] @ D[f'sc{t}'], AGG[n:], D[f'si2{t}'], out=Yg[n:])
+            else:
+                torch.mm(AGG[n:], D[f'si2{t}'], out=Yg[n:])
+            Xn = blocks[t + 1]['X'] if t + 1 < len(blocks) else S['XL']
+            self.gates[t].jvp(Yg[:n], Yg[n:], out=Xn[n:])
+        XL = S['XL']
+        hidd = XL[n:] @ D['r1']
         ed = (hidd @ D['r2'])[:, 0]
 
         # ---- one reverse sweep over (primal, tangent); seeds cE on E, 1 on E'
         G = self.bank.grads()
         scale = S['scale']
         atb = cE[batch]                       # d L / d atomic
-        eb = atb * scale
-        edb = scale                           # seed 1 on sum of atomic'
         gsc = self._G('rescale_atomic_energy.scale')
         if gsc is not None:
             gsc.index_add_(0, types, atb * S['e'] + ed)
         gsh = self._G('rescale_atomic_energy.shift')
         if gsh is not None:
             gsh.index_add_(0, types, atb)
-        hid = S['hid']
-        G['r2'].addmm_(hid.t(), eb.unsqueeze(-1)).addmm_(hidd.t(), edb.unsqueeze(-1))
-        r2 = D['r2'][:, 0].unsqueeze(0)
-        hidb = eb.unsqueeze(-1) * r2
-        hiddb = edb.unsqueeze(-1) * r2
-        G['r1'].addmm_(S['xL'].t(), hidb).addmm_(xd.t(), hiddb)
-        xb = hidb @ D['r1'].t()
-        xdb = hiddb @ D['r1'].t()
-        embb = torch.zeros_like(g['emb'])
-        embdb = torch.zeros_like(g['emb'])
+        # [e-bar; e'-bar] = [cE scale; scale]
+        EB = torch.cat([atb * scale, scale]).unsqueeze(-1)
+        HID = torch.cat([S['hid'], hidd])
+        G['r2'].addmm_(HID.t(), EB)
+        HIDB = EB * D['r2'][:, 0].unsqueeze(0)
+        G['r1'].addmm_(XL.t(), HIDB)
+        XB = HIDB @ D['r1'].t()               # [x-bar; x'-bar] of the last block's output
+        EMBB = torch.zeros(2 * E, 8, device=dev, dtype=dt)
+        new = lambda *shape: torch.empty(*shape, device=dev, dtype=dt)   # noqa: E731
         for t in range(len(blocks) - 1, -1, -1):
             b, blk = blocks[t], m.blocks[t]
             k = blk['kind']
             pre = f'{t}_convolution'
-            yb, ydb = self.gates[t].dual_vjp(b['y'], b['yd'], xb, xdb)
-            G[f'si2{t}'].addmm_(b['aggs'].t(), yb).addmm_(b['aggsd'].t(), ydb)
-            aggsb = yb @ D[f'si2{t}'].t()
-            aggsdb = ydb @ D[f'si2{t}'].t()
+            Yg, AGG, X, H = b['Y'], b['AGG'], b['X'], b['H']
+            YB = new(2 * n, Yg.shape[1])
+            self.gates[t].dual_vjp(Yg[:n], Yg[n:], XB[:n], XB[n:], out0=YB[:n], out1=YB[n:])
+            G[f'si2{t}'].addmm_(AGG.t(), YB)
+            AGGB = YB @ D[f'si2{t}'].t()
             gden = self._G(f'{pre}.denominator')
             if gden is not None:
-                gden.sub_(((aggsb * b['aggs']).sum() + (aggsdb * b['aggsd']).sum()) / b['den'])
-            ab = aggsb / b['den']
-            adb = aggsdb / b['den']
-            h, w, Y = b['h'], b['w'], g['Y']
+                gden.sub_(torch.dot(AGGB.view(-1), AGG.view(-1)) / b['den'])
+            AB = AGGB / b['den']
+            ab, adb = AB[:n], AB[n:]
+            h, hd = H[:n], H[n:]
+            WT = b['WT']
+            w, wd = WT[:E], WT[E:]
             # trilinear agg = C(h, Y, w): B(h', Y', w'; c) = (B_h(Y', w'), B_Y(h', w'), B_w(h', Y'))
-            hb, _, wb = be.backward(k, graph, h, Y, w, ab)                  # B_h(Y,w;a), B_w(h,Y;a)
-            t_h, _, t_w = be.backward(k, graph, h, Yd, w, adb)              # B_h(Y',w), B_w(h,Y')
-            hb, wb = hb + t_h, wb + t_w
-            t_h, _, wdb = be.backward(k, graph, h, Y, b['wd'], adb)         # B_h(Y,w'), B_w(h,Y) = w'-bar
-            hb = hb + t_h
-            hdb = None
-            if b['hd'] is not None:
-                hdb, _, t_w = be.backward(k, graph, b['hd'], Y, w, adb)    # B_h(Y,w) = h'-bar, B_w(h',Y)
-                wb = wb + t_w
-            # radial MLP
+            HB, WB = new(2 * n, H.shape[1]), new(2 * E, WT.shape[1])
+            be.backward(k, graph, h, Y, w, ab, dh_out=HB[:n], dw_out=WB[:E])      # B_h(Y,w;a), B_w(h,Y;a)
+            t_h, _, t_w = be.backward(k, graph, h, Yd, w, adb)                      # B_h(Y',w), B_w(h,Y')
+            HB[:n] += t_h
+            WB[:E] += t_w
+            t_h, _, _ = be.backward(k, graph, h, Y, wd, adb, dw_out=WB[E:])        # B_h(Y,w'), w'-bar
+            HB[:n] += t_h
+            if t > 0:
+                _, _, t_w = be.backward(k, graph, hd, Y, w, adb, dh_out=HB[n:])    # h'-bar, B_w(h',Y)
+                WB[:E] += t_w
+            else:
+                HB[n:].zero_()                # x0' = 0: no h' (its rows meet zero rows of X)
+            # radial MLP, primal and tangent rows together
             W0, W1, W2 = b['W']
             gw2 = self._G(f'{pre}.weight_nn.layer2.weight')
-            s2 = 1.0 / math.sqrt(W2.shape[0])
             if gw2 is not None:
-                gw2.addmm_(b['h2'].t(), wb, alpha=s2).addmm_(b['h2d'].t(), wdb, alpha=s2)
-            h2b, h2db = wb @ W2.t(), wdb @ W2.t()
-            a2b, a2db = self.p.act_dual(b['a2'], b['a2d'], h2b, h2db)
+                _wgrad(gw2, b['H2'], WB, 1.0 / math.sqrt(W2.shape[0]))
+            H2B = WB @ W2.t()
+            A2B = new(2 * E, W1.shape[1])
+            self.p.act_dual(b['A2'][:E], b['A2'][E:], H2B[:E], H2B[E:], out0=A2B[:E], out1=A2B[E:])
             gw1 = self._G(f'{pre}.weight_nn.layer1.weight')
-            s1 = 1.0 / math.sqrt(W1.shape[0])
             if gw1 is not None:
-                gw1.addmm_(b['h1'].t(), a2b, alpha=s1).addmm_(b['h1d'].t(), a2db, alpha=s1)
-            h1b, h1db = a2b @ W1.t(), a2db @ W1.t()
-            a1b, a1db = self.p.act_dual(b['a1'], b['a1d'], h1b, h1db)
+                _wgrad(gw1, b['H1'], A2B, 1.0 / math.sqrt(W1.shape[0]))
+            H1B = A2B @ W1.t()
+            A1B = new(2 * E, W0.shape[1])
+            self.p.act_dual(b['A1'][:E], b['A1'][E:], H1B[:E], H1B[E:], out0=A1B[:E], out1=A1B[E:])
             gw0 = self._G(f'{pre}.weight_nn.layer0.weight')
-            s0 = 1.0 / math.sqrt(W0.shape[0])
             if gw0 is not None:
-                gw0.addmm_(g['emb'].t(), a1b, alpha=s0).addmm_(embd.t(), a1db, alpha=s0)
-            embb += a1b @ W0.t()
-            embdb += a1db @ W0.t()
+                _wgrad(gw0, EMB, A1B, 1.0 / math.sqrt(W0.shape[0]))
+            EMBB.addmm_(A1B, W0.t())
             # self-interaction 1 and self-connection (sc-bar = y-bar)
-            x = b['x']
-            G[f'si1{t}'].addmm_(x.t(), hb)
-            G[f'sc{t}'].addmm_(x.t(), yb)
-            if b['xd'] is not None:
-                G[f'si1{t}'].addmm_(b['xd'].t(), hdb)
-                G[f'sc{t}'].addmm_(b['xd'].t(), ydb)
-            xb = torch.addmm(hb @ D[f'si1{t}'].t(), yb, D[f'sc{t}'].t())
-            xdb = torch.addmm(hdb @ D[f'si1{t}'].t(), ydb, D[f'sc{t}'].t()) \
-                if hdb is not None else None
+            G[f'si1{t}'].addmm_(X.t(), HB)
+            G[f'sc{t}'].addmm_(X.t(), YB)
+            XB = torch.addmm(HB @ D[f'si1{t}'].t(), YB, D[f'sc{t}'].t())
         # embedding (x0 = W[types] / sqrt(nsp)) and the radial basis coefficients
         gemb = self._G('onehot_to_feature_x.linear.weight')
         if gemb is not None:
-            gemb.view(m.nsp, -1).index_add_(0, types, xb / math.sqrt(m.nsp))
+            gemb.view(m.nsp, -1).index_add_(0, types, XB[:n] / math.sqrt(m.nsp))
         gco = self._G('edge_embedding.basis_function.coeffs')
         if gco is not None:
             coeffs = self._P('edge_embedding.basis_function.coeffs').detach()
-            gco.add_(self.geo.coeff_grad(g, embb, embdb, rd, coeffs))
+            gco.add_(self.geo.coeff_grad(g, EMBB[:E], EMBB[E:], rd, coeffs))
         self.bank.flush(m.flat_grad)

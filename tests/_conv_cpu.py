@@ -30,7 +30,14 @@ class CpuConvBackend:
     def build(self, g, into=None):
         return {} if into is None else into
 
-    def forward(self, kind, g, h, Y, w):
+    def forward(self, kind, g, h, Y, w, out=None):
+        agg = self._forward(kind, g, h, Y, w)
+        if out is not None:
+            out.copy_(agg)
+            return out
+        return agg
+
+    def _forward(self, kind, g, h, Y, w):
         irr, ins, perm = self.tables[kind]
         xs = h[g.edge_nbr.long()]
         e = xs.shape[0]
@@ -50,15 +57,19 @@ class CpuConvBackend:
         return torch.zeros(g.n_nodes, msg.shape[1], dtype=h.dtype).index_add(
             0, g.edge_center.long(), msg)
 
-    def backward(self, kind, g, h, Y, w, gagg, need_h=True):
+    def backward(self, kind, g, h, Y, w, gagg, need_h=True, dh_out=None, dw_out=None):
         with torch.enable_grad():
             hh, YY, ww = (t.detach().requires_grad_(True) for t in (h, Y, w))
-            s = (self.forward(kind, g, hh, YY, ww) * gagg.detach()).sum()
+            s = (self._forward(kind, g, hh, YY, ww) * gagg.detach()).sum()
             dh, dY, dw = torch.autograd.grad(s, [hh, YY, ww], allow_unused=True)
         zero = torch.zeros_like
         dh = dh if dh is not None else zero(h)
         dY = dY if dY is not None else zero(Y)
         dw = dw if dw is not None else zero(w)
+        if dw_out is not None:
+            dw = dw_out.copy_(dw)
+        if dh_out is not None and need_h:
+            dh = dh_out.copy_(dh)
         return (dh if need_h else None), dY, dw
 
 

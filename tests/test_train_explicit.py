@@ -108,3 +108,16 @@ def test_explicit_gradient_unsorted_edges_and_frozen_parameters():
     assert torch.allclose(ge, ga, rtol=1e-9, atol=1e-9 * float(ga.abs().max()))
     off, n, _ = m.slices['rescale_atomic_energy.scale']
     assert float(ge[off:off + n].abs().max()) == 0.0
+
+
+def test_split_k_weight_gradient():
+    """_wgrad's chunked batched GEMM + sum equals A^T B (K = 24,192 rows, the
+    fine-tune step's stacked edge count)."""
+    from sevennet_finetuning_amd.train_explicit import _wgrad
+    g = torch.Generator().manual_seed(0)
+    A = torch.randn(24192, 64, generator=g, dtype=torch.float64)
+    B = torch.randn(24192, 64, generator=g, dtype=torch.float64)
+    G = torch.randn(64, 64, generator=g, dtype=torch.float64)
+    ref = G + 0.5 * A.t() @ B
+    _wgrad(G, A, B, 0.5)
+    assert torch.allclose(G, ref, rtol=1e-12, atol=1e-10)
