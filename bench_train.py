@@ -89,6 +89,8 @@ def main():
     ap.add_argument('--eager', action='store_true',
                     help='no HIP-graph capture of the step (always eager for N > 1)')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
+    ap.add_argument('--blas', default='rocblas', choices=['rocblas', 'hipblaslt'],
+                    help='torch GEMM backend for the linears and the radial MLP')
     ap.add_argument('--autograd', action='store_true',
                     help='the loss gradient by autograd double backward instead of the '
                          'hand-scheduled derivatives (train_explicit.py)')
@@ -111,7 +113,7 @@ def main():
            'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
            'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
            'scheduler_param': {'gamma': 0.99}, 'is_ddp': world > 1, 'device': device,
-           'hip_graph': not args.eager, 'explicit_grad': not args.autograd,
+           'hip_graph': not args.eager, 'explicit_grad': not args.autograd, 'blas': args.blas,
            'continue': {'fisher_information': fisher, 'opt_params': opt, 'ewc_lambda': 1e5}}
     tr = train.Trainer(model, cfg)
     n_b = 4
@@ -163,7 +165,7 @@ def main():
                        'atoms_per_rank_step': atoms_per_step, 'edges_per_batch': edges,
                        'parallelism': f'dp{world}',
                        'hip_graph': bool(tr.hip_graph),
-                       'explicit_grad': tr.explicit is not None},
+                       'explicit_grad': tr.explicit is not None, 'blas': args.blas},
             'atoms_per_s': round(atoms_per_step * world * args.steps / dt, 1),
             'loss': float(loss), 'mem_loss': float(mloss), 'cpu_baseline': cpu}), flush=True)
     if world > 1:

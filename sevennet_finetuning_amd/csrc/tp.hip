@@ -65,11 +65,13 @@ __device__ __forceinline__ void tp_acc(const float* x, const float* y, float w, 
 }
 
 // ------------------------------------------------------------------ forward
+// edges beg + k0 * STEP, beg + (k0 + ks) * STEP, ... of the centre (ks waves
+// share a centre's edges in the split kernel; 0 / 1 otherwise); out[] = sum * scale
 template <class L, int L1>
 __device__ __forceinline__ void fwd_part(int lane, int beg, int end, const int* __restrict__ nbr,
                                          const float* __restrict__ Y, const float* __restrict__ w,
                                          const float* __restrict__ h, float* __restrict__ out,
-                                         float denom) {
+                                         float scale, int k0 = 0, int ks = 1) {
   constexpr int MUL = part_mul<L, L1>();
   if constexpr (MUL == 0) {
     return;
@@ -87,7 +89,7 @@ __device__ __forceinline__ void fwd_part(int lane, int beg, int end, const int* 
     });
     const int u0 = PAIR ? (lane & 31) : lane;
     constexpr int STEP = PAIR ? 2 : 1;
-    for (int e0 = beg; e0 < end; e0 += STEP) {
+    for (int e0 = beg + k0 * STEP; e0 < end; e0 += STEP * ks) {
       const int e = PAIR ? e0 + (lane >> 5) : e0;
       if (PAIR && e >= end) continue;
       const int j = nbr[e];
@@ -120,7 +122,7 @@ __device__ __forceinline__ void fwd_part(int lane, int beg, int end, const int* 
           for (int k = 0; k < D3; ++k) {
             float v = acc[pi][s][k];
             if (PAIR) v += __shfl_down(v, 32, 64);
-            if (!PAIR || lane < 32) out[p.moff + (u0 + 64 * s) * D3 + k] = v / denom;
+            if (!PAIR || lane < 32) out[p.moff + (u0 + 64 * s) * D3 + k] = v * scale;
           }
         }
       }
@@ -145,9 +147,44 @@ __global__ __launch_bounds__(192) void k_tp_fwd(const int* __restrict__ row_ptr,
   const int lane = threadIdx.x & 63;
   const int beg = row_ptr[c], end = row_ptr[c + 1];
   float* out = agg + (int64_t)c * L::DM;
-  if (part == 0) fwd_part<L, 0>(lane, beg, end, nbr, Y, w, h, out, denom);
-  else if (part == 1) fwd_part<L, 1>(lane, beg, end, nbr, Y, w, h, out, denom);
-  else fwd_part<L, 2>(lane, beg, end, nbr, Y, w, h, out, denom);
+  const float sc = 1.f / denom;
+  if (part == 0) fwd_part<L, 0>(lane, beg, end, nbr, Y, w, h, out, sc);
+  else if (part == 1) fwd_part<L, 1>(lane, beg, end, nbr, Y, w, h, out, sc);
+  else fwd_part<L, 2>(lane, beg, end, nbr, Y, w, h, out, sc);
+}
+
+// Small batches (the fine-tune step: a few hundred centres): FS waves per
+// input irrep share a centre's edges (wave k takes edges k, k + FS, ...), each
+// writes its partial message row to LDS, and the row is summed over k in a
+// fixed order (deterministic): 3 FS waves per centre instead of 3.
+constexpr int FS = 4;
+template <class L>
+__global__ __launch_bounds__(192 * FS) void k_tp_fwd_split(const int* __restrict__ row_ptr,
+                                                          const int* __restrict__ nbr,
+                                                          const float* __restrict__ Y,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ h,
+                                                          float* __restrict__ agg, int n_centers,
+                                                          float denom) {
+  __shared__ float red[FS][L::DM];
+  const int c = blockIdx.x;
+  if (c >= n_centers) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int part = wave % 3, k0 = wave / 3;
+  const int lane = threadIdx.x & 63;
+  const int beg = row_ptr[c], end = row_ptr[c + 1];
+  if (part == 0) fwd_part<L, 0>(lane, beg, end, nbr, Y, w, h, red[k0], 1.f, k0, FS);
+  else if (part == 1) fwd_part<L, 1>(lane, beg, end, nbr, Y, w, h, red[k0], 1.f, k0, FS);
+  else fwd_part<L, 2>(lane, beg, end, nbr, Y, w, h, red[k0], 1.f, k0, FS);
+  __syncthreads();
+  const float sc = 1.f / denom;
+  float* out = agg + (int64_t)c * L::DM;
+  for (int i = threadIdx.x; i < L::DM; i += blockDim.x) {
+    float v = red[0][i];
+#pragma unroll
+    for (int k = 1; k < FS; ++k) v += red[k][i];
+    out[i] = v * sc;
+  }
 }
 
 // ------------------------------------------------------------------ backward
@@ -281,14 +318,21 @@ __global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
 template <class L>
 static hipError_t tp_fwd_impl(const TpArgs& a, hipStream_t s) {
   if (a.n_centers <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_tp_fwd<L>, dim3(a.n_centers), dim3(192), 0, s, a.row_ptr, a.nbr, a.Y, a.w,
-                     a.h, a.agg, a.n_centers, a.denom);
+  if (a.n_centers < 8192)
+    hipLaunchKernelGGL(k_tp_fwd_split<L>, dim3(a.n_centers), dim3(192 * FS), 0, s, a.row_ptr, a.nbr,
+                       a.Y, a.w, a.h, a.agg, a.n_centers, a.denom);
+  else
+    hipLaunchKernelGGL(k_tp_fwd<L>, dim3(a.n_centers), dim3(192), 0, s, a.row_ptr, a.nbr, a.Y, a.w,
+                       a.h, a.agg, a.n_centers, a.denom);
   return hipGetLastError();
 }
 template <class L>
 static hipError_t tp_bwd_impl(const TpArgs& a, hipStream_t s) {
   if (a.n_centers <= 0) return hipSuccess;
-  const int split = std::max(1, std::min(8, 16384 / a.n_centers));
+  // small batches (the fine-tune step: 432 centres x 28 edges) split each
+  // centre's edges over up to 32 waves -- about one edge per wave, the
+  // centre's dE/dagg row loaded by each: ~14k waves instead of 3.5k
+  const int split = std::max(1, std::min(32, 32768 / a.n_centers));
   const int64_t waves = (int64_t)a.n_centers * split;
   hipLaunchKernelGGL(k_tp_bwd<L>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a.row_ptr,
                      a.nbr, a.Y, a.w, a.h, a.gagg, a.dw, a.dxc, a.dYacc, a.n_centers, split);

@@ -41,6 +41,7 @@ for s in "$@"; do
     benchtrain) step benchtrain 300 python bench_train.py --steps 10 --warmup 3 ;;
     benchtrain2) step benchtrain2 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchtrainblk) step benchtrainblk 300 env E3GNN_TRAIN_DENSE_LINEAR=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    benchtrainlt) step benchtrainlt 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline --blas hipblaslt ;;
     benchtrainag) step benchtrainag 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline --autograd ;;
     proftrainx) step proftrainx 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trainx -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     fullsize2) step fullsize2 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v --timeout 600 --timeout-method thread -k edge_gradients ;;

@@ -18,8 +18,17 @@ bs = bt.make_batches(0, 2, 8, m.chemical_symbols)
 b = [train.collate(x, device=dev, dtype=torch.float32) for x in bs]
 m.train(True)
 tr.rehearsal_step(b[0], b[1]); torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
     tr.rehearsal_step(b[0], b[1]); torch.cuda.synchronize()
+print('explicit path:', tr.explicit is not None)
+# where the element-wise launches come from (source line of the calling frame)
+by_src = collections.Counter()
+for e in prof.events():
+    if e.name.startswith('aten::') and e.stack and e.device_time_total > 0:
+        fr = [s for s in e.stack if 'sevennet_finetuning_amd' in s]
+        by_src[(e.name, fr[0] if fr else '?')] += 1
+for (name, src), c in by_src.most_common(40):
+    print(c, name, src)
 rows = []
 for e in prof.key_averages():
     if e.key.startswith('aten::'):
