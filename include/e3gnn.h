@@ -184,6 +184,17 @@ int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_
                         const int32_t* edge_nbr, const int32_t* src_ptr, const int32_t* src_perm,
                         const float* h, const float* Y, const float* w, const float* gagg,
                         float* dh, float* dY, float* dw, float* dxc, void* stream);
+/* The same with accumulation (the hand-scheduled fine-tune derivatives sum
+ * several trilinear products into one buffer): forward accumulate & 1: agg +=;
+ * backward accumulate bits 1 / 2 / 4: dh / dY / dw += instead of =. */
+int e3gnn_conv_forward_acc(int kind, int64_t n_nodes, const int32_t* row_ptr,
+                           const int32_t* edge_nbr, const float* h, const float* Y, const float* w,
+                           float* agg, int accumulate, void* stream);
+int e3gnn_conv_backward_acc(int kind, int64_t n_nodes, int64_t n_edges, const int32_t* row_ptr,
+                            const int32_t* edge_nbr, const int32_t* src_ptr,
+                            const int32_t* src_perm, const float* h, const float* Y, const float* w,
+                            const float* gagg, float* dh, float* dY, float* dw, float* dxc,
+                            int accumulate, void* stream);
 
 /* ---- generic path tables: the convolution of any nequip-family model ----
  * Same contract as e3gnn_conv_forward / _backward (IrrepsConvolution,

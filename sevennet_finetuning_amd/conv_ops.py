@@ -101,21 +101,31 @@ class HipConvBackend:
                 raise _lib.E3GNNError(f'conv kind {kind}: {name} must be float32 {shape} on '
                                       f'the GPU, got {t.dtype} {tuple(t.shape)} on {t.device}')
 
-    def forward(self, kind, g, h, Y, w, out=None):
+    def forward(self, kind, g, h, Y, w, out=None, acc=False):
+        """agg; ``acc``: add into ``out`` instead of overwriting it"""
         self._check(kind, g, h, Y, w)
+        if acc and out is None:
+            raise _lib.E3GNNError('conv forward: acc needs an output buffer')
         h, Y, w = h.contiguous(), Y.contiguous(), w.contiguous()
         agg = _out(out, (g.n_nodes, self.dims[kind][2]), h.device)
         a = g.aux
-        _lib.check(self.lib.e3gnn_conv_forward(
+        _lib.check(self.lib.e3gnn_conv_forward_acc(
             kind, g.n_nodes, a['row_ptr'].data_ptr(), a['nbr'].data_ptr(), h.data_ptr(),
-            Y.data_ptr(), w.data_ptr(), agg.data_ptr(), self._stream(h)))
+            Y.data_ptr(), w.data_ptr(), agg.data_ptr(), int(bool(acc)), self._stream(h)))
         return agg
 
-    def backward(self, kind, g, h, Y, w, gagg, need_h=True, dh_out=None, dw_out=None):
-        """(dh, dY, dw); ``dh_out`` / ``dw_out``: contiguous float32 buffers
-        of the right shape to write dh / dw into (the explicit fine-tune
-        derivatives stack primal and tangent rows)"""
+    def backward(self, kind, g, h, Y, w, gagg, need_h=True, dh_out=None, dw_out=None,
+                 dY_out=None, acc=0):
+        """(dh, dY, dw); ``dh_out`` / ``dw_out`` / ``dY_out``: contiguous
+        float32 buffers of the right shape to write dh / dw / dY into (the
+        explicit fine-tune derivatives stack primal and tangent rows); ``acc``
+        bits ACC_DH / ACC_DY / ACC_DW add into those buffers instead"""
         self._check(kind, g, h, Y, w)
+        for bit, buf in ((ACC_DH, dh_out), (ACC_DY, dY_out), (ACC_DW, dw_out)):
+            if acc & bit and buf is None:
+                raise _lib.E3GNNError('conv backward: accumulation needs its output buffer')
+        if acc & ACC_DH and not need_h:
+            raise _lib.E3GNNError('conv backward: ACC_DH without need_h')
         dx, dwd, dm = self.dims[kind]
         h, Y, w = h.contiguous(), Y.contiguous(), w.contiguous()
         gagg = gagg.to(torch.float32).contiguous()
@@ -123,18 +133,22 @@ class HipConvBackend:
             raise _lib.E3GNNError(f'conv kind {kind}: gagg must be {(g.n_nodes, dm)}')
         dev = h.device
         E = g.n_edges
-        dY = torch.empty(E, 9, device=dev)
+        dY = _out(dY_out, (E, 9), dev)
         dw = _out(dw_out, (E, dwd), dev)
         dh = _out(dh_out, (g.n_nodes, dx), dev) if need_h else None
         dxc = torch.empty(E, dx, device=dev) if need_h and E else None
         a = g.aux
-        _lib.check(self.lib.e3gnn_conv_backward(
+        _lib.check(self.lib.e3gnn_conv_backward_acc(
             kind, g.n_nodes, E, a['row_ptr'].data_ptr(), a['nbr'].data_ptr(),
             a['src_ptr'].data_ptr(), a['src_perm'].data_ptr(), h.data_ptr(), Y.data_ptr(),
             w.data_ptr(), gagg.data_ptr(), dh.data_ptr() if dh is not None else None,
             dY.data_ptr(), dw.data_ptr(), dxc.data_ptr() if dxc is not None else None,
-            self._stream(h)))
+            int(acc), self._stream(h)))
         return dh, dY, dw
+
+
+# accumulation bits of HipConvBackend.backward (e3gnn_conv_backward_acc)
+ACC_DH, ACC_DY, ACC_DW = 1, 2, 4
 
 
 def _out(buf, shape, device):

@@ -1578,6 +1578,12 @@ int e3gnn_conv_graph(int64_t n_nodes, int64_t n_edges, const int32_t* edge_cente
 int e3gnn_conv_forward(int kind, int64_t n_nodes, const int32_t* row_ptr, const int32_t* edge_nbr,
                        const float* h, const float* Y, const float* w, float* agg,
                        void* stream) {
+  return e3gnn_conv_forward_acc(kind, n_nodes, row_ptr, edge_nbr, h, Y, w, agg, 0, stream);
+}
+
+int e3gnn_conv_forward_acc(int kind, int64_t n_nodes, const int32_t* row_ptr,
+                           const int32_t* edge_nbr, const float* h, const float* Y, const float* w,
+                           float* agg, int accumulate, void* stream) {
   int dx, W, dm;
   if (!conv_kind_dims(kind, &dx, &W, &dm)) return fail(E3GNN_ERR_ARG, "conv kind must be 0, 1 or 2");
   if (n_nodes <= 0) return E3GNN_OK;
@@ -1591,6 +1597,7 @@ int e3gnn_conv_forward(int kind, int64_t n_nodes, const int32_t* row_ptr, const 
   a.agg = agg;
   a.n_centers = (int)n_nodes;
   a.denom = 1.0f;
+  a.acc_out = accumulate & 1;
   HIPCHK(launch_tp_fwd(kind, a, (hipStream_t)stream));
   return E3GNN_OK;
 }
@@ -1599,16 +1606,28 @@ int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_
                         const int32_t* edge_nbr, const int32_t* src_ptr, const int32_t* src_perm,
                         const float* h, const float* Y, const float* w, const float* gagg,
                         float* dh, float* dY, float* dw, float* dxc, void* stream) {
+  return e3gnn_conv_backward_acc(kind, n_nodes, n_edges, row_ptr, edge_nbr, src_ptr, src_perm, h, Y,
+                                 w, gagg, dh, dY, dw, dxc, 0, stream);
+}
+
+int e3gnn_conv_backward_acc(int kind, int64_t n_nodes, int64_t n_edges, const int32_t* row_ptr,
+                            const int32_t* edge_nbr, const int32_t* src_ptr,
+                            const int32_t* src_perm, const float* h, const float* Y, const float* w,
+                            const float* gagg, float* dh, float* dY, float* dw, float* dxc,
+                            int accumulate, void* stream) {
   int dx, W, dm;
   if (!conv_kind_dims(kind, &dx, &W, &dm)) return fail(E3GNN_ERR_ARG, "conv kind must be 0, 1 or 2");
   hipStream_t s = (hipStream_t)stream;
-  if (dh && n_nodes > 0) HIPCHK(launch_zero(dh, n_nodes * dx, s));
-  if (n_edges <= 0 || n_nodes <= 0) return E3GNN_OK;
+  const int acc_dh = accumulate & 1, acc_dY = accumulate & 2, acc_dw = accumulate & 4;
+  if (n_edges <= 0 || n_nodes <= 0) {
+    // no edges: zero gradients (the accumulated ones keep their values)
+    if (dh && n_nodes > 0 && !acc_dh) HIPCHK(launch_zero(dh, n_nodes * dx, s));
+    return E3GNN_OK;
+  }
   if (!row_ptr || !edge_nbr || !h || !Y || !w || !gagg || !dY || !dw)
     return fail(E3GNN_ERR_ARG, "null conv operand");
   if (dh && (!dxc || !src_ptr || !src_perm))
     return fail(E3GNN_ERR_ARG, "dh needs dxc scratch and the transposed CSR");
-  HIPCHK(launch_zero(dY, n_edges * 9, s));
   TpArgs a{};
   a.row_ptr = row_ptr;
   a.nbr = edge_nbr;
@@ -1621,8 +1640,11 @@ int e3gnn_conv_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_
   a.dYacc = dY;
   a.n_centers = (int)n_nodes;
   a.denom = 1.0f;
+  a.acc_out = acc_dw ? 1 : 0;
+  a.dy_assign = acc_dY ? 0 : 1;   // every edge's dY has one writer: no zeroing launch
   HIPCHK(launch_tp_bwd(kind, a, s));
-  if (dh) HIPCHK(launch_gather_rows((int)n_nodes, dx, src_ptr, src_perm, dxc, dh, s));
+  // the gather writes every row (zero without incoming edges): no zeroing launch
+  if (dh) HIPCHK(launch_gather_rows((int)n_nodes, dx, src_ptr, src_perm, dxc, dh, s, acc_dh ? 1 : 0));
   return E3GNN_OK;
 }
 

@@ -28,11 +28,12 @@ int sum_blocks(int64_t n);
 hipError_t launch_sum(int64_t n, const float* a, float* part, float* out, hipStream_t s);
 hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStream_t s);
 hipError_t launch_zero(float* p, int64_t n, hipStream_t s);
+// acc: dst += the sums instead of dst = (the explicit fine-tune derivatives)
 hipError_t launch_gather_rows(int n, int D, const int* ptr, const int* perm, const float* src,
-                              float* dst, hipStream_t s);
+                              float* dst, hipStream_t s, int acc = 0);
 // the same over neighbour nodes [j_begin, j_end) only
 hipError_t launch_gather_rows_range(int j_begin, int j_end, int D, const int* ptr, const int* perm,
-                                    const float* src, float* dst, hipStream_t s);
+                                    const float* src, float* dst, hipStream_t s, int acc = 0);
 hipError_t launch_pack(int64_t n, int dim, const int* idx, const float* src, int64_t ss, float* dst,
                        hipStream_t s);
 hipError_t launch_unpack(int64_t n, int dim, const int* idx, const float* src, float* dst,

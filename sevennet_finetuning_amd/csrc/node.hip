@@ -391,7 +391,7 @@ __global__ __launch_bounds__(256) void k_final_sum(int nb, int k, const float* _
 // dh[j] = sum_{e: nbr[e] == j} dxc[e]  (transposed CSR, ascending edge order)
 __global__ void k_gather_rows(int j_begin, int n, int D, const int* __restrict__ ptr,
                               const int* __restrict__ perm, const float* __restrict__ src,
-                              float* __restrict__ dst) {
+                              float* __restrict__ dst, int acc) {
   const int j = j_begin + blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
@@ -399,7 +399,8 @@ __global__ void k_gather_rows(int j_begin, int n, int D, const int* __restrict__
   for (int c = lane; c < D; c += 64) {
     float s = 0.f;
     for (int q = b; q < en; ++q) s += src[(int64_t)perm[q] * D + c];
-    dst[(int64_t)j * D + c] = s;
+    float* o = dst + (int64_t)j * D + c;
+    *o = acc ? *o + s : s;
   }
 }
 
@@ -407,7 +408,7 @@ __global__ void k_gather_rows(int j_begin, int n, int D, const int* __restrict__
 // keep the ascending edge order, so the result is bitwise that of k_gather_rows
 __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict__ ptr,
                                const int* __restrict__ perm, const float4* __restrict__ src,
-                               float4* __restrict__ dst) {
+                               float4* __restrict__ dst, int acc) {
   const int j = j_begin + xcd_block() * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
@@ -433,6 +434,10 @@ __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict
       s.y += v.y;
       s.z += v.z;
       s.w += v.w;
+    }
+    if (acc) {
+      const float4 o = dst[(int64_t)j * D4 + c];
+      s = make_float4(o.x + s.x, o.y + s.y, o.z + s.z, o.w + s.w);
     }
     dst[(int64_t)j * D4 + c] = s;
   }
@@ -556,19 +561,19 @@ hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStr
   return hipGetLastError();
 }
 hipError_t launch_gather_rows(int n, int D, const int* ptr, const int* perm, const float* src,
-                              float* dst, hipStream_t s) {
-  return launch_gather_rows_range(0, n, D, ptr, perm, src, dst, s);
+                              float* dst, hipStream_t s, int acc) {
+  return launch_gather_rows_range(0, n, D, ptr, perm, src, dst, s, acc);
 }
 hipError_t launch_gather_rows_range(int j_begin, int j_end, int D, const int* ptr, const int* perm,
-                                    const float* src, float* dst, hipStream_t s) {
+                                    const float* src, float* dst, hipStream_t s, int acc) {
   const int n = j_end - j_begin;
   if (n <= 0) return hipGetLastError();
   if (D % 4 == 0) {
     hipLaunchKernelGGL(k_gather_rows4, dim3((n + 3) / 4), dim3(256), 0, s, j_begin, j_end, D / 4,
-                       ptr, perm, (const float4*)src, (float4*)dst);
+                       ptr, perm, (const float4*)src, (float4*)dst, acc);
   } else {
     hipLaunchKernelGGL(k_gather_rows, dim3((n + 3) / 4), dim3(256), 0, s, j_begin, j_end, D, ptr,
-                       perm, src, dst);
+                       perm, src, dst, acc);
   }
   return hipGetLastError();
 }

@@ -55,6 +55,8 @@ struct TpArgs {
   float* dYacc;        // bwd in/out: [E, 9] accumulated dE/dY
   int n_centers;
   float denom;
+  int acc_out = 0;     // fwd: agg += (instead of =); bwd: dw +=
+  int dy_assign = 0;   // bwd: dY = (instead of the default +=: no zeroing launch)
 };
 
 hipError_t launch_tp_fwd(int kind, const TpArgs& a, hipStream_t s);

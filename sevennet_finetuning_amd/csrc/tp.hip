@@ -71,7 +71,7 @@ template <class L, int L1>
 __device__ __forceinline__ void fwd_part(int lane, int beg, int end, const int* __restrict__ nbr,
                                          const float* __restrict__ Y, const float* __restrict__ w,
                                          const float* __restrict__ h, float* __restrict__ out,
-                                         float scale, int k0 = 0, int ks = 1) {
+                                         float scale, int k0 = 0, int ks = 1, int acc_out = 0) {
   constexpr int MUL = part_mul<L, L1>();
   if constexpr (MUL == 0) {
     return;
@@ -122,7 +122,10 @@ __device__ __forceinline__ void fwd_part(int lane, int beg, int end, const int* 
           for (int k = 0; k < D3; ++k) {
             float v = acc[pi][s][k];
             if (PAIR) v += __shfl_down(v, 32, 64);
-            if (!PAIR || lane < 32) out[p.moff + (u0 + 64 * s) * D3 + k] = v * scale;
+            if (!PAIR || lane < 32) {
+              float* o = out + p.moff + (u0 + 64 * s) * D3 + k;
+              *o = acc_out ? *o + v * scale : v * scale;
+            }
           }
         }
       }
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(192) void k_tp_fwd(const int* __restrict__ row_ptr,
                                                 const float* __restrict__ w,
                                                 const float* __restrict__ h,
                                                 float* __restrict__ agg, int n_centers,
-                                                float denom) {
+                                                float denom, int acc_out) {
   // one workgroup per centre, one wave per input irrep (its paths write
   // disjoint message slots): 3x the waves of a wave-per-centre mapping, which
   // matters for the small batched graphs of the fine-tune step
@@ -148,9 +151,9 @@ __global__ __launch_bounds__(192) void k_tp_fwd(const int* __restrict__ row_ptr,
   const int beg = row_ptr[c], end = row_ptr[c + 1];
   float* out = agg + (int64_t)c * L::DM;
   const float sc = 1.f / denom;
-  if (part == 0) fwd_part<L, 0>(lane, beg, end, nbr, Y, w, h, out, sc);
-  else if (part == 1) fwd_part<L, 1>(lane, beg, end, nbr, Y, w, h, out, sc);
-  else fwd_part<L, 2>(lane, beg, end, nbr, Y, w, h, out, sc);
+  if (part == 0) fwd_part<L, 0>(lane, beg, end, nbr, Y, w, h, out, sc, 0, 1, acc_out);
+  else if (part == 1) fwd_part<L, 1>(lane, beg, end, nbr, Y, w, h, out, sc, 0, 1, acc_out);
+  else fwd_part<L, 2>(lane, beg, end, nbr, Y, w, h, out, sc, 0, 1, acc_out);
 }
 
 // Small batches (the fine-tune step: a few hundred centres): FS waves per
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(192 * FS) void k_tp_fwd_split(const int* __restrict
                                                           const float* __restrict__ w,
                                                           const float* __restrict__ h,
                                                           float* __restrict__ agg, int n_centers,
-                                                          float denom) {
+                                                          float denom, int acc_out) {
   __shared__ float red[FS][L::DM];
   const int c = blockIdx.x;
   if (c >= n_centers) return;
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(192 * FS) void k_tp_fwd_split(const int* __restrict
     float v = red[0][i];
 #pragma unroll
     for (int k = 1; k < FS; ++k) v += red[k][i];
-    out[i] = v * sc;
+    out[i] = acc_out ? out[i] + v * sc : v * sc;
   }
 }
 
@@ -235,7 +238,7 @@ struct BwdPart {
   __device__ __forceinline__ void edge(int lane, int64_t e, int j, const float* y,
                                        const float* __restrict__ w, const float* __restrict__ h,
                                        float* __restrict__ dw, float* __restrict__ dxc,
-                                       float* dy) {
+                                       float* dy, int acc_dw) {
     if constexpr (MUL > 0) {
       if (MUL == 32 && lane >= 32) return;
       const float* wr = w + e * L::W;
@@ -253,9 +256,9 @@ struct BwdPart {
         static_for<L::NP>([&](auto pi) {
           constexpr PathDef p = L::P[pi];
           if constexpr (p.l1 == L1) {
-            dwr[p.woff + u] =
-                tp_bwd<p.l1, p.l2, p.l3>(x, y + yoff(p.l2), wr[p.woff + u], g[pi][s], dx,
-                                         dy + yoff(p.l2));
+            const float dwv = tp_bwd<p.l1, p.l2, p.l3>(x, y + yoff(p.l2), wr[p.woff + u], g[pi][s],
+                                                       dx, dy + yoff(p.l2));
+            dwr[p.woff + u] = acc_dw ? dwr[p.woff + u] + dwv : dwv;
           }
         });
         if (dxc) {
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
                                                 const float* __restrict__ gagg,
                                                 float* __restrict__ dw, float* __restrict__ dxc,
                                                 float* __restrict__ dYacc, int n_centers,
-                                                int split) {
+                                                int split, int acc_dw, int dy_assign) {
   // `split` waves per centre, wave k taking the centre's edges k, k + split, ...
   // (every per-edge output has one writer); split > 1 only when there are few
   // centres (the fine-tune step's batches)
@@ -300,16 +303,19 @@ __global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
       y[q] = Y[(int64_t)e * 9 + q];
       dy[q] = 0.f;
     }
-    pa.edge(lane, e, j, y, w, h, dw, dxc, dy);
-    pb.edge(lane, e, j, y, w, h, dw, dxc, dy);
-    pc.edge(lane, e, j, y, w, h, dw, dxc, dy);
+    pa.edge(lane, e, j, y, w, h, dw, dxc, dy, acc_dw);
+    pb.edge(lane, e, j, y, w, h, dw, dxc, dy, acc_dw);
+    pc.edge(lane, e, j, y, w, h, dw, dxc, dy, acc_dw);
     float mine = 0.f;
 #pragma unroll
     for (int q = 0; q < 9; ++q) {
       const float s = wave_sum(dy[q]);
       if (lane == q) mine = s;
     }
-    if (lane < 9) dYacc[(int64_t)e * 9 + lane] += mine;
+    if (lane < 9) {
+      float* o = dYacc + (int64_t)e * 9 + lane;
+      *o = dy_assign ? mine : *o + mine;
+    }
   }
 }
 
@@ -320,10 +326,10 @@ static hipError_t tp_fwd_impl(const TpArgs& a, hipStream_t s) {
   if (a.n_centers <= 0) return hipSuccess;
   if (a.n_centers < 8192)
     hipLaunchKernelGGL(k_tp_fwd_split<L>, dim3(a.n_centers), dim3(192 * FS), 0, s, a.row_ptr, a.nbr,
-                       a.Y, a.w, a.h, a.agg, a.n_centers, a.denom);
+                       a.Y, a.w, a.h, a.agg, a.n_centers, a.denom, a.acc_out);
   else
     hipLaunchKernelGGL(k_tp_fwd<L>, dim3(a.n_centers), dim3(192), 0, s, a.row_ptr, a.nbr, a.Y, a.w,
-                       a.h, a.agg, a.n_centers, a.denom);
+                       a.h, a.agg, a.n_centers, a.denom, a.acc_out);
   return hipGetLastError();
 }
 template <class L>
@@ -335,7 +341,8 @@ static hipError_t tp_bwd_impl(const TpArgs& a, hipStream_t s) {
   const int split = std::max(1, std::min(32, 32768 / a.n_centers));
   const int64_t waves = (int64_t)a.n_centers * split;
   hipLaunchKernelGGL(k_tp_bwd<L>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a.row_ptr,
-                     a.nbr, a.Y, a.w, a.h, a.gagg, a.dw, a.dxc, a.dYacc, a.n_centers, split);
+                     a.nbr, a.Y, a.w, a.h, a.gagg, a.dw, a.dxc, a.dYacc, a.n_centers, split,
+                     a.acc_out, a.dy_assign);
   return hipGetLastError();
 }
 

@@ -42,6 +42,7 @@ import torch
 
 from . import _keys as KEY
 from . import conv_ops
+from .conv_ops import ACC_DH, ACC_DW, ACC_DY
 
 
 def supported(model):
@@ -509,15 +510,15 @@ class ExplicitStep:
 
         # ---- first reverse: dE/dr per edge (seed dE/d atomic = 1)
         xb = (scale.unsqueeze(-1) * D['r2'][:, 0].unsqueeze(0)) @ D['r1'].t()
-        Yb = torch.zeros_like(g['Y'])
+        Yb = torch.empty_like(g['Y'])         # the last block's launch assigns, the others add
         embb = torch.zeros_like(g['emb'])
         for t in range(len(blocks) - 1, -1, -1):
             b, blk = blocks[t], m.blocks[t]
             yb = self.gates[t].vjp(b['Y'][:n], xb)
             ab = (yb @ D[f'si2{t}'].t()) / b['den']
-            hb, dY, wb = be.backward(blk['kind'], graph, b['H'][:n], g['Y'], b['WT'][:E], ab,
-                                     need_h=t > 0)
-            Yb += dY
+            hb, _, wb = be.backward(blk['kind'], graph, b['H'][:n], g['Y'], b['WT'][:E], ab,
+                                    need_h=t > 0, dY_out=Yb,
+                                    acc=ACC_DY if t < len(blocks) - 1 else 0)
             W0, W1, W2 = b['W']
             a2b = self.p.act_jvp(b['A2'][:E], wb @ W2.t())
             a1b = self.p.act_jvp(b['A1'][:E], a2b @ W1.t())
@@ -580,14 +581,15 @@ class ExplicitStep:
             self.p.act_jvp(A2[:E], A2[E:], out=H2[E:])
             torch.mm(H2[E:], W2, out=WT[E:])
             h, w = b['H'][:n], WT[:E]
-            aggd = be.forward(k, graph, h, Yd, w)
-            aggd += be.forward(k, graph, h, Y, WT[E:])
+            AGG, Yg = b['AGG'], b['Y']
+            aggd = AGG[n:]                       # C(h, Y', w) + C(h, Y, w') + C(h', Y, w)
+            be.forward(k, graph, h, Yd, w, out=aggd)
+            be.forward(k, graph, h, Y, WT[E:], out=aggd, acc=True)
             X = b['X']
             if t > 0:
                 torch.mm(X[n:], D[f'si1{t}'], out=b['H'][n:])
-                aggd += be.forward(k, graph, b['H'][n:], Y, w)
-            AGG, Yg = b['AGG'], b['Y']
-            torch.div(aggd, b['den'], out=AGG[n:])
+                be.forward(k, graph, b['H'][n:], Y, w, out=aggd, acc=True)
+            aggd.div_(b['den'])
             if t > 0:
                 torch.addmm(X[n:] @ D[f'sc{t}'], AGG[n:], D[f'si2{t}'], out=Yg[n:])
             else:
@@ -617,6 +619,7 @@ class ExplicitStep:
         XB = HIDB @ D['r1'].t()               # [x-bar; x'-bar] of the last block's output
         EMBB = torch.zeros(2 * E, 8, device=dev, dtype=dt)
         new = lambda *shape: torch.empty(*shape, device=dev, dtype=dt)   # noqa: E731
+        dYs = new(E, 9)                       # scratch for the unused dY outputs
         for t in range(len(blocks) - 1, -1, -1):
             b, blk = blocks[t], m.blocks[t]
             k = blk['kind']
@@ -635,16 +638,18 @@ class ExplicitStep:
             WT = b['WT']
             w, wd = WT[:E], WT[E:]
             # trilinear agg = C(h, Y, w): B(h', Y', w'; c) = (B_h(Y', w'), B_Y(h', w'), B_w(h', Y'))
+            # (the accumulating launches add into HB / WB; dY is not needed: Y and
+            # Y' do not depend on the parameters)
             HB, WB = new(2 * n, H.shape[1]), new(2 * E, WT.shape[1])
-            be.backward(k, graph, h, Y, w, ab, dh_out=HB[:n], dw_out=WB[:E])      # B_h(Y,w;a), B_w(h,Y;a)
-            t_h, _, t_w = be.backward(k, graph, h, Yd, w, adb)                      # B_h(Y',w), B_w(h,Y')
-            HB[:n] += t_h
-            WB[:E] += t_w
-            t_h, _, _ = be.backward(k, graph, h, Y, wd, adb, dw_out=WB[E:])        # B_h(Y,w'), w'-bar
-            HB[:n] += t_h
+            hb, wb, hdb, wdb = HB[:n], WB[:E], HB[n:], WB[E:]
+            be.backward(k, graph, h, Y, w, ab, dh_out=hb, dw_out=wb, dY_out=dYs)   # B_h(Y,w;a), B_w(h,Y;a)
+            be.backward(k, graph, h, Yd, w, adb, dh_out=hb, dw_out=wb, dY_out=dYs,
+                        acc=ACC_DH | ACC_DW)                                      # + B_h(Y',w), B_w(h,Y')
+            be.backward(k, graph, h, Y, wd, adb, dh_out=hb, dw_out=wdb, dY_out=dYs,
+                        acc=ACC_DH)                                               # + B_h(Y,w'); w'-bar
             if t > 0:
-                _, _, t_w = be.backward(k, graph, hd, Y, w, adb, dh_out=HB[n:])    # h'-bar, B_w(h',Y)
-                WB[:E] += t_w
+                be.backward(k, graph, hd, Y, w, adb, dh_out=hdb, dw_out=wb, dY_out=dYs,
+                            acc=ACC_DW)                                           # h'-bar; + B_w(h',Y)
             else:
                 HB[n:].zero_()                # x0' = 0: no h' (its rows meet zero rows of X)
             # radial MLP, primal and tangent rows together

@@ -30,11 +30,14 @@ class CpuConvBackend:
     def build(self, g, into=None):
         return {} if into is None else into
 
-    def forward(self, kind, g, h, Y, w, out=None):
+    def forward(self, kind, g, h, Y, w, out=None, acc=False):
         agg = self._forward(kind, g, h, Y, w)
         if out is not None:
+            if acc:
+                return out.add_(agg)
             out.copy_(agg)
             return out
+        assert not acc
         return agg
 
     def _forward(self, kind, g, h, Y, w):
@@ -57,7 +60,8 @@ class CpuConvBackend:
         return torch.zeros(g.n_nodes, msg.shape[1], dtype=h.dtype).index_add(
             0, g.edge_center.long(), msg)
 
-    def backward(self, kind, g, h, Y, w, gagg, need_h=True, dh_out=None, dw_out=None):
+    def backward(self, kind, g, h, Y, w, gagg, need_h=True, dh_out=None, dw_out=None,
+                 dY_out=None, acc=0):
         with torch.enable_grad():
             hh, YY, ww = (t.detach().requires_grad_(True) for t in (h, Y, w))
             s = (self._forward(kind, g, hh, YY, ww) * gagg.detach()).sum()
@@ -66,10 +70,16 @@ class CpuConvBackend:
         dh = dh if dh is not None else zero(h)
         dY = dY if dY is not None else zero(Y)
         dw = dw if dw is not None else zero(w)
-        if dw_out is not None:
-            dw = dw_out.copy_(dw)
-        if dh_out is not None and need_h:
-            dh = dh_out.copy_(dh)
+        # accumulation bits as conv_ops.ACC_DH / ACC_DY / ACC_DW
+        def put(buf, v, bit):
+            if buf is None:
+                assert not acc & bit
+                return v
+            return buf.add_(v) if acc & bit else buf.copy_(v)
+        dw = put(dw_out, dw, 4)
+        dY = put(dY_out, dY, 2)
+        if need_h:
+            dh = put(dh_out, dh, 1)
         return (dh if need_h else None), dY, dw
 
 
