@@ -196,6 +196,29 @@ int e3gnn_conv_backward_acc(int kind, int64_t n_nodes, int64_t n_edges, const in
                             const float* gagg, float* dh, float* dY, float* dw, float* dxc,
                             int accumulate, void* stream);
 
+/* The fine-tune step's derivatives of the trilinear agg = C(h, Y, w) along a
+ * tangent (h', Y', w') (train_explicit.py), one launch each:
+ *   tangent forward  agg' (= or += with accumulate & 1)
+ *                    = C(h, Y', w) + C(h, Y, w') + C(h', Y, w);
+ *   dual backward, cotangents (g, g') of (agg, agg'):
+ *     dh  = B_h(Y, w; g) + B_h(Y', w; g') + B_h(Y, w'; g')   dh' = B_h(Y, w; g')
+ *     dw  = B_w(h, Y; g) + B_w(h, Y'; g') + B_w(h', Y; g')   dw' = B_w(h, Y; g')
+ * (B_h / B_w: e3gnn_conv_backward's dh / dw).  hd may be NULL (no h'; then
+ * dhd must be NULL too).  dxc: scratch of [2 n_edges, DX] floats ([n_edges,
+ * DX] without h').  Outputs are overwritten.  Replaces the reference's
+ * autograd double backward of convolution.py:104-123 under
+ * force_output.py:158-215 (create_graph=True, trainer.py:155-222). */
+int e3gnn_conv_tangent_forward(int kind, int64_t n_nodes, const int32_t* row_ptr,
+                               const int32_t* edge_nbr, const float* h, const float* hd,
+                               const float* Y, const float* Yd, const float* w, const float* wd,
+                               float* agg, int accumulate, void* stream);
+int e3gnn_conv_dual_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_t* row_ptr,
+                             const int32_t* edge_nbr, const int32_t* src_ptr,
+                             const int32_t* src_perm, const float* h, const float* hd,
+                             const float* Y, const float* Yd, const float* w, const float* wd,
+                             const float* g, const float* gd, float* dh, float* dhd, float* dw,
+                             float* dwd, float* dxc, void* stream);
+
 /* ---- generic path tables: the convolution of any nequip-family model ----
  * Same contract as e3gnn_conv_forward / _backward (IrrepsConvolution,
  * sevenn/nn/convolution.py:36-123), with the instruction list given at run

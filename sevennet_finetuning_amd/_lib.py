@@ -51,6 +51,9 @@ SIGNATURES = {
                                         _vp]),
     'e3gnn_conv_backward_acc': (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                          _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp]),
+    'e3gnn_conv_tangent_forward': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                            _vp, _vp, _c_int, _vp]),
+    'e3gnn_conv_dual_backward': (_c_int, [_c_int, _c_i64, _c_i64] + [_vp] * 17 + [_vp]),
     'e3gnn_gtp_create': (_vp, [_c_int, _vp, _c_int, _c_int, _c_int, _c_int]),
     'e3gnn_gtp_free': (None, [_vp]),
     'e3gnn_gtp_dims': (_c_int, [_vp, _P(_c_int), _P(_c_int), _P(_c_int), _P(_c_int)]),

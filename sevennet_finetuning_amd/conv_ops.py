@@ -147,6 +147,50 @@ class HipConvBackend:
         return dh, dY, dw
 
 
+    def tangent_forward(self, kind, g, h, hd, Y, Yd, w, wd, out, acc=False):
+        """agg' = C(h, Y', w) + C(h, Y, w') + C(h', Y, w) into ``out`` (added
+        with ``acc``); ``hd`` None: no h' term (e3gnn_conv_tangent_forward)"""
+        self._check(kind, g, h, Y, w)
+        self._check(kind, g, hd if hd is not None else h, Yd, wd)
+        out = _out(out, (g.n_nodes, self.dims[kind][2]), h.device)
+        a = g.aux
+        _lib.check(self.lib.e3gnn_conv_tangent_forward(
+            kind, g.n_nodes, a['row_ptr'].data_ptr(), a['nbr'].data_ptr(), h.data_ptr(),
+            hd.data_ptr() if hd is not None else None, Y.data_ptr(), Yd.data_ptr(), w.data_ptr(),
+            wd.data_ptr(), out.data_ptr(), int(bool(acc)), self._stream(h)))
+        return out
+
+    def dual_backward(self, kind, g, h, hd, Y, Yd, w, wd, ga, gad, dh_out, dhd_out, dw_out,
+                      dwd_out):
+        """The reverse of (agg, agg') for cotangents (ga, gad): writes
+        dh = B_h(Y,w;ga) + B_h(Y',w;gad) + B_h(Y,w';gad), dh' = B_h(Y,w;gad),
+        dw = B_w(h,Y;ga) + B_w(h,Y';gad) + B_w(h',Y;gad), dw' = B_w(h,Y;gad)
+        (``hd`` / ``dhd_out`` None together: no h'); e3gnn_conv_dual_backward"""
+        self._check(kind, g, h, Y, w)
+        self._check(kind, g, hd if hd is not None else h, Yd, wd)
+        if (hd is None) != (dhd_out is None):
+            raise _lib.E3GNNError("dual conv backward: h' and dh' go together")
+        dx, dwd, dm = self.dims[kind]
+        n, E, dev = g.n_nodes, g.n_edges, h.device
+        for t in (ga, gad):
+            if tuple(t.shape) != (n, dm) or t.dtype != torch.float32 or not t.is_contiguous():
+                raise _lib.E3GNNError(f'conv kind {kind}: cotangents must be contiguous float32 '
+                                      f'{(n, dm)}')
+        dh_out, dw_out, dwd_out = (_out(dh_out, (n, dx), dev), _out(dw_out, (E, dwd), dev),
+                                   _out(dwd_out, (E, dwd), dev))
+        if dhd_out is not None:
+            dhd_out = _out(dhd_out, (n, dx), dev)
+        dxc = torch.empty((2 if hd is not None else 1) * max(E, 1), dx, device=dev)
+        a = g.aux
+        ptr = lambda t: t.data_ptr() if t is not None else None   # noqa: E731
+        _lib.check(self.lib.e3gnn_conv_dual_backward(
+            kind, n, E, a['row_ptr'].data_ptr(), a['nbr'].data_ptr(), a['src_ptr'].data_ptr(),
+            a['src_perm'].data_ptr(), h.data_ptr(), ptr(hd), Y.data_ptr(), Yd.data_ptr(),
+            w.data_ptr(), wd.data_ptr(), ga.data_ptr(), gad.data_ptr(), dh_out.data_ptr(),
+            ptr(dhd_out), dw_out.data_ptr(), dwd_out.data_ptr(), dxc.data_ptr(), self._stream(h)))
+        return dh_out, dhd_out, dw_out, dwd_out
+
+
 # accumulation bits of HipConvBackend.backward (e3gnn_conv_backward_acc)
 ACC_DH, ACC_DY, ACC_DW = 1, 2, 4
 

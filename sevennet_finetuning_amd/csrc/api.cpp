@@ -1648,6 +1648,72 @@ int e3gnn_conv_backward_acc(int kind, int64_t n_nodes, int64_t n_edges, const in
   return E3GNN_OK;
 }
 
+int e3gnn_conv_tangent_forward(int kind, int64_t n_nodes, const int32_t* row_ptr,
+                               const int32_t* edge_nbr, const float* h, const float* hd,
+                               const float* Y, const float* Yd, const float* w, const float* wd,
+                               float* agg, int accumulate, void* stream) {
+  int dx, W, dm;
+  if (!conv_kind_dims(kind, &dx, &W, &dm)) return fail(E3GNN_ERR_ARG, "conv kind must be 0, 1 or 2");
+  if (n_nodes <= 0) return E3GNN_OK;
+  if (!row_ptr || !h || !Y || !Yd || !w || !wd || !agg) return fail(E3GNN_ERR_ARG, "null conv operand");
+  TpDualArgs a{};
+  a.row_ptr = row_ptr;
+  a.nbr = edge_nbr;
+  a.Y = Y;
+  a.Yd = Yd;
+  a.w = w;
+  a.wd = wd;
+  a.h = h;
+  a.hd = hd;
+  a.agg = agg;
+  a.n_centers = (int)n_nodes;
+  a.acc_out = accumulate & 1;
+  HIPCHK(launch_tp_fwd_tan(kind, a, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_conv_dual_backward(int kind, int64_t n_nodes, int64_t n_edges, const int32_t* row_ptr,
+                             const int32_t* edge_nbr, const int32_t* src_ptr,
+                             const int32_t* src_perm, const float* h, const float* hd,
+                             const float* Y, const float* Yd, const float* w, const float* wd,
+                             const float* g, const float* gd, float* dh, float* dhd, float* dw,
+                             float* dwd, float* dxc, void* stream) {
+  int dx, W, dm;
+  if (!conv_kind_dims(kind, &dx, &W, &dm)) return fail(E3GNN_ERR_ARG, "conv kind must be 0, 1 or 2");
+  hipStream_t s = (hipStream_t)stream;
+  if (n_nodes <= 0) return E3GNN_OK;
+  if ((hd == nullptr) != (dhd == nullptr))
+    return fail(E3GNN_ERR_ARG, "dual conv backward: h' and dh' go together");
+  if (n_edges <= 0) {
+    HIPCHK(launch_zero(dh, n_nodes * dx, s));
+    if (dhd) HIPCHK(launch_zero(dhd, n_nodes * dx, s));
+    return E3GNN_OK;
+  }
+  if (!row_ptr || !edge_nbr || !src_ptr || !src_perm || !h || !Y || !Yd || !w || !wd || !g || !gd ||
+      !dh || !dw || !dwd || !dxc)
+    return fail(E3GNN_ERR_ARG, "null conv operand");
+  TpDualArgs a{};
+  a.row_ptr = row_ptr;
+  a.nbr = edge_nbr;
+  a.Y = Y;
+  a.Yd = Yd;
+  a.w = w;
+  a.wd = wd;
+  a.h = h;
+  a.hd = hd;
+  a.g = g;
+  a.gd = gd;
+  a.dw = dw;
+  a.dwd = dwd;
+  a.dxc = dxc;
+  a.dxcd = dhd ? dxc + n_edges * dx : nullptr;
+  a.n_centers = (int)n_nodes;
+  HIPCHK(launch_tp_bwd_dual(kind, a, s));
+  HIPCHK(launch_gather_rows((int)n_nodes, dx, src_ptr, src_perm, dxc, dh, s, 0));
+  if (dhd) HIPCHK(launch_gather_rows((int)n_nodes, dx, src_ptr, src_perm, a.dxcd, dhd, s, 0));
+  return E3GNN_OK;
+}
+
 // ------------------------------------------------------------ generic path tables
 // (gtp.hip): the convolution of any nequip-family model from its instruction list
 namespace {

@@ -243,6 +243,56 @@ __device__ __forceinline__ void nl_epilogue(const NlProb& P, const f32x16& acc, 
   }
 }
 
+// Epilogue for plain / accumulating outputs (epi 0 / 1): the accumulators
+// are written to LDS in the OUTPUT's memory order (node, column * R + m), so
+// the copy-out is one b128 LDS read + one b128 store per 4 floats with no
+// per-element index arithmetic (the generic epilogue above spent ~0.5 VALU
+// instructions per output float on it: the si2^T launches are 1.2 GB of
+// output).  Starts with a barrier: the caller's LDS readers are done.
+#ifndef E3GNN_NL_RUNS
+#define E3GNN_NL_RUNS 1
+#endif
+template <int WN, int R>
+__device__ __forceinline__ void nl_epilogue_runs(const NlProb& P, const f32x16& acc, int node0,
+                                                 int n0, float* lds) {
+  constexpr int BM = 128 / WN, CW = 32 * WN;
+  constexpr int T = BM / R, ROWS = T * R;
+  constexpr int RUN = CW * R, LDR = RUN + 4;  // 16-byte aligned node runs
+  static_assert(T * LDR <= NL_LDS, "C runs must fit the LDS stages");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  __syncthreads();
+  const int cR = (wc * 32 + (lane & 31)) * R;
+  const int rbase = wr * 32 + 4 * (lane >> 5);
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = rbase + (reg & 3) + 8 * (reg >> 2);
+    const int nl = row / R, m = row - nl * R;
+    if (row < ROWS) lds[nl * LDR + cR + m] = acc[reg];
+  }
+  __syncthreads();
+  const int ncol = P.N - n0 < CW ? P.N - n0 : CW;  // a multiple of 4 (add_nl)
+  if (ncol <= 0) return;
+  const int len = ncol * R;
+  constexpr int SEGC = RUN / 4, UC = T * SEGC;
+#pragma unroll 1
+  for (int u = tid; u < UC; u += 256) {
+    const int nl = u / SEGC, j = 4 * (u - nl * SEGC);
+    const int node = node0 + nl;
+    if (j >= len || node >= P.nodes) continue;
+    float4 v = *reinterpret_cast<const float4*>(lds + nl * LDR + j);
+    float4* cp = reinterpret_cast<float4*>(P.C + (int64_t)node * P.ldc + P.c_off + n0 * R + j);
+    if (P.epi == 1) {
+      const float4 o = *cp;
+      v.x += o.x;
+      v.y += o.y;
+      v.z += o.z;
+      v.w += o.w;
+    }
+    *cp = v;
+  }
+}
+
 template <int WN, int NS, int R>
 __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) {
   using S = NlShape<WN, NS>;
@@ -364,7 +414,12 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
       for (int i = 0; i < 16; ++i) acc[sub][i] += acc2[sub][i];
   }
 #pragma unroll
-  for (int sub = 0; sub < NS; ++sub) nl_epilogue<WN, R>(P, acc[sub], node0, n0 + sub * 32 * WN, lds);
+  for (int sub = 0; sub < NS; ++sub) {
+    if (E3GNN_NL_RUNS && P.epi <= 1)
+      nl_epilogue_runs<WN, R>(P, acc[sub], node0, n0 + sub * 32 * WN, lds);
+    else
+      nl_epilogue<WN, R>(P, acc[sub], node0, n0 + sub * 32 * WN, lds);
+  }
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_NL_WAVES, 8))) void
@@ -375,7 +430,10 @@ k_nodelin(NlBatch batch) {
 #pragma unroll 1
   for (int i = 1; i < batch.nprob; ++i)
     if (tile >= batch.p[i].tile_begin) pi = i;
-  const NlProb& P = batch.p[pi];
+  NlProb P = batch.p[0];
+  if (pi == 1) P = batch.p[1];
+  if (pi == 2) P = batch.p[2];
+  if (pi == 3) P = batch.p[3];
   const int local = tile - P.tile_begin;
   if (P.wn == 1) {
     switch (P.R) {

@@ -59,7 +59,31 @@ struct TpArgs {
   int dy_assign = 0;   // bwd: dY = (instead of the default +=: no zeroing launch)
 };
 
+// The fine-tune step's derivatives of the trilinear agg = C(h, Y, w) along a
+// tangent (h', Y', w') (train_explicit.py): one launch each instead of three
+// forward / four backward ones.
+//   tangent forward:  agg' (=, += with acc_out) = C(h, Y', w) + C(h, Y, w') + C(h', Y, w)
+//   dual backward, cotangents (g, g') of (agg, agg'):
+//     dxc  = B_h(Y, w; g) + B_h(Y', w; g') + B_h(Y, w'; g')   -> dh  (gathered)
+//     dxcd = B_h(Y, w; g')                                     -> dh' (gathered)
+//     dw   = B_w(h, Y; g) + B_w(h, Y'; g') + B_w(h', Y; g')
+//     dwd  = B_w(h, Y; g')
+// h' may be null (the first block's input has no tangent): its terms vanish.
+struct TpDualArgs {
+  const int* row_ptr;
+  const int* nbr;
+  const float *Y, *Yd, *w, *wd, *h, *hd;
+  float* agg;                  // tangent forward out [n_centers, DM]
+  const float *g, *gd;         // dual backward in [n_centers, DM]
+  float *dw, *dwd;             // [E, W]
+  float *dxc, *dxcd;           // [E, DX] (dxcd null when hd is)
+  int n_centers;
+  int acc_out = 0;
+};
+
 hipError_t launch_tp_fwd(int kind, const TpArgs& a, hipStream_t s);
+hipError_t launch_tp_fwd_tan(int kind, const TpDualArgs& a, hipStream_t s);
+hipError_t launch_tp_bwd_dual(int kind, const TpDualArgs& a, hipStream_t s);
 hipError_t launch_tp_bwd(int kind, const TpArgs& a, hipStream_t s);
 
 }  // namespace e3gnn

@@ -319,6 +319,244 @@ __global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
   }
 }
 
+// ------------------------------------------------------------------ dual
+// Tangent forward of one input irrep part: per path
+//   acc_k += w sum_ij C (x_i y'_j + x'_i y_j) + w' sum_ij C x_i y_j
+template <class L, int L1>
+__device__ __forceinline__ void fwd_tan_part(int lane, int beg, int end,
+                                             const int* __restrict__ nbr, const TpDualArgs& a,
+                                             float* __restrict__ out, int k0, int ks) {
+  constexpr int MUL = part_mul<L, L1>();
+  if constexpr (MUL == 0) {
+    return;
+  } else {
+    constexpr int D1 = 2 * L1 + 1;
+    constexpr int XOFF = part_xoff<L, L1>();
+    constexpr bool PAIR = MUL == 32;
+    constexpr int UPL = MUL == 128 ? 2 : 1;
+    const bool has_xd = a.hd != nullptr;
+    float acc[L::NP][UPL][5];
+    static_for<L::NP>([&](auto pi) {
+#pragma unroll
+      for (int s = 0; s < UPL; ++s)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) acc[pi][s][k] = 0.f;
+    });
+    const int u0 = PAIR ? (lane & 31) : lane;
+    constexpr int STEP = PAIR ? 2 : 1;
+    for (int e0 = beg + k0 * STEP; e0 < end; e0 += STEP * ks) {
+      const int e = PAIR ? e0 + (lane >> 5) : e0;
+      if (PAIR && e >= end) continue;
+      const int j = nbr[e];
+      float y[9], yd[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        y[q] = a.Y[(int64_t)e * 9 + q];
+        yd[q] = a.Yd[(int64_t)e * 9 + q];
+      }
+      const float* wr = a.w + (int64_t)e * L::W;
+      const float* wdr = a.wd + (int64_t)e * L::W;
+#pragma unroll
+      for (int s = 0; s < UPL; ++s) {
+        const int u = u0 + 64 * s;
+        float x[D1], xd[D1];
+#pragma unroll
+        for (int i = 0; i < D1; ++i) {
+          x[i] = a.h[(int64_t)j * L::DX + XOFF + u * D1 + i];
+          xd[i] = has_xd ? a.hd[(int64_t)j * L::DX + XOFF + u * D1 + i] : 0.f;
+        }
+        static_for<L::NP>([&](auto pi) {
+          constexpr PathDef p = L::P[pi];
+          if constexpr (p.l1 == L1) {
+            using C = CG<p.l1, p.l2, p.l3>;
+            constexpr int D3 = 2 * p.l3 + 1;
+            const float* yy = y + yoff(p.l2);
+            const float* yyd = yd + yoff(p.l2);
+            float ta[D3], tb[D3];
+#pragma unroll
+            for (int k = 0; k < D3; ++k) ta[k] = tb[k] = 0.f;
+#pragma unroll
+            for (int q = 0; q < C::n; ++q) {
+              const int i = C::e[q].i, jj = C::e[q].j, k = C::e[q].k;
+              ta[k] += C::e[q].c * (x[i] * yyd[jj] + xd[i] * yy[jj]);
+              tb[k] += C::e[q].c * (x[i] * yy[jj]);
+            }
+            const float wv = wr[p.woff + u], wdv = wdr[p.woff + u];
+#pragma unroll
+            for (int k = 0; k < D3; ++k) acc[pi][s][k] += wv * ta[k] + wdv * tb[k];
+          }
+        });
+      }
+    }
+    static_for<L::NP>([&](auto pi) {
+      constexpr PathDef p = L::P[pi];
+      if constexpr (p.l1 == L1) {
+        constexpr int D3 = 2 * p.l3 + 1;
+#pragma unroll
+        for (int s = 0; s < UPL; ++s) {
+#pragma unroll
+          for (int k = 0; k < D3; ++k) {
+            float v = acc[pi][s][k];
+            if (PAIR) v += __shfl_down(v, 32, 64);
+            if (!PAIR || lane < 32) out[p.moff + (u0 + 64 * s) * D3 + k] = v;
+          }
+        }
+      }
+    });
+  }
+}
+
+// FS waves per input irrep share a centre's edges; partial rows summed in a
+// fixed order through LDS (as k_tp_fwd_split)
+template <class L>
+__global__ __launch_bounds__(192 * FS) void k_tp_fwd_tan(TpDualArgs a) {
+  __shared__ float red[FS][L::DM];
+  const int c = blockIdx.x;
+  if (c >= a.n_centers) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int part = wave % 3, k0 = wave / 3;
+  const int lane = threadIdx.x & 63;
+  const int beg = a.row_ptr[c], end = a.row_ptr[c + 1];
+  if (part == 0) fwd_tan_part<L, 0>(lane, beg, end, a.nbr, a, red[k0], k0, FS);
+  else if (part == 1) fwd_tan_part<L, 1>(lane, beg, end, a.nbr, a, red[k0], k0, FS);
+  else fwd_tan_part<L, 2>(lane, beg, end, a.nbr, a, red[k0], k0, FS);
+  // (the parts' paths cover every message slot of a row: no zeroing)
+  __syncthreads();
+  float* out = a.agg + (int64_t)c * L::DM;
+  for (int i = threadIdx.x; i < L::DM; i += blockDim.x) {
+    float v = red[0][i];
+#pragma unroll
+    for (int k = 1; k < FS; ++k) v += red[k][i];
+    out[i] = a.acc_out ? out[i] + v : v;
+  }
+}
+
+// Dual backward of one input irrep part over one edge: with cg = C g_k,
+// cgd = C g'_k per CG entry (i, j, k):
+//   dw  += cg x_i y_j + cgd (x_i y'_j + x'_i y_j)     dwd += cgd x_i y_j
+//   dx_i += w (cg y_j + cgd y'_j) + w' cgd y_j         dxd_i += w cgd y_j
+template <class L, int L1>
+struct DualPart {
+  static constexpr int MUL = part_mul<L, L1>();
+  static constexpr int D1 = 2 * L1 + 1;
+  static constexpr int XOFF = part_xoff<L, L1>();
+  static constexpr int UPL = MUL == 128 ? 2 : 1;
+  float g[L::NP][UPL][5], gd[L::NP][UPL][5];
+
+  __device__ __forceinline__ void load(int lane, const float* __restrict__ gc,
+                                       const float* __restrict__ gdc) {
+    const int u0 = MUL == 32 ? (lane & 31) : lane;
+    static_for<L::NP>([&](auto pi) {
+      constexpr PathDef p = L::P[pi];
+      if constexpr (p.l1 == L1) {
+        constexpr int D3 = 2 * p.l3 + 1;
+#pragma unroll
+        for (int s = 0; s < UPL; ++s)
+#pragma unroll
+          for (int k = 0; k < D3; ++k) {
+            g[pi][s][k] = gc[p.moff + (u0 + 64 * s) * D3 + k];
+            gd[pi][s][k] = gdc[p.moff + (u0 + 64 * s) * D3 + k];
+          }
+      }
+    });
+  }
+
+  __device__ __forceinline__ void edge(int lane, int64_t e, int j, const float* y, const float* yd,
+                                       const TpDualArgs& a) {
+    if (MUL == 32 && lane >= 32) return;
+    const float* wr = a.w + e * L::W;
+    const float* wdr = a.wd + e * L::W;
+    const bool has_xd = a.hd != nullptr;
+#pragma unroll
+    for (int s = 0; s < UPL; ++s) {
+      const int u = lane + 64 * s;
+      float x[D1], xd[D1], dx[D1], dxd[D1];
+#pragma unroll
+      for (int i = 0; i < D1; ++i) {
+        x[i] = a.h[(int64_t)j * L::DX + XOFF + u * D1 + i];
+        xd[i] = has_xd ? a.hd[(int64_t)j * L::DX + XOFF + u * D1 + i] : 0.f;
+        dx[i] = dxd[i] = 0.f;
+      }
+      static_for<L::NP>([&](auto pi) {
+        constexpr PathDef p = L::P[pi];
+        if constexpr (p.l1 == L1) {
+          using C = CG<p.l1, p.l2, p.l3>;
+          const float* yy = y + yoff(p.l2);
+          const float* yyd = yd + yoff(p.l2);
+          const float wv = wr[p.woff + u], wdv = wdr[p.woff + u];
+          float dwv = 0.f, dwdv = 0.f;
+#pragma unroll
+          for (int q = 0; q < C::n; ++q) {
+            const int i = C::e[q].i, jj = C::e[q].j, k = C::e[q].k;
+            const float cg = C::e[q].c * g[pi][s][k], cgd = C::e[q].c * gd[pi][s][k];
+            const float xy = x[i] * yy[jj];
+            dwv += cg * xy + cgd * (x[i] * yyd[jj] + xd[i] * yy[jj]);
+            dwdv += cgd * xy;
+            dx[i] += wv * (cg * yy[jj] + cgd * yyd[jj]) + wdv * (cgd * yy[jj]);
+            dxd[i] += wv * (cgd * yy[jj]);
+          }
+          a.dw[e * L::W + p.woff + u] = dwv;
+          a.dwd[e * L::W + p.woff + u] = dwdv;
+        }
+      });
+#pragma unroll
+      for (int i = 0; i < D1; ++i) {
+        a.dxc[e * L::DX + XOFF + u * D1 + i] = dx[i];
+        if (a.dxcd) a.dxcd[e * L::DX + XOFF + u * D1 + i] = dxd[i];
+      }
+    }
+  }
+};
+
+template <class L>
+constexpr int n_parts() {
+  return (part_mul<L, 0>() > 0) + (part_mul<L, 1>() > 0) + (part_mul<L, 2>() > 0);
+}
+
+// wave -> (centre, edge split k0, input irrep part): the parts write disjoint
+// slices of every per-edge output, so each edge's outputs have one writer
+template <class L>
+__global__ __launch_bounds__(256) void k_tp_bwd_dual(TpDualArgs a, int split) {
+  constexpr int NPART = n_parts<L>();
+  static_assert(part_mul<L, 0>() > 0 && (NPART == 1 || NPART == 3), "parts are l1 = 0 .. NPART-1");
+  const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int part = wg % NPART, rest = wg / NPART;
+  const int c = rest / split, k0 = rest - c * split;
+  if (c >= a.n_centers) return;
+  const int lane = threadIdx.x & 63;
+  const int beg = a.row_ptr[c], end = a.row_ptr[c + 1];
+  const float* gc = a.g + (int64_t)c * L::DM;
+  const float* gdc = a.gd + (int64_t)c * L::DM;
+  auto run = [&](auto& P) {
+    P.load(lane, gc, gdc);
+    for (int e = beg + k0; e < end; e += split) {
+      const int j = a.nbr[e];
+      float y[9], yd[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        y[q] = a.Y[(int64_t)e * 9 + q];
+        yd[q] = a.Yd[(int64_t)e * 9 + q];
+      }
+      P.edge(lane, e, j, y, yd, a);
+    }
+  };
+  if constexpr (NPART == 1) {
+    DualPart<L, 0> p0;
+    run(p0);
+  } else {
+    if (part == 0) {
+      DualPart<L, 0> p0;
+      run(p0);
+    } else if (part == 1) {
+      DualPart<L, 1> p1;
+      run(p1);
+    } else {
+      DualPart<L, 2> p2;
+      run(p2);
+    }
+  }
+}
+
 }  // namespace
 
 template <class L>
@@ -344,6 +582,35 @@ static hipError_t tp_bwd_impl(const TpArgs& a, hipStream_t s) {
                      a.nbr, a.Y, a.w, a.h, a.gagg, a.dw, a.dxc, a.dYacc, a.n_centers, split,
                      a.acc_out, a.dy_assign);
   return hipGetLastError();
+}
+
+template <class L>
+static hipError_t tp_fwd_tan_impl(const TpDualArgs& a, hipStream_t s) {
+  if (a.n_centers <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tp_fwd_tan<L>, dim3(a.n_centers), dim3(192 * FS), 0, s, a);
+  return hipGetLastError();
+}
+template <class L>
+static hipError_t tp_bwd_dual_impl(const TpDualArgs& a, hipStream_t s) {
+  if (a.n_centers <= 0) return hipSuccess;
+  const int split = std::max(1, std::min(32, 32768 / a.n_centers));
+  const int64_t waves = (int64_t)a.n_centers * split * n_parts<L>();
+  hipLaunchKernelGGL(k_tp_bwd_dual<L>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a, split);
+  return hipGetLastError();
+}
+hipError_t launch_tp_fwd_tan(int kind, const TpDualArgs& a, hipStream_t s) {
+  switch (kind) {
+    case 0: return tp_fwd_tan_impl<LayerFirst>(a, s);
+    case 1: return tp_fwd_tan_impl<LayerMid>(a, s);
+    default: return tp_fwd_tan_impl<LayerLast>(a, s);
+  }
+}
+hipError_t launch_tp_bwd_dual(int kind, const TpDualArgs& a, hipStream_t s) {
+  switch (kind) {
+    case 0: return tp_bwd_dual_impl<LayerFirst>(a, s);
+    case 1: return tp_bwd_dual_impl<LayerMid>(a, s);
+    default: return tp_bwd_dual_impl<LayerLast>(a, s);
+  }
 }
 
 hipError_t launch_tp_fwd(int kind, const TpArgs& a, hipStream_t s) {

@@ -565,6 +565,9 @@ class ExplicitStep:
                                  c[:, 1] * r[:, 1] + c[:, 3] * r[:, 0],
                                  c[:, 2] * r[:, 2] + c[:, 4] * r[:, 1]], 1)
         # ---- tangent forward along v (second halves of the stacked buffers)
+        # (fused: the backend's one-launch tangent forward / dual backward of
+        # the convolution; the generic engine's backend composes them)
+        fused = hasattr(be, 'dual_backward') and hasattr(be, 'tangent_forward')
         Yd, embd, rd = self.geo.jvp(g, v)
         EMB = S['EMB']
         EMB[E:].copy_(embd)
@@ -583,12 +586,17 @@ class ExplicitStep:
             h, w = b['H'][:n], WT[:E]
             AGG, Yg = b['AGG'], b['Y']
             aggd = AGG[n:]                       # C(h, Y', w) + C(h, Y, w') + C(h', Y, w)
-            be.forward(k, graph, h, Yd, w, out=aggd)
-            be.forward(k, graph, h, Y, WT[E:], out=aggd, acc=True)
             X = b['X']
             if t > 0:
                 torch.mm(X[n:], D[f'si1{t}'], out=b['H'][n:])
-                be.forward(k, graph, b['H'][n:], Y, w, out=aggd, acc=True)
+            hd = b['H'][n:] if t > 0 else None   # x0' = 0: no h' term
+            if fused:
+                be.tangent_forward(k, graph, h, hd, Y, Yd, w, WT[E:], out=aggd)
+            else:
+                be.forward(k, graph, h, Yd, w, out=aggd)
+                be.forward(k, graph, h, Y, WT[E:], out=aggd, acc=True)
+                if hd is not None:
+                    be.forward(k, graph, hd, Y, w, out=aggd, acc=True)
             aggd.div_(b['den'])
             if t > 0:
                 torch.addmm(X[n:] @ D[f'sc{t}'], AGG[n:], D[f'si2{t}'], out=Yg[n:])
@@ -642,15 +650,19 @@ class ExplicitStep:
             # Y' do not depend on the parameters)
             HB, WB = new(2 * n, H.shape[1]), new(2 * E, WT.shape[1])
             hb, wb, hdb, wdb = HB[:n], WB[:E], HB[n:], WB[E:]
-            be.backward(k, graph, h, Y, w, ab, dh_out=hb, dw_out=wb, dY_out=dYs)   # B_h(Y,w;a), B_w(h,Y;a)
-            be.backward(k, graph, h, Yd, w, adb, dh_out=hb, dw_out=wb, dY_out=dYs,
-                        acc=ACC_DH | ACC_DW)                                      # + B_h(Y',w), B_w(h,Y')
-            be.backward(k, graph, h, Y, wd, adb, dh_out=hb, dw_out=wdb, dY_out=dYs,
-                        acc=ACC_DH)                                               # + B_h(Y,w'); w'-bar
-            if t > 0:
-                be.backward(k, graph, hd, Y, w, adb, dh_out=hdb, dw_out=wb, dY_out=dYs,
-                            acc=ACC_DW)                                           # h'-bar; + B_w(h',Y)
+            if fused:                         # the four products below in one launch
+                be.dual_backward(k, graph, h, hd if t > 0 else None, Y, Yd, w, wd, ab, adb,
+                                 hb, hdb if t > 0 else None, wb, wdb)
             else:
+                be.backward(k, graph, h, Y, w, ab, dh_out=hb, dw_out=wb, dY_out=dYs)  # B_h(Y,w;a), B_w(h,Y;a)
+                be.backward(k, graph, h, Yd, w, adb, dh_out=hb, dw_out=wb, dY_out=dYs,
+                            acc=ACC_DH | ACC_DW)                                     # + B_h(Y',w), B_w(h,Y')
+                be.backward(k, graph, h, Y, wd, adb, dh_out=hb, dw_out=wdb, dY_out=dYs,
+                            acc=ACC_DH)                                              # + B_h(Y,w'); w'-bar
+                if t > 0:
+                    be.backward(k, graph, hd, Y, w, adb, dh_out=hdb, dw_out=wb, dY_out=dYs,
+                                acc=ACC_DW)                                          # h'-bar; + B_w(h',Y)
+            if t == 0:
                 HB[n:].zero_()                # x0' = 0: no h' (its rows meet zero rows of X)
             # radial MLP, primal and tangent rows together
             W0, W1, W2 = b['W']

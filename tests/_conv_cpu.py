@@ -83,6 +83,37 @@ class CpuConvBackend:
         return (dh if need_h else None), dY, dw
 
 
+def _tangent_forward(self, kind, g, h, hd, Y, Yd, w, wd, out, acc=False):
+    """the fused tangent forward as its three trilinear terms (the HIP
+    e3gnn_conv_tangent_forward's definition)"""
+    t = self._forward(kind, g, h, Yd, w) + self._forward(kind, g, h, Y, wd)
+    if hd is not None:
+        t = t + self._forward(kind, g, hd, Y, w)
+    return out.add_(t) if acc else out.copy_(t)
+
+
+def _dual_backward(self, kind, g, h, hd, Y, Yd, w, wd, ga, gad, dh_out, dhd_out, dw_out, dwd_out):
+    """the fused dual backward as four backward products (the HIP
+    e3gnn_conv_dual_backward's definition)"""
+    dh, _, dw = self.backward(kind, g, h, Y, w, ga)
+    t_h, _, t_w = self.backward(kind, g, h, Yd, w, gad)
+    dh, dw = dh + t_h, dw + t_w
+    t_h, _, dwd = self.backward(kind, g, h, Y, wd, gad)
+    dh = dh + t_h
+    if hd is not None:
+        dhd, _, t_w = self.backward(kind, g, hd, Y, w, gad)
+        dw = dw + t_w
+        dhd_out.copy_(dhd)
+    dh_out.copy_(dh)
+    dw_out.copy_(dw)
+    dwd_out.copy_(dwd)
+    return dh_out, dhd_out, dw_out, dwd_out
+
+
+CpuConvBackend.tangent_forward = _tangent_forward
+CpuConvBackend.dual_backward = _dual_backward
+
+
 class GenericCpuConvBackend:
     """CPU double of conv_ops.GenericHipConvBackend: the runtime path tables
     (nn.path_table rows: l1, l2, l3, mul, x/Y/w/agg offsets) evaluated with
@@ -113,4 +144,5 @@ class GenericCpuConvBackend:
             msg = msg.index_add(1, torch.arange(mo, mo + mul * (2 * l3 + 1)), m.reshape(e, -1))
         return torch.zeros(g.n_nodes, dm, dtype=h.dtype).index_add(0, g.edge_center.long(), msg)
 
+    _forward = forward
     backward = CpuConvBackend.backward

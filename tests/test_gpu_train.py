@@ -86,6 +86,54 @@ def test_conv_op_first_and_second_derivatives(hip_backend, kind):
         assert _rel(a, b) < 2e-5
 
 
+@pytest.mark.parametrize('kind', [0, 1, 2])
+@pytest.mark.parametrize('with_hd', [True, False])
+def test_fused_tangent_forward_and_dual_backward(hip_backend, kind, with_hd):
+    """e3gnn_conv_tangent_forward / e3gnn_conv_dual_backward (one launch each)
+    against their definition -- three forward / four backward products --
+    on the fp64 CPU double, over a ragged graph (isolated centres, a 40-edge
+    centre, repeated neighbours); plus the accumulating forward / backward."""
+    center, nbr, (h, Y, w), g, (hd, Yd, wd) = _problem(kind, hip_backend.dims, seed=10 + kind)
+    gd = np.random.default_rng(99).normal(size=g.shape)
+    cpu = CpuConvBackend()
+    n, E = len(g), len(center)
+    dx, dwd, dm = hip_backend.dims[kind]
+    gc = conv_ops.ConvGraph(n, torch.tensor(center), torch.tensor(nbr), cpu)
+    gh = conv_ops.ConvGraph(n, torch.tensor(center, device=DEV), torch.tensor(nbr, device=DEV),
+                            hip_backend)
+    T64 = lambda a: torch.tensor(a, dtype=torch.float64)                     # noqa: E731
+    T32 = lambda a: torch.tensor(a, dtype=torch.float32, device=DEV)         # noqa: E731
+    hd_c = T64(hd) if with_hd else None
+    hd_h = T32(hd) if with_hd else None
+    ref = cpu.tangent_forward(kind, gc, T64(h), hd_c, T64(Y), T64(Yd), T64(w), T64(wd),
+                              out=torch.empty(n, dm, dtype=torch.float64))
+    got = hip_backend.tangent_forward(kind, gh, T32(h), hd_h, T32(Y), T32(Yd), T32(w), T32(wd),
+                                      out=torch.empty(n, dm, device=DEV))
+    assert _rel(got, ref) < 2e-5
+    base = T32(g)
+    hip_backend.tangent_forward(kind, gh, T32(h), hd_h, T32(Y), T32(Yd), T32(w), T32(wd),
+                                out=base, acc=True)
+    assert _rel(base, ref + T64(g)) < 2e-5
+    z = lambda *sh: torch.empty(*sh, dtype=torch.float64)                    # noqa: E731
+    r = cpu.dual_backward(kind, gc, T64(h), hd_c, T64(Y), T64(Yd), T64(w), T64(wd), T64(g),
+                          T64(gd), z(n, dx), z(n, dx) if with_hd else None, z(E, dwd), z(E, dwd))
+    e = lambda *sh: torch.empty(*sh, device=DEV)                             # noqa: E731
+    o = hip_backend.dual_backward(kind, gh, T32(h), hd_h, T32(Y), T32(Yd), T32(w), T32(wd),
+                                  T32(g), T32(gd), e(n, dx), e(n, dx) if with_hd else None,
+                                  e(E, dwd), e(E, dwd))
+    for a, b in zip(o, r):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert _rel(a, b) < 2e-5
+    # accumulating single products: dh += , dY += , dw +=
+    dh0, dY0, dw0 = T32(hd), T32(Yd), T32(wd)
+    hip_backend.backward(kind, gh, T32(h), T32(Y), T32(w), T32(g), dh_out=dh0, dY_out=dY0,
+                         dw_out=dw0, acc=conv_ops.ACC_DH | conv_ops.ACC_DY | conv_ops.ACC_DW)
+    rh, rY, rw = cpu.backward(kind, gc, T64(h), T64(Y), T64(w), T64(g))
+    for a, b in ((dh0, rh + T64(hd)), (dY0, rY + T64(Yd)), (dw0, rw + T64(wd))):
+        assert _rel(a, b) < 2e-5
+
+
 def test_conv_graph_rejects_unsorted(hip_backend):
     from sevennet_finetuning_amd._lib import E3GNNError
     with pytest.raises(E3GNNError, match='not sorted'):
