@@ -196,6 +196,36 @@ int e3gnn_conv_backward_acc(int kind, int64_t n_nodes, int64_t n_edges, const in
                             const float* gagg, float* dh, float* dY, float* dw, float* dxc,
                             int accumulate, void* stream);
 
+/* Edge geometry of the fine-tune step (train_explicit.py), float32, one thread
+ * per edge; raw_sh as the model's sh_normalize == false:
+ *   e3gnn_edge_geometry      Y [E, 9], emb [E, 8] (EdgeEmbedding.forward,
+ *                            edge_embedding.py:220-230; as e3gnn_energy_forces)
+ *   e3gnn_edge_geometry_vjp  fij [E, 3] = dE/dr_e from dE/dY, dE/demb
+ *                            (force_output.py:158-215's autograd.grad)
+ *   e3gnn_edge_geometry_jvp  the tangent along v_e = cF[center] - cF[nbr]
+ *                            - (c0 r0 + c5 r2, c1 r1 + c3 r0, c2 r2 + c4 r1),
+ *                            c = cS[batch[nbr]] / vol[batch[nbr]] (cS, batch,
+ *                            vol NULL: no stress term): Yd [E, 9], embd [E, 8],
+ *                            rd [E] = r_hat . v
+ *   e3gnn_edge_geometry_coeff_grad  out [E, 8]: per-edge d/dc_n of
+ *                            <embb, emb> + <embdb, emb'> (Bessel coefficients)
+ *   e3gnn_edge_forces_to_atoms  F_i = sum_{centre i} fij - sum_{nbr i} fij
+ *                            over the CSR of e3gnn_conv_graph (fixed order) */
+int e3gnn_edge_geometry(int64_t n_edges, const float* vec, const float* coeffs, float rc, float ron,
+                        int raw_sh, float* Y, float* emb, void* stream);
+int e3gnn_edge_geometry_jvp(int64_t n_edges, const float* vec, const float* coeffs, float rc,
+                            float ron, int raw_sh, const int32_t* center, const int32_t* nbr,
+                            const int64_t* batch, const float* cF, const float* cS,
+                            const float* vol, float* Yd, float* embd, float* rd, void* stream);
+int e3gnn_edge_geometry_vjp(int64_t n_edges, const float* vec, const float* coeffs, float rc,
+                            float ron, int raw_sh, const float* Yb, const float* embb, float* fij,
+                            void* stream);
+int e3gnn_edge_geometry_coeff_grad(int64_t n_edges, const float* vec, const float* coeffs, float rc,
+                                   float ron, const float* embb, const float* embdb, const float* rd,
+                                   float* out, void* stream);
+int e3gnn_edge_forces_to_atoms(int64_t n_nodes, const int32_t* row_ptr, const int32_t* src_ptr,
+                               const int32_t* src_perm, const float* fij, float* F, void* stream);
+
 /* The fine-tune step's derivatives of the trilinear agg = C(h, Y, w) along a
  * tangent (h', Y', w') (train_explicit.py), one launch each:
  *   tangent forward  agg' (= or += with accumulate & 1)

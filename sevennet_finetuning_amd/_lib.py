@@ -54,6 +54,11 @@ SIGNATURES = {
     'e3gnn_conv_tangent_forward': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                             _vp, _vp, _c_int, _vp]),
     'e3gnn_conv_dual_backward': (_c_int, [_c_int, _c_i64, _c_i64] + [_vp] * 17 + [_vp]),
+    'e3gnn_edge_geometry': (_c_int, [_c_i64, _vp, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp]),
+    'e3gnn_edge_geometry_jvp': (_c_int, [_c_i64, _vp, _vp, _c_f, _c_f, _c_int] + [_vp] * 10),
+    'e3gnn_edge_geometry_vjp': (_c_int, [_c_i64, _vp, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp, _vp]),
+    'e3gnn_edge_geometry_coeff_grad': (_c_int, [_c_i64, _vp, _vp, _c_f, _c_f] + [_vp] * 5),
+    'e3gnn_edge_forces_to_atoms': (_c_int, [_c_i64] + [_vp] * 6),
     'e3gnn_gtp_create': (_vp, [_c_int, _vp, _c_int, _c_int, _c_int, _c_int]),
     'e3gnn_gtp_free': (None, [_vp]),
     'e3gnn_gtp_dims': (_c_int, [_vp, _P(_c_int), _P(_c_int), _P(_c_int), _P(_c_int)]),

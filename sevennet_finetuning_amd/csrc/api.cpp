@@ -1648,6 +1648,58 @@ int e3gnn_conv_backward_acc(int kind, int64_t n_nodes, int64_t n_edges, const in
   return E3GNN_OK;
 }
 
+// ------------------------------------------------------------ fine-tune edge geometry
+int e3gnn_edge_geometry(int64_t n_edges, const float* vec, const float* coeffs, float rc, float ron,
+                        int raw_sh, float* Y, float* emb, void* stream) {
+  if (n_edges <= 0) return E3GNN_OK;
+  if (!vec || !coeffs || !Y || !emb) return fail(E3GNN_ERR_ARG, "null edge geometry operand");
+  HIPCHK(launch_edge_embed(n_edges, vec, coeffs, rc, ron, raw_sh, Y, emb, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_edge_geometry_jvp(int64_t n_edges, const float* vec, const float* coeffs, float rc,
+                            float ron, int raw_sh, const int32_t* center, const int32_t* nbr,
+                            const int64_t* batch, const float* cF, const float* cS,
+                            const float* vol, float* Yd, float* embd, float* rd, void* stream) {
+  if (n_edges <= 0) return E3GNN_OK;
+  if (!vec || !coeffs || !center || !nbr || !cF || !Yd || !embd || !rd ||
+      (cS && (!batch || !vol)))
+    return fail(E3GNN_ERR_ARG, "null edge geometry operand");
+  HIPCHK(launch_edge_geom_jvp(n_edges, vec, coeffs, rc, ron, raw_sh, center, nbr, batch, cF, cS, vol,
+                              Yd, embd, rd, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_edge_geometry_vjp(int64_t n_edges, const float* vec, const float* coeffs, float rc,
+                            float ron, int raw_sh, const float* Yb, const float* embb, float* fij,
+                            void* stream) {
+  if (n_edges <= 0) return E3GNN_OK;
+  if (!vec || !coeffs || !Yb || !embb || !fij) return fail(E3GNN_ERR_ARG, "null edge geometry operand");
+  HIPCHK(launch_edge_force(n_edges, vec, coeffs, rc, ron, raw_sh, Yb, nullptr, embb, fij, nullptr,
+                           (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_edge_geometry_coeff_grad(int64_t n_edges, const float* vec, const float* coeffs, float rc,
+                                   float ron, const float* embb, const float* embdb, const float* rd,
+                                   float* out, void* stream) {
+  if (n_edges <= 0) return E3GNN_OK;
+  if (!vec || !coeffs || !embb || !embdb || !rd || !out)
+    return fail(E3GNN_ERR_ARG, "null edge geometry operand");
+  HIPCHK(launch_edge_geom_coeff(n_edges, vec, coeffs, rc, ron, embb, embdb, rd, out,
+                                (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_edge_forces_to_atoms(int64_t n_nodes, const int32_t* row_ptr, const int32_t* src_ptr,
+                               const int32_t* src_perm, const float* fij, float* F, void* stream) {
+  if (n_nodes <= 0) return E3GNN_OK;
+  if (!row_ptr || !src_ptr || !src_perm || !fij || !F) return fail(E3GNN_ERR_ARG, "null force operand");
+  HIPCHK(launch_atom_force((int)n_nodes, (int)n_nodes, row_ptr, src_ptr, src_perm, fij, F,
+                           (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
 int e3gnn_conv_tangent_forward(int kind, int64_t n_nodes, const int32_t* row_ptr,
                                const int32_t* edge_nbr, const float* h, const float* hd,
                                const float* Y, const float* Yd, const float* w, const float* wd,

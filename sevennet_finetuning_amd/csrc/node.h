@@ -6,10 +6,18 @@
 namespace e3gnn {
 hipError_t launch_edge_embed(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
                              int raw_sh, float* Y, float* emb, hipStream_t s);
+// the fine-tune step's edge-geometry tangent / coefficient gradient (node.hip)
+hipError_t launch_edge_geom_jvp(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
+                                int raw_sh, const int* center, const int* nbr, const int64_t* batch,
+                                const float* cF, const float* cS, const float* vol, float* Yd,
+                                float* embd, float* rd, hipStream_t s);
+hipError_t launch_edge_geom_coeff(int64_t E, const float* vec, const float* coeffs, float rc,
+                                  float ron, const float* embb, const float* embdb, const float* rd,
+                                  float* out, hipStream_t s);
 int edge_force_blocks(int64_t E);
 hipError_t launch_edge_force(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
                              int raw_sh, const float* dY, const float* dgu, const float* demb, float* fe,
-                             float* vir_part, hipStream_t s);
+                             float* vir_part, hipStream_t s);  // vir_part nullable
 hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, const int* src_ptr,
                              const int* src_perm, const float* fe, float* F, hipStream_t s);
 hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* center,

@@ -120,6 +120,7 @@ __global__ void k_edge_force(int64_t E, const float* __restrict__ vec, const flo
     v6[4] = -0.5f * (vy * fz + vz * fy);
     v6[5] = -0.5f * (vx * fz + vz * fx);
   }
+  if (!vir_part) return;   // (uniform) the fine-tune step's dE/dr needs no virial here
 #pragma unroll
   for (int q = 0; q < 6; ++q) red[q][threadIdx.x] = v6[q];
   __syncthreads();
@@ -130,6 +131,105 @@ __global__ void k_edge_force(int64_t E, const float* __restrict__ vec, const flo
     __syncthreads();
   }
   if (threadIdx.x < 6) vir_part[(int64_t)blockIdx.x * 6 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// XPLOR envelope and its r-derivative (edge_embedding.py:163-173)
+__device__ __forceinline__ void xplor(float r, float rc, float ron, float& env, float& denv) {
+  env = 1.f;
+  denv = 0.f;
+  if (r >= ron) {
+    const float rc2 = rc * rc, r2 = r * r, ron2 = ron * ron;
+    const float a = rc2 - r2, d = rc2 - ron2, d3 = d * d * d;
+    env = a * a * (rc2 + 2.f * r2 - 3.f * ron2) / d3;
+    denv = 12.f * r * a * (ron2 - r2) / d3;
+  }
+}
+
+// Tangent of the edge geometry for the fine-tune step's reverse-over-forward
+// derivatives (train_explicit.py): the per-edge direction is the loss
+// cotangent of f_e = dE/dr_e,
+//   v_e = dL/dF[centre] - dL/dF[nbr] - (c0 r0 + c5 r2, c1 r1 + c3 r0, c2 r2 + c4 r1),
+//   c = dL/dS[graph of nbr] / volume   (stress = -sum_e voigt(r_e, f_e) / volume),
+// and the outputs are Y' = dY/dr . v, emb' = demb/dr (r_hat . v), r' = r_hat . v.
+__global__ void k_edge_geom_jvp(int64_t E, const float* __restrict__ vec,
+                                const float* __restrict__ coeffs, float rc, float ron, int raw_sh,
+                                const int* __restrict__ center, const int* __restrict__ nbr,
+                                const int64_t* __restrict__ batch, const float* __restrict__ cF,
+                                const float* __restrict__ cS, const float* __restrict__ vol,
+                                float* __restrict__ Yd, float* __restrict__ embd,
+                                float* __restrict__ rd_out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const float vx = vec[3 * e], vy = vec[3 * e + 1], vz = vec[3 * e + 2];
+  const int ic = center[e], jn = nbr[e];
+  float tx = cF[3 * ic] - cF[3 * jn], ty = cF[3 * ic + 1] - cF[3 * jn + 1],
+        tz = cF[3 * ic + 2] - cF[3 * jn + 2];
+  if (cS) {
+    const int64_t b = batch[jn];
+    const float iv = 1.f / vol[b];
+    const float* c = cS + 6 * b;
+    tx -= (c[0] * vx + c[5] * vz) * iv;
+    ty -= (c[1] * vy + c[3] * vx) * iv;
+    tz -= (c[2] * vz + c[4] * vy) * iv;
+  }
+  const float r = sqrtf(vx * vx + vy * vy + vz * vz), ir = 1.f / r;
+  const float ux = vx * ir, uy = vy * ir, uz = vz * ir;
+  const float rd = ux * tx + uy * ty + uz * tz;
+  // SH argument a (unit or raw vector) and its tangent a'
+  float ax = vx, ay = vy, az = vz, dx = tx, dy = ty, dz = tz;
+  if (!raw_sh) {
+    ax = ux;
+    ay = uy;
+    az = uz;
+    dx = (tx - ux * rd) * ir;
+    dy = (ty - uy * rd) * ir;
+    dz = (tz - uz * rd) * ir;
+  }
+  const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f, c15 = s3 * s5;
+  float* yo = Yd + 9 * e;
+  yo[0] = 0.f;
+  yo[1] = s3 * dx;
+  yo[2] = s3 * dy;
+  yo[3] = s3 * dz;
+  yo[4] = c15 * (dx * az + ax * dz);
+  yo[5] = c15 * (dx * ay + ax * dy);
+  yo[6] = s5 * (2.f * ay * dy - (ax * dx + az * dz));
+  yo[7] = c15 * (dy * az + ay * dz);
+  yo[8] = c15 * (az * dz - ax * dx);
+  float env, denv;
+  xplor(r, rc, ron, env, denv);
+  float* eo = embd + 8 * e;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const float cn = coeffs[n];
+    const float sn = sinf(cn * r), cs = cosf(cn * r);
+    const float b = (2.f / rc) * sn * ir;
+    const float db = (2.f / rc) * (cn * cs * r - sn) * ir * ir;
+    eo[n] = (db * env + b * denv) * rd;
+  }
+  rd_out[e] = rd;
+}
+
+// per-edge d/dc_n of <emb-bar, emb> + <emb'-bar, emb'> (the Bessel
+// coefficients' gradient, summed over edges by the caller)
+__global__ void k_edge_geom_coeff(int64_t E, const float* __restrict__ vec,
+                                  const float* __restrict__ coeffs, float rc, float ron,
+                                  const float* __restrict__ embb, const float* __restrict__ embdb,
+                                  const float* __restrict__ rd, float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const float vx = vec[3 * e], vy = vec[3 * e + 1], vz = vec[3 * e + 2];
+  const float r = sqrtf(vx * vx + vy * vy + vz * vz);
+  float env, denv;
+  xplor(r, rc, ron, env, denv);
+  const float k = 2.f / rc, t = rd[e];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const float cn = coeffs[n];
+    const float sn = sinf(cn * r), cs = cosf(cn * r);
+    out[8 * e + n] = embb[8 * e + n] * (k * cs * env) +
+                     embdb[8 * e + n] * (k * (cs * denv - cn * sn * env)) * t;
+  }
 }
 
 // F_i = sum_{e: center=i} f_e - sum_{e: nbr=i} f_e  (pair_e3gnn_parallel.cpp:482-484)
@@ -404,8 +504,11 @@ __global__ void k_gather_rows(int j_begin, int n, int D, const int* __restrict__
   }
 }
 
-// same sum, 4 columns per lane (D % 4 == 0) and 4 rows in flight; the adds
-// keep the ascending edge order, so the result is bitwise that of k_gather_rows
+// same sum, float4 columns (D % 4 == 0): each lane takes two columns 64 apart
+// (a 480-wide row is 120 float4: one pass instead of two) and 8 rows are in
+// flight (16 b128 loads per lane), the next group's row ids read ahead; the
+// adds keep the ascending edge order, so the result is bitwise that of
+// k_gather_rows
 __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict__ ptr,
                                const int* __restrict__ perm, const float4* __restrict__ src,
                                float4* __restrict__ dst, int acc) {
@@ -413,33 +516,48 @@ __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
   const int b = ptr[j], en = ptr[j + 1];
-  for (int c = lane; c < D4; c += 64) {
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add = [](float4& s, const float4& v) {
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  };
+  for (int cb = 0; cb < D4; cb += 128) {
+    const int c0 = cb + lane, c1 = c0 + 64;
+    const bool h0 = c0 < D4, h1 = c1 < D4;
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
     int q = b;
-    for (; q + 4 <= en; q += 4) {
-      float4 v[4];
+    for (; q + 8 <= en; q += 8) {
+      int r[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = src[(int64_t)perm[q + u] * D4 + c];
+      for (int u = 0; u < 8; ++u) r[u] = perm[q + u];
+      float4 v0[8], v1[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        s.x += v[u].x;
-        s.y += v[u].y;
-        s.z += v[u].z;
-        s.w += v[u].w;
+      for (int u = 0; u < 8; ++u) {
+        const float4* row = src + (int64_t)r[u] * D4;
+        v0[u] = h0 ? row[c0] : s0;
+        v1[u] = h1 ? row[c1] : s1;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        add(s0, v0[u]);
+        add(s1, v1[u]);
       }
     }
     for (; q < en; ++q) {
-      const float4 v = src[(int64_t)perm[q] * D4 + c];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
+      const float4* row = src + (int64_t)perm[q] * D4;
+      if (h0) add(s0, row[c0]);
+      if (h1) add(s1, row[c1]);
     }
-    if (acc) {
-      const float4 o = dst[(int64_t)j * D4 + c];
-      s = make_float4(o.x + s.x, o.y + s.y, o.z + s.z, o.w + s.w);
+    float4* o = dst + (int64_t)j * D4;
+    if (h0) {
+      if (acc) add(s0, o[c0]);
+      o[c0] = s0;
     }
-    dst[(int64_t)j * D4 + c] = s;
+    if (h1) {
+      if (acc) add(s1, o[c1]);
+      o[c1] = s1;
+    }
   }
 }
 
@@ -472,6 +590,22 @@ __global__ void k_unpack(int64_t n, int dim, const int* __restrict__ idx, const 
 hipError_t launch_edge_embed(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
                              int raw_sh, float* Y, float* emb, hipStream_t s) {
   LAUNCH(k_edge_embed, nblk(E), E, vec, coeffs, rc, ron, raw_sh, Y, emb);
+  return hipGetLastError();
+}
+hipError_t launch_edge_geom_jvp(int64_t E, const float* vec, const float* coeffs, float rc, float ron,
+                                int raw_sh, const int* center, const int* nbr, const int64_t* batch,
+                                const float* cF, const float* cS, const float* vol, float* Yd,
+                                float* embd, float* rd, hipStream_t s) {
+  if (E <= 0) return hipSuccess;
+  LAUNCH(k_edge_geom_jvp, nblk(E), E, vec, coeffs, rc, ron, raw_sh, center, nbr, batch, cF, cS, vol,
+         Yd, embd, rd);
+  return hipGetLastError();
+}
+hipError_t launch_edge_geom_coeff(int64_t E, const float* vec, const float* coeffs, float rc,
+                                  float ron, const float* embb, const float* embdb, const float* rd,
+                                  float* out, hipStream_t s) {
+  if (E <= 0) return hipSuccess;
+  LAUNCH(k_edge_geom_coeff, nblk(E), E, vec, coeffs, rc, ron, embb, embdb, rd, out);
   return hipGetLastError();
 }
 int edge_force_blocks(int64_t E) { return nblk(E); }

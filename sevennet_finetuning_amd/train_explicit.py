@@ -251,12 +251,23 @@ class _Geometry:
     with the tangent along a direction v and the transposes the reverse
     sweeps need."""
 
-    def __init__(self, model):
+    def __init__(self, model, prims):
         from .nn import _sh_map
         self.rc = float(model.cutoff)
         self.ron = float(model.r_on)
         self.normalize = bool(model.sh_normalize)
         self._map = lambda dev, dt: _sh_map(2, dev, dt)   # noqa: E731
+        self.lib = prims.lib   # float32 device tensors: the HIP kernels (e3gnn_edge_geometry*)
+
+    def _hip(self, vec):
+        return self.lib is not None and vec.is_cuda and vec.dtype == torch.float32
+
+    def _args(self, g):
+        return (g['E'], g['vec'].data_ptr(), g['coeffs'].data_ptr(), self.rc, self.ron)
+
+    @staticmethod
+    def _stream(t):
+        return torch.cuda.current_stream(t.device).cuda_stream
 
     def _env(self, r):
         rc2, ron2 = self.rc * self.rc, self.ron * self.ron
@@ -267,7 +278,23 @@ class _Geometry:
         denv = torch.where(r * r > ron2, 12.0 * r * (rc2 - s) * (ron2 - s) / d3, torch.zeros_like(r))
         return env, denv
 
-    def forward(self, vec, coeffs):
+    def forward(self, vec, coeffs, emb_out=None):
+        if self._hip(vec):
+            from . import _lib
+            vec, coeffs = vec.contiguous(), coeffs.contiguous()
+            E = int(vec.shape[0])
+            Y = torch.empty(E, 9, device=vec.device)
+            emb = torch.empty(E, 8, device=vec.device) if emb_out is None else emb_out
+            g = {'E': E, 'vec': vec, 'coeffs': coeffs, 'Y': Y, 'emb': emb}
+            _lib.check(self.lib.e3gnn_edge_geometry(*self._args(g), int(not self.normalize),
+                                                    Y.data_ptr(), emb.data_ptr(), self._stream(vec)))
+            return g
+        g = self._forward_torch(vec, coeffs)
+        if emb_out is not None:
+            emb_out.copy_(g['emb'])
+        return g
+
+    def _forward_torch(self, vec, coeffs):
         r = torch.linalg.norm(vec, dim=-1)
         u = vec / r.unsqueeze(-1) if self.normalize else vec
         mono = torch.cat([torch.ones_like(u[:, :1]), u, (u.unsqueeze(-1) * u.unsqueeze(-2)).reshape(-1, 9)], 1)
@@ -283,7 +310,7 @@ class _Geometry:
         db = k * (coeffs * cs * ur - sn) / (ur * ur)
         demb = db * env.unsqueeze(-1) + b * denv.unsqueeze(-1)
         return {'r': r, 'u': u, 'Y': Y, 'emb': emb, 'demb': demb, 'env': env, 'denv': denv,
-                'sn': sn, 'cs': cs}
+                'sn': sn, 'cs': cs, 'E': int(vec.shape[0]), 'vec': vec, 'coeffs': coeffs}
 
     def sh_vjp_u(self, G, u):
         """dE/du from dE/dY"""
@@ -293,6 +320,13 @@ class _Geometry:
 
     def vjp(self, g, Yb, embb):
         """dE/dvec from dE/dY and dE/demb"""
+        if 'u' not in g:
+            from . import _lib
+            fij = torch.empty(g['E'], 3, device=Yb.device)
+            _lib.check(self.lib.e3gnn_edge_geometry_vjp(
+                *self._args(g), int(not self.normalize), Yb.contiguous().data_ptr(),
+                embb.contiguous().data_ptr(), fij.data_ptr(), self._stream(Yb)))
+            return fij
         u, r = g['u'], g['r']
         ub = self.sh_vjp_u(Yb, u)
         rb = (embb * g['demb']).sum(-1)
@@ -303,6 +337,37 @@ class _Geometry:
             uhat = u / r.unsqueeze(-1)
             vb = ub
         return vb + uhat * rb.unsqueeze(-1)
+
+    def tangent(self, g, S, cF, cS, embd_out):
+        """(Y', emb' -> embd_out, r') along the loss cotangent of the edge
+        forces: v_e = cF[centre] - cF[nbr] minus the stress term (forces F_i
+        = sum_{centre i} f_e - sum_{nbr i} f_e, stress from the edges)"""
+        center, nbr, batch = S['center'], S['nbr'], S['batch']
+        if 'u' not in g:
+            from . import _lib
+            aux = S['graph'].aux
+            E = g['E']
+            Yd = torch.empty(E, 9, device=cF.device)
+            rd = torch.empty(E, device=cF.device)
+            cS_, vol = (cS.contiguous(), S['vol'].contiguous()) if cS is not None else (None, None)
+            ptr = lambda t: t.data_ptr() if t is not None else None   # noqa: E731
+            _lib.check(self.lib.e3gnn_edge_geometry_jvp(
+                *self._args(g), int(not self.normalize), aux['center'].data_ptr(),
+                aux['nbr'].data_ptr(), batch.contiguous().data_ptr(), cF.contiguous().data_ptr(),
+                ptr(cS_), ptr(vol), Yd.data_ptr(), embd_out.data_ptr(), rd.data_ptr(),
+                self._stream(cF)))
+            return Yd, rd
+        v = cF[center] - cF[nbr]
+        if cS is not None:
+            vol = S['vol']
+            c = cS[batch[nbr]] / vol[batch[nbr]].unsqueeze(-1)
+            r = S['vec']
+            v = v - torch.stack([c[:, 0] * r[:, 0] + c[:, 5] * r[:, 2],
+                                 c[:, 1] * r[:, 1] + c[:, 3] * r[:, 0],
+                                 c[:, 2] * r[:, 2] + c[:, 4] * r[:, 1]], 1)
+        Yd, embd, rd = self.jvp(g, v)
+        embd_out.copy_(embd)
+        return Yd, rd
 
     def jvp(self, g, v):
         """(Y', emb') along the direction v"""
@@ -318,6 +383,13 @@ class _Geometry:
 
     def coeff_grad(self, g, embb, embdb, rd, coeffs):
         """d/dc of <emb-bar, emb> + <emb'-bar, emb'>"""
+        if 'u' not in g:
+            from . import _lib
+            per = torch.empty(g['E'], 8, device=embb.device)
+            _lib.check(self.lib.e3gnn_edge_geometry_coeff_grad(
+                *self._args(g), embb.contiguous().data_ptr(), embdb.contiguous().data_ptr(),
+                rd.contiguous().data_ptr(), per.data_ptr(), self._stream(embb)))
+            return per.sum(0)
         k = 2.0 / self.rc
         env, denv = g['env'].unsqueeze(-1), g['denv'].unsqueeze(-1)
         sn, cs = g['sn'], g['cs']
@@ -401,7 +473,7 @@ class ExplicitStep:
             raise ValueError('the explicit fine-tune derivatives cover SevenNet-0\'s architecture only')
         self.m = model
         self.p = _Prims(model)
-        self.geo = _Geometry(model)
+        self.geo = _Geometry(model, self.p)
         self.gates = [_Gate(b['gate'], self.p) for b in model.blocks]
         ent = []
         for t, blk in enumerate(model.blocks):
@@ -455,10 +527,9 @@ class ExplicitStep:
         S = self.S = {'n': n, 'E': E, 'nb': nb, 'types': types, 'batch': batch, 'center': center,
                       'nbr': nbr, 'graph': graph, 'vec': vec_k}
         coeffs = self._P('edge_embedding.basis_function.coeffs').detach()
-        g = self.geo.forward(vec_k, coeffs)
-        S['geo'] = g
         EMB = torch.empty(2 * E, 8, device=dev, dtype=dt)
-        EMB[:E].copy_(g['emb'])
+        g = self.geo.forward(vec_k, coeffs, emb_out=EMB[:E])
+        S['geo'] = g
         S['EMB'] = EMB
         D = S['D'] = self.bank.build()
         P = lambda name: self._P(name).detach()   # noqa: E731
@@ -527,8 +598,16 @@ class ExplicitStep:
                 xb = torch.addmm(hb @ D[f'si1{t}'].t(), yb, D[f'sc{t}'].t())
         fij = self.geo.vjp(g, Yb, embb)                    # dE/dr_e, centre-sorted order
         S['fij'] = fij
-        force = torch.zeros(n, 3, device=dev, dtype=fij.dtype).index_add(
-            0, torch.cat([center, nbr]), torch.cat([fij, -fij]))
+        aux = graph.aux
+        if 'row_ptr' in aux and fij.is_cuda and fij.dtype == torch.float32:
+            from . import _lib
+            force = torch.empty(n, 3, device=dev)
+            _lib.check(self.p.lib.e3gnn_edge_forces_to_atoms(
+                n, aux['row_ptr'].data_ptr(), aux['src_ptr'].data_ptr(), aux['src_perm'].data_ptr(),
+                fij.data_ptr(), force.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+        else:
+            force = torch.zeros(n, 3, device=dev, dtype=fij.dtype).index_add(
+                0, torch.cat([center, nbr]), torch.cat([fij, -fij]))
         voigt = vec_k.repeat(1, 2) * torch.cat([fij, fij.roll(-1, dims=1)], dim=1)
         s_graph = torch.zeros(nb, 6, device=dev, dtype=fij.dtype).index_add(0, batch[nbr], voigt)
         out = dict(data)
@@ -555,22 +634,12 @@ class ExplicitStep:
         dev = types.device
         cE = cE.to(dt) if cE is not None else torch.zeros(S['nb'], device=dev, dtype=dt)
         cF = cF.to(dt) if cF is not None else torch.zeros(n, 3, device=dev, dtype=dt)
-        # v_e = dL/df_e: forces F_i = sum_{centre i} f_e - sum_{nbr i} f_e, stress from the edges
-        v = cF[center] - cF[nbr]
-        if cS is not None:
-            vol = S['vol']
-            c = cS.to(dt)[batch[nbr]] / vol[batch[nbr]].unsqueeze(-1)
-            r = S['vec']
-            v = v - torch.stack([c[:, 0] * r[:, 0] + c[:, 5] * r[:, 2],
-                                 c[:, 1] * r[:, 1] + c[:, 3] * r[:, 0],
-                                 c[:, 2] * r[:, 2] + c[:, 4] * r[:, 1]], 1)
-        # ---- tangent forward along v (second halves of the stacked buffers)
-        # (fused: the backend's one-launch tangent forward / dual backward of
-        # the convolution; the generic engine's backend composes them)
+        # ---- tangent forward along v_e = dL/df_e (second halves of the stacked
+        # buffers; fused: the backend's one-launch tangent forward / dual
+        # backward of the convolution; the generic engine's backend composes them)
         fused = hasattr(be, 'dual_backward') and hasattr(be, 'tangent_forward')
-        Yd, embd, rd = self.geo.jvp(g, v)
         EMB = S['EMB']
-        EMB[E:].copy_(embd)
+        Yd, rd = self.geo.tangent(g, S, cF, cS.to(dt) if cS is not None else None, EMB[E:])
         blocks = S['blocks']
         Y = g['Y']
         for t, blk in enumerate(m.blocks):

@@ -134,6 +134,69 @@ def test_fused_tangent_forward_and_dual_backward(hip_backend, kind, with_hd):
         assert _rel(a, b) < 2e-5
 
 
+@pytest.mark.parametrize('normalize', [True, False])
+def test_edge_geometry_kernels_vs_fp64(hip_backend, normalize):
+    """The explicit step's edge-geometry kernels (e3gnn_edge_geometry*: Y /
+    emb, dE/dr from (dE/dY, dE/demb), the tangent along the loss cotangent of
+    the edge forces incl. the stress term, the Bessel-coefficient gradient,
+    the per-atom force sum) against the float64 torch formulas of
+    train_explicit._Geometry; unit-vector and raw-vector SH."""
+    from sevennet_finetuning_amd import _lib
+    from sevennet_finetuning_amd.train_explicit import _Geometry
+
+    class M:
+        cutoff, r_on, sh_normalize = 5.0, 4.5, normalize
+
+    class P:
+        lib = None
+
+    class PH:
+        lib = _lib.load()
+
+    rng = np.random.default_rng(7)
+    n, E, nb = 40, 300, 2
+    center = np.sort(rng.integers(0, n, E))
+    nbr = rng.integers(0, n, E)
+    d = rng.normal(size=(E, 3))
+    vec = d / np.linalg.norm(d, axis=1, keepdims=True) * rng.uniform(0.8, 4.99, (E, 1))
+    batch = (np.arange(n) >= n // 2).astype(np.int64)
+    coeffs = np.pi * np.arange(1, 9) / 5.0 * rng.uniform(0.9, 1.1, 8)
+    cF, cS, vol = rng.normal(size=(n, 3)), rng.normal(size=(nb, 6)), rng.uniform(50, 80, nb)
+    Yb, embb, embdb = rng.normal(size=(E, 9)), rng.normal(size=(E, 8)), rng.normal(size=(E, 8))
+    T64 = lambda a: torch.tensor(a, dtype=torch.float64)                        # noqa: E731
+    T32 = lambda a: torch.tensor(a, dtype=torch.float32, device=DEV)            # noqa: E731
+    Tl = lambda a, dev: torch.tensor(a, dtype=torch.long, device=dev)           # noqa: E731
+    gc, gh = _Geometry(M, P), _Geometry(M, PH)
+    rc_ = gc.forward(T64(vec), T64(coeffs))
+    rh = gh.forward(T32(vec), T32(coeffs))
+    assert _rel(rh['Y'], rc_['Y']) < 1e-5 and _rel(rh['emb'], rc_['emb']) < 1e-5
+    assert _rel(gh.vjp(rh, T32(Yb), T32(embb)), gc.vjp(rc_, T64(Yb), T64(embb))) < 1e-5
+    graph = conv_ops.ConvGraph(n, Tl(center, DEV), Tl(nbr, DEV), hip_backend)
+    Sc = {'center': Tl(center, 'cpu'), 'nbr': Tl(nbr, 'cpu'), 'batch': Tl(batch, 'cpu'),
+          'vec': T64(vec), 'vol': T64(vol)}
+    Sh = {'center': Tl(center, DEV), 'nbr': Tl(nbr, DEV), 'batch': Tl(batch, DEV),
+          'vec': T32(vec), 'vol': T32(vol), 'graph': graph}
+    for with_stress in (True, False):
+        ec, eh = torch.empty(E, 8, dtype=torch.float64), torch.empty(E, 8, device=DEV)
+        Ydc, rdc = gc.tangent(rc_, Sc, T64(cF), T64(cS) if with_stress else None, ec)
+        Ydh, rdh = gh.tangent(rh, Sh, T32(cF), T32(cS) if with_stress else None, eh)
+        for a, b in ((Ydh, Ydc), (eh, ec), (rdh, rdc)):
+            assert _rel(a, b) < 1e-5
+    cc = gc.coeff_grad(rc_, T64(embb), T64(embdb), rdc, T64(coeffs))
+    ch = gh.coeff_grad(rh, T32(embb), T32(embdb), rdh, T32(coeffs))
+    assert _rel(ch, cc) < 1e-5
+    # per-atom force sum over the graph's CSR
+    fij = rng.normal(size=(E, 3))
+    F = torch.empty(n, 3, device=DEV)
+    aux = graph.aux
+    _lib.check(PH.lib.e3gnn_edge_forces_to_atoms(
+        n, aux['row_ptr'].data_ptr(), aux['src_ptr'].data_ptr(), aux['src_perm'].data_ptr(),
+        T32(fij).data_ptr(), F.data_ptr(), torch.cuda.current_stream().cuda_stream))
+    ref = torch.zeros(n, 3, dtype=torch.float64).index_add(
+        0, torch.cat([Tl(center, 'cpu'), Tl(nbr, 'cpu')]), torch.cat([T64(fij), -T64(fij)]))
+    assert _rel(F, ref) < 1e-5
+
+
 def test_conv_graph_rejects_unsorted(hip_backend):
     from sevennet_finetuning_amd._lib import E3GNNError
     with pytest.raises(E3GNNError, match='not sorted'):
