@@ -293,6 +293,24 @@ __device__ __forceinline__ void nl_epilogue_runs(const NlProb& P, const f32x16& 
   }
 }
 
+// Operand loads through buffer descriptors based at the tile (a 32-bit lane
+// offset fixed over the k loop, the k-step's advance a scalar offset: no
+// 64-bit addresses to keep live) and, for the 64 x 64 tiles, two register
+// slots: the loads of k-step kt + 2 are in flight while step kt computes (one
+// slot leaves a k-step's MFMA work as the only cover for a global-load round
+// trip; the wider tiles' second slot does not fit the register budget of
+// five waves per SIMD).  Rows past the problem's nodes read 0 (outside the
+// descriptor).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t nl_rsrc(const float* p, int64_t nbytes) {
+  const int n = nbytes <= 0 ? 0 : (nbytes > 0x7fffffff ? 0x7fffffff : (int)nbytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, n, 0x00020000);
+}
+__device__ __forceinline__ float4 nl_ld4(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
+  const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vbytes, sbytes, 0));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
 template <int WN, int NS, int R>
 __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) {
   using S = NlShape<WN, NS>;
@@ -306,46 +324,62 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
   const int wr = wave / WN, wc = wave % WN;
   const int tm = local / P.tiles_n, tn = local - tm * P.tiles_n;
   const int node0 = tm * T, n0 = tn * BN;
+  const int vn = min(T, P.nodes - node0);  // nodes of this tile
 
-  float4 ra[NA], rb[NB];
-  auto load = [&](int k0) {
+  // descriptors: the tile's rows of A (and A2), B from column n0 on
+  const __amdgpu_buffer_rsrc_t RA =
+      nl_rsrc(P.A + (int64_t)node0 * P.lda + P.a_off, ((int64_t)(vn - 1) * P.lda + P.K1 * R) * 4);
+  const __amdgpu_buffer_rsrc_t RA2 =
+      P.K > P.K1 ? nl_rsrc(P.A2 + (int64_t)node0 * P.lda2 + P.a_off2,
+                           ((int64_t)(vn - 1) * P.lda2 + (P.K - P.K1) * R) * 4)
+                 : RA;
+  const __amdgpu_buffer_rsrc_t RB = nl_rsrc(P.B + n0, ((int64_t)P.K * P.N - n0) * 4);
+  int a_v[NA], a_v2[NA], b_v[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int u = tid + 256 * i;
+    const int nl = u / SEG4, j = 4 * (u - nl * SEG4);
+    const bool ok = (UA % 256 == 0 || u < UA) && nl < vn;
+    a_v[i] = ok ? (nl * (int)P.lda + j) * 4 : 0x7ffffff0;   // out of range: reads 0
+    a_v2[i] = ok ? (nl * (int)P.lda2 + j) * 4 : 0x7ffffff0;
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int u = tid + 256 * i;
+    const int k = u / (BN / 4), c = 4 * (u - k * (BN / 4));
+    b_v[i] = (UB % 256 == 0 || u < UB) ? (k * P.N + c) * 4 : 0x7ffffff0;
+  }
+  // two register slots where the registers allow it (64 x 64 tiles: one
+  // float4 of A and one of B per thread and slot); one otherwise
+  constexpr int DEPTH = (WN == 2 && NS == 1) ? 2 : 1;
+  float4 ra[DEPTH][NA], rb[DEPTH][NB];
+  auto load = [&](int k0, float4(&xa)[NA], float4(&xb)[NB]) __attribute__((always_inline)) {
     const bool second = k0 >= P.K1;
-    const float* src = second ? P.A2 : P.A;
-    const int64_t ld = second ? P.lda2 : P.lda;
     const int kk0 = second ? k0 - P.K1 : k0;
     const int kend = second ? P.K - P.K1 : P.K1;
-    const int off = (second ? P.a_off2 : P.a_off) + kk0 * R;
-    const bool full = kk0 + BK <= kend;
+    // a K tail (not met by SevenNet-0's linears) masks the elements past
+    // kend: inside the row they are the next block's values, past the last
+    // row the descriptor returns 0
+    const bool tail = kk0 + BK > kend;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int u = tid + 256 * i;
-      const int nl = u / SEG4, j = 4 * (u - nl * SEG4);
-      const int node = node0 + nl;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if ((UA % 256 == 0 || u < UA) && node < P.nodes) {
-        const float* p = src + (int64_t)node * ld + off + j;
-        if (full) {
-          v = *reinterpret_cast<const float4*>(p);
-        } else {  // K tail: element-wise, masked
-          v.x = kk0 + (j + 0) / R < kend ? p[0] : 0.f;
-          v.y = kk0 + (j + 1) / R < kend ? p[1] : 0.f;
-          v.z = kk0 + (j + 2) / R < kend ? p[2] : 0.f;
-          v.w = kk0 + (j + 3) / R < kend ? p[3] : 0.f;
-        }
+      float4 v = second ? nl_ld4(RA2, a_v2[i], kk0 * R * 4) : nl_ld4(RA, a_v[i], kk0 * R * 4);
+      if (tail) {
+        const int u = tid + 256 * i;
+        const int j = 4 * (u - (u / SEG4) * SEG4);
+        v.x = kk0 + (j + 0) / R < kend ? v.x : 0.f;
+        v.y = kk0 + (j + 1) / R < kend ? v.y : 0.f;
+        v.z = kk0 + (j + 2) / R < kend ? v.z : 0.f;
+        v.w = kk0 + (j + 3) / R < kend ? v.w : 0.f;
       }
-      ra[i] = v;
+      xa[i] = v;
     }
+    // B rows >= K and columns past N's row end read 0 or columns that only
+    // feed discarded outputs
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int u = tid + 256 * i;
-      const int k = u / (BN / 4), c = 4 * (u - k * (BN / 4));
-      const int gk = k0 + k, col = n0 + c;
-      rb[i] = ((UB % 256 == 0 || u < UB) && gk < P.K && col < P.N)
-                  ? *reinterpret_cast<const float4*>(P.B + (int64_t)gk * P.N + col)
-                  : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int i = 0; i < NB; ++i) xb[i] = nl_ld4(RB, b_v[i], k0 * P.N * 4);
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const float4(&xa)[NA], const float4(&xb)[NB]) __attribute__((always_inline)) {
     float* As = lds + buf * S::STAGE;
     float* Bs = As + S::A_FLOATS;
 #pragma unroll
@@ -353,7 +387,7 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
       const int u = tid + 256 * i;
       if (UA % 256 != 0 && u >= UA) continue;
       const int nl = u / SEG4, j = 4 * (u - nl * SEG4);
-      const float e[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+      const float e[4] = {xa[i].x, xa[i].y, xa[i].z, xa[i].w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int k = (j + q) / R, m = (j + q) - k * R;
@@ -365,17 +399,18 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
       const int u = tid + 256 * i;
       if (UB % 256 != 0 && u >= UB) continue;
       const int k = u / (BN / 4), c = 4 * (u - k * (BN / 4));
-      *reinterpret_cast<float4*>(Bs + k * S::LDB + c) = rb[i];
+      *reinterpret_cast<float4*>(Bs + k * S::LDB + c) = xb[i];
     }
   };
 
   const int nk = (P.K + BK - 1) / BK;
   const int nk1 = (NS == 1 && P.K > P.K1) ? P.K1 / BK : nk;
+  // step kt (DEPTH 2): LDS stage kt & 1 holds kt; register slot (kt + 1) & 1
+  // holds step kt + 1 and slot kt & 1 step kt + 2 (both in flight).
   // wave (wr, wc), sub-tile s: columns s * 32 * WN + wc * 32 + (0..31), so
   // chunk s of the epilogue is one contiguous 32 * WN column range
-  auto step = [&](int kt, f32x16 (&c)[NS]) {
-    if (kt + 1 < nk) load((kt + 1) * BK);
-    const float* As = lds + (kt & 1) * S::STAGE;
+  auto compute = [&](int buf, f32x16(&c)[NS]) __attribute__((always_inline)) {
+    const float* As = lds + buf * S::STAGE;
     const float* Bs = As + S::A_FLOATS;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
@@ -386,7 +421,23 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
         c[sub] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c[sub], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) store((kt + 1) & 1);
+  };
+  auto step = [&](int kt, f32x16(&c)[NS]) __attribute__((always_inline)) {
+    if constexpr (DEPTH == 2) {
+      if (kt & 1) {
+        compute(1, c);
+        if (kt + 1 < nk) store(0, ra[0], rb[0]);
+        if (kt + 3 < nk) load((kt + 3) * BK, ra[0], rb[0]);
+      } else {
+        compute(0, c);
+        if (kt + 1 < nk) store(1, ra[DEPTH - 1], rb[DEPTH - 1]);
+        if (kt + 3 < nk) load((kt + 3) * BK, ra[DEPTH - 1], rb[DEPTH - 1]);
+      }
+    } else {  // one slot: step kt + 1's loads cover step kt's MFMA work
+      if (kt + 1 < nk) load((kt + 1) * BK, ra[0], rb[0]);
+      compute(kt & 1, c);
+      if (kt + 1 < nk) store((kt + 1) & 1, ra[0], rb[0]);
+    }
     __syncthreads();
   };
   f32x16 acc[NS];
@@ -394,9 +445,14 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
   for (int sub = 0; sub < NS; ++sub)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[sub][i] = 0.f;
-  load(0);
-  store(0);
+  load(0, ra[0], rb[0]);
+  store(0, ra[0], rb[0]);
+  if constexpr (DEPTH == 2) {
+    if (nk > 1) load(BK, ra[DEPTH - 1], rb[DEPTH - 1]);
+    if (nk > 2) load(2 * BK, ra[0], rb[0]);
+  }
   __syncthreads();
+#pragma unroll 1
   for (int kt = 0; kt < nk1; ++kt) step(kt, acc);
   // (wide tiles are only chosen for unsplit K: add_nl)
   if (NS == 1 && nk1 < nk) {
@@ -407,6 +463,7 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
     for (int sub = 0; sub < NS; ++sub)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc2[sub][i] = 0.f;
+#pragma unroll 1
     for (int kt = nk1; kt < nk; ++kt) step(kt, acc2);
 #pragma unroll
     for (int sub = 0; sub < NS; ++sub)
