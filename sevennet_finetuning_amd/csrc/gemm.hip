@@ -295,12 +295,15 @@ __device__ __forceinline__ void nl_epilogue_runs(const NlProb& P, const f32x16& 
 
 // Operand loads through buffer descriptors based at the tile (a 32-bit lane
 // offset fixed over the k loop, the k-step's advance a scalar offset: no
-// 64-bit addresses to keep live) and, for the 64 x 64 tiles, two register
-// slots: the loads of k-step kt + 2 are in flight while step kt computes (one
-// slot leaves a k-step's MFMA work as the only cover for a global-load round
-// trip; the wider tiles' second slot does not fit the register budget of
-// five waves per SIMD).  Rows past the problem's nodes read 0 (outside the
-// descriptor).
+// 64-bit addresses to keep live).  Optionally (E3GNN_NL_DEPTH2, 64 x 64 tiles
+// only: the wider tiles' second slot does not fit five waves per SIMD) two
+// register slots keep the loads of k-step kt + 2 in flight while step kt
+// computes.  Rows past the problem's nodes read 0 (outside the descriptor).
+// (a second register slot for the 64 x 64 tiles measured 0.17 ms per step
+// SLOWER: 5.36 vs 5.19 ms of node linears, same box; kept as an option)
+#ifndef E3GNN_NL_DEPTH2
+#define E3GNN_NL_DEPTH2 0
+#endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t nl_rsrc(const float* p, int64_t nbytes) {
   const int n = nbytes <= 0 ? 0 : (nbytes > 0x7fffffff ? 0x7fffffff : (int)nbytes);
@@ -351,7 +354,7 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
   }
   // two register slots where the registers allow it (64 x 64 tiles: one
   // float4 of A and one of B per thread and slot); one otherwise
-  constexpr int DEPTH = (WN == 2 && NS == 1) ? 2 : 1;
+  constexpr int DEPTH = (E3GNN_NL_DEPTH2 && WN == 2 && NS == 1) ? 2 : 1;
   float4 ra[DEPTH][NA], rb[DEPTH][NB];
   auto load = [&](int k0, float4(&xa)[NA], float4(&xb)[NB]) __attribute__((always_inline)) {
     const bool second = k0 >= P.K1;

@@ -504,14 +504,18 @@ __global__ void k_gather_rows(int j_begin, int n, int D, const int* __restrict__
   }
 }
 
-// same sum, float4 columns (D % 4 == 0): each lane takes two columns 64 apart
-// (a 480-wide row is 120 float4: one pass instead of two) and 8 rows are in
-// flight (16 b128 loads per lane), the next group's row ids read ahead; the
-// adds keep the ascending edge order, so the result is bitwise that of
-// k_gather_rows
+// same sum, float4 columns (D % 4 == 0), one column per lane and pass, U rows
+// in flight; the adds keep the ascending edge order, so the result is bitwise
+// that of k_gather_rows.  (Measured against two columns per lane with 8 rows
+// in flight -- 85 VGPRs, 5 waves per SIMD: 1.39 vs 0.94 ms per 480-wide
+// launch; the occupancy of this 20-register form hides the row latency better.)
+#ifndef E3GNN_GATHER_U
+#define E3GNN_GATHER_U 4
+#endif
 __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict__ ptr,
                                const int* __restrict__ perm, const float4* __restrict__ src,
                                float4* __restrict__ dst, int acc) {
+  constexpr int U = E3GNN_GATHER_U;
   const int j = j_begin + xcd_block() * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
@@ -522,42 +526,19 @@ __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict
     s.z += v.z;
     s.w += v.w;
   };
-  for (int cb = 0; cb < D4; cb += 128) {
-    const int c0 = cb + lane, c1 = c0 + 64;
-    const bool h0 = c0 < D4, h1 = c1 < D4;
-    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+  for (int c = lane; c < D4; c += 64) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     int q = b;
-    for (; q + 8 <= en; q += 8) {
-      int r[8];
+    for (; q + U <= en; q += U) {
+      float4 v[U];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) r[u] = perm[q + u];
-      float4 v0[8], v1[8];
+      for (int u = 0; u < U; ++u) v[u] = src[(int64_t)perm[q + u] * D4 + c];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float4* row = src + (int64_t)r[u] * D4;
-        v0[u] = h0 ? row[c0] : s0;
-        v1[u] = h1 ? row[c1] : s1;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        add(s0, v0[u]);
-        add(s1, v1[u]);
-      }
+      for (int u = 0; u < U; ++u) add(s, v[u]);
     }
-    for (; q < en; ++q) {
-      const float4* row = src + (int64_t)perm[q] * D4;
-      if (h0) add(s0, row[c0]);
-      if (h1) add(s1, row[c1]);
-    }
-    float4* o = dst + (int64_t)j * D4;
-    if (h0) {
-      if (acc) add(s0, o[c0]);
-      o[c0] = s0;
-    }
-    if (h1) {
-      if (acc) add(s1, o[c1]);
-      o[c1] = s1;
-    }
+    for (; q < en; ++q) add(s, src[(int64_t)perm[q] * D4 + c]);
+    if (acc) add(s, dst[(int64_t)j * D4 + c]);
+    dst[(int64_t)j * D4 + c] = s;
   }
 }
 

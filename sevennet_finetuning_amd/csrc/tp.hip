@@ -435,28 +435,29 @@ __global__ __launch_bounds__(192 * FS) void k_tp_fwd_tan(TpDualArgs a) {
 // cgd = C g'_k per CG entry (i, j, k):
 //   dw  += cg x_i y_j + cgd (x_i y'_j + x'_i y_j)     dwd += cgd x_i y_j
 //   dx_i += w (cg y_j + cgd y'_j) + w' cgd y_j         dxd_i += w cgd y_j
-template <class L, int L1>
+// HALF: which 64 channels of a 128-channel irrep (two waves share it: one
+// channel per lane, half the live cotangent registers)
+template <class L, int L1, int HALF = 0>
 struct DualPart {
   static constexpr int MUL = part_mul<L, L1>();
   static constexpr int D1 = 2 * L1 + 1;
   static constexpr int XOFF = part_xoff<L, L1>();
-  static constexpr int UPL = MUL == 128 ? 2 : 1;
+  static constexpr int UPL = 1, CB = 64 * HALF;
+  static_assert(MUL <= 64 || MUL == 128, "channel blocks");
   float g[L::NP][UPL][5], gd[L::NP][UPL][5];
 
   __device__ __forceinline__ void load(int lane, const float* __restrict__ gc,
                                        const float* __restrict__ gdc) {
-    const int u0 = MUL == 32 ? (lane & 31) : lane;
+    const int u0 = (MUL == 32 ? (lane & 31) : lane) + CB;
     static_for<L::NP>([&](auto pi) {
       constexpr PathDef p = L::P[pi];
       if constexpr (p.l1 == L1) {
         constexpr int D3 = 2 * p.l3 + 1;
 #pragma unroll
-        for (int s = 0; s < UPL; ++s)
-#pragma unroll
-          for (int k = 0; k < D3; ++k) {
-            g[pi][s][k] = gc[p.moff + (u0 + 64 * s) * D3 + k];
-            gd[pi][s][k] = gdc[p.moff + (u0 + 64 * s) * D3 + k];
-          }
+        for (int k = 0; k < D3; ++k) {
+          g[pi][0][k] = gc[p.moff + u0 * D3 + k];
+          gd[pi][0][k] = gdc[p.moff + u0 * D3 + k];
+        }
       }
     });
   }
@@ -469,7 +470,7 @@ struct DualPart {
     const bool has_xd = a.hd != nullptr;
 #pragma unroll
     for (int s = 0; s < UPL; ++s) {
-      const int u = lane + 64 * s;
+      const int u = lane + CB + 64 * s;
       float x[D1], xd[D1], dx[D1], dxd[D1];
 #pragma unroll
       for (int i = 0; i < D1; ++i) {
@@ -508,9 +509,11 @@ struct DualPart {
   }
 };
 
+// waves per (centre, edge split): a 128-channel irrep takes two
 template <class L>
 constexpr int n_parts() {
-  return (part_mul<L, 0>() > 0) + (part_mul<L, 1>() > 0) + (part_mul<L, 2>() > 0);
+  return (part_mul<L, 0>() == 128 ? 2 : (part_mul<L, 0>() > 0)) + (part_mul<L, 1>() > 0) +
+         (part_mul<L, 2>() > 0);
 }
 
 // wave -> (centre, edge split k0, input irrep part): the parts write disjoint
@@ -518,7 +521,9 @@ constexpr int n_parts() {
 template <class L>
 __global__ __launch_bounds__(256) void k_tp_bwd_dual(TpDualArgs a, int split) {
   constexpr int NPART = n_parts<L>();
-  static_assert(part_mul<L, 0>() > 0 && (NPART == 1 || NPART == 3), "parts are l1 = 0 .. NPART-1");
+  static_assert(part_mul<L, 0>() == 128 && part_mul<L, 1>() <= 64 && part_mul<L, 2>() <= 64 &&
+                    (NPART == 2 || NPART == 4),
+                "parts: l1 = 0 (two halves), then l1 = 1, 2");
   const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int part = wg % NPART, rest = wg / NPART;
   const int c = rest / split, k0 = rest - c * split;
@@ -540,19 +545,19 @@ __global__ __launch_bounds__(256) void k_tp_bwd_dual(TpDualArgs a, int split) {
       P.edge(lane, e, j, y, yd, a);
     }
   };
-  if constexpr (NPART == 1) {
-    DualPart<L, 0> p0;
-    run(p0);
-  } else {
-    if (part == 0) {
-      DualPart<L, 0> p0;
-      run(p0);
-    } else if (part == 1) {
-      DualPart<L, 1> p1;
-      run(p1);
+  if (part == 0) {
+    DualPart<L, 0, 0> p;
+    run(p);
+  } else if (part == 1) {
+    DualPart<L, 0, 1> p;
+    run(p);
+  } else if constexpr (NPART == 4) {
+    if (part == 2) {
+      DualPart<L, 1> p;
+      run(p);
     } else {
-      DualPart<L, 2> p2;
-      run(p2);
+      DualPart<L, 2> p;
+      run(p);
     }
   }
 }

@@ -27,6 +27,7 @@ for s in "$@"; do
     benchnl0) step benchnl0 600 env E3GNN_NODELIN=0 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     benchnl) step benchnl 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     benchq) step bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10 ;;
+    benchf_*) step $s 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchf) step benchf 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchmorton) step benchmorton 600 env E3GNN_BENCH_ORDER=morton python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchmorton_*) v=${s#benchmorton_}; step benchmorton_$v 600 env E3GNN_BENCH_ORDER=morton E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
