@@ -196,6 +196,29 @@ int e3gnn_conv_backward_acc(int kind, int64_t n_nodes, int64_t n_edges, const in
                             const float* gagg, float* dh, float* dY, float* dw, float* dxc,
                             int accumulate, void* stream);
 
+/* Radial MLP of the fine-tune step (convolution.py:97-106's weight_nn, e ->
+ * W0 -> phi -> W1 -> phi -> W2, phi = 1.6792 silu = act_scale * silu; W0
+ * [8, 64], W1 [64, 64], W2 [64, width] row-major, already scaled by
+ * 1/sqrt(fan-in)), whole chains per 16-row tile (mlp_train.hip):
+ *   e3gnn_radial_mlp_forward   a1 = e W0, h1 = phi(a1), a2 = h1 W1,
+ *                              h2 = phi(a2), w = h2 W2 (rows of 8 / 64 / width);
+ *                              with a1_primal / a2_primal: the tangent chain
+ *                              (h1 = phi'(a1_primal) a1, h2 = phi'(a2_primal) a2)
+ *   e3gnn_radial_mlp_backward  h2b = wb W2^T, a2b = phi'(a2) h2b,
+ *                              h1b = a2b W1^T, a1b = phi'(a1) h1b, embb += a1b W0^T;
+ *                              with a1_tangent / a2_tangent: the reverse of the
+ *                              (primal, tangent) pairs over 2 n_rows rows of wb /
+ *                              a2b / a1b / embb (primal rows first);
+ *                              a2b / a1b nullable; width % 16 == 0. */
+int e3gnn_radial_mlp_forward(int64_t n_rows, int width, const float* emb, const float* W0,
+                             const float* W1, const float* W2, const float* a1_primal,
+                             const float* a2_primal, float* a1, float* h1, float* a2, float* h2,
+                             float* w, float act_scale, void* stream);
+int e3gnn_radial_mlp_backward(int64_t n_rows, int width, const float* wb, const float* W0,
+                              const float* W1, const float* W2, const float* a1, const float* a2,
+                              const float* a1_tangent, const float* a2_tangent, float* a2b,
+                              float* a1b, float* embb, float act_scale, void* stream);
+
 /* Edge geometry of the fine-tune step (train_explicit.py), float32, one thread
  * per edge; raw_sh as the model's sh_normalize == false:
  *   e3gnn_edge_geometry      Y [E, 9], emb [E, 8] (EdgeEmbedding.forward,

@@ -1648,6 +1648,39 @@ int e3gnn_conv_backward_acc(int kind, int64_t n_nodes, int64_t n_edges, const in
   return E3GNN_OK;
 }
 
+// ------------------------------------------------------------ fine-tune radial MLP
+int e3gnn_radial_mlp_forward(int64_t n_rows, int width, const float* emb, const float* W0,
+                             const float* W1, const float* W2, const float* a1_primal,
+                             const float* a2_primal, float* a1, float* h1, float* a2, float* h2,
+                             float* w, float act_scale, void* stream) {
+  if (n_rows <= 0) return E3GNN_OK;
+  if (n_rows > INT32_MAX || width <= 0) return fail(E3GNN_ERR_ARG, "radial MLP: bad sizes");
+  if (!emb || !W0 || !W1 || !W2 || !a1 || !h1 || !a2 || !h2 || !w ||
+      ((a1_primal == nullptr) != (a2_primal == nullptr)))
+    return fail(E3GNN_ERR_ARG, "null radial MLP operand");
+  HIPCHK(launch_mlp_fwd((int)n_rows, width, emb, W0, W1, W2, a1_primal, a2_primal, a1, h1, a2, h2, w,
+                        act_scale, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_radial_mlp_backward(int64_t n_rows, int width, const float* wb, const float* W0,
+                              const float* W1, const float* W2, const float* a1, const float* a2,
+                              const float* a1_tangent, const float* a2_tangent, float* a2b,
+                              float* a1b, float* embb, float act_scale, void* stream) {
+  if (n_rows <= 0) return E3GNN_OK;
+  if (n_rows > INT32_MAX || width <= 0 || width % 16)
+    return fail(E3GNN_ERR_ARG, "radial MLP backward: width must be a multiple of 16");
+  if (!wb || !W0 || !W1 || !W2 || !a1 || !a2 || !embb ||
+      ((a1_tangent == nullptr) != (a2_tangent == nullptr)))
+    return fail(E3GNN_ERR_ARG, "null radial MLP operand");
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al(wb) || !al(W0) || !al(W1) || !al(W2))
+    return fail(E3GNN_ERR_ARG, "radial MLP backward: wb / W0 / W1 / W2 must be 16-byte aligned");
+  HIPCHK(launch_mlp_bwd((int)n_rows, width, wb, W0, W1, W2, a1, a2, a1_tangent, a2_tangent, a2b, a1b,
+                        embb, act_scale, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
 // ------------------------------------------------------------ fine-tune edge geometry
 int e3gnn_edge_geometry(int64_t n_edges, const float* vec, const float* coeffs, float rc, float ron,
                         int raw_sh, float* Y, float* emb, void* stream) {

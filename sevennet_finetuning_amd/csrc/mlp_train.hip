@@ -1,0 +1,297 @@
+// Radial MLP of the fine-tune step (train_explicit.py), whole chains per
+// 16-edge row tile on f32 MFMA (v_mfma_f32_16x16x4_f32: exact f32 products).
+//
+// Reference: IrrepsConvolution's weight_nn (sevenn/nn/convolution.py:97-106,
+// e3nn FullyConnectedNet 8 -> 64 -> 64 -> W with the normalised SiLU) and the
+// derivatives the reference takes through autograd under create_graph
+// (force_output.py:158-215, trainer.py:155-222).  The hand-scheduled step needs
+// four row-wise chains per interaction block:
+//   forward   a1 = e W0, h1 = phi(a1), a2 = h1 W1, h2 = phi(a2), w = h2 W2
+//   tangent   a1' = e' W0, h1' = phi'(a1) a1', a2' = h1' W1, h2' = phi'(a2) a2', w' = h2' W2
+//   reverse   h2b = wb W2^T, a2b = phi'(a2) h2b, h1b = a2b W1^T, a1b = phi'(a1) h1b,
+//             eb += a1b W0^T
+//   dual      the reverse of (primal, tangent) pairs: [h2b; h2b'] = [wb; wb'] W2^T,
+//             (a2b, a2b') = (h2b phi' + h2b' phi'' a2', h2b' phi'), the same for
+//             layer 1, [eb; eb'] += [a1b; a1b'] W0^T
+// (W0, W1, W2 already carry the 1/sqrt(fan-in) of e3nn's normalisation).
+// Each was three GEMM launches and two element-wise ones; the intermediate
+// rows never leave the workgroup here.
+//
+// MFMA lane layout: A lane l = A[i = l&15][k = l>>4], B lane l = B[k = l>>4]
+// [j = l&15], D lane l reg r = D[4(l>>4) + r][l&15].  The reductions over the
+// long K of the reverse products take k in the order 16t + 4(l>>4) + (s&3)
+// for MFMA s = 4t + (s&3), so A rows and W rows are read as float4 (the sum
+// order changes, not the arithmetic).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace e3gnn {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+__device__ __forceinline__ float sig(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// c silu, its first and second derivatives (train_ops.hip's formulas)
+__device__ __forceinline__ float phi(float x, float c) { return c * x * sig(x); }
+__device__ __forceinline__ float dphi(float x, float c) {
+  const float s = sig(x);
+  return c * s * (1.0f + x * (1.0f - s));
+}
+__device__ __forceinline__ float ddphi(float x, float c) {
+  const float s = sig(x);
+  return c * s * (1.0f - s) * (2.0f + x * (1.0f - 2.0f * s));
+}
+
+constexpr int H = 64;        // hidden width
+constexpr int LDH = H + 1;   // LDS row stride of the 16 x 64 hidden tiles
+
+// forward (TAN = false) / tangent (TAN = true) chain; grid (row tiles of 16,
+// column groups of 64 of W); wave w owns hidden columns 16w..16w+15 and output
+// columns 64 cg + 16w .. +15.  Layers 0/1 are recomputed by every column group
+// (4.6k of the 70k multiply-adds per row); group 0 writes them.
+template <bool TAN>
+__global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __restrict__ emb,
+                                                 const float* __restrict__ W0,
+                                                 const float* __restrict__ W1,
+                                                 const float* __restrict__ W2,
+                                                 const float* __restrict__ A1p,
+                                                 const float* __restrict__ A2p,
+                                                 float* __restrict__ A1, float* __restrict__ H1,
+                                                 float* __restrict__ A2, float* __restrict__ H2,
+                                                 float* __restrict__ WT, float c) {
+  __shared__ float hs[2][16 * LDH];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int r0 = blockIdx.x * 16, cg = blockIdx.y;
+  const int n = 64 * cg + 16 * w + cl;  // output column of this lane
+  const int hcol = 16 * w + cl;         // hidden column of this lane
+  const bool first_group = cg == 0;
+  // operands issued up front: W1 / W2 columns for 16 k-steps each
+  float b1[16], b2[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    b1[s] = W1[(4 * s + g) * H + hcol];
+    b2[s] = n < W ? W2[(int64_t)(4 * s + g) * W + n] : 0.f;
+  }
+  // primal pre-activations at this lane's D positions (tangent chain)
+  float p1[4], p2[4];
+  if (TAN) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + 4 * g + r;
+      p1[r] = row < E ? A1p[(int64_t)row * H + hcol] : 0.f;
+      p2[r] = row < E ? A2p[(int64_t)row * H + hcol] : 0.f;
+    }
+  }
+  const int arow = r0 + cl;  // A-operand row of this lane
+  // layer 0: K = 8
+  f32x4 acc = zero4();
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const float a = arow < E ? emb[(int64_t)arow * 8 + 4 * s + g] : 0.f;
+    acc = mfma4(a, W0[(4 * s + g) * H + hcol], acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = r0 + 4 * g + r;
+    const float h = TAN ? dphi(p1[r], c) * acc[r] : phi(acc[r], c);
+    hs[0][(4 * g + r) * LDH + hcol] = h;
+    if (first_group && row < E) {
+      A1[(int64_t)row * H + hcol] = acc[r];
+      H1[(int64_t)row * H + hcol] = h;
+    }
+  }
+  __syncthreads();
+  // layer 1: K = 64
+  acc = zero4();
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma4(hs[0][cl * LDH + 4 * s + g], b1[s], acc);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = r0 + 4 * g + r;
+    const float h = TAN ? dphi(p2[r], c) * acc[r] : phi(acc[r], c);
+    hs[1][(4 * g + r) * LDH + hcol] = h;
+    if (first_group && row < E) {
+      A2[(int64_t)row * H + hcol] = acc[r];
+      H2[(int64_t)row * H + hcol] = h;
+    }
+  }
+  __syncthreads();
+  // layer 2: K = 64, this lane's output column n
+  acc = zero4();
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma4(hs[1][cl * LDH + 4 * s + g], b2[s], acc);
+  if (n < W) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + 4 * g + r;
+      if (row < E) WT[(int64_t)row * W + n] = acc[r];
+    }
+  }
+}
+
+// reverse (DUAL = false: rows [0, E) of wb) / dual (rows r and E + r of WB
+// together) chain; grid: row tiles of 16; wave w owns hidden columns
+// 16w..16w+15.  Outputs A2B / A1B (nullable; [E or 2E, 64]) and EB += ([E or
+// 2E, 8]).
+template <bool DUAL>
+__global__ __launch_bounds__(256) void k_mlp_bwd(int E, int W, const float* __restrict__ WB,
+                                                 const float* __restrict__ W0,
+                                                 const float* __restrict__ W1,
+                                                 const float* __restrict__ W2,
+                                                 const float* __restrict__ A1,
+                                                 const float* __restrict__ A2,
+                                                 const float* __restrict__ A1d,
+                                                 const float* __restrict__ A2d,
+                                                 float* __restrict__ A2B, float* __restrict__ A1B,
+                                                 float* __restrict__ EB, float c) {
+  constexpr int NS = DUAL ? 2 : 1;  // row sets: primal (and tangent)
+  __shared__ float hs[NS][16 * LDH];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int r0 = blockIdx.x * 16;
+  const int hcol = 16 * w + cl;
+  const int arow = r0 + cl;
+  const bool aok = arow < E;
+  // h2b = wb W2^T: K = W in groups of 16 (W % 16 == 0), float4 reads of the
+  // wb rows and of W2's row hcol
+  f32x4 acc[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) acc[q] = zero4();
+  const float4* w2r = reinterpret_cast<const float4*>(W2 + (int64_t)hcol * W) + g;
+  const float4* wbr[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+    wbr[q] = reinterpret_cast<const float4*>(WB + ((int64_t)q * E + (aok ? arow : 0)) * W) + g;
+  const int T = W / 16;
+#pragma unroll 2
+  for (int t = 0; t < T; ++t) {
+    const float4 b = w2r[4 * t];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      float4 a = wbr[q][4 * t];
+      if (!aok) a = make_float4(0.f, 0.f, 0.f, 0.f);
+      acc[q] = mfma4(a.x, b.x, acc[q]);
+      acc[q] = mfma4(a.y, b.y, acc[q]);
+      acc[q] = mfma4(a.z, b.z, acc[q]);
+      acc[q] = mfma4(a.w, b.w, acc[q]);
+    }
+  }
+  // through phi at a2 (and the dual pair)
+  auto through = [&](const float* __restrict__ X, const float* __restrict__ Xd, float* __restrict__ OUT,
+                     int lds) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r0 + 4 * g + r;
+      const bool ok = row < E;
+      const float x = ok ? X[(int64_t)row * H + hcol] : 0.f;
+      float o0, o1 = 0.f;
+      if (DUAL) {
+        const float xd = ok ? Xd[(int64_t)row * H + hcol] : 0.f;
+        const float d1 = dphi(x, c);
+        o0 = acc[0][r] * d1 + acc[NS - 1][r] * ddphi(x, c) * xd;
+        o1 = acc[NS - 1][r] * d1;
+      } else {
+        o0 = acc[0][r] * dphi(x, c);
+      }
+      hs[0][(4 * g + r) * LDH + hcol] = o0;
+      if (DUAL) hs[NS - 1][(4 * g + r) * LDH + hcol] = o1;
+      if (OUT && ok) {
+        OUT[(int64_t)row * H + hcol] = o0;
+        if (DUAL) OUT[((int64_t)E + row) * H + hcol] = o1;
+      }
+    }
+    (void)lds;
+  };
+  through(A2, A2d, A2B, 0);
+  __syncthreads();
+  // h1b = a2b W1^T: K = 64 (W1 row hcol as float4 over k)
+#pragma unroll
+  for (int q = 0; q < NS; ++q) acc[q] = zero4();
+  const float4* w1r = reinterpret_cast<const float4*>(W1 + (int64_t)hcol * H) + g;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float4 b = w1r[4 * t];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      const float* hr = &hs[q][cl * LDH + 16 * t + 4 * g];
+      acc[q] = mfma4(hr[0], b.x, acc[q]);
+      acc[q] = mfma4(hr[1], b.y, acc[q]);
+      acc[q] = mfma4(hr[2], b.z, acc[q]);
+      acc[q] = mfma4(hr[3], b.w, acc[q]);
+    }
+  }
+  __syncthreads();  // every wave has read a2b
+  through(A1, A1d, A1B, 0);
+  __syncthreads();
+  // eb += a1b W0^T: 8 output columns, one wave; lanes with cl >= 8 idle in B
+  if (w == 0) {
+#pragma unroll
+    for (int q = 0; q < NS; ++q) acc[q] = zero4();
+    const float4* w0r = reinterpret_cast<const float4*>(W0 + (int64_t)(cl < 8 ? cl : 0) * H) + g;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float4 b = w0r[4 * t];
+      if (cl >= 8) b = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        const float* hr = &hs[q][cl * LDH + 16 * t + 4 * g];
+        acc[q] = mfma4(hr[0], b.x, acc[q]);
+        acc[q] = mfma4(hr[1], b.y, acc[q]);
+        acc[q] = mfma4(hr[2], b.z, acc[q]);
+        acc[q] = mfma4(hr[3], b.w, acc[q]);
+      }
+    }
+    if (cl < 8) {
+#pragma unroll
+      for (int q = 0; q < NS; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = r0 + 4 * g + r;
+          if (row < E) {
+            float* o = EB + ((int64_t)q * E + row) * 8 + cl;
+            *o += acc[q][r];
+          }
+        }
+    }
+  }
+}
+
+}  // namespace
+
+// W0 [8, 64], W1 [64, 64], W2 [64, W] row-major; rows of 8 / 64 / W floats.
+// Tangent chain when A1p / A2p (the primal pre-activations) are given.
+hipError_t launch_mlp_fwd(int E, int W, const float* emb, const float* W0, const float* W1,
+                          const float* W2, const float* A1p, const float* A2p, float* A1, float* H1,
+                          float* A2, float* H2, float* WT, float c, hipStream_t s) {
+  if (E <= 0) return hipSuccess;
+  const dim3 grid((E + 15) / 16, (W + 63) / 64);
+  if (A1p)
+    hipLaunchKernelGGL(k_mlp_fwd<true>, grid, dim3(256), 0, s, E, W, emb, W0, W1, W2, A1p, A2p, A1, H1,
+                       A2, H2, WT, c);
+  else
+    hipLaunchKernelGGL(k_mlp_fwd<false>, grid, dim3(256), 0, s, E, W, emb, W0, W1, W2, A1p, A2p, A1,
+                       H1, A2, H2, WT, c);
+  return hipGetLastError();
+}
+// W % 16 == 0; dual when A1d / A2d (tangent pre-activations) are given: WB,
+// A2B, A1B, EB then hold 2E rows (primal first)
+hipError_t launch_mlp_bwd(int E, int W, const float* WB, const float* W0, const float* W1,
+                          const float* W2, const float* A1, const float* A2, const float* A1d,
+                          const float* A2d, float* A2B, float* A1B, float* EB, float c,
+                          hipStream_t s) {
+  if (E <= 0) return hipSuccess;
+  const dim3 grid((E + 15) / 16);
+  if (A1d)
+    hipLaunchKernelGGL(k_mlp_bwd<true>, grid, dim3(256), 0, s, E, W, WB, W0, W1, W2, A1, A2, A1d, A2d,
+                       A2B, A1B, EB, c);
+  else
+    hipLaunchKernelGGL(k_mlp_bwd<false>, grid, dim3(256), 0, s, E, W, WB, W0, W1, W2, A1, A2, A1d,
+                       A2d, A2B, A1B, EB, c);
+  return hipGetLastError();
+}
+
+}  // namespace e3gnn

@@ -21,4 +21,14 @@ hipError_t launch_act_dual(int64_t n, const float* x, const float* xd, const flo
 hipError_t launch_gate_dual(int op, int64_t n, const int* dims, const float* y, const float* yd,
                             const float* xb, const float* xdb, float* out0, float* out1, float c,
                             hipStream_t s);
+// the fine-tune step's radial-MLP chains (mlp_train.hip): forward / tangent
+// (A1p, A2p: primal pre-activations) and reverse / dual (A1d, A2d: tangent
+// pre-activations; 2E rows) of e -> W0 -> phi -> W1 -> phi -> W2
+hipError_t launch_mlp_fwd(int E, int W, const float* emb, const float* W0, const float* W1,
+                          const float* W2, const float* A1p, const float* A2p, float* A1, float* H1,
+                          float* A2, float* H2, float* WT, float c, hipStream_t s);
+hipError_t launch_mlp_bwd(int E, int W, const float* WB, const float* W0, const float* W1,
+                          const float* W2, const float* A1, const float* A2, const float* A1d,
+                          const float* A2d, float* A2B, float* A1B, float* EB, float c,
+                          hipStream_t s);
 }  // namespace e3gnn

@@ -487,6 +487,70 @@ class ExplicitStep:
     def _P(self, name):
         return self.m.param(name)
 
+    # ---- the radial MLP chains: one HIP launch each (e3gnn_radial_mlp_*) on
+    # float32 device tensors, the same GEMMs + element-wise steps otherwise
+    def _mlp_hip(self, t):
+        return self.p._hip(t)
+
+    @staticmethod
+    def _stream(t):
+        return torch.cuda.current_stream(t.device).cuda_stream
+
+    def _mlp_fwd(self, e, Ws, a1p, a2p, A1, H1, A2, H2, WT):
+        """forward chain (a1p None) or the tangent chain along e' = ``e``"""
+        W0, W1, W2 = Ws
+        if self._mlp_hip(e):
+            from . import _lib
+            ptr = lambda t: t.data_ptr() if t is not None else None   # noqa: E731
+            _lib.check(self.p.lib.e3gnn_radial_mlp_forward(
+                int(e.shape[0]), int(W2.shape[1]), e.data_ptr(), W0.data_ptr(), W1.data_ptr(),
+                W2.data_ptr(), ptr(a1p), ptr(a2p), A1.data_ptr(), H1.data_ptr(), A2.data_ptr(),
+                H2.data_ptr(), WT.data_ptr(), self.p.c, self._stream(e)))
+            return
+        torch.mm(e, W0, out=A1)
+        if a1p is None:
+            self.p.act(A1, out=H1)
+        else:
+            self.p.act_jvp(a1p, A1, out=H1)
+        torch.mm(H1, W1, out=A2)
+        if a2p is None:
+            self.p.act(A2, out=H2)
+        else:
+            self.p.act_jvp(a2p, A2, out=H2)
+        torch.mm(H2, W2, out=WT)
+
+    def _mlp_rev(self, wb, Ws, a1, a2, embb):
+        """embb += the reverse chain of wb (first reverse)"""
+        W0, W1, W2 = Ws
+        if self._mlp_hip(wb) and W2.shape[1] % 16 == 0:
+            from . import _lib
+            _lib.check(self.p.lib.e3gnn_radial_mlp_backward(
+                int(wb.shape[0]), int(W2.shape[1]), wb.contiguous().data_ptr(), W0.data_ptr(),
+                W1.data_ptr(), W2.data_ptr(), a1.data_ptr(), a2.data_ptr(), None, None, None, None,
+                embb.data_ptr(), self.p.c, self._stream(wb)))
+            return
+        a2b = self.p.act_jvp(a2, wb @ W2.t())
+        a1b = self.p.act_jvp(a1, a2b @ W1.t())
+        embb.addmm_(a1b, W0.t())
+
+    def _mlp_dual(self, WB, Ws, A1, A2, A2B, A1B, EMBB):
+        """reverse of the (primal, tangent) chains: A2B, A1B ([2E, 64]) and
+        EMBB += (A1, A2: stacked [primal; tangent] pre-activations)"""
+        W0, W1, W2 = Ws
+        E = A1.shape[0] // 2
+        if self._mlp_hip(WB) and W2.shape[1] % 16 == 0:
+            from . import _lib
+            _lib.check(self.p.lib.e3gnn_radial_mlp_backward(
+                E, int(W2.shape[1]), WB.data_ptr(), W0.data_ptr(), W1.data_ptr(), W2.data_ptr(),
+                A1[:E].data_ptr(), A2[:E].data_ptr(), A1[E:].data_ptr(), A2[E:].data_ptr(),
+                A2B.data_ptr(), A1B.data_ptr(), EMBB.data_ptr(), self.p.c, self._stream(WB)))
+            return
+        H2B = WB @ W2.t()
+        self.p.act_dual(A2[:E], A2[E:], H2B[:E], H2B[E:], out0=A2B[:E], out1=A2B[E:])
+        H1B = A2B @ W1.t()
+        self.p.act_dual(A1[:E], A1[E:], H1B[:E], H1B[E:], out0=A1B[:E], out1=A1B[E:])
+        EMBB.addmm_(A1B, W0.t())
+
     def _G(self, name):
         """the gradient view of a parameter (a slice of flat_grad), or None when frozen"""
         p = self.m.param(name)
@@ -554,11 +618,7 @@ class ExplicitStep:
             A1, H1 = new(2 * E, W0.shape[1]), new(2 * E, W0.shape[1])
             A2, H2 = new(2 * E, W1.shape[1]), new(2 * E, W1.shape[1])
             WT = new(2 * E, W2.shape[1])
-            torch.mm(EMB[:E], W0, out=A1[:E])
-            self.p.act(A1[:E], out=H1[:E])
-            torch.mm(H1[:E], W1, out=A2[:E])
-            self.p.act(A2[:E], out=H2[:E])
-            torch.mm(H2[:E], W2, out=WT[:E])
+            self._mlp_fwd(EMB[:E], (W0, W1, W2), None, None, A1[:E], H1[:E], A2[:E], H2[:E], WT[:E])
             den = P(f'{pre}.denominator')
             agg = be.forward(blk['kind'], graph, H[:n], g['Y'], WT[:E])
             AGG = new(2 * n, agg.shape[1])
@@ -590,10 +650,7 @@ class ExplicitStep:
             hb, _, wb = be.backward(blk['kind'], graph, b['H'][:n], g['Y'], b['WT'][:E], ab,
                                     need_h=t > 0, dY_out=Yb,
                                     acc=ACC_DY if t < len(blocks) - 1 else 0)
-            W0, W1, W2 = b['W']
-            a2b = self.p.act_jvp(b['A2'][:E], wb @ W2.t())
-            a1b = self.p.act_jvp(b['A1'][:E], a2b @ W1.t())
-            embb.addmm_(a1b, W0.t())
+            self._mlp_rev(wb, b['W'], b['A1'][:E], b['A2'][:E], embb)
             if t > 0:
                 xb = torch.addmm(hb @ D[f'si1{t}'].t(), yb, D[f'sc{t}'].t())
         fij = self.geo.vjp(g, Yb, embb)                    # dE/dr_e, centre-sorted order
@@ -645,13 +702,8 @@ class ExplicitStep:
         for t, blk in enumerate(m.blocks):
             b = blocks[t]
             k = blk['kind']
-            W0, W1, W2 = b['W']
             A1, H1, A2, H2, WT = b['A1'], b['H1'], b['A2'], b['H2'], b['WT']
-            torch.mm(EMB[E:], W0, out=A1[E:])
-            self.p.act_jvp(A1[:E], A1[E:], out=H1[E:])
-            torch.mm(H1[E:], W1, out=A2[E:])
-            self.p.act_jvp(A2[:E], A2[E:], out=H2[E:])
-            torch.mm(H2[E:], W2, out=WT[E:])
+            self._mlp_fwd(EMB[E:], b['W'], A1[:E], A2[:E], A1[E:], H1[E:], A2[E:], H2[E:], WT[E:])
             h, w = b['H'][:n], WT[:E]
             AGG, Yg = b['AGG'], b['Y']
             aggd = AGG[n:]                       # C(h, Y', w) + C(h, Y, w') + C(h', Y, w)
@@ -738,19 +790,14 @@ class ExplicitStep:
             gw2 = self._G(f'{pre}.weight_nn.layer2.weight')
             if gw2 is not None:
                 _wgrad(gw2, b['H2'], WB, 1.0 / math.sqrt(W2.shape[0]))
-            H2B = WB @ W2.t()
-            A2B = new(2 * E, W1.shape[1])
-            self.p.act_dual(b['A2'][:E], b['A2'][E:], H2B[:E], H2B[E:], out0=A2B[:E], out1=A2B[E:])
+            A2B, A1B = new(2 * E, W1.shape[1]), new(2 * E, W0.shape[1])
+            self._mlp_dual(WB, b['W'], b['A1'], b['A2'], A2B, A1B, EMBB)
             gw1 = self._G(f'{pre}.weight_nn.layer1.weight')
             if gw1 is not None:
                 _wgrad(gw1, b['H1'], A2B, 1.0 / math.sqrt(W1.shape[0]))
-            H1B = A2B @ W1.t()
-            A1B = new(2 * E, W0.shape[1])
-            self.p.act_dual(b['A1'][:E], b['A1'][E:], H1B[:E], H1B[E:], out0=A1B[:E], out1=A1B[E:])
             gw0 = self._G(f'{pre}.weight_nn.layer0.weight')
             if gw0 is not None:
                 _wgrad(gw0, EMB, A1B, 1.0 / math.sqrt(W0.shape[0]))
-            EMBB.addmm_(A1B, W0.t())
             # self-interaction 1 and self-connection (sc-bar = y-bar)
             G[f'si1{t}'].addmm_(X.t(), HB)
             G[f'sc{t}'].addmm_(X.t(), YB)

@@ -197,6 +197,55 @@ def test_edge_geometry_kernels_vs_fp64(hip_backend, normalize):
     assert _rel(F, ref) < 1e-5
 
 
+@pytest.mark.parametrize('width', [384, 960, 224])
+def test_radial_mlp_chain_kernels_vs_fp64(width):
+    """e3gnn_radial_mlp_forward / _backward (whole chains per 16-row tile) vs
+    the same chains as float64 GEMMs + element-wise steps (train_explicit's
+    torch path): forward, tangent, first reverse and dual reverse; a row
+    count that is not a multiple of 16; the three block widths."""
+    from sevennet_finetuning_amd import _lib
+    from sevennet_finetuning_amd.train_explicit import ExplicitStep, _Prims
+
+    class FM:
+        silu_norm = 1.679177
+        def __init__(self, dev):
+            self.flat = torch.empty(1, device=dev)
+        def _act_lib(self):
+            return _lib.load()
+
+    def host(dev):
+        h = type('Host', (), {k: getattr(ExplicitStep, k) for k in
+                              ('_mlp_hip', '_mlp_fwd', '_mlp_rev', '_mlp_dual')})()
+        h._stream = ExplicitStep._stream
+        h.p = _Prims(FM(dev))
+        return h
+
+    rng = np.random.default_rng(width)
+    E = 301
+    Wn = [rng.normal(size=(8, 64)) / np.sqrt(8), rng.normal(size=(64, 64)) / 8,
+          rng.normal(size=(64, width)) / 8]
+    emb, embd = rng.normal(size=(E, 8)), rng.normal(size=(E, 8))
+    WB = rng.normal(size=(2 * E, width))
+    embb0 = rng.normal(size=(2 * E, 8))
+    out = {}
+    for dev, dt in (('cpu', torch.float64), (DEV, torch.float32)):
+        T = lambda a: torch.tensor(a, dtype=dt, device=dev)           # noqa: E731
+        z = lambda *sh: torch.zeros(*sh, dtype=dt, device=dev)        # noqa: E731
+        h = host(dev)
+        Ws = tuple(T(w) for w in Wn)
+        A1, H1, A2, H2, WT = z(2 * E, 64), z(2 * E, 64), z(2 * E, 64), z(2 * E, 64), z(2 * E, width)
+        h._mlp_fwd(T(emb), Ws, None, None, A1[:E], H1[:E], A2[:E], H2[:E], WT[:E])
+        h._mlp_fwd(T(embd), Ws, A1[:E], A2[:E], A1[E:], H1[E:], A2[E:], H2[E:], WT[E:])
+        eb1 = T(embb0[:E])
+        h._mlp_rev(T(WB[:E]), Ws, A1[:E], A2[:E], eb1)
+        A2B, A1B, EBB = z(2 * E, 64), z(2 * E, 64), T(embb0)
+        h._mlp_dual(T(WB), Ws, A1, A2, A2B, A1B, EBB)
+        out[dev] = (A1, H1, A2, H2, WT, eb1, A2B, A1B, EBB)
+    names = ('A1', 'H1', 'A2', 'H2', 'WT', 'embb', 'A2B', 'A1B', 'EMBB')
+    for nm, a, b in zip(names, out[DEV], out['cpu']):
+        assert _rel(a, b) < 2e-5, nm
+
+
 def test_conv_graph_rejects_unsorted(hip_backend):
     from sevennet_finetuning_amd._lib import E3GNNError
     with pytest.raises(E3GNNError, match='not sorted'):
