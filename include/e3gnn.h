@@ -209,7 +209,7 @@ int e3gnn_conv_backward_acc(int kind, int64_t n_nodes, int64_t n_edges, const in
  *                              with a1_tangent / a2_tangent: the reverse of the
  *                              (primal, tangent) pairs over 2 n_rows rows of wb /
  *                              a2b / a1b / embb (primal rows first);
- *                              a2b / a1b nullable; width % 16 == 0. */
+ *                              a2b / a1b nullable.  width % 16 == 0 (both). */
 int e3gnn_radial_mlp_forward(int64_t n_rows, int width, const float* emb, const float* W0,
                              const float* W1, const float* W2, const float* a1_primal,
                              const float* a2_primal, float* a1, float* h1, float* a2, float* h2,

@@ -1654,7 +1654,8 @@ int e3gnn_radial_mlp_forward(int64_t n_rows, int width, const float* emb, const 
                              const float* a2_primal, float* a1, float* h1, float* a2, float* h2,
                              float* w, float act_scale, void* stream) {
   if (n_rows <= 0) return E3GNN_OK;
-  if (n_rows > INT32_MAX || width <= 0) return fail(E3GNN_ERR_ARG, "radial MLP: bad sizes");
+  if (n_rows > INT32_MAX || width <= 0 || width % 16)
+    return fail(E3GNN_ERR_ARG, "radial MLP: width must be a positive multiple of 16");
   if (!emb || !W0 || !W1 || !W2 || !a1 || !h1 || !a2 || !h2 || !w ||
       ((a1_primal == nullptr) != (a2_primal == nullptr)))
     return fail(E3GNN_ERR_ARG, "null radial MLP operand");

@@ -50,10 +50,10 @@ __device__ __forceinline__ float ddphi(float x, float c) {
 constexpr int H = 64;        // hidden width
 constexpr int LDH = H + 1;   // LDS row stride of the 16 x 64 hidden tiles
 
-// forward (TAN = false) / tangent (TAN = true) chain; grid (row tiles of 16,
-// column groups of 64 of W); wave w owns hidden columns 16w..16w+15 and output
-// columns 64 cg + 16w .. +15.  Layers 0/1 are recomputed by every column group
-// (4.6k of the 70k multiply-adds per row); group 0 writes them.
+// forward (TAN = false) / tangent (TAN = true) chain; one workgroup per
+// 16-row tile; wave w owns hidden columns 16w..16w+15 of layers 0 / 1 and the
+// output column blocks w, w + 4, ... of layer 2 (its A operand, the tile's h2
+// rows, held in 16 registers; each block's W2 operand loaded one block ahead).
 template <bool TAN>
 __global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __restrict__ emb,
                                                  const float* __restrict__ W0,
@@ -66,17 +66,18 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __re
                                                  float* __restrict__ WT, float c) {
   __shared__ float hs[2][16 * LDH];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
-  const int r0 = blockIdx.x * 16, cg = blockIdx.y;
-  const int n = 64 * cg + 16 * w + cl;  // output column of this lane
-  const int hcol = 16 * w + cl;         // hidden column of this lane
-  const bool first_group = cg == 0;
-  // operands issued up front: W1 / W2 columns for 16 k-steps each
-  float b1[16], b2[16];
+  const int r0 = blockIdx.x * 16;
+  const int hcol = 16 * w + cl;  // hidden column of this lane
+  const int NB = W / 16;         // output column blocks (W % 16 == 0)
+  float b1[16], b2[2][16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    b1[s] = W1[(4 * s + g) * H + hcol];
-    b2[s] = n < W ? W2[(int64_t)(4 * s + g) * W + n] : 0.f;
-  }
+  for (int s = 0; s < 16; ++s) b1[s] = W1[(4 * s + g) * H + hcol];
+  auto load_b2 = [&](int blk, float(&o)[16]) __attribute__((always_inline)) {
+    const int n = 16 * (blk < NB ? blk : 0) + cl;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) o[s] = W2[(int64_t)(4 * s + g) * W + n];
+  };
+  load_b2(w, b2[0]);
   // primal pre-activations at this lane's D positions (tangent chain)
   float p1[4], p2[4];
   if (TAN) {
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __re
     const int row = r0 + 4 * g + r;
     const float h = TAN ? dphi(p1[r], c) * acc[r] : phi(acc[r], c);
     hs[0][(4 * g + r) * LDH + hcol] = h;
-    if (first_group && row < E) {
+    if (row < E) {
       A1[(int64_t)row * H + hcol] = acc[r];
       H1[(int64_t)row * H + hcol] = h;
     }
@@ -115,22 +116,33 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __re
     const int row = r0 + 4 * g + r;
     const float h = TAN ? dphi(p2[r], c) * acc[r] : phi(acc[r], c);
     hs[1][(4 * g + r) * LDH + hcol] = h;
-    if (first_group && row < E) {
+    if (row < E) {
       A2[(int64_t)row * H + hcol] = acc[r];
       H2[(int64_t)row * H + hcol] = h;
     }
   }
   __syncthreads();
-  // layer 2: K = 64, this lane's output column n
-  acc = zero4();
+  // layer 2: the tile's h2 rows as A operands, column blocks w, w + 4, ...
+  float a2[16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) acc = mfma4(hs[1][cl * LDH + 4 * s + g], b2[s], acc);
-  if (n < W) {
+  for (int s = 0; s < 16; ++s) a2[s] = hs[1][cl * LDH + 4 * s + g];
+  auto block = [&](int blk, const float(&b)[16]) __attribute__((always_inline)) {
+    f32x4 o = zero4();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) o = mfma4(a2[s], b[s], o);
+    const int n = 16 * blk + cl;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = r0 + 4 * g + r;
-      if (row < E) WT[(int64_t)row * W + n] = acc[r];
+      if (row < E) WT[(int64_t)row * W + n] = o[r];
     }
+  };
+  for (int blk = w; blk < NB; blk += 8) {
+    load_b2(blk + 4, b2[1]);
+    block(blk, b2[0]);
+    if (blk + 4 >= NB) break;
+    load_b2(blk + 8, b2[0]);
+    block(blk + 4, b2[1]);
   }
 }
 
@@ -166,19 +178,38 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int E, int W, const float* __re
 #pragma unroll
   for (int q = 0; q < NS; ++q)
     wbr[q] = reinterpret_cast<const float4*>(WB + ((int64_t)q * E + (aok ? arow : 0)) * W) + g;
+  // chunks of 4 k-groups (64 k), the next chunk's float4s loaded while the
+  // current one is multiplied; groups past W read 0 (W % 16 == 0)
   const int T = W / 16;
-#pragma unroll 2
-  for (int t = 0; t < T; ++t) {
-    const float4 b = w2r[4 * t];
+  float4 bq[2][4], aq[2][NS][4];
+  auto load_chunk = [&](int t0, float4(&b)[4], float4(&a)[NS][4]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < NS; ++q) {
-      float4 a = wbr[q][4 * t];
-      if (!aok) a = make_float4(0.f, 0.f, 0.f, 0.f);
-      acc[q] = mfma4(a.x, b.x, acc[q]);
-      acc[q] = mfma4(a.y, b.y, acc[q]);
-      acc[q] = mfma4(a.z, b.z, acc[q]);
-      acc[q] = mfma4(a.w, b.w, acc[q]);
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + u;
+      const bool ok = t < T;
+      b[u] = ok ? w2r[4 * t] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < NS; ++q) a[q][u] = (ok && aok) ? wbr[q][4 * t] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  };
+  auto mul_chunk = [&](const float4(&b)[4], const float4(&a)[NS][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        acc[q] = mfma4(a[q][u].x, b[u].x, acc[q]);
+        acc[q] = mfma4(a[q][u].y, b[u].y, acc[q]);
+        acc[q] = mfma4(a[q][u].z, b[u].z, acc[q]);
+        acc[q] = mfma4(a[q][u].w, b[u].w, acc[q]);
+      }
+  };
+  load_chunk(0, bq[0], aq[0]);
+  for (int t0 = 0; t0 < T; t0 += 8) {
+    load_chunk(t0 + 4, bq[1], aq[1]);
+    mul_chunk(bq[0], aq[0]);
+    if (t0 + 4 >= T) break;
+    load_chunk(t0 + 8, bq[0], aq[0]);
+    mul_chunk(bq[1], aq[1]);
   }
   // through phi at a2 (and the dual pair)
   auto through = [&](const float* __restrict__ X, const float* __restrict__ Xd, float* __restrict__ OUT,
@@ -268,7 +299,7 @@ hipError_t launch_mlp_fwd(int E, int W, const float* emb, const float* W0, const
                           const float* W2, const float* A1p, const float* A2p, float* A1, float* H1,
                           float* A2, float* H2, float* WT, float c, hipStream_t s) {
   if (E <= 0) return hipSuccess;
-  const dim3 grid((E + 15) / 16, (W + 63) / 64);
+  const dim3 grid((E + 15) / 16);
   if (A1p)
     hipLaunchKernelGGL(k_mlp_fwd<true>, grid, dim3(256), 0, s, E, W, emb, W0, W1, W2, A1p, A2p, A1, H1,
                        A2, H2, WT, c);

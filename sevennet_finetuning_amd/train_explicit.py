@@ -499,7 +499,7 @@ class ExplicitStep:
     def _mlp_fwd(self, e, Ws, a1p, a2p, A1, H1, A2, H2, WT):
         """forward chain (a1p None) or the tangent chain along e' = ``e``"""
         W0, W1, W2 = Ws
-        if self._mlp_hip(e):
+        if self._mlp_hip(e) and W2.shape[1] % 16 == 0:
             from . import _lib
             ptr = lambda t: t.data_ptr() if t is not None else None   # noqa: E731
             _lib.check(self.p.lib.e3gnn_radial_mlp_forward(
