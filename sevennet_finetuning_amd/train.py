@@ -469,6 +469,14 @@ class Trainer:
             optim_param['capturable'] = True
             optim_param['lr'] = torch.tensor(float(optim_param.get('lr', 1e-3)),
                                              device=self.device)
+        # Adam / AdamW on the GPU: torch's fused kernel (one multi-tensor launch
+        # per update; the default foreach form issued ~70 launches per update,
+        # 1/3 of the fine-tune step's element-wise kernels).  Same update rule;
+        # 'optim_fused': False keeps the foreach form.
+        if (self.device.type == 'cuda' and config[OPTIMIZER].lower() in ('adam', 'adamw')
+                and bool(config.get('optim_fused', True))
+                and 'foreach' not in optim_param and 'fused' not in optim_param):
+            optim_param['fused'] = True
         self.optimizer = opt(params, **optim_param)
         sch = scheduler_dict[config[SCHEDULER].lower()]
         self.scheduler = sch(self.optimizer, **config.get(SCHEDULER_PARAM, {}))

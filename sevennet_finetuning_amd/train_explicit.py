@@ -113,6 +113,9 @@ def _put(out, v):
     return out
 
 
+_ONES = {}
+
+
 def _wgrad(G, A, B, alpha=1.0):
     """G += alpha A^T B for a tall K (edges) and a small output: split over
     K-chunks as one batched GEMM and a sum (a single GEMM with K = 24k rows
@@ -126,7 +129,12 @@ def _wgrad(G, A, B, alpha=1.0):
         G.addmm_(A.t(), B, alpha=alpha)
         return
     part = torch.bmm(A.view(S, K // S, -1).transpose(1, 2), B.view(S, K // S, -1))
-    G.add_(part.sum(0), alpha=alpha)
+    # the S partial products summed into G by one GEMM (ones[1, S] @ part)
+    ones = _ONES.get((S, part.dtype, part.device))
+    if ones is None:
+        ones = _ONES[(S, part.dtype, part.device)] = torch.ones(1, S, dtype=part.dtype,
+                                                                device=part.device)
+    G.view(1, -1).addmm_(ones, part.view(S, -1), alpha=alpha)
 
 
 class _Gate:
@@ -483,6 +491,31 @@ class ExplicitStep:
         ent += [('r1', model.readout1, 'reduce_input_to_hidden.linear.weight'),
                 ('r2', model.readout2, 'reduce_hidden_to_energy.linear.weight')]
         self.bank = _DenseBank(model, ent)
+        # the radial MLP weights of every block, scaled by 1/sqrt(fan-in)
+        # (e3nn FullyConnectedNet), gathered into one buffer by one launch
+        idx, scl, self.mlp_views = [], [], []
+        off = 0
+        for t in range(len(model.blocks)):
+            views = []
+            for li in range(3):
+                o, cnt, shape = model.slices[f'{t}_convolution.weight_nn.layer{li}.weight']
+                idx.append(np.arange(o, o + cnt))
+                scl.append(np.full(cnt, 1.0 / math.sqrt(shape[0])))
+                views.append((off, shape))
+                off += cnt
+            self.mlp_views.append(views)
+        dev, dt = model.flat.device, model.flat.dtype
+        self.mlp_idx = torch.as_tensor(np.concatenate(idx), device=dev)
+        self.mlp_scl = torch.as_tensor(np.concatenate(scl), device=dev, dtype=dt)
+        self.mlp_buf = torch.empty(off, device=dev, dtype=dt)
+
+    def _mlp_weights(self):
+        """[(W0, W1, W2) per block], each scaled by 1/sqrt(fan-in), views of one
+        buffer filled by one gather-multiply (16-byte aligned when the counts
+        are multiples of 4)"""
+        torch.mul(self.m.flat.detach()[self.mlp_idx], self.mlp_scl, out=self.mlp_buf)
+        return [tuple(self.mlp_buf[o:o + int(np.prod(sh))].view(*sh) for o, sh in views)
+                for views in self.mlp_views]
 
     def _P(self, name):
         return self.m.param(name)
@@ -596,6 +629,7 @@ class ExplicitStep:
         S['geo'] = g
         S['EMB'] = EMB
         D = S['D'] = self.bank.build()
+        MW = self._mlp_weights()
         P = lambda name: self._P(name).detach()   # noqa: E731
         emb_w = P('onehot_to_feature_x.linear.weight').view(m.nsp, -1)
         X = torch.empty(2 * n, emb_w.shape[1], device=dev, dtype=dt)
@@ -606,13 +640,8 @@ class ExplicitStep:
         new = lambda *shape: torch.empty(*shape, device=dev, dtype=dt)   # noqa: E731
         for t, blk in enumerate(m.blocks):
             pre = f'{t}_convolution'
-            W0 = P(f'{pre}.weight_nn.layer0.weight')
-            W1 = P(f'{pre}.weight_nn.layer1.weight')
-            W2 = P(f'{pre}.weight_nn.layer2.weight')
-            W0, W1, W2 = (W0 / math.sqrt(W0.shape[0]), W1 / math.sqrt(W1.shape[0]),
-                          W2 / math.sqrt(W2.shape[0]))
+            W0, W1, W2 = MW[t]
             x = X[:n]
-            sc = x @ D[f'sc{t}']
             H = new(2 * n, D[f'si1{t}'].shape[1])
             torch.mm(x, D[f'si1{t}'], out=H[:n])
             A1, H1 = new(2 * E, W0.shape[1]), new(2 * E, W0.shape[1])
@@ -624,7 +653,8 @@ class ExplicitStep:
             AGG = new(2 * n, agg.shape[1])
             torch.div(agg, den, out=AGG[:n])
             Yg = new(2 * n, D[f'si2{t}'].shape[1])
-            torch.addmm(sc, AGG[:n], D[f'si2{t}'], out=Yg[:n])
+            torch.mm(x, D[f'sc{t}'], out=Yg[:n])          # (GEMM into the output, then
+            Yg[:n].addmm_(AGG[:n], D[f'si2{t}'])            # accumulate: no bias copy)
             Xn = new(2 * n, self.gates[t].dims[3] if self.gates[t].ng else Yg.shape[1])
             self.gates[t].fwd(Yg[:n], out=Xn[:n])
             blocks.append({'X': X, 'H': H, 'A1': A1, 'H1': H1, 'A2': A2, 'H2': H2, 'WT': WT,
@@ -652,7 +682,7 @@ class ExplicitStep:
                                     acc=ACC_DY if t < len(blocks) - 1 else 0)
             self._mlp_rev(wb, b['W'], b['A1'][:E], b['A2'][:E], embb)
             if t > 0:
-                xb = torch.addmm(hb @ D[f'si1{t}'].t(), yb, D[f'sc{t}'].t())
+                xb = (hb @ D[f'si1{t}'].t()).addmm_(yb, D[f'sc{t}'].t())
         fij = self.geo.vjp(g, Yb, embb)                    # dE/dr_e, centre-sorted order
         S['fij'] = fij
         aux = graph.aux
@@ -720,7 +750,8 @@ class ExplicitStep:
                     be.forward(k, graph, hd, Y, w, out=aggd, acc=True)
             aggd.div_(b['den'])
             if t > 0:
-                torch.addmm(X[n:] @ D[f'sc{t}'], AGG[n:], D[f'si2{t}'], out=Yg[n:])
+                torch.mm(X[n:], D[f'sc{t}'], out=Yg[n:])
+                Yg[n:].addmm_(AGG[n:], D[f'si2{t}'])
             else:
                 torch.mm(AGG[n:], D[f'si2{t}'], out=Yg[n:])
             Xn = blocks[t + 1]['X'] if t + 1 < len(blocks) else S['XL']
@@ -801,7 +832,7 @@ class ExplicitStep:
             # self-interaction 1 and self-connection (sc-bar = y-bar)
             G[f'si1{t}'].addmm_(X.t(), HB)
             G[f'sc{t}'].addmm_(X.t(), YB)
-            XB = torch.addmm(HB @ D[f'si1{t}'].t(), YB, D[f'sc{t}'].t())
+            XB = (HB @ D[f'si1{t}'].t()).addmm_(YB, D[f'sc{t}'].t())
         # embedding (x0 = W[types] / sqrt(nsp)) and the radial basis coefficients
         gemb = self._G('onehot_to_feature_x.linear.weight')
         if gemb is not None:
