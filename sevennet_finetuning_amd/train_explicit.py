@@ -414,14 +414,19 @@ class _DenseBank:
     sum over the 2l+1 copies of u of the dense gradient (a padded gather and a
     row sum -- no atomics, deterministic)."""
 
-    def __init__(self, model, entries):
-        # entries: (key, _Linear, parameter name)
+    def __init__(self, model, entries, divisors=None):
+        # entries: (key, _Linear, parameter name); divisors: key -> parameter
+        # name of a scalar the whole matrix (and its gradient) is divided by
+        # (a frozen convolution denominator folded into si2)
         self.model = model
         self.views = {}
         pos, src, scl, self.shapes = [], [], [], {}
         off = 0
         upos, usrc, uscl = [], [], []
+        dsrc, udsrc = [], []
+        divisors = divisors or {}
         for key, lin, pname in entries:
+            dv = model.slices[divisors[key]][0] if key in divisors else -1
             din, dout = lin.in_off[-1], lin.out_off[-1]
             poff = model.slices[pname][0]
             woff = 0
@@ -433,6 +438,7 @@ class _DenseBank:
                 pos.append(p.ravel())
                 src.append((poff + woff + u * mo + v).ravel())
                 scl.append(np.full(u.size, lin.alpha[j]))
+                dsrc.append(np.full(u.size, dv))
                 # reverse map: flat element (u, v) <- its d dense positions
                 pr = p.reshape(mi * mo, d)
                 pad = np.full((mi * mo, 5), -1, dtype=np.int64)
@@ -440,6 +446,7 @@ class _DenseBank:
                 upos.append(pad)
                 usrc.append(poff + woff + np.arange(mi * mo))
                 uscl.append(np.full(mi * mo, lin.alpha[j]))
+                udsrc.append(np.full(mi * mo, dv))
                 woff += mi * mo
             self.shapes[key] = (off, din, dout)
             off += din * dout
@@ -455,10 +462,26 @@ class _DenseBank:
         self.uscl = torch.as_tensor(np.concatenate(uscl), device=dev, dtype=dt)
         self.buf = torch.zeros(off, device=dev, dtype=dt)
         self.gbuf = torch.zeros(off + 1, device=dev, dtype=dt)
+        # divisor sources: index into [flat; 1.0] (the extra slot: no divisor)
+        self.div = bool(divisors)
+        if self.div:
+            nf = model.flat.numel()
+            d, ud = np.concatenate(dsrc), np.concatenate(udsrc)
+            self.dsrc = torch.as_tensor(np.where(d < 0, nf, d), device=dev)
+            self.udsrc = torch.as_tensor(np.where(ud < 0, nf, ud), device=dev)
+            self.flat1 = torch.ones(nf + 1, device=dev, dtype=dt)
+
+    def _flat1(self):
+        """[flat; 1.0]: the divisor table"""
+        self.flat1[:-1].copy_(self.model.flat.detach())
+        return self.flat1
 
     def build(self):
         flat = self.model.flat.detach()
-        self.buf.index_put_((self.pos,), flat[self.src] * self.scl)
+        vals = flat[self.src] * self.scl
+        if self.div:
+            vals.div_(self._flat1()[self.dsrc])
+        self.buf.index_put_((self.pos,), vals)
         return {k: self.buf[o:o + a * b].view(a, b) for k, (o, a, b) in self.shapes.items()}
 
     def grads(self):
@@ -467,6 +490,8 @@ class _DenseBank:
 
     def flush(self, flat_grad):
         vals = self.gbuf[self.upos].sum(1) * self.uscl
+        if self.div:
+            vals.div_(self._flat1()[self.udsrc])
         flat_grad.index_add_(0, self.usrc, vals)
 
 
@@ -490,7 +515,13 @@ class ExplicitStep:
                     (f'si2{t}', blk['si2'], f'{t}_self_interaction_2.linear.weight')]
         ent += [('r1', model.readout1, 'reduce_input_to_hidden.linear.weight'),
                 ('r2', model.readout2, 'reduce_hidden_to_energy.linear.weight')]
-        self.bank = _DenseBank(model, ent)
+        # frozen convolution denominators (the default) are folded into si2:
+        # agg / den W = agg (W / den), and the si2 gradient divided by den in
+        # the flush -- no division launches on the activations
+        dens = [f'{t}_convolution.denominator' for t in range(len(model.blocks))]
+        self.fold_den = not any(model.param(d).requires_grad for d in dens)
+        self.bank = _DenseBank(model, ent, {f'si2{t}': d for t, d in enumerate(dens)}
+                               if self.fold_den else None)
         # the radial MLP weights of every block, scaled by 1/sqrt(fan-in)
         # (e3nn FullyConnectedNet), gathered into one buffer by one launch
         idx, scl, self.mlp_views = [], [], []
@@ -599,7 +630,7 @@ class ExplicitStep:
 
         Activations live in STACKED buffers, primal rows first and their
         tangents (filled by backward()) after them -- [emb; emb'], [a1; a1'],
-        [h1; h1'], ..., [x; x'], [agg/den; agg'/den], [y; y'] -- so the reverse
+        [h1; h1'], ..., [x; x'], [agg; agg'] (/den unless folded into si2), [y; y'] -- so the reverse
         sweep forms each weight gradient x^T y-bar + x'^T y'-bar and each input
         gradient [y-bar; y'-bar] W^T as ONE GEMM."""
         m = self.m
@@ -649,9 +680,10 @@ class ExplicitStep:
             WT = new(2 * E, W2.shape[1])
             self._mlp_fwd(EMB[:E], (W0, W1, W2), None, None, A1[:E], H1[:E], A2[:E], H2[:E], WT[:E])
             den = P(f'{pre}.denominator')
-            agg = be.forward(blk['kind'], graph, H[:n], g['Y'], WT[:E])
-            AGG = new(2 * n, agg.shape[1])
-            torch.div(agg, den, out=AGG[:n])
+            AGG = new(2 * n, D[f'si2{t}'].shape[0])
+            be.forward(blk['kind'], graph, H[:n], g['Y'], WT[:E], out=AGG[:n])
+            if not self.fold_den:            # (folded: D[si2] is si2 / den)
+                AGG[:n].div_(den)
             Yg = new(2 * n, D[f'si2{t}'].shape[1])
             torch.mm(x, D[f'sc{t}'], out=Yg[:n])          # (GEMM into the output, then
             Yg[:n].addmm_(AGG[:n], D[f'si2{t}'])            # accumulate: no bias copy)
@@ -676,7 +708,9 @@ class ExplicitStep:
         for t in range(len(blocks) - 1, -1, -1):
             b, blk = blocks[t], m.blocks[t]
             yb = self.gates[t].vjp(b['Y'][:n], xb)
-            ab = (yb @ D[f'si2{t}'].t()) / b['den']
+            ab = yb @ D[f'si2{t}'].t()
+            if not self.fold_den:
+                ab.div_(b['den'])
             hb, _, wb = be.backward(blk['kind'], graph, b['H'][:n], g['Y'], b['WT'][:E], ab,
                                     need_h=t > 0, dY_out=Yb,
                                     acc=ACC_DY if t < len(blocks) - 1 else 0)
@@ -748,7 +782,8 @@ class ExplicitStep:
                 be.forward(k, graph, h, Y, WT[E:], out=aggd, acc=True)
                 if hd is not None:
                     be.forward(k, graph, hd, Y, w, out=aggd, acc=True)
-            aggd.div_(b['den'])
+            if not self.fold_den:
+                aggd.div_(b['den'])
             if t > 0:
                 torch.mm(X[n:], D[f'sc{t}'], out=Yg[n:])
                 Yg[n:].addmm_(AGG[n:], D[f'si2{t}'])
@@ -792,7 +827,7 @@ class ExplicitStep:
             gden = self._G(f'{pre}.denominator')
             if gden is not None:
                 gden.sub_(torch.dot(AGGB.view(-1), AGG.view(-1)) / b['den'])
-            AB = AGGB / b['den']
+            AB = AGGB if self.fold_den else AGGB / b['den']
             ab, adb = AB[:n], AB[n:]
             h, hd = H[:n], H[n:]
             WT = b['WT']
