@@ -168,49 +168,67 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int E, int W, const float* __re
   const int hcol = 16 * w + cl;
   const int arow = r0 + cl;
   const bool aok = arow < E;
-  // h2b = wb W2^T: K = W in groups of 16 (W % 16 == 0), float4 reads of the
-  // wb rows and of W2's row hcol
-  f32x4 acc[NS];
+  // h2b = wb W2^T, K = W (W % 16 == 0): the four waves split the k groups
+  // (t = w, w + 4, ...; 16 k each) and each forms all 64 hidden columns (four
+  // independent accumulator chains per row set), the next group's float4s
+  // (wb rows, W2 rows 16 hb + cl) loaded while the current one is multiplied;
+  // the four partial tiles are summed through LDS in a fixed order
+  __shared__ float part[4][NS][16 * LDH];
+  const int T = W / 16;
+  f32x4 pacc[NS][4];
 #pragma unroll
-  for (int q = 0; q < NS; ++q) acc[q] = zero4();
-  const float4* w2r = reinterpret_cast<const float4*>(W2 + (int64_t)hcol * W) + g;
+  for (int q = 0; q < NS; ++q)
+#pragma unroll
+    for (int hb = 0; hb < 4; ++hb) pacc[q][hb] = zero4();
   const float4* wbr[NS];
 #pragma unroll
   for (int q = 0; q < NS; ++q)
     wbr[q] = reinterpret_cast<const float4*>(WB + ((int64_t)q * E + (aok ? arow : 0)) * W) + g;
-  // chunks of 4 k-groups (64 k), the next chunk's float4s loaded while the
-  // current one is multiplied; groups past W read 0 (W % 16 == 0)
-  const int T = W / 16;
-  float4 bq[2][4], aq[2][NS][4];
-  auto load_chunk = [&](int t0, float4(&b)[4], float4(&a)[NS][4]) __attribute__((always_inline)) {
+  const float4* w2r[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = t0 + u;
-      const bool ok = t < T;
-      b[u] = ok ? w2r[4 * t] : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int hb = 0; hb < 4; ++hb) w2r[hb] = reinterpret_cast<const float4*>(W2 + (int64_t)(16 * hb + cl) * W) + g;
+  float4 bq[2][4], aq[2][NS];
+  auto load_t = [&](int t, float4(&b)[4], float4(&a)[NS]) __attribute__((always_inline)) {
+    const bool ok = t < T;
 #pragma unroll
-      for (int q = 0; q < NS; ++q) a[q][u] = (ok && aok) ? wbr[q][4 * t] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int hb = 0; hb < 4; ++hb) b[hb] = ok ? w2r[hb][4 * t] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < NS; ++q) a[q] = (ok && aok) ? wbr[q][4 * t] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
-  auto mul_chunk = [&](const float4(&b)[4], const float4(&a)[NS][4]) __attribute__((always_inline)) {
+  auto mul_t = [&](const float4(&b)[4], const float4(&a)[NS]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int q = 0; q < NS; ++q)
 #pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        acc[q] = mfma4(a[q][u].x, b[u].x, acc[q]);
-        acc[q] = mfma4(a[q][u].y, b[u].y, acc[q]);
-        acc[q] = mfma4(a[q][u].z, b[u].z, acc[q]);
-        acc[q] = mfma4(a[q][u].w, b[u].w, acc[q]);
+      for (int hb = 0; hb < 4; ++hb) {
+        pacc[q][hb] = mfma4(a[q].x, b[hb].x, pacc[q][hb]);
+        pacc[q][hb] = mfma4(a[q].y, b[hb].y, pacc[q][hb]);
+        pacc[q][hb] = mfma4(a[q].z, b[hb].z, pacc[q][hb]);
+        pacc[q][hb] = mfma4(a[q].w, b[hb].w, pacc[q][hb]);
       }
   };
-  load_chunk(0, bq[0], aq[0]);
-  for (int t0 = 0; t0 < T; t0 += 8) {
-    load_chunk(t0 + 4, bq[1], aq[1]);
-    mul_chunk(bq[0], aq[0]);
-    if (t0 + 4 >= T) break;
-    load_chunk(t0 + 8, bq[0], aq[0]);
-    mul_chunk(bq[1], aq[1]);
+  load_t(w, bq[0], aq[0]);
+  for (int t = w; t < T; t += 8) {
+    load_t(t + 4, bq[1], aq[1]);
+    mul_t(bq[0], aq[0]);
+    if (t + 4 >= T) break;
+    load_t(t + 8, bq[0], aq[0]);
+    mul_t(bq[1], aq[1]);
   }
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+#pragma unroll
+    for (int hb = 0; hb < 4; ++hb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[w][q][(4 * g + r) * LDH + 16 * hb + cl] = pacc[q][hb][r];
+  __syncthreads();
+  f32x4 acc[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = (4 * g + r) * LDH + hcol;
+      acc[q][r] = ((part[0][q][o] + part[1][q][o]) + part[2][q][o]) + part[3][q][o];
+    }
   // through phi at a2 (and the dual pair)
   auto through = [&](const float* __restrict__ X, const float* __restrict__ Xd, float* __restrict__ OUT,
                      int lds) __attribute__((always_inline)) {
