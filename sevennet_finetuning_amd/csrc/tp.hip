@@ -464,13 +464,13 @@ struct DualPart {
 
   __device__ __forceinline__ void edge(int lane, int64_t e, int j, const float* y, const float* yd,
                                        const TpDualArgs& a) {
-    if (MUL == 32 && lane >= 32) return;
+    // (a 32-channel irrep: the two half-waves take two edges, lane = channel)
     const float* wr = a.w + e * L::W;
     const float* wdr = a.wd + e * L::W;
     const bool has_xd = a.hd != nullptr;
 #pragma unroll
     for (int s = 0; s < UPL; ++s) {
-      const int u = lane + CB + 64 * s;
+      const int u = (MUL == 32 ? (lane & 31) : lane) + CB + 64 * s;
       float x[D1], xd[D1], dx[D1], dxd[D1];
 #pragma unroll
       for (int i = 0; i < D1; ++i) {
@@ -518,14 +518,20 @@ constexpr int n_parts() {
 
 // wave -> (centre, edge split k0, input irrep part): the parts write disjoint
 // slices of every per-edge output, so each edge's outputs have one writer
-template <class L>
+// PSET: which parts this launch runs (-1 all; 0 the two l1 = 0 halves; 1 the
+// l1 = 1 part; 2 the l1 = 2 part): the middle block's l1 >= 1 parts need
+// 218 / 256 VGPRs against 80 for l1 = 0, so it runs three launches, each with
+// its own register allocation (occupancy) instead of the largest one
+template <class L, int PSET>
 __global__ __launch_bounds__(256) void k_tp_bwd_dual(TpDualArgs a, int split) {
-  constexpr int NPART = n_parts<L>();
+  constexpr int NALL = n_parts<L>();
   static_assert(part_mul<L, 0>() == 128 && part_mul<L, 1>() <= 64 && part_mul<L, 2>() <= 64 &&
-                    (NPART == 2 || NPART == 4),
+                    (NALL == 2 || NALL == 4),
                 "parts: l1 = 0 (two halves), then l1 = 1, 2");
+  constexpr int NPART = PSET < 0 ? NALL : (PSET == 0 ? 2 : 1);
+  constexpr int P0 = PSET <= 0 ? 0 : PSET + 1;  // first part of this launch
   const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  const int part = wg % NPART, rest = wg / NPART;
+  const int part = P0 + wg % NPART, rest = wg / NPART;
   const int c = rest / split, k0 = rest - c * split;
   if (c >= a.n_centers) return;
   const int lane = threadIdx.x & 63;
@@ -533,8 +539,13 @@ __global__ __launch_bounds__(256) void k_tp_bwd_dual(TpDualArgs a, int split) {
   const float* gc = a.g + (int64_t)c * L::DM;
   const float* gdc = a.gd + (int64_t)c * L::DM;
   auto run = [&](auto& P) {
+    using PT = std::remove_reference_t<decltype(P)>;
+    constexpr int PAIR = PT::MUL == 32 ? 2 : 1;  // edges per wave step
     P.load(lane, gc, gdc);
-    for (int e = beg + k0; e < end; e += split) {
+    const int eoff = PAIR == 2 && lane >= 32 ? split : 0;
+    for (int e0 = beg + k0; e0 < end; e0 += PAIR * split) {
+      const int e = e0 + eoff;
+      if (e >= end) continue;
       const int j = a.nbr[e];
       float y[9], yd[9];
 #pragma unroll
@@ -545,17 +556,26 @@ __global__ __launch_bounds__(256) void k_tp_bwd_dual(TpDualArgs a, int split) {
       P.edge(lane, e, j, y, yd, a);
     }
   };
-  if (part == 0) {
-    DualPart<L, 0, 0> p;
-    run(p);
-  } else if (part == 1) {
-    DualPart<L, 0, 1> p;
-    run(p);
-  } else if constexpr (NPART == 4) {
+  if constexpr (PSET <= 0) {
+    if (part == 0) {
+      DualPart<L, 0, 0> p;
+      run(p);
+      return;
+    } else if (part == 1) {
+      DualPart<L, 0, 1> p;
+      run(p);
+      return;
+    }
+  }
+  if constexpr (NALL == 4 && (PSET < 0 || PSET == 1)) {
     if (part == 2) {
       DualPart<L, 1> p;
       run(p);
-    } else {
+      return;
+    }
+  }
+  if constexpr (NALL == 4 && (PSET < 0 || PSET == 2)) {
+    if (part == 3) {
       DualPart<L, 2> p;
       run(p);
     }
@@ -599,8 +619,19 @@ template <class L>
 static hipError_t tp_bwd_dual_impl(const TpDualArgs& a, hipStream_t s) {
   if (a.n_centers <= 0) return hipSuccess;
   const int split = std::max(1, std::min(32, 32768 / a.n_centers));
-  const int64_t waves = (int64_t)a.n_centers * split * n_parts<L>();
-  hipLaunchKernelGGL(k_tp_bwd_dual<L>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a, split);
+  auto grid = [&](int parts) {
+    return dim3((unsigned)(((int64_t)a.n_centers * split * parts + 3) / 4));
+  };
+  if constexpr (std::is_same<L, LayerMid>::value) {
+    hipLaunchKernelGGL((k_tp_bwd_dual<L, 0>), grid(2), dim3(256), 0, s, a, split);
+    hipLaunchKernelGGL((k_tp_bwd_dual<L, 1>), grid(1), dim3(256), 0, s, a, split);
+    // the 32-channel part takes two edges per wave step: half the split
+    const int split2 = std::max(1, split / 2);
+    hipLaunchKernelGGL((k_tp_bwd_dual<L, 2>), dim3((unsigned)(((int64_t)a.n_centers * split2 + 3) / 4)),
+                       dim3(256), 0, s, a, split2);
+  } else {
+    hipLaunchKernelGGL((k_tp_bwd_dual<L, -1>), grid(n_parts<L>()), dim3(256), 0, s, a, split);
+  }
   return hipGetLastError();
 }
 hipError_t launch_tp_fwd_tan(int kind, const TpDualArgs& a, hipStream_t s) {
