@@ -270,7 +270,12 @@ struct BwdPart {
   }
 };
 
-template <class L>
+// PL: the input irrep part this launch runs (-1: all three).  The middle
+// block runs its parts as three launches (l1 = 1 and 2 need far more
+// registers than l1 = 0: each launch gets its own occupancy); part 0 writes
+// (or adds, per dy_assign) the edge's dE/dY partial, parts 1 and 2 add theirs
+// in that order (one writer per edge per launch: deterministic)
+template <class L, int PL>
 __global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
                                                 const int* __restrict__ nbr,
                                                 const float* __restrict__ Y,
@@ -289,12 +294,13 @@ __global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
   const int lane = threadIdx.x & 63;
   const int beg = row_ptr[c], end = row_ptr[c + 1];
   const float* gc = gagg + (int64_t)c * L::DM;
-  BwdPart<L, 0> pa;
-  BwdPart<L, 1> pb;
-  BwdPart<L, 2> pc;
+  BwdPart<L, PL < 0 ? 0 : PL> pa;
+  BwdPart<L, PL < 0 ? 1 : 3> pb;   // (l1 = 3: no channels, a no-op part)
+  BwdPart<L, PL < 0 ? 2 : 3> pc;
   pa.load(lane, gc);
   pb.load(lane, gc);
   pc.load(lane, gc);
+  const bool assign = dy_assign && PL <= 0;
   for (int e = beg + k0; e < end; e += split) {
     const int j = nbr[e];
     float y[9], dy[9];
@@ -314,7 +320,7 @@ __global__ __launch_bounds__(256) void k_tp_bwd(const int* __restrict__ row_ptr,
     }
     if (lane < 9) {
       float* o = dYacc + (int64_t)e * 9 + lane;
-      *o = dy_assign ? mine : *o + mine;
+      *o = assign ? mine : *o + mine;
     }
   }
 }
@@ -603,9 +609,18 @@ static hipError_t tp_bwd_impl(const TpArgs& a, hipStream_t s) {
   // centre's dE/dagg row loaded by each: ~14k waves instead of 3.5k
   const int split = std::max(1, std::min(32, 32768 / a.n_centers));
   const int64_t waves = (int64_t)a.n_centers * split;
-  hipLaunchKernelGGL(k_tp_bwd<L>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a.row_ptr,
-                     a.nbr, a.Y, a.w, a.h, a.gagg, a.dw, a.dxc, a.dYacc, a.n_centers, split,
-                     a.acc_out, a.dy_assign);
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  if constexpr (std::is_same<L, LayerMid>::value) {
+    hipLaunchKernelGGL((k_tp_bwd<L, 0>), grid, dim3(256), 0, s, a.row_ptr, a.nbr, a.Y, a.w, a.h, a.gagg,
+                       a.dw, a.dxc, a.dYacc, a.n_centers, split, a.acc_out, a.dy_assign);
+    hipLaunchKernelGGL((k_tp_bwd<L, 1>), grid, dim3(256), 0, s, a.row_ptr, a.nbr, a.Y, a.w, a.h, a.gagg,
+                       a.dw, a.dxc, a.dYacc, a.n_centers, split, a.acc_out, a.dy_assign);
+    hipLaunchKernelGGL((k_tp_bwd<L, 2>), grid, dim3(256), 0, s, a.row_ptr, a.nbr, a.Y, a.w, a.h, a.gagg,
+                       a.dw, a.dxc, a.dYacc, a.n_centers, split, a.acc_out, a.dy_assign);
+  } else {
+    hipLaunchKernelGGL((k_tp_bwd<L, -1>), grid, dim3(256), 0, s, a.row_ptr, a.nbr, a.Y, a.w, a.h,
+                       a.gagg, a.dw, a.dxc, a.dYacc, a.n_centers, split, a.acc_out, a.dy_assign);
+  }
   return hipGetLastError();
 }
 
