@@ -515,6 +515,23 @@ class ExplicitStep:
                     (f'si2{t}', blk['si2'], f'{t}_self_interaction_2.linear.weight')]
         ent += [('r1', model.readout1, 'reduce_input_to_hidden.linear.weight'),
                 ('r2', model.readout2, 'reduce_hidden_to_energy.linear.weight')]
+        # si2 (mid irreps -> gate input, block-diagonal by l: ~10x zeros in its
+        # dense matrix) products per instruction block instead of dense
+        self.si2_blocks = []
+        for t, blk in enumerate(model.blocks):
+            lin = blk['si2']
+            bl = [(lin.in_off[i], lin.in_off[i] + lin.irreps_in[i][0] * (2 * lin.irreps_in[i][1] + 1),
+                   lin.out_off[j], lin.out_off[j] + lin.irreps_out[j][0] * (2 * lin.irreps_out[j][1] + 1))
+                  for i, j in lin.ins]
+            cover = sorted({(a, b) for a, b, _, _ in bl})
+            gaps, pos = [], 0
+            for a, b in cover:
+                if a > pos:
+                    gaps.append((pos, a))
+                pos = max(pos, b)
+            if pos < lin.in_off[-1]:
+                gaps.append((pos, lin.in_off[-1]))
+            self.si2_blocks.append((bl, gaps))
         # frozen convolution denominators (the default) are folded into si2:
         # agg / den W = agg (W / den), and the si2 gradient divided by den in
         # the flush -- no division launches on the activations
@@ -550,6 +567,31 @@ class ExplicitStep:
 
     def _P(self, name):
         return self.m.param(name)
+
+    # ---- si2 products over its instruction blocks (views, no copies)
+    def _si2_fwd(self, t, A, Dm, out):
+        """out += A Dm (the gate-input rows)"""
+        for i0, i1, o0, o1 in self.si2_blocks[t][0]:
+            out[:, o0:o1].addmm_(A[:, i0:i1], Dm[i0:i1, o0:o1])
+
+    def _si2_t(self, t, A, Dm):
+        """A Dm^T (cotangent rows of the mid irreps)"""
+        bl, gaps = self.si2_blocks[t]
+        out = torch.empty(A.shape[0], Dm.shape[0], device=A.device, dtype=A.dtype)
+        seen = set()
+        for i0, i1, o0, o1 in bl:
+            out[:, i0:i1].addmm_(A[:, o0:o1], Dm[i0:i1, o0:o1].t(),
+                                 beta=1.0 if (i0, i1) in seen else 0.0)
+            seen.add((i0, i1))
+        for a, b in gaps:
+            out[:, a:b].zero_()
+        return out
+
+    def _si2_wgrad(self, t, Gm, A, B):
+        """Gm += A^T B on si2's blocks (the other entries of the dense gradient
+        map to no weight)"""
+        for i0, i1, o0, o1 in self.si2_blocks[t][0]:
+            Gm[i0:i1, o0:o1].addmm_(A[:, i0:i1].t(), B[:, o0:o1])
 
     # ---- the radial MLP chains: one HIP launch each (e3gnn_radial_mlp_*) on
     # float32 device tensors, the same GEMMs + element-wise steps otherwise
@@ -686,7 +728,7 @@ class ExplicitStep:
                 AGG[:n].div_(den)
             Yg = new(2 * n, D[f'si2{t}'].shape[1])
             torch.mm(x, D[f'sc{t}'], out=Yg[:n])          # (GEMM into the output, then
-            Yg[:n].addmm_(AGG[:n], D[f'si2{t}'])            # accumulate: no bias copy)
+            self._si2_fwd(t, AGG[:n], D[f'si2{t}'], Yg[:n])  # accumulate: no bias copy)
             Xn = new(2 * n, self.gates[t].dims[3] if self.gates[t].ng else Yg.shape[1])
             self.gates[t].fwd(Yg[:n], out=Xn[:n])
             blocks.append({'X': X, 'H': H, 'A1': A1, 'H1': H1, 'A2': A2, 'H2': H2, 'WT': WT,
@@ -708,7 +750,7 @@ class ExplicitStep:
         for t in range(len(blocks) - 1, -1, -1):
             b, blk = blocks[t], m.blocks[t]
             yb = self.gates[t].vjp(b['Y'][:n], xb)
-            ab = yb @ D[f'si2{t}'].t()
+            ab = self._si2_t(t, yb, D[f'si2{t}'])
             if not self.fold_den:
                 ab.div_(b['den'])
             hb, _, wb = be.backward(blk['kind'], graph, b['H'][:n], g['Y'], b['WT'][:E], ab,
@@ -786,9 +828,9 @@ class ExplicitStep:
                 aggd.div_(b['den'])
             if t > 0:
                 torch.mm(X[n:], D[f'sc{t}'], out=Yg[n:])
-                Yg[n:].addmm_(AGG[n:], D[f'si2{t}'])
             else:
-                torch.mm(AGG[n:], D[f'si2{t}'], out=Yg[n:])
+                Yg[n:].zero_()
+            self._si2_fwd(t, AGG[n:], D[f'si2{t}'], Yg[n:])
             Xn = blocks[t + 1]['X'] if t + 1 < len(blocks) else S['XL']
             self.gates[t].jvp(Yg[:n], Yg[n:], out=Xn[n:])
         XL = S['XL']
@@ -822,8 +864,8 @@ class ExplicitStep:
             Yg, AGG, X, H = b['Y'], b['AGG'], b['X'], b['H']
             YB = new(2 * n, Yg.shape[1])
             self.gates[t].dual_vjp(Yg[:n], Yg[n:], XB[:n], XB[n:], out0=YB[:n], out1=YB[n:])
-            G[f'si2{t}'].addmm_(AGG.t(), YB)
-            AGGB = YB @ D[f'si2{t}'].t()
+            self._si2_wgrad(t, G[f'si2{t}'], AGG, YB)
+            AGGB = self._si2_t(t, YB, D[f'si2{t}'])
             gden = self._G(f'{pre}.denominator')
             if gden is not None:
                 gden.sub_(torch.dot(AGGB.view(-1), AGG.view(-1)) / b['den'])
