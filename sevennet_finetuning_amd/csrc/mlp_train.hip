@@ -126,10 +126,9 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __re
   float a2[16];
 #pragma unroll
   for (int s = 0; s < 16; ++s) a2[s] = hs[1][cl * LDH + 4 * s + g];
-  auto block = [&](int blk, const float(&b)[16]) __attribute__((always_inline)) {
-    f32x4 o = zero4();
-#pragma unroll
-    for (int s = 0; s < 16; ++s) o = mfma4(a2[s], b[s], o);
+  // two column blocks at a time (independent accumulator chains), the next
+  // pair's W2 operands loaded while this pair is multiplied
+  auto store = [&](int blk, const f32x4& o) __attribute__((always_inline)) {
     const int n = 16 * blk + cl;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -139,10 +138,15 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __re
   };
   for (int blk = w; blk < NB; blk += 8) {
     load_b2(blk + 4, b2[1]);
-    block(blk, b2[0]);
-    if (blk + 4 >= NB) break;
-    load_b2(blk + 8, b2[0]);
-    block(blk + 4, b2[1]);
+    f32x4 o0 = zero4(), o1 = zero4();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      o0 = mfma4(a2[s], b2[0][s], o0);
+      o1 = mfma4(a2[s], b2[1][s], o1);
+    }
+    if (blk + 8 < NB) load_b2(blk + 8, b2[0]);
+    store(blk, o0);
+    if (blk + 4 < NB) store(blk + 4, o1);
   }
 }
 
