@@ -265,3 +265,62 @@ def test_native_engine_hfo2_decomposed_matches_serial(hfo2_native, tmp_path):
     assert np.abs(got['forces'] - one['forces']).max() <= 2e-5
     vol = abs(np.linalg.det(cell4))
     assert np.abs(got['virial'] / vol - one['stress']).max() <= 2e-6
+
+
+def _odd_gate_deployment(out_dir):
+    """A small parity model whose gates include the two layouts the HfO2
+    example lacks: a block output listing 0e before 0o ('4x0e+4x0o+...': e3nn
+    sorts 0o first, so the gate's pieces are not in their natural order) and
+    one without 0e ('4x0o+4x1o': odd gates, tanh).  Random weights (seeded),
+    atomic-energy scale 20 so forces are O(1-100)."""
+    from _conv_cpu import GenericCpuConvBackend
+    from sevennet_finetuning_amd import model_build as mb
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    cfg = {'chemical_species': ['Hf', 'O'], 'cutoff': 4.0, 'channel': 4, 'is_parity': True,
+           'lmax': 1, 'num_convolution_layer': 5,
+           'irreps_manual': ['4x0e', '4x0e+4x1o', '4x0e+4x1o+4x1e', '4x0e+4x0o+4x1o+4x1e',
+                             '4x0o+4x1o', '4x0e'],
+           'weight_nn_hidden_neurons': [16, 16],
+           'radial_basis': {'radial_basis_name': 'bessel', 'bessel_basis_num': 8},
+           'cutoff_function': {'cutoff_function_name': 'poly_cut', 'poly_cut_p_value': 6},
+           'act_gate': {'e': 'silu', 'o': 'tanh'}, 'act_scalar': {'e': 'silu', 'o': 'tanh'},
+           'self_connection_type': 'nequip', 'conv_denominator': 10.0}
+    c = mb.resolve_config(cfg)
+    man = mb.model_manifest(c)
+    m = SevenNetTrainable(device='cpu', conv_backend=GenericCpuConvBackend(), manifest=man,
+                          weights=mb.init_weights(man, c, 3))
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(5)
+        m.flat.add_(torch.randn(m.flat.shape, generator=g, dtype=m.flat.dtype) * 0.6)
+        o, k, _ = m.slices['rescale_atomic_energy.scale']
+        m.flat[o:o + k] = 20.0
+    return mb.deploy(m, out_dir)
+
+
+def test_odd_and_unsorted_gates_on_the_native_engine_vs_oracle(tmp_path):
+    """The generic C-ABI engine and the torch-side generic model on a parity
+    model with odd gates and a gate input listed 0e-before-0o, against the fp64
+    oracle/nequip_ref.py (whose gate layout is pinned against a hand-derived
+    e3nn Gate in tests/test_generic.py): E 2e-6 relative, forces 2e-5 and
+    stress 1e-4 relative to their largest component."""
+    from oracle.neighbor import neighbor_list
+    from oracle.nequip_ref import NequIPRef
+    from sevennet_finetuning_amd.model import E3GNNModel, load_model
+    dep = _odd_gate_deployment(str(tmp_path / 'odd'))
+    man = json.load(open(os.path.join(dep, 'manifest.json')))
+    assert man['irreps_manual'][4] == '4x0o+4x1o'
+    rng = np.random.default_rng(0)
+    cell = np.array([[6.0, 0.0, 0.0], [0.4, 6.2, 0.0], [-0.3, 0.5, 5.8]])
+    pos = rng.uniform(0, 1, (24, 3)) @ cell
+    types = rng.integers(0, 2, 24)
+    ref_m = NequIPRef(dep)
+    ei, sh = neighbor_list(pos, cell, ref_m.cutoff)
+    ref = ref_m(torch.tensor(pos), torch.tensor(types), torch.tensor(ei), torch.tensor(sh),
+                torch.tensor(cell))
+    F, S = ref['forces'].numpy(), ref['stress'].numpy()
+    assert np.abs(F).max() > 0.1          # a non-degenerate model
+    for model in (E3GNNModel(dep, device=DEV), load_model(dep, device=DEV, engine='torch')):
+        got = _run(model, pos, cell, types)
+        assert abs(got['energy'] - float(ref['energy'])) <= 2e-6 * abs(float(ref['energy']))
+        assert np.abs(got['forces'] - F).max() <= 2e-5 * np.abs(F).max()
+        assert np.abs(got['stress'] - S).max() <= 1e-4 * np.abs(S).max()
