@@ -36,6 +36,7 @@ self-connection, XPLOR cutoff, normalised or raw SH, silu gates); other
 members of the family keep the autograd path.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -518,11 +519,15 @@ class ExplicitStep:
         # si2 (mid irreps -> gate input, block-diagonal by l: ~10x zeros in its
         # dense matrix) products per instruction block instead of dense
         self.si2_blocks = []
+        # (E3GNN_TRAIN_SI2_BLOCKS=0: one dense product per use, for A/B)
+        dense_si2 = os.environ.get('E3GNN_TRAIN_SI2_BLOCKS', '1') == '0'
         for t, blk in enumerate(model.blocks):
             lin = blk['si2']
             bl = [(lin.in_off[i], lin.in_off[i] + lin.irreps_in[i][0] * (2 * lin.irreps_in[i][1] + 1),
                    lin.out_off[j], lin.out_off[j] + lin.irreps_out[j][0] * (2 * lin.irreps_out[j][1] + 1))
                   for i, j in lin.ins]
+            if dense_si2:
+                bl = [(0, lin.in_off[-1], 0, lin.out_off[-1])]
             cover = sorted({(a, b) for a, b, _, _ in bl})
             gaps, pos = [], 0
             for a, b in cover:

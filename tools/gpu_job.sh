@@ -40,6 +40,9 @@ for s in "$@"; do
     proftrain) step proftrain 600 rocprofv3 --kernel-trace --stats -d /tmp/prof_train -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 && mkdir -p gpurun_out/prof_train && cp /tmp/prof_train/*/*stats* /tmp/prof_train/*stats* gpurun_out/prof_train/ 2>/dev/null; ls gpurun_out/prof_train ;;
     traintests) step traintests 400 python -m pytest tests/test_gpu_train.py -x -q --timeout 200 --timeout-method thread ;;
     benchtrain) step benchtrain 300 python bench_train.py --steps 10 --warmup 3 ;;
+    benchtrain2_*) step $s 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    benchtrainsd) step benchtrainsd 300 env E3GNN_TRAIN_SI2_BLOCKS=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    benchtrainv_*) v=${s#benchtrainv_}; step benchtrain_$v 300 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchtrain2) step benchtrain2 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchtrainblk) step benchtrainblk 300 env E3GNN_TRAIN_DENSE_LINEAR=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchtrainlt) step benchtrainlt 300 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline --blas hipblaslt ;;
