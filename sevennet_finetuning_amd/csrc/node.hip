@@ -508,23 +508,11 @@ __global__ void k_gather_rows(int j_begin, int n, int D, const int* __restrict__
 // in flight; the adds keep the ascending edge order, so the result is bitwise
 // that of k_gather_rows.  (Measured against two columns per lane with 8 rows
 // in flight -- 85 VGPRs, 5 waves per SIMD: 1.39 vs 0.94 ms per 480-wide
-// launch; the occupancy of this 20-register form hides the row latency better.)
+// launch; the occupancy of this 20-register form hides the row latency better;
+// rows in flight U = 2 / 4 / 8 and non-temporal loads measured the same.)
 #ifndef E3GNN_GATHER_U
 #define E3GNN_GATHER_U 4
 #endif
-// (A/B option: the per-edge rows are read once -- non-temporal loads)
-#ifndef E3GNN_GATHER_NT
-#define E3GNN_GATHER_NT 0
-#endif
-__device__ __forceinline__ float4 gather_ld(const float4* p) {
-#if E3GNN_GATHER_NT
-  typedef float v4 __attribute__((ext_vector_type(4)));
-  const v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4*>(p));
-  return make_float4(v[0], v[1], v[2], v[3]);
-#else
-  return *p;
-#endif
-}
 __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict__ ptr,
                                const int* __restrict__ perm, const float4* __restrict__ src,
                                float4* __restrict__ dst, int acc) {
@@ -545,11 +533,11 @@ __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict
     for (; q + U <= en; q += U) {
       float4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = gather_ld(src + (int64_t)perm[q + u] * D4 + c);
+      for (int u = 0; u < U; ++u) v[u] = src[(int64_t)perm[q + u] * D4 + c];
 #pragma unroll
       for (int u = 0; u < U; ++u) add(s, v[u]);
     }
-    for (; q < en; ++q) add(s, gather_ld(src + (int64_t)perm[q] * D4 + c));
+    for (; q < en; ++q) add(s, src[(int64_t)perm[q] * D4 + c]);
     if (acc) add(s, dst[(int64_t)j * D4 + c]);
     dst[(int64_t)j * D4 + c] = s;
   }

@@ -516,11 +516,13 @@ class ExplicitStep:
                     (f'si2{t}', blk['si2'], f'{t}_self_interaction_2.linear.weight')]
         ent += [('r1', model.readout1, 'reduce_input_to_hidden.linear.weight'),
                 ('r2', model.readout2, 'reduce_hidden_to_energy.linear.weight')]
-        # si2 (mid irreps -> gate input, block-diagonal by l: ~10x zeros in its
-        # dense matrix) products per instruction block instead of dense
+        # si2 (mid irreps -> gate input) is block-diagonal by l: ~10x zeros in
+        # its dense matrix.  Its products per instruction block (strided views,
+        # E3GNN_TRAIN_SI2_BLOCKS=1) measured SLOWER at the fine-tune batch size
+        # (10.05-10.2 vs 8.14 ms per step, same box): three small strided GEMMs
+        # cost more than one dense one.  Default: one dense product per use.
         self.si2_blocks = []
-        # (E3GNN_TRAIN_SI2_BLOCKS=0: one dense product per use, for A/B)
-        dense_si2 = os.environ.get('E3GNN_TRAIN_SI2_BLOCKS', '1') == '0'
+        dense_si2 = os.environ.get('E3GNN_TRAIN_SI2_BLOCKS', '0') != '1'
         for t, blk in enumerate(model.blocks):
             lin = blk['si2']
             bl = [(lin.in_off[i], lin.in_off[i] + lin.irreps_in[i][0] * (2 * lin.irreps_in[i][1] + 1),
