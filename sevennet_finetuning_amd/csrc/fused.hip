@@ -976,10 +976,10 @@ __device__ __forceinline__ void dh2_pair(f32x4 (&dh2)[4], const float (&da)[4], 
 // tiles of the workgroup's centres [cb, cb + 4) clipped to c_end: the lock-step
 // loop count (min_one: a centre without edges still has its one (empty) tile)
 __device__ __forceinline__ int ls_tiles(const int* __restrict__ row_ptr, int cb, int c_end,
-                                        bool min_one) {
+                                        bool min_one, int wpg = 4) {
   int T = 0;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
+  for (int w = 0; w < wpg; ++w) {
     const int cc = cb + w;
     if (cc < c_end) {
       const int t = (row_ptr[cc + 1] - row_ptr[cc] + 15) >> 4;
@@ -1002,24 +1002,36 @@ template <class L>
 struct BwdLsWaves {
   static constexpr int v = std::is_same<L, LayerFirst>::value ? 3 : 2;
 };
+// centres (waves) per workgroup: 4; E3GNN_BWD_WPG = 8 (A/B) gives the middle
+// block one 8-wave workgroup per CU sharing each staged W2 pair (124 KB LDS)
+#ifndef E3GNN_BWD_WPG
+#define E3GNN_BWD_WPG 4
+#endif
 template <class L>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdLsWaves<L>::v, BwdLsWaves<L>::v))) void k_conv_bwd_ls(
+struct BwdWpg {
+  static constexpr int v = std::is_same<L, LayerMid>::value ? E3GNN_BWD_WPG : 4;
+};
+template <class L>
+__global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_eu(BwdLsWaves<L>::v, BwdLsWaves<L>::v))) void k_conv_bwd_ls(
     const int* __restrict__ row_ptr, const int* __restrict__ nbr, const float* __restrict__ emb,
     const float* __restrict__ Y, const float* __restrict__ h, const float* __restrict__ gagg, MlpW W,
     float* __restrict__ dxc, float* __restrict__ dgu, float* __restrict__ demb, int c_begin,
     int c_end, int n_nodes) {
   constexpr int NBLK = L::W / 16, NPAIR = NBLK / 2;
   static_assert(NBLK % 2 == 0, "weight blocks come in pairs");
-  constexpr int NW = LS_PAIR_W / 16 / 256, ND = LS_PAIR_D / 16 / 256;
-  __shared__ __attribute__((aligned(16))) float smem[4 * L::DM + (LS_PAIR_W + LS_PAIR_D) / 4];
+  constexpr int WPG = BwdWpg<L>::v, NT = 64 * WPG;
+  // staging pieces (b128) of a pair: the w-recompute operands, then the dH2 ones
+  constexpr int NWP = LS_PAIR_W / 16, NST = (LS_PAIR_W + LS_PAIR_D) / 16 / NT;
+  static_assert((LS_PAIR_W + LS_PAIR_D) / 16 % NT == 0 && NWP % 64 == 0, "staging pieces per thread");
+  __shared__ __attribute__((aligned(16))) float smem[WPG * L::DM + (LS_PAIR_W + LS_PAIR_D) / 4];
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, g = lane >> 4, col = lane & 15;
-  const int cb = c_begin + blockIdx.x * 4;
+  const int cb = c_begin + blockIdx.x * WPG;
   const int c = cb + wid;
   const bool valid = c < c_end;
   const int beg = valid ? row_ptr[c] : 0, end = valid ? row_ptr[c + 1] : 0;
-  const int T = ls_tiles(row_ptr, cb, c_end, false);
+  const int T = ls_tiles(row_ptr, cb, c_end, false, WPG);
   float* dacc = smem + wid * L::DM;
-  char* img = reinterpret_cast<char*>(smem + 4 * L::DM);
+  char* img = reinterpret_cast<char*>(smem + WPG * L::DM);
   if (valid && end > beg) {
     const float4* s4 = reinterpret_cast<const float4*>(gagg + (int64_t)c * L::DM);
     float4* d4 = reinterpret_cast<float4*>(dacc);
@@ -1027,17 +1039,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BwdLsWaves<
   }
   const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
-  f32x4 st[NW + ND];
+  f32x4 st[NST];
   auto issue = [&](int P) {
+    if constexpr (NWP % NT == 0) {  // (4 waves: each thread's pieces all W, then all D)
+      constexpr int NW = NWP / NT;
 #pragma unroll
-    for (int i = 0; i < NW; ++i) st[i] = ldw4(R.w2v, (tid + 256 * i) * 16, P * LS_PAIR_W);
+      for (int i = 0; i < NW; ++i) st[i] = ldw4(R.w2v, (tid + NT * i) * 16, P * LS_PAIR_W);
 #pragma unroll
-    for (int i = 0; i < ND; ++i) st[NW + i] = ldw4(R.w2d, (tid + 256 * i) * 16, P * LS_PAIR_D);
+      for (int i = NW; i < NST; ++i) st[i] = ldw4(R.w2d, (tid + NT * i - NWP) * 16, P * LS_PAIR_D);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NST; ++i) {
+        const int idx = tid + NT * i;
+        const bool isw = idx < NWP;  // wave-uniform (NWP % 64 == 0)
+        st[i] = isw ? ldw4(R.w2v, idx * 16, P * LS_PAIR_W) : ldw4(R.w2d, (idx - NWP) * 16, P * LS_PAIR_D);
+      }
+    }
   };
   auto commit = [&]() {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < NW + ND; ++i) *reinterpret_cast<f32x4*>(img + (tid + 256 * i) * 16) = st[i];
+    for (int i = 0; i < NST; ++i) *reinterpret_cast<f32x4*>(img + (tid + NT * i) * 16) = st[i];
     __syncthreads();
   };
   issue(0);
@@ -1191,12 +1213,14 @@ hipError_t launch_conv_bwd_ls(int kind, const FusedArgs& a, hipStream_t s) {
   const int nc = a.c_end - a.c_begin;
   if (nc <= 0 || a.n_nodes <= 0) return hipSuccess;
   const dim3 grid((nc + 3) / 4), block(256);
+  constexpr int WM = BwdWpg<LayerMid>::v;
   switch (kind) {
     case 0: hipLaunchKernelGGL(k_conv_bwd_ls<LayerFirst>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb, a.Y,
                                a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb, a.c_begin, a.c_end, a.n_nodes);
       break;
-    case 1: hipLaunchKernelGGL(k_conv_bwd_ls<LayerMid>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb, a.Y,
-                               a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb, a.c_begin, a.c_end, a.n_nodes);
+    case 1: hipLaunchKernelGGL(k_conv_bwd_ls<LayerMid>, dim3((nc + WM - 1) / WM), dim3(64 * WM), 0, s,
+                               a.row_ptr, a.nbr, a.emb, a.Y, a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb,
+                               a.c_begin, a.c_end, a.n_nodes);
       break;
     default: return hipErrorInvalidValue;  // the last block: launch_conv_bwd_nbr_last
   }

@@ -73,6 +73,7 @@ for s in "$@"; do
     pmcsq2f) step pmcsq2f 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT --kernel-trace --output-format csv -d gpurun_out/pmc_sq2f -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     pmcsq3f) step pmcsq3f 600 rocprofv3 --pmc SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_WR SQ_WAIT_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS --kernel-trace --output-format csv -d gpurun_out/pmc_sq3f -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     proftracev_*) v=${s#proftracev_}; step proftrace_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so rocprofv3 --kernel-trace --output-format csv -d gpurun_out/proftrace_$v -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
+    testsv_*) v=${s#testsv_}; step testsv_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread ;;
     benchv_*) v=${s#benchv_}; step bench_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     testsv_*) v=${s#testsv_}; step tests_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -m pytest tests -m gpu -x -q ;;
     bench2self) step bench2self 600 python bench.py --gpus 2 --same-device --steps 2 --warmup 1 --cells 11 --no-cpu-baseline ;;
