@@ -293,6 +293,85 @@ __device__ __forceinline__ void nl_epilogue_runs(const NlProb& P, const f32x16& 
   }
 }
 
+// The gate epilogues (epi 2 / 3) in the same run form.  epi 2 (the 0e block,
+// R = 1): C = the pre-activations, xo = act(scalars) for columns < n_act.
+// epi 3 (l > 0): C = the pre-gate values, xo = act(gate) * value; the tile's
+// T x CW gate pre-activations (written to C by the 0e launch) are loaded
+// once per tile, activated once per (node, column) instead of once
+// per output element, and read back from LDS by the copy-out (the generic
+// epilogue above issued four dependent scalar global loads and four
+// activations per float4).  Gate problems split K (si2 + self-connection), so
+// only the single-block (NS = 1) tiles instantiate it.
+#ifndef E3GNN_NL_GATE_RUNS
+#define E3GNN_NL_GATE_RUNS 1
+#endif
+template <int WN, int R>
+__device__ __forceinline__ void nl_epilogue_gate(const NlProb& P, const f32x16& acc, int node0,
+                                                 int n0, float* lds) {
+  constexpr int BM = 128 / WN, CW = 32 * WN;
+  constexpr int T = BM / R, ROWS = T * R;
+  constexpr int RUN = CW * R, LDR = RUN + 4;
+  constexpr int GS = R > 1 ? T * CW : 0, NG = (GS + 255) / 256;
+  static_assert(T * LDR + GS <= NL_LDS, "C runs and gate factors must fit the LDS stages");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const int ncol = P.N - n0 < CW ? P.N - n0 : CW;  // a multiple of 4 (add_nl)
+  const int vn = min(T, P.nodes - node0);
+  __syncthreads();
+  const int cR = (wc * 32 + (lane & 31)) * R;
+  const int rbase = wr * 32 + 4 * (lane >> 5);
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = rbase + (reg & 3) + 8 * (reg >> 2);
+    const int nl = row / R, m = row - nl * R;
+    if (row < ROWS) lds[nl * LDR + cR + m] = acc[reg];
+  }
+  float* gl = lds + T * LDR;
+  if constexpr (GS > 0) {
+    float gv[NG];
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int u = tid + 256 * i;
+      const int nl = u / CW, c = u - nl * CW;
+      gv[i] = (u < GS && nl < vn && c < ncol)
+                  ? P.C[(int64_t)(node0 + nl) * P.ldc + P.gate_off + n0 + c]
+                  : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int u = tid + 256 * i;
+      if (u < GS) gl[u] = act_fwd(gv[i]);
+    }
+  }
+  __syncthreads();
+  if (ncol <= 0) return;
+  const int len = ncol * R;
+  constexpr int SEGC = RUN / 4, UC = T * SEGC;
+#pragma unroll 1
+  for (int u = tid; u < UC; u += 256) {
+    const int nl = u / SEGC, j = 4 * (u - nl * SEGC);
+    const int node = node0 + nl;
+    if (j >= len || node >= P.nodes) continue;
+    const float4 v = *reinterpret_cast<const float4*>(lds + nl * LDR + j);
+    *reinterpret_cast<float4*>(P.C + (int64_t)node * P.ldc + P.c_off + n0 * R + j) = v;
+    float* xp = P.xo + (int64_t)node * P.ldxo + P.xo_off + n0 * R + j;
+    if constexpr (R == 1) {  // epi 2: element q is column n0 + j + q
+      if (n0 + j + 3 < P.n_act) {
+        *reinterpret_cast<float4*>(xp) = make_float4(act_fwd(v.x), act_fwd(v.y), act_fwd(v.z), act_fwd(v.w));
+      } else {
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (n0 + j + q < P.n_act) xp[q] = act_fwd(e[q]);
+      }
+    } else {  // epi 3: element q is column (j + q) / R of the tile
+      const float* gn = gl + nl * CW;
+      *reinterpret_cast<float4*>(xp) = make_float4(gn[(j + 0) / R] * v.x, gn[(j + 1) / R] * v.y,
+                                                   gn[(j + 2) / R] * v.z, gn[(j + 3) / R] * v.w);
+    }
+  }
+}
+
 // Operand loads through buffer descriptors based at the tile (a 32-bit lane
 // offset fixed over the k loop, the k-step's advance a scalar offset: no
 // 64-bit addresses to keep live).  Optionally (E3GNN_NL_DEPTH2, 64 x 64 tiles
@@ -477,6 +556,8 @@ __device__ __forceinline__ void nl_tile(const NlProb& P, int local, float* lds) 
   for (int sub = 0; sub < NS; ++sub) {
     if (E3GNN_NL_RUNS && P.epi <= 1)
       nl_epilogue_runs<WN, R>(P, acc[sub], node0, n0 + sub * 32 * WN, lds);
+    else if (E3GNN_NL_GATE_RUNS && NS == 1 && P.epi >= 2 && (R > 1) == (P.epi == 3))
+      nl_epilogue_gate<WN, R>(P, acc[sub], node0, n0 + sub * 32 * WN, lds);
     else
       nl_epilogue<WN, R>(P, acc[sub], node0, n0 + sub * 32 * WN, lds);
   }

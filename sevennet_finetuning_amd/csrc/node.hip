@@ -4,6 +4,8 @@
 // Every reduction here is deterministic: per-atom sums walk CSR lists in edge
 // order (no float atomics); scalar totals use a fixed two-level tree.
 #include "common.h"
+
+#include <climits>
 #include "node.h"
 
 namespace e3gnn {
@@ -296,7 +298,74 @@ __global__ void k_count_nbr(int64_t E, const int* __restrict__ nbr, int n_nodes,
   if (j >= 0 && j < n_nodes) atomicAdd(cnt + j, 1);
 }
 
-// exclusive scan of cnt[0..n) into out[0..n], single workgroup of 1024.
+// exclusive scan of cnt[0..n) into out[0..n].  Three launches: k_scan_blocks
+// (1,024 counts per workgroup, 4 consecutive per thread: local exclusive
+// prefixes to out, the block total to bsum), k_scan_top (one workgroup scans
+// the block totals in place, out[n] = the grand total), k_scan_add (adds each
+// block's offset).  The old single-workgroup scan (strided per-thread chunks)
+// took 164 us for 97k nodes.
+constexpr int SCAN_B = 1024;
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+__global__ __launch_bounds__(256) void k_scan_blocks(int n, const int* __restrict__ cnt,
+                                                     int* __restrict__ out, int* __restrict__ bsum) {
+  __shared__ int wsum[4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int i0 = blockIdx.x * SCAN_B + 4 * t;
+  int c[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) c[q] = i0 + q < n ? cnt[i0 + q] : 0;
+  const int ts = c[0] + c[1] + c[2] + c[3];
+  const int incl = wave_incl_scan(ts, lane);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) base += q < w ? wsum[q] : 0;
+  int run = base + incl - ts;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (i0 + q < n) out[i0 + q] = run;
+    run += c[q];
+  }
+  if (t == 255) bsum[blockIdx.x] = base + incl;
+}
+__global__ __launch_bounds__(1024) void k_scan_top(int nb, int n, int* __restrict__ bsum,
+                                                   int* __restrict__ out) {
+  __shared__ int wsum[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int carry = 0;
+  for (int c0 = 0; c0 < nb; c0 += 1024) {
+    const int v = c0 + t < nb ? bsum[c0 + t] : 0;
+    const int incl = wave_incl_scan(v, lane);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int base = carry;
+    for (int q = 0; q < w; ++q) base += wsum[q];
+    int total = carry;
+    for (int q = 0; q < 16; ++q) total += wsum[q];
+    if (c0 + t < nb) bsum[c0 + t] = base + incl - v;
+    carry = total;
+    __syncthreads();
+  }
+  if (t == 0) out[n] = carry;
+}
+__global__ __launch_bounds__(256) void k_scan_add(int n, const int* __restrict__ bsum,
+                                                  int* __restrict__ out) {
+  const int i0 = blockIdx.x * SCAN_B + 4 * threadIdx.x;
+  const int add = bsum[blockIdx.x];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (i0 + q < n) out[i0 + q] += add;
+}
+// single workgroup fallback (graphs with fewer edges than count blocks: the
+// block totals borrow the edge permutation's storage)
 __global__ __launch_bounds__(1024) void k_scan(int n, const int* __restrict__ cnt,
                                                int* __restrict__ out) {
   __shared__ int part[1024];
@@ -332,12 +401,27 @@ __global__ void k_scatter_perm(int64_t E, const int* __restrict__ nbr, int n_nod
   perm[ptr[j] + slot] = (int)e;
 }
 
-// make each neighbour's edge list ascending in edge id (deterministic order)
-__global__ void k_sort_segments(int n, const int* __restrict__ ptr, int* __restrict__ perm) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// make each neighbour's edge list ascending in edge id (deterministic order):
+// one wave per neighbour, segments of up to 64 edges sorted by rank (lane k
+// holds element k; its rank = the number of smaller elements, the ids being
+// distinct), longer ones by an insertion sort in lane 0.  (A thread-per-node
+// insertion sort on global memory took 138 us on the 97k-atom graph and 89 us
+// on a fine-tune batch: every shift a dependent L2 round trip.)
+__global__ __launch_bounds__(256) void k_sort_segments(int n, const int* __restrict__ ptr,
+                                                       int* __restrict__ perm) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (j >= n) return;
-  const int b = ptr[j], en = ptr[j + 1];
-  for (int i = b + 1; i < en; ++i) {
+  const int b = ptr[j], len = ptr[j + 1] - b;
+  if (len <= 1) return;
+  if (len <= 64) {
+    const int v = lane < len ? perm[b + lane] : INT_MAX;
+    int rank = 0;
+    for (int k = 0; k < len; ++k) rank += __shfl(v, k) < v;
+    if (lane < len) perm[b + rank] = v;
+    return;
+  }
+  if (lane != 0) return;
+  for (int i = b + 1; i < b + len; ++i) {
     const int v = perm[i];
     int k = i - 1;
     while (k >= b && perm[k] > v) {
@@ -624,10 +708,18 @@ hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* 
   LAUNCH(k_row_ptr, nblk(E), E, n_centers, n_nodes, n_interior, center, nbr, row_ptr, err);
   LAUNCH(k_fill_int, nblk(n_nodes), n_nodes, 0, cnt);
   LAUNCH(k_count_nbr, nblk(E), E, nbr, n_nodes, cnt);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, n_nodes, cnt, src_ptr);
+  const int nb = (n_nodes + SCAN_B - 1) / SCAN_B;
+  if (nb > 0 && E >= nb) {  // block totals in src_perm[0, nb): k_scatter_perm overwrites them
+    hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(256), 0, s, n_nodes, cnt, src_ptr, src_perm);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, s, nb, n_nodes, src_perm, src_ptr);
+    hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(256), 0, s, n_nodes, src_perm, src_ptr);
+  } else {
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, n_nodes, cnt, src_ptr);
+  }
   LAUNCH(k_fill_int, nblk(n_nodes), n_nodes, 0, cnt);
   LAUNCH(k_scatter_perm, nblk(E), E, nbr, n_nodes, src_ptr, cnt, src_perm);
-  LAUNCH(k_sort_segments, nblk(n_nodes), n_nodes, src_ptr, src_perm);
+  if (n_nodes > 0)
+    hipLaunchKernelGGL(k_sort_segments, dim3((n_nodes + 3) / 4), dim3(256), 0, s, n_nodes, src_ptr, src_perm);
   return hipGetLastError();
 }
 hipError_t launch_embed(int n, const int* type, int nsp, const float* W, float* x, int* err,

@@ -246,6 +246,31 @@ def test_radial_mlp_chain_kernels_vs_fp64(width):
         assert _rel(a, b) < 2e-5, nm
 
 
+@pytest.mark.parametrize('n,mean_deg,hub', [(5, 2, 0), (3000, 0.0005, 0), (3000, 6, 150), (20000, 28, 90)])
+def test_conv_graph_csr_matches_numpy(hip_backend, n, mean_deg, hub):
+    """row_ptr / src_ptr / src_perm of e3gnn_conv_graph against numpy: the
+    transposed CSR lists each neighbour's edges in ascending edge id.  Sizes
+    span one and several 1,024-count scan blocks, nodes without edges, and a
+    hub neighbour with more than 64 incoming edges (the long-segment sort)."""
+    rng = np.random.default_rng(n)
+    deg = rng.poisson(mean_deg, n)
+    deg[::11] = 0
+    center = np.repeat(np.arange(n), deg)
+    nbr = rng.integers(0, n, len(center))
+    if hub:
+        nbr[rng.choice(len(center), hub, replace=False)] = n // 2
+    g = conv_ops.ConvGraph(n, torch.tensor(center, device=DEV), torch.tensor(nbr, device=DEV),
+                           hip_backend)
+    aux = g.aux
+    row_ptr = np.concatenate([[0], np.cumsum(deg)])
+    cnt = np.bincount(nbr, minlength=n)
+    src_ptr = np.concatenate([[0], np.cumsum(cnt)])
+    src_perm = np.argsort(nbr, kind='stable')
+    assert np.array_equal(aux['row_ptr'].cpu().numpy(), row_ptr)
+    assert np.array_equal(aux['src_ptr'].cpu().numpy(), src_ptr)
+    assert np.array_equal(aux['src_perm'].cpu().numpy()[:len(center)], src_perm)
+
+
 def test_conv_graph_rejects_unsorted(hip_backend):
     from sevennet_finetuning_amd._lib import E3GNNError
     with pytest.raises(E3GNNError, match='not sorted'):
