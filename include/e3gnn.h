@@ -91,7 +91,8 @@ void e3gnn_ctx_free(e3gnn_ctx* c);
  * deployed_serial.pt).  type[n_atoms] (species index), edge_center/edge_nbr[E]
  * int32, edge_vec[E*3].  Outputs (each nullable except energy): energy[1],
  * atomic_energy[n_atoms], forces[n_atoms*3], virial6[6], edge_grad[E*3] =
- * dE/dedge_vec.  Synchronises `stream` before returning. */
+ * dE/dedge_vec.  Synchronises `stream` before returning unless the context is
+ * in stream-ordered mode (e3gnn_set_stream_ordered). */
 int e3gnn_energy_forces(e3gnn_ctx* c, int64_t n_atoms, int64_t n_edges, const int32_t* type,
                         const int32_t* edge_center, const int32_t* edge_nbr,
                         const float* edge_vec, float* energy, float* atomic_energy,
@@ -376,6 +377,13 @@ int e3gnn_d3_compute(e3gnn_d3* h, int64_t n, const double* pos, const double* ce
 int e3gnn_set_impl(e3gnn_ctx* c, int impl);
 /* enable per-kernel-class HIP-event timing on the context */
 int e3gnn_set_timing(e3gnn_ctx* c, int enable);
+/* Stream-ordered mode (default off): e3gnn_energy_forces returns once its
+ * work is enqueued on `stream` (the inputs already copied and the graph
+ * validated) instead of synchronising it -- the outputs are ready in stream
+ * order, as a PyTorch module's outputs are (the reference's deployed model
+ * called from Python, deploy.py:20-32).  Hosts that read the outputs from
+ * other streams or the CPU synchronise the stream themselves. */
+int e3gnn_set_stream_ordered(e3gnn_ctx* c, int enable);
 /* Number of kernel classes recorded; fills up to `max` entries: name (static
  * string), total ms, launches, algorithmic FLOP and algorithmic HBM bytes. */
 int e3gnn_kernel_stats(e3gnn_ctx* c, const char** names, double* ms, int64_t* launches,

@@ -81,6 +81,7 @@ SIGNATURES = {
     'e3gnn_nlist_fetch': (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_set_impl': (_c_int, [_vp, _c_int]),
     'e3gnn_set_timing': (_c_int, [_vp, _c_int]),
+    'e3gnn_set_stream_ordered': (_c_int, [_vp, _c_int]),
     'e3gnn_kernel_stats': (_c_int, [_vp, _P(_cp), _P(ctypes.c_double), _P(_c_i64),
                                     _P(ctypes.c_double), _P(ctypes.c_double), _c_int]),
     'e3gnn_reset_stats': (_c_int, [_vp]),

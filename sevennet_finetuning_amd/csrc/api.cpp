@@ -245,6 +245,7 @@ struct e3gnn_ctx {
   std::vector<DBuf> x, grad, h, y, w, a1, a2;
   DBuf H1, H2, agg, dw, dxc, dy, dh, eat, part, vpart, scratch6;
   bool timing = false;
+  bool stream_ordered = false;  // e3gnn_set_stream_ordered
   Stat stats[C_NCLS];
   std::vector<Pending> pending;
   std::vector<hipEvent_t> evpool;
@@ -1506,7 +1507,7 @@ int e3gnn_energy_forces(e3gnn_ctx* c, int64_t n_atoms, int64_t n_edges, const in
   for (int t = L - 1; t >= 0; --t)
     if ((rc = e3gnn_layer_backward(c, t, stream))) return rc;
   if ((rc = e3gnn_forces(c, forces, virial6, edge_grad, stream))) return rc;
-  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  if (!c->stream_ordered) HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   return E3GNN_OK;
 }
 
@@ -2140,6 +2141,11 @@ int e3gnn_set_timing(e3gnn_ctx* c, int enable) {
   if (!c) return fail(E3GNN_ERR_ARG, "null context");
   c->flush();
   c->timing = enable != 0;
+  return E3GNN_OK;
+}
+int e3gnn_set_stream_ordered(e3gnn_ctx* c, int enable) {
+  if (!c) return fail(E3GNN_ERR_ARG, "null context");
+  c->stream_ordered = enable != 0;
   return E3GNN_OK;
 }
 int e3gnn_kernel_stats(e3gnn_ctx* c, const char** names, double* ms, int64_t* launches,

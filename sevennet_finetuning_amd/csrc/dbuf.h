@@ -24,11 +24,18 @@ struct DBuf {
     return *this;
   }
   ~DBuf() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      (void)hipDeviceSynchronize();   // (see ensure)
+      (void)hipFree(p);
+    }
   }
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     if (p) {
+      // work still queued may read the old buffer (a stream-ordered
+      // e3gnn_energy_forces returns before its kernels finish): drain the
+      // device before freeing (growth only, so once per new maximum size)
+      (void)hipDeviceSynchronize();
       (void)hipFree(p);
       p = nullptr;
       cap = 0;

@@ -57,6 +57,10 @@ class E3GNNModel:
         _lib.check(self.lib.e3gnn_model_info(h, ns, co, nl, cs))
         self.num_species, self.num_layers, self.comm_size = ns.value, nl.value, cs.value
         self.is_batch_data = False
+        # outputs are device tensors on torch's current stream: return once the
+        # evaluation is enqueued (stream order, like a torch module) rather than
+        # synchronising; E3GNN_SYNC=1 restores the blocking call
+        self.set_stream_ordered(os.environ.get('E3GNN_SYNC', '0') != '1')
 
     # --------------------------------------------------------------- metadata
     def type_map(self):
@@ -113,6 +117,9 @@ class E3GNNModel:
     def set_impl(self, impl):
         """'fused' (default) or 'v1' (unfused kernels, cross-check)."""
         _lib.check(self.lib.e3gnn_set_impl(self._ctx, {'fused': 0, 'v1': 1}[impl]))
+
+    def set_stream_ordered(self, enable=True):
+        _lib.check(self.lib.e3gnn_set_stream_ordered(self._ctx, int(enable)))
 
     def set_timing(self, enable=True):
         _lib.check(self.lib.e3gnn_set_timing(self._ctx, int(enable)))

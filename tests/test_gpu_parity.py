@@ -379,3 +379,30 @@ def test_raw_vector_sh_on_the_fused_kernels(raw_sh_dir, model, name):
     # the flag matters: the normalised model gives another energy
     norm = run(model, pos, cell, types)
     assert abs(norm['energy'] - got['energy']) > 1e-3
+
+
+def test_stream_ordered_calls_match_blocking_calls(model):
+    """e3gnn_set_stream_ordered: back-to-back calls on growing systems (the
+    second and third grow the workspace while the first is still queued) give
+    bit-identical outputs to blocking calls, read after one synchronize."""
+    from sevennet_finetuning_amd.neighbor import DeviceNeighborList
+    dev = model.device
+    nl = DeviceNeighborList(dev)
+    calls = []
+    for name in ('si_rng0_2x2x1', 'si_rng0_3x3x3', 'mixed_2x2x2'):
+        pos, cell, types = system(name, SYMS)
+        c, nb, _, vec = nl(pos, cell, model.cutoff)
+        calls.append((torch.tensor(types, dtype=torch.int32, device=dev), c.clone(), nb.clone(),
+                      vec.clone()))
+    fresh = type(model)(device=dev)   # a new context: its workspace grows call by call
+    try:
+        fresh.set_stream_ordered(True)
+        queued = [fresh.energy_forces(*a) for a in calls]
+        torch.cuda.synchronize()
+        fresh.set_stream_ordered(False)
+        for a, q in zip(calls, queued):
+            ref = fresh.energy_forces(*a)
+            for k in ('energy', 'atomic_energy', 'forces', 'virial'):
+                assert torch.equal(q[k], ref[k]), k
+    finally:
+        fresh.close()

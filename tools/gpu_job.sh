@@ -29,6 +29,7 @@ for s in "$@"; do
     benchq) step bench 600 python bench.py --steps 3 --warmup 1 --cpu-seconds 10 ;;
     benchf_*) step $s 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchf) step benchf 600 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
+    benchsync_*) step $s 600 env E3GNN_SYNC=1 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchmorton) step benchmorton 600 env E3GNN_BENCH_ORDER=morton python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     benchmorton_*) v=${s#benchmorton_}; step benchmorton_$v 600 env E3GNN_BENCH_ORDER=morton E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     t_*) t=${s#t_}; step t_$t 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k $t ;;
