@@ -150,8 +150,9 @@ def cpu_baseline(seconds, cells):
     """Oracle (plain-PyTorch CPU restatement of the reference) on a bounded
     sample of the same workload: a cells^3 Si box (default 6^3 = 1,728 atoms,
     where the reference CPU path is already at its flat large-box throughput,
-    SURVEY.md 6), the same recipe as the bench box, timed for >= 1 evaluation
-    and ~`seconds` of CPU work on the host's thread share."""
+    SURVEY.md 6), the same recipe as the bench box: one untimed warm-up call,
+    then >= 3 timed evaluations and >= `seconds` of CPU work on the host's
+    thread share."""
     from oracle.neighbor import neighbor_list
     from oracle.sevennet_ref import SevenNet0Ref
     from sevennet_finetuning_amd.structures import si_diamond
@@ -166,8 +167,9 @@ def cpu_baseline(seconds, cells):
     args = (torch.tensor(pos, dtype=torch.float32), torch.full((len(pos),), 69),
             torch.tensor(ei), torch.tensor(sh, dtype=torch.float32),
             torch.tensor(cell, dtype=torch.float32))
+    ref(*args)   # warm-up call (allocator, thread pool, kernel selection): not timed
     t0, n = time.perf_counter(), 0
-    while n == 0 or time.perf_counter() - t0 < seconds:
+    while n < 3 or time.perf_counter() - t0 < seconds:
         ref(*args)
         n += 1
     dt = time.perf_counter() - t0
@@ -175,7 +177,7 @@ def cpu_baseline(seconds, cells):
             'kind': 'port',
             'sample': f'{n} energy+force+stress evals of a {len(pos)}-atom Si box ({cells}^3 '
                       f'cells, {ei.shape[1]} edges) in {dt:.1f} s, oracle/sevennet_ref.py fp32, '
-                      f'torch CPU, first call included',
+                      f'torch CPU, after one untimed warm-up call',
             'reference_context': 'the reference frozen TorchScript CPU path measured in the '
                                  'survey container: 272 atoms/s at 10,648 atoms, 8 threads '
                                  '(SURVEY.md 8d); not re-run here (a shipped program), not '
@@ -281,30 +283,31 @@ def free_port():
         return s.getsockname()[1]
 
 
-def launcher_cmd(argv, n, port):
-    """The torch.distributed.run command that starts `n` local ranks of this
-    script with the same arguments (one process per GPU)."""
+def launcher_cmd(argv, n, port, script=None):
+    """The torch.distributed.run command that starts `n` local ranks of
+    `script` (default: this file) with the same arguments (one process per GPU)."""
     return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
             f'--nproc-per-node={n}', '--master-addr=127.0.0.1', f'--master-port={port}',
-            os.path.abspath(__file__), *argv]
+            os.path.abspath(script or __file__), *argv]
 
 
-def maybe_launch(args, argv):
+def maybe_launch(args, argv, script=None):
     """`python bench.py --gpus N` with no launcher around it: start the N ranks
     as child processes (before anything touches the GPU in this process) and
-    return their exit code; None when this process is a rank itself."""
+    return their exit code; None when this process is a rank itself.
+    bench_train.py shares it (`script`)."""
     if args.gpus <= 1 or 'WORLD_SIZE' in os.environ:
         return None
     import subprocess
-    cmd = launcher_cmd(argv, args.gpus, free_port())
+    cmd = launcher_cmd(argv, args.gpus, free_port(), script)
     log(f'launching {args.gpus} ranks: {" ".join(cmd)}')
     return subprocess.call(cmd)
 
 
-def check_world(args, world):
+def check_world(args, world, script='bench.py'):
     """A rank must see exactly the --gpus N world it was asked for."""
     if world != args.gpus:
-        raise RuntimeError(f'bench.py --gpus {args.gpus} but WORLD_SIZE={world}: '
+        raise RuntimeError(f'{script} --gpus {args.gpus} but WORLD_SIZE={world}: '
                            'run it directly or under torch.distributed.run with '
                            f'--nproc-per-node {args.gpus}')
 

@@ -1,7 +1,7 @@
 """Benchmark of the fine-tune step (BASELINE config 5).
 
-``python bench_train.py --gpus N --steps K --warmup W`` (N > 1 under torchrun,
-one process per GPU, RCCL).  A step = one iteration of the reference's
+``python bench_train.py --gpus N --steps K --warmup W`` (N > 1: one process
+per GPU over RCCL; started under torchrun, or it launches its N ranks itself).  A step = one iteration of the reference's
 RehearsalTrainer.run_one_epoch_rehearsal (trainer.py:174-206) with the
 FT_w_reEWC recipe (Huber delta 0.01, force weight 1, stress weight 0.01, EWC
 lambda 1e5, Adam): forward + force/stress (create_graph) + loss backward
@@ -87,7 +87,8 @@ def main():
     ap.add_argument('--batch', type=int, default=8)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--eager', action='store_true',
-                    help='no HIP-graph capture of the step (always eager for N > 1)')
+                    help='no HIP-graph capture of the step (for N > 1 the graphed step '
+                         'is three captured segments around the two gradient all-reduces)')
     ap.add_argument('--cpu-seconds', type=float, default=10.0)
     ap.add_argument('--blas', default='rocblas', choices=['rocblas', 'hipblaslt'],
                     help='torch GEMM backend for the linears and the radial MLP')
@@ -95,16 +96,21 @@ def main():
                     help='the loss gradient by autograd double backward instead of the '
                          'hand-scheduled derivatives (train_explicit.py)')
     args = ap.parse_args()
+    import bench
+    # `--gpus N` without a launcher: start the N ranks as children before this
+    # process touches the GPU, and exit with their code (bench.py's contract)
+    rc = bench.maybe_launch(args, sys.argv[1:], script=__file__)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    device = torch.device('cuda', local)
-    torch.cuda.set_device(device)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=device)
-
+    bench.check_world(args, world, 'bench_train.py')
     from sevennet_finetuning_amd import train
+    if world > 1:
+        rank, world, local, device = train.setup_distributed()
+    else:
+        rank, local, device = 0, 0, torch.device('cuda', 0)
+        torch.cuda.set_device(device)
+
     from sevennet_finetuning_amd.nn import SevenNetTrainable
     model = SevenNetTrainable(device=device)
     fisher = {n: torch.full_like(p, 1e-3) for n, p in model.named_parameters()}

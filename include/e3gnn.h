@@ -382,7 +382,10 @@ int e3gnn_set_timing(e3gnn_ctx* c, int enable);
  * validated) instead of synchronising it -- the outputs are ready in stream
  * order, as a PyTorch module's outputs are (the reference's deployed model
  * called from Python, deploy.py:20-32).  Hosts that read the outputs from
- * other streams or the CPU synchronise the stream themselves. */
+ * other streams or the CPU synchronise the stream themselves.  The context's
+ * workspaces are shared between calls: a call on a different stream than the
+ * previous stream-ordered evaluation first makes its stream wait (device-side
+ * event) for that evaluation's end. */
 int e3gnn_set_stream_ordered(e3gnn_ctx* c, int enable);
 /* Number of kernel classes recorded; fills up to `max` entries: name (static
  * string), total ms, launches, algorithmic FLOP and algorithmic HBM bytes. */

@@ -281,6 +281,18 @@ class GenericHipConvBackend(HipConvBackend):
             self._stream(h)))
         return dh, dY, dw
 
+    # The one-launch tangent forward / dual backward exist for SevenNet-0's
+    # three compile-time kinds only (kind there is 0/1/2, here a block index):
+    # refuse instead of running the wrong kernel (train_explicit.supported()
+    # keeps runtime-table models on the autograd path).
+    def tangent_forward(self, *a, **k):
+        raise _lib.E3GNNError('GenericHipConvBackend has no fused tangent forward: '
+                              'runtime-table models train through autograd')
+
+    def dual_backward(self, *a, **k):
+        raise _lib.E3GNNError('GenericHipConvBackend has no fused dual backward: '
+                              'runtime-table models train through autograd')
+
 
 def _add(acc, t):
     if t is None:
@@ -451,8 +463,15 @@ def _gate_dual_call(lib, op, dims, y, yd, xb=None, xdb=None, out0=None, out1=Non
     """e3gnn_gate_dual: op 0 out0 = J yd; op 1 out0 = J^T xb + d/dy <xdb, J yd>,
     out1 = J^T xdb (train_explicit.py)"""
     p = lambda t: t.contiguous().data_ptr() if t is not None else None  # noqa: E731
+
+    def o(t, name):   # outputs are written in place: a contiguous copy would be lost
+        if t is None:
+            return None
+        if not t.is_contiguous():
+            raise _lib.E3GNNError(f'e3gnn_gate_dual: {name} must be contiguous')
+        return t.data_ptr()
     _lib.check(lib.e3gnn_gate_dual(op, y.shape[0], dims.ctypes.data, p(y), p(yd), p(xb), p(xdb),
-                                   p(out0), p(out1), ctypes.c_float(scale),
+                                   o(out0, 'out0'), o(out1, 'out1'), ctypes.c_float(scale),
                                    torch.cuda.current_stream(y.device).cuda_stream))
 
 

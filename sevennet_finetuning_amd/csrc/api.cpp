@@ -246,6 +246,12 @@ struct e3gnn_ctx {
   DBuf H1, H2, agg, dw, dxc, dy, dh, eat, part, vpart, scratch6;
   bool timing = false;
   bool stream_ordered = false;  // e3gnn_set_stream_ordered
+  // stream-ordered mode: the end of the last evaluation on `done_stream`; a
+  // call on another stream waits for it before touching the shared
+  // workspaces (inputs are copied into them at graph_set)
+  hipEvent_t done_ev = nullptr;
+  hipStream_t done_stream = nullptr;
+  bool done_pending = false;
   Stat stats[C_NCLS];
   std::vector<Pending> pending;
   std::vector<hipEvent_t> evpool;
@@ -278,6 +284,10 @@ struct e3gnn_ctx {
   ~e3gnn_ctx() {
     if (gen) gen_ctx_free(gen);
     flush();
+    if (done_ev) {
+      (void)hipEventSynchronize(done_ev);
+      (void)hipEventDestroy(done_ev);
+    }
     for (auto e : evpool) (void)hipEventDestroy(e);
   }
 };
@@ -990,6 +1000,8 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   e3gnn_model* m = c->m;
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
+  if (c->done_pending && c->done_stream != s) HIPCHK(hipStreamWaitEvent(s, c->done_ev, 0));
+  c->done_pending = false;
   const int64_t n = n_local + n_ghost, nl = n_local, E = n_edges;
   c->n = n;
   c->nl = nl;
@@ -1507,7 +1519,14 @@ int e3gnn_energy_forces(e3gnn_ctx* c, int64_t n_atoms, int64_t n_edges, const in
   for (int t = L - 1; t >= 0; --t)
     if ((rc = e3gnn_layer_backward(c, t, stream))) return rc;
   if ((rc = e3gnn_forces(c, forces, virial6, edge_grad, stream))) return rc;
-  if (!c->stream_ordered) HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  if (!c->stream_ordered) {
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  } else {
+    if (!c->done_ev) HIPCHK(hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->done_ev, (hipStream_t)stream));
+    c->done_stream = (hipStream_t)stream;
+    c->done_pending = true;
+  }
   return E3GNN_OK;
 }
 

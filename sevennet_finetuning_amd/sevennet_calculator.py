@@ -41,9 +41,20 @@ class SevenNetCalculator(Calculator):
         file_type = file_type.lower()
         if file_type not in ('checkpoint', 'torchscript', 'deployed'):
             raise ValueError('file_type should be checkpoint or torchscript')
+        if not isinstance(device, (str, torch.device)):
+            raise ValueError('device must be an instance of torch.device or str.')
         if isinstance(device, str) and device == 'auto':
+            # the reference falls back to 'cpu' here (sevennet_calculator.py:57-62);
+            # this build has no CPU engine, so 'auto' means the first GPU
             device = torch.device('cuda', 0)
         self.device = torch.device(device)
+        if self.device.type != 'cuda':
+            # an explicit refusal, never a silent CPU fallback: the evaluation
+            # runs only in libe3gnn_hip.so's HIP kernels
+            raise ValueError(
+                f"SevenNetCalculator(device='{self.device}'): this build evaluates the "
+                "model only on an AMD GPU through its HIP library (libe3gnn_hip.so); "
+                "there is no CPU path. Use device='cuda' / 'cuda:N' (ROCm) or 'auto'.")
         import os
         path = model if os.path.isdir(str(model)) else pretrained_name_to_path(model)
         # the native SevenNet-0 engine, or the generic one for other models of

@@ -764,11 +764,26 @@ class GraphedRehearsalStep:
 
 def setup_distributed(backend=None):
     """One process per GPU from torchrun's env (RANK/LOCAL_RANK/WORLD_SIZE/
-    MASTER_*); backend "nccl" (RCCL) on GPUs, "gloo" otherwise."""
+    MASTER_*); backend "nccl" (RCCL) on GPUs, "gloo" otherwise.
+
+    The rank's device is bound BEFORE the process group exists (as the
+    reference's entry point does, sevenn/main/sevenn.py:39-49 with
+    torch.cuda.set_device(local_rank) ahead of init_process_group): RCCL takes
+    its device from the current one, so without it every rank of a node would
+    drive cuda:0.  Returns (rank, world_size, local_rank, device); build the
+    model on that device."""
     import torch.distributed as dist
+    local = int(os.environ.get('LOCAL_RANK', 0))
+    gpu = torch.cuda.is_available()
+    device = torch.device('cuda', local) if gpu else torch.device('cpu')
+    if gpu:
+        if local >= torch.cuda.device_count():
+            raise RuntimeError(f'LOCAL_RANK={local} but only {torch.cuda.device_count()} '
+                               'GPU(s) are visible: one process per GPU')
+        torch.cuda.set_device(device)
     if not dist.is_initialized():
         if backend is None:
-            backend = 'nccl' if torch.cuda.is_available() else 'gloo'
-        dist.init_process_group(backend)
-    local = int(os.environ.get('LOCAL_RANK', 0))
-    return dist.get_rank(), dist.get_world_size(), local
+            backend = 'nccl' if gpu else 'gloo'
+        kw = {'device_id': device} if (gpu and backend == 'nccl') else {}
+        dist.init_process_group(backend, **kw)
+    return dist.get_rank(), dist.get_world_size(), local, device

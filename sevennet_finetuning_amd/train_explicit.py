@@ -51,6 +51,11 @@ def supported(model):
     from .nn import sevennet0_kinds
     if sevennet0_kinds(model.manifest, conv_only=True) is None:
         return False
+    # the explicit step drives the specialised SevenNet-0 kernels (out= / acc=
+    # conv launches, the fused tangent forward and dual backward); a model on
+    # the runtime-table backend keeps the autograd path
+    if getattr(getattr(model, 'conv_backend', None), 'generic', False):
+        return False
     if model.sc_type != 'linear' or model.cut.get('name', 'XPLOR') != 'XPLOR':
         return False
     if model.lmax_edge != 2 or model.filter_parity != 1:
@@ -425,8 +430,11 @@ class _DenseBank:
         off = 0
         upos, usrc, uscl = [], [], []
         dsrc, udsrc = [], []
+        self.pnames, ucount = [], []   # per entry: its parameter, its flat elements
         divisors = divisors or {}
         for key, lin, pname in entries:
+            self.pnames.append(pname)
+            ucount.append(sum(lin.irreps_in[i][0] * lin.irreps_out[j][0] for i, j in lin.ins))
             dv = model.slices[divisors[key]][0] if key in divisors else -1
             din, dout = lin.in_off[-1], lin.out_off[-1]
             poff = model.slices[pname][0]
@@ -461,6 +469,8 @@ class _DenseBank:
         self.upos = torch.as_tensor(up, device=dev)
         self.usrc = torch.as_tensor(np.concatenate(usrc), device=dev)
         self.uscl = torch.as_tensor(np.concatenate(uscl), device=dev, dtype=dt)
+        self.uent = np.repeat(np.arange(len(entries)), ucount)   # entry of each reverse row
+        self._mask_key, self._rows = None, None
         self.buf = torch.zeros(off, device=dev, dtype=dt)
         self.gbuf = torch.zeros(off + 1, device=dev, dtype=dt)
         # divisor sources: index into [flat; 1.0] (the extra slot: no divisor)
@@ -489,11 +499,33 @@ class _DenseBank:
         self.gbuf.zero_()
         return {k: self.gbuf[o:o + a * b].view(a, b) for k, (o, a, b) in self.shapes.items()}
 
+    def _trainable_rows(self):
+        """Reverse-map rows of the linears that require grad (None: all do).
+        A frozen linear gets no gradient, as under autograd -- the flat
+        gradient buffer is what the all-reduce, grad norms and the optimizer
+        read.  Re-derived when a parameter's requires_grad flips."""
+        key = tuple(self.model.param(n).requires_grad for n in self.pnames)
+        if key != self._mask_key:
+            self._mask_key = key
+            keep = np.asarray(key)[self.uent]
+            self._rows = None if keep.all() else torch.as_tensor(
+                np.nonzero(keep)[0], device=self.usrc.device)
+        return self._rows
+
     def flush(self, flat_grad):
-        vals = self.gbuf[self.upos].sum(1) * self.uscl
+        rows = self._trainable_rows()
+        if rows is None:
+            upos, usrc, uscl = self.upos, self.usrc, self.uscl
+            udsrc = self.udsrc if self.div else None
+        else:
+            if rows.numel() == 0:
+                return
+            upos, usrc, uscl = self.upos[rows], self.usrc[rows], self.uscl[rows]
+            udsrc = self.udsrc[rows] if self.div else None
+        vals = self.gbuf[upos].sum(1) * uscl
         if self.div:
-            vals.div_(self._flat1()[self.udsrc])
-        flat_grad.index_add_(0, self.usrc, vals)
+            vals.div_(self._flat1()[udsrc])
+        flat_grad.index_add_(0, usrc, vals)
 
 
 # ------------------------------------------------------------------ the step

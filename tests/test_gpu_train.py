@@ -420,6 +420,34 @@ def test_explicit_and_autograd_trainers_take_the_same_step(models):
     assert float((deltas[0] - deltas[1]).norm() / deltas[1].norm()) < 1e-4
 
 
+def test_trainer_on_the_runtime_table_backend_uses_autograd(models):
+    """SevenNet-0 on GenericHipConvBackend: the Trainer must not pick the
+    explicit step (it drives the specialised kernels only), and its SGD step
+    equals the specialised backend's explicit step."""
+    from sevennet_finetuning_amd import conv_ops
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    cfg = {'loss': 'mse', 'force_loss_weight': 0.5, 'stress_loss_weight': 1e-3,
+           'is_train_stress': True, 'optimizer': 'sgd', 'optim_param': {'lr': 1e-3},
+           'scheduler': 'exponentiallr', 'scheduler_param': {'gamma': 0.99},
+           'continue': {'fisher_information': False, 'opt_params': False}}
+    b = train.collate(_batch([11, 12]), device=DEV, dtype=torch.float32)
+    mem = train.collate(_batch([13]), device=DEV, dtype=torch.float32)
+    deltas = []
+    for generic in (False, True):
+        kw = {'conv_backend': conv_ops.GenericHipConvBackend()} if generic else {}
+        m = SevenNetTrainable(device=DEV, **kw)
+        before = m.flat.detach().clone()
+        tr = train.Trainer(m, cfg)
+        assert (tr.explicit is None) == generic
+        tr.rehearsal_step(b, mem)
+        deltas.append((m.flat.detach() - before).double())
+    with pytest.raises(Exception, match='no fused tangent forward'):
+        conv_ops.GenericHipConvBackend().tangent_forward(0, None, None, None, None, None,
+                                                         None, None, None)
+    assert float(deltas[0].norm()) > 0
+    assert float((deltas[0] - deltas[1]).norm() / deltas[0].norm()) < 1e-4
+
+
 def test_rehearsal_ewc_steps_reduce_loss(models):
     """A few rehearsal+EWC Adam steps (the reference's FT_w_reEWC recipe,
     Huber delta 0.01) on fixed batches lower the data loss of both batches,

@@ -110,6 +110,31 @@ def test_explicit_gradient_unsorted_edges_and_frozen_parameters():
     assert float(ge[off:off + n].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize('frozen', ['2_self_interaction_1.linear.weight',
+                                    '3_self_interaction_2.linear.weight',
+                                    'reduce_hidden_to_energy.linear.weight'])
+def test_explicit_gradient_frozen_linear(frozen):
+    """A frozen e3nn Linear gets no gradient in the flat buffer (autograd
+    leaves its slice at zero), and every other parameter's gradient is
+    unchanged: the dense-bank flush skips it (si2 with its denominator fold
+    included)."""
+    m = SevenNetTrainable(device='cpu', conv_backend=CpuConvBackend(), dtype=torch.float64)
+    batch = _batch(seeds=(4,))
+    fns = _losses('mse')
+    _, _, g_all = _explicit(m, batch, fns)
+    m.param(frozen).requires_grad_(False)
+    _, _, ga = _autograd(m, batch, fns)
+    _, _, ge = _explicit(m, batch, fns)
+    off, n, _ = m.slices[frozen]
+    assert float(ga[off:off + n].abs().max()) == 0.0
+    assert float(ge[off:off + n].abs().max()) == 0.0
+    assert float(g_all[off:off + n].abs().max()) > 0
+    assert torch.allclose(ge, ga, rtol=1e-9, atol=1e-9 * float(ga.abs().max()))
+    keep = torch.ones_like(ge, dtype=torch.bool)
+    keep[off:off + n] = False
+    assert torch.allclose(ge[keep], g_all[keep], rtol=1e-12, atol=1e-14)
+
+
 def test_split_k_weight_gradient():
     """_wgrad's chunked batched GEMM + sum equals A^T B (K = 24,192 rows, the
     fine-tune step's stacked edge count)."""
