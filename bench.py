@@ -70,10 +70,14 @@ def parse():
                     help='N > 1 rehearsal: every rank on cuda:0, gloo instead of RCCL')
     ap.add_argument('--profile-only', action='store_true',
                     help='warmup + steps only, no stats pass (for rocprofv3)')
+    ap.add_argument('--model-config', default=None, metavar='cCHlL',
+                    help='instead of SevenNet-0: the SevenNet-0 preset with channel CH and L '
+                         'blocks (e.g. c64l4), built by model_build (e3nn init, seed 0) and '
+                         'deployed to a temporary directory')
     return ap.parse_args()
 
 
-def make_box(cells, device):
+def make_box(cells, device, si=69):
     from sevennet_finetuning_amd.neighbor import neighbor_list
     from sevennet_finetuning_amd.structures import si_diamond
     pos, cell = si_diamond((cells,) * 3, sigma=0.05)
@@ -88,7 +92,7 @@ def make_box(cells, device):
     return {
         'pos': pos, 'cell': cell, 'host_nl_ms': host_nl_s * 1e3,
         'n': len(pos), 'E': ei.shape[1],
-        'types': torch.full((len(pos),), 69, dtype=torch.int32, device=device),  # Si
+        'types': torch.full((len(pos),), si, dtype=torch.int32, device=device),  # Si
         'center': torch.tensor(ei[0], dtype=torch.int32, device=device),
         'nbr': torch.tensor(ei[1], dtype=torch.int32, device=device),
         'vec': torch.tensor(vec, dtype=torch.float32, device=device),
@@ -146,7 +150,7 @@ def pmc_traffic(kernel, cells):
     return None
 
 
-def cpu_baseline(seconds, cells):
+def cpu_baseline(seconds, cells, model_dir=None):
     """Oracle (plain-PyTorch CPU restatement of the reference) on a bounded
     sample of the same workload: a cells^3 Si box (default 6^3 = 1,728 atoms,
     where the reference CPU path is already at its flat large-box throughput,
@@ -154,6 +158,7 @@ def cpu_baseline(seconds, cells):
     then >= 3 timed evaluations and >= `seconds` of CPU work on the host's
     thread share."""
     from oracle.neighbor import neighbor_list
+    from oracle.nequip_ref import NequIPRef
     from oracle.sevennet_ref import SevenNet0Ref
     from sevennet_finetuning_amd.structures import si_diamond
     # the box's CPU share is OMP_NUM_THREADS (16); sched_getaffinity reports the
@@ -161,10 +166,13 @@ def cpu_baseline(seconds, cells):
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get('OMP_NUM_THREADS', '16')))
     torch.set_num_threads(threads)
     log(f'cpu baseline: {threads} threads, {cells}^3 cells, ~{seconds:.0f} s')
-    ref = SevenNet0Ref(dtype=torch.float32)
+    # --model-config: the same deployment on the family's restatement
+    ref = SevenNet0Ref(dtype=torch.float32) if model_dir is None else \
+        NequIPRef(model_dir, dtype=torch.float32)
+    si = 69 if model_dir is None else ref.symbols.index('Si')
     pos, cell = si_diamond((cells,) * 3, sigma=0.05)
     ei, sh = neighbor_list(pos, cell, 5.0)
-    args = (torch.tensor(pos, dtype=torch.float32), torch.full((len(pos),), 69),
+    args = (torch.tensor(pos, dtype=torch.float32), torch.full((len(pos),), si),
             torch.tensor(ei), torch.tensor(sh, dtype=torch.float32),
             torch.tensor(cell, dtype=torch.float32))
     ref(*args)   # warm-up call (allocator, thread pool, kernel selection): not timed
@@ -184,7 +192,7 @@ def cpu_baseline(seconds, cells):
                                  'part of vs_baseline'}
 
 
-def parity_check_serial(model, cells, device):
+def parity_check_serial(model, cells, device, si=69):
     """Full-size property check outside the timed region: a displaced 8-atom
     cell tiled cells^3 times (same size as the bench box) has E = cells^3
     E_cell and per-image forces equal to the cell's (tests/test_gpu_fullsize.py)."""
@@ -194,11 +202,11 @@ def parity_check_serial(model, cells, device):
     ei, sh = neighbor_list(pos1, cell1, 5.0)
     vec1 = pos1[ei[1]] + sh @ cell1 - pos1[ei[0]]
     t = lambda a, dt=torch.int32: torch.as_tensor(a, dtype=dt, device=device)
-    one = model.energy_forces(t(np.full(8, 69)), t(ei[0]), t(ei[1]), t(vec1, torch.float32))
+    one = model.energy_forces(t(np.full(8, si)), t(ei[0]), t(ei[1]), t(vec1, torch.float32))
     e1, f1 = float(one['energy']), one['forces'].cpu().numpy()
     posk, cellk = tile(pos1, cell1, (cells,) * 3)
     c, nb, _, vec = DeviceNeighborList(device)(posk, cellk, 5.0)
-    big = model.energy_forces(t(np.full(len(posk), 69)), c, nb, vec)
+    big = model.energy_forces(t(np.full(len(posk), si)), c, nb, vec)
     k3 = cells ** 3
     de = abs(float(big['energy']) - k3 * e1) / abs(k3 * e1)
     df = float(np.abs(big['forces'].cpu().numpy().reshape(k3, 8, 3) - f1[None]).max())
@@ -207,7 +215,7 @@ def parity_check_serial(model, cells, device):
             'ok': bool(de <= 2e-6 and df <= 1e-4)}
 
 
-def parity_check_parallel(model, cells_total, grid, rank, device):
+def parity_check_parallel(model, cells_total, grid, rank, device, si=69):
     """Same property through the decomposed path (halo exchanges over the
     process group): tiled 8-atom cell over the whole box."""
     from sevennet_finetuning_amd.neighbor import neighbor_list
@@ -217,10 +225,10 @@ def parity_check_parallel(model, cells_total, grid, rank, device):
     ei, sh = neighbor_list(pos1, cell1, 5.0)
     vec1 = pos1[ei[1]] + sh @ cell1 - pos1[ei[0]]
     t = lambda a, dt=torch.int32: torch.as_tensor(a, dtype=dt, device=device)
-    one = model.energy_forces(t(np.full(8, 69)), t(ei[0]), t(ei[1]), t(vec1, torch.float32))
+    one = model.energy_forces(t(np.full(8, si)), t(ei[0]), t(ei[1]), t(vec1, torch.float32))
     e1, f1 = float(one['energy']), one['forces'].cpu().numpy()
     posk, cellk = tile(pos1, cell1, cells_total)
-    rg = build_rank_graph(posk, cellk, np.full(len(posk), 69), 5.0, grid, rank)
+    rg = build_rank_graph(posk, cellk, np.full(len(posk), si), 5.0, grid, rank)
     drv = ParallelE3GNN(HipSegmentEngine(model))
     drv.set_graph(rg)
     out = drv.evaluate()
@@ -323,26 +331,41 @@ def box_plan(args, world):
     return cells, grid, total
 
 
-def describe(n_total, world, cells, strong, grid=(1, 1, 1)):
+def describe(n_total, world, cells, strong, grid=(1, 1, 1), model='SevenNet-0'):
     """(metric, workload) of a bench line, naming the box actually evaluated:
     BASELINE.json's metric is quoted on the 100k-atom box per GPU; a weak
     multi-rank run evaluates world x that box, a strong run one box split over
     the ranks (46^3 cells = 778,688 atoms: config 4, the 800k box)."""
-    base = 'atoms/sec energy+force, SevenNet-0 lmax=2'
+    base = f'atoms/sec energy+force, {model} lmax=2'
     g = 'x'.join(str(v) for v in grid)
     if world == 1:
         metric = f'{base}, {n_total:,}-atom box @1 GPU'
-        work = f'SevenNet-0 energy+force+virial, {n_total:,}-atom periodic Si box ({cells}^3 cells), 1 GPU'
+        work = f'{model} energy+force+virial, {n_total:,}-atom periodic Si box ({cells}^3 cells), 1 GPU'
     elif strong:
         metric = f'{base}, {n_total:,}-atom box split over {world} GPUs (strong scaling)'
-        work = (f'SevenNet-0 energy+force+virial, one {n_total:,}-atom periodic Si box ({cells}^3 cells) '
+        work = (f'{model} energy+force+virial, one {n_total:,}-atom periodic Si box ({cells}^3 cells) '
                 f'domain-decomposed {g} over {world} GPUs, halo exchange per layer')
     else:
         per = n_total // world
         metric = f'{base}, {per:,}-atom box per GPU = {n_total:,}-atom box @{world} GPUs (weak scaling)'
-        work = (f'SevenNet-0 energy+force+virial, {n_total:,}-atom periodic Si box ({world} bricks of '
+        work = (f'{model} energy+force+virial, {n_total:,}-atom periodic Si box ({world} bricks of '
                 f'{cells}^3 cells, {g}) over {world} GPUs, halo exchange per layer')
     return metric, work
+
+
+def model_config_deployment(spec):
+    """'c64l4' -> (deployment dir, label): the SevenNet-0 preset with channel 64
+    and 4 blocks (model_build.sevennet_shaped_config), written by
+    model_build.deploy_config to a temporary directory."""
+    import re
+    import tempfile
+    from sevennet_finetuning_amd import model_build as mb
+    m = re.fullmatch(r'c(\d+)l(\d+)', spec)
+    if not m:
+        raise SystemExit(f'--model-config {spec!r}: expected cCHlL, e.g. c64l4')
+    ch, nl = int(m.group(1)), int(m.group(2))
+    d = mb.deploy_config(mb.sevennet_shaped_config(ch, nl, species=['Si']), tempfile.mkdtemp(), seed=0)
+    return d, f'SevenNet-0 preset with channel {ch}, {nl} blocks'
 
 
 def main():
@@ -367,17 +390,21 @@ def main():
     torch.cuda.set_device(device)
 
     from sevennet_finetuning_amd.model import E3GNNModel
-    model = E3GNNModel(device=device)
+    model_dir, label = None, 'SevenNet-0'
+    if args.model_config:
+        model_dir, label = model_config_deployment(args.model_config)
+    model = E3GNNModel(device=device) if model_dir is None else E3GNNModel(model_dir, device=device)
+    si = model.chemical_symbols.index('Si')
     cells, grid, total = box_plan(args, world)
     scaling = 'strong' if args.strong else 'weak'
     parity = None
     if world == 1:
-        box = make_box(cells, device)
+        box = make_box(cells, device, si)
         n, E = box['n'], box['E']
         n_rank, parallelism = n, 'single'
         log(f'box: {n} atoms, {E} edges; workspace after first step follows')
         if not args.no_parity_check:
-            parity = parity_check_serial(model, cells, device)
+            parity = parity_check_serial(model, cells, device, si)
             log(f'parity check: {parity}')
 
         def step():
@@ -391,9 +418,9 @@ def main():
         from sevennet_finetuning_amd.structures import si_diamond
         pos, cell = si_diamond(total, sigma=0.05)
         n = len(pos)
-        rg = build_rank_graph(pos, cell, np.full(n, 69), 5.0, grid, rank)
+        rg = build_rank_graph(pos, cell, np.full(n, si), 5.0, grid, rank)
         if not args.no_parity_check:
-            parity = parity_check_parallel(model, total, grid, rank, device)
+            parity = parity_check_parallel(model, total, grid, rank, device, si)
             log(f'parity check: {parity}')
         drv = ParallelE3GNN(HipSegmentEngine(model))
         drv.set_graph(rg)
@@ -477,17 +504,19 @@ def main():
         log(f'neighbour list: device {nl["device_ms"]} ms, host {nl["host_ms"]} ms')
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1 and not args.profile_only:
-        cpu = cpu_baseline(args.cpu_seconds, args.cpu_cells)
+        cpu = cpu_baseline(args.cpu_seconds, args.cpu_cells, model_dir)
 
     if rank == 0:
-        metric, workload = describe(n, world, cells, args.strong, grid)
+        metric, workload = describe(n, world, cells, args.strong, grid, label)
         line = {
             'metric': metric,
             'value': round(value, 2), 'unit': 'atoms/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
             'higher_is_better': True, 'scaling': scaling, 'vs_baseline': None, 'dtype': 'f32',
             'data': 'synthetic Si diamond box, default_rng(0) 0.05 A displacements; '
-                    'SevenNet-0 weights (reference opt_params_sevenn.pt)',
+                    + ('SevenNet-0 weights (reference opt_params_sevenn.pt)' if model_dir is None else
+                       f'{label}: e3nn initialisation (model_build, seed 0), fused-kernel family '
+                       f'{model.family}'),
             'config': {'workload': workload, 'total_atoms': n, 'scaling': scaling,
                        'atoms_per_rank': n_rank, 'edges_per_rank': E,
                        'parallelism': parallelism},

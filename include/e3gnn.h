@@ -83,6 +83,12 @@ void e3gnn_free(e3gnn_model* m);
  * comm_size (features exchanged per ghost atom between layers). */
 int e3gnn_model_info(const e3gnn_model* m, int* num_species, float* cutoff, int* num_layers,
                      int* comm_size);
+/* Which engine serves the deployment: the channel family of the fused
+ * radial-MLP + tensor-product kernels (>= 0: 0 SevenNet-0's 128x0e+64x1e+32x2e,
+ * 1 uniform 64, 2 uniform 32 channels; lmax 2, even parity, XPLOR, linear
+ * self-connection, 8 Bessel, 64-64 radial MLP, any number of blocks >= 2), or
+ * -1: the generic runtime-path-table engine (every other nequip-family model). */
+int e3gnn_model_family(const e3gnn_model* m);
 
 e3gnn_ctx* e3gnn_ctx_create(e3gnn_model* m);
 void e3gnn_ctx_free(e3gnn_ctx* c);

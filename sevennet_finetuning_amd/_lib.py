@@ -25,6 +25,7 @@ SIGNATURES = {
     'e3gnn_load': (_vp, [_cp, _cp, _c_int]),
     'e3gnn_free': (None, [_vp]),
     'e3gnn_model_info': (_c_int, [_vp, _P(_c_int), _P(_c_f), _P(_c_int), _P(_c_int)]),
+    'e3gnn_model_family': (_c_int, [_vp]),
     'e3gnn_ctx_create': (_vp, [_vp]),
     'e3gnn_ctx_free': (None, [_vp]),
     'e3gnn_energy_forces': (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

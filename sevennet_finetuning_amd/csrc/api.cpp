@@ -144,6 +144,13 @@ struct LinPair {
 struct e3gnn_model {
   int device = 0;
   int nsp = 0, nlayer = 0;
+  // channel family of the fused kernels (tp.h Family<f>): 0 SevenNet-0,
+  // 1 uniform 64, 2 uniform 32
+  int family = 0;
+  // kernel kind code of block t (tp.h: 3 * family + first / middle / last)
+  int kcode(int t) const { return 3 * family + (t == 0 ? 0 : (t == nlayer - 1 ? 2 : 1)); }
+  std::vector<GateDims> gdims;  // gate layout per block (node.h)
+  int max_dx = 0, max_dg = 0;
   float cutoff = 5.f, r_on = 4.5f;
   int raw_sh = 0;   // SH of the raw edge vector (sh_normalize false: checkpoints before sevenn 0.9)
   std::vector<Irreps> irreps;  // irreps_manual per layer boundary (merged)
@@ -210,10 +217,9 @@ enum Cls {
 };
 static_assert(sizeof(kClassNames) / sizeof(kClassNames[0]) == C_NCLS, "class names");
 
-// algorithmic per-edge FLOP of one TP forward
-double tp_flops_per_edge(int kind) {
-  return kind == 0 ? 3456.0 : (kind == 1 ? 16832.0 : 1184.0);
-}
+// algorithmic per-edge FLOP of one TP forward (SevenNet-0:
+// 3,456 / 16,832 / 1,184 for the first / middle / last block)
+double tp_flops_per_edge(int code) { return fused_kind_tp_flops(code); }
 
 }  // namespace
 
@@ -506,30 +512,40 @@ int build_pair(LinPair& P, const Linear& a, bool ta, const Linear* b, bool tb) {
   return 0;
 }
 
+// the path table of a fused kind code (tp.h)
+std::vector<PathDef> kind_paths(int code) {
+  std::vector<PathDef> P(16);
+  P.resize(fused_kind_paths(code, P.data(), (int)P.size()));
+  return P;
+}
+
 // Column start of every 16-channel weight block in the order the fused
 // kernels visit them (input irrep I, channel block jj, then the paths of I in
 // instruction order): pairs of consecutive blocks form one K = 32 MFMA operand
 // of the lock-step backward's dH2 product (MlpW::w2d).
-template <class L>
-std::vector<int> bwd_w_block_cols() {
+std::vector<int> bwd_w_block_cols(int code) {
+  const auto P = kind_paths(code);
   std::vector<int> cols;
   for (int I = 0; I < 3; ++I) {
     int mul = 0;
-    for (int p = 0; p < L::NP; ++p)
-      if (L::P[p].l1 == I) mul = L::P[p].mul;
+    for (auto& p : P)
+      if (p.l1 == I) mul = p.mul;
     for (int jj = 0; jj < mul / 16; ++jj)
-      for (int p = 0; p < L::NP; ++p)
-        if (L::P[p].l1 == I) cols.push_back(L::P[p].woff + 16 * jj);
+      for (auto& p : P)
+        if (p.l1 == I) cols.push_back(p.woff + 16 * jj);
   }
   return cols;
 }
 
-// IrrepsConvolution instruction list (convolution.py:72-95) vs the kernel tables
-template <class LT>
-bool check_paths(const Irreps& x, int lmax_out) {
+// IrrepsConvolution instruction list (convolution.py:72-95) vs the kernel
+// tables of kind code `code`
+bool check_paths(int code, const Irreps& x, int lmax_out) {
   struct Ins {
     int l1, l2, l3, mul, xoff;
   };
+  const auto P = kind_paths(code);
+  int DX = 0, W = 0, DM = 0;
+  if (P.empty() || !fused_kind_dims(code, &DX, &W, &DM)) return false;
   std::vector<Ins> ins;
   int xoff = 0;
   for (auto& i : x) {
@@ -538,7 +554,7 @@ bool check_paths(const Irreps& x, int lmax_out) {
         if (l3 <= lmax_out) ins.push_back({i.l, l2, l3, i.mul, xoff});
     xoff += i.mul * (2 * i.l + 1);
   }
-  if ((int)ins.size() != LT::NP) return false;
+  if (ins.size() != P.size()) return false;
   // mid slots: stable sort by l3
   std::vector<int> moff(ins.size());
   int off = 0;
@@ -548,16 +564,16 @@ bool check_paths(const Irreps& x, int lmax_out) {
         moff[k] = off;
         off += ins[k].mul * (2 * l3 + 1);
       }
-  if (off != LT::DM) return false;
+  if (off != DM) return false;
   int woff = 0;
   for (size_t k = 0; k < ins.size(); ++k) {
-    const PathDef& p = LT::P[k];
+    const PathDef& p = P[k];
     if (p.l1 != ins[k].l1 || p.l2 != ins[k].l2 || p.l3 != ins[k].l3 || p.mul != ins[k].mul ||
         p.xoff != ins[k].xoff || p.woff != woff || p.moff != moff[k])
       return false;
     woff += ins[k].mul;
   }
-  return woff == LT::W && xoff == LT::DX;
+  return woff == W && xoff == DX;
 }
 
 }  // namespace
@@ -590,29 +606,53 @@ GenGraph gen_graph(e3gnn_ctx* c) {
                   c->src_ptr.i(), c->src_perm.i(), c->err.i()};
 }
 
-// The SevenNet-0 architecture test (the same knobs as nn.sevennet0_kinds, plus
-// what the specialised kernels hard-code: 5 blocks, 8 Bessel functions, a
-// 64-64 radial MLP)
-bool is_sevennet0(const minijson::Value& man) {
-  if (man.has("is_parity") && man["is_parity"].boolean()) return false;
+// The SevenNet-0-shaped family test: what the specialised engine serves.
+// The knobs of nn.sevennet0_kinds (even parity, lmax 2, linear
+// self-connection, XPLOR cutoff), what the fused kernels hard-code (8 Bessel
+// functions, a 64-64 radial MLP), at least 2 blocks, and the irreps of one
+// compiled channel family (tp.h): A x0e -> (L - 1) x C0x0e+C1x1e+C2x2e -> D x0e.
+// Returns the family, or -1 (the generic engine serves the deployment).
+int fused_family(const minijson::Value& man) {
+  // E3GNN_GENERIC=1: every deployment on the generic engine (cross-checks)
+  if (const char* g = std::getenv("E3GNN_GENERIC"); g && g[0] == '1') return -1;
+  if (man.has("is_parity") && man["is_parity"].boolean()) return -1;
   const int lmax = man.has("lmax_edge") ? (int)man["lmax_edge"].num()
                                         : (man.has("lmax") ? (int)man["lmax"].num() : 2);
-  if (lmax != 2) return false;
-  if (man.has("self_connection_type") && man["self_connection_type"].str() != "linear") return false;
-  if (!man.has("cutoff_function") || man["cutoff_function"]["name"].str() != "XPLOR") return false;
-  if ((int)man["num_convolution_layer"].num() != 5) return false;
+  if (lmax != 2) return -1;
+  if (man.has("self_connection_type") && man["self_connection_type"].str() != "linear") return -1;
+  if (!man.has("cutoff_function") || man["cutoff_function"]["name"].str() != "XPLOR") return -1;
+  const int L = (int)man["num_convolution_layer"].num();
+  if (L < 2) return -1;
   if (man.has("weight_nn_hidden_neurons")) {
     const auto& h = man["weight_nn_hidden_neurons"].arr();
-    if (h.size() != 2 || (int)h[0].num() != 64 || (int)h[1].num() != 64) return false;
+    if (h.size() != 2 || (int)h[0].num() != 64 || (int)h[1].num() != 64) return -1;
   }
   if (man.has("radial_basis") && man["radial_basis"].has("num") && (int)man["radial_basis"]["num"].num() != 8)
-    return false;
+    return -1;
   const auto& ir = man["irreps_manual"].arr();
-  const std::string mid = "128x0e+64x1e+32x2e";
-  if (ir.size() != 6 || ir[0].str() != "128x0e" || ir[5].str() != "128x0e") return false;
-  for (int t = 1; t < 5; ++t)
-    if (ir[t].str() != mid) return false;
-  return true;
+  if ((int)ir.size() != L + 1) return -1;
+  Irreps first, mid, last;
+  try {
+    first = merged(parse_irreps(ir[0].str()));
+    mid = merged(parse_irreps(ir[1].str()));
+    last = merged(parse_irreps(ir[L].str()));
+  } catch (...) {
+    return -1;
+  }
+  if (first.size() != 1 || first[0].l != 0 || last.size() != 1 || last[0].l != 0) return -1;
+  for (int t = 1; t < L; ++t)
+    if (ir[t].str() != ir[1].str()) return -1;
+  if (L > 1 && (mid.size() != 3 || mid[0].l != 0 || mid[1].l != 1 || mid[2].l != 2)) return -1;
+  for (int f = 0; f < N_FAMILIES; ++f) {
+    PathDef P0[16], P1[16];
+    fused_kind_paths(3 * f, P0, 16);
+    fused_kind_paths(3 * f + 1, P1, 16);
+    // first block's input A; middle irreps C0 / C1 / C2 (paths 0, 3, 9 of the middle table)
+    if (first[0].mul == P0[0].mul && mid[0].mul == P1[0].mul && mid[1].mul == P1[3].mul &&
+        mid[2].mul == P1[9].mul)
+      return f;
+  }
+  return -1;
 }
 }  // namespace
 
@@ -662,7 +702,8 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
       throw std::runtime_error("unsupported model_type");
     // SevenNet-0's architecture runs on the specialised kernels below; every
     // other member of the family on the generic engine (generic.cpp)
-    if (!is_sevennet0(man)) {
+    const int family = fused_family(man);
+    if (family < 0) {
       m->gen = gen_load(man, flat);
       m->nsp = gen_num_species(m->gen);
       m->nlayer = gen_num_layers(m->gen);
@@ -676,6 +717,7 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
     // sh_normalize false (checkpoints before sevenn 0.9, util.py:130-146): the
     // same kernels, the SH polynomials of the raw vector (node.hip)
     m->raw_sh = man.has("sh_normalize") && !man["sh_normalize"].boolean() ? 1 : 0;
+    m->family = family;
     if (man.has("is_parity") && man["is_parity"].boolean())
       throw std::runtime_error("odd-parity filters are not SevenNet-0's architecture");
     if (man.has("self_connection_type") && man["self_connection_type"].str() != "linear")
@@ -705,21 +747,25 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
       return flat.data() + it->second.first;
     };
     auto numel = [&](const std::string& n) { return T.at(n).second; };
-    if (m->nlayer != 5) throw std::runtime_error("kernel path tables are SevenNet-0's (5 layers)");
     // geometry / embedding / readout
     const float* cf = get("edge_embedding.basis_function.coeffs", 8);
     if (upload(m->coeffs, std::vector<float>(cf, cf + 8)) != hipSuccess) throw std::runtime_error("upload");
-    const float* we = get("onehot_to_feature_x.linear.weight", (size_t)m->nsp * 128);
-    std::vector<float> emb((size_t)m->nsp * 128);
+    const int d0 = irreps_dim(m->irreps[0]);
+    const float* we = get("onehot_to_feature_x.linear.weight", (size_t)m->nsp * d0);
+    std::vector<float> emb((size_t)m->nsp * d0);
     for (size_t i = 0; i < emb.size(); ++i) emb[i] = (float)(we[i] / std::sqrt((double)m->nsp));
     if (upload(m->embed, emb) != hipSuccess) throw std::runtime_error("upload");
-    const float* wh = get("reduce_input_to_hidden.linear.weight", 128 * 64);
-    const float* wo = get("reduce_hidden_to_energy.linear.weight", 64);
-    std::vector<float> v(128);
-    for (int c = 0; c < 128; ++c) {
+    // two linears without activation (D x0e -> H x0e -> 1x0e) folded into one
+    // vector, e3nn path weights 1 / sqrt(fan_in) each
+    const int dl = irreps_dim(m->irreps[m->nlayer]);
+    const int hid = (int)numel("reduce_hidden_to_energy.linear.weight");
+    const float* wh = get("reduce_input_to_hidden.linear.weight", (size_t)dl * hid);
+    const float* wo = get("reduce_hidden_to_energy.linear.weight", hid);
+    std::vector<float> v(dl);
+    for (int c = 0; c < dl; ++c) {
       double s = 0;
-      for (int k = 0; k < 64; ++k) s += (double)wh[c * 64 + k] * wo[k];
-      v[c] = (float)(s / (std::sqrt(128.0) * 8.0));
+      for (int k = 0; k < hid; ++k) s += (double)wh[c * hid + k] * wo[k];
+      v[c] = (float)(s / (std::sqrt((double)dl) * std::sqrt((double)hid)));
     }
     if (upload(m->readout_v, v) != hipSuccess) throw std::runtime_error("upload");
     trace_point("load:readout");
@@ -741,10 +787,20 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
       for (auto& i : xout)
         if (i.l > 0) gin.push_back(i);
       const int lmax_out = last ? 0 : 2;
-      bool ok = t == 0 ? check_paths<LayerFirst>(xin, lmax_out)
-                       : (last ? check_paths<LayerLast>(xin, lmax_out)
-                               : check_paths<LayerMid>(xin, lmax_out));
-      if (!ok) throw std::runtime_error("convolution path table mismatch at layer " + std::to_string(t));
+      if (!check_paths(m->kcode(t), xin, lmax_out))
+        throw std::runtime_error("convolution path table mismatch at layer " + std::to_string(t));
+      {
+        // gate layout (node.h GateDims): scalars, then the gated 1e / 2e blocks
+        GateDims gd{0, 0, 0};
+        for (auto& i : xout) (i.l == 0 ? gd.ns : (i.l == 1 ? gd.g1 : gd.g2)) += i.mul;
+        if (last ? (gd.g1 || gd.g2) : false)
+          throw std::runtime_error("the last block's output must be scalars");
+        for (size_t k = 1; k < xout.size(); ++k)
+          if (xout[k].l < xout[k - 1].l) throw std::runtime_error("output irreps must be sorted by l");
+        m->gdims.push_back(gd);
+        m->max_dx = std::max(m->max_dx, irreps_dim(xin));
+        m->max_dg = std::max(m->max_dg, gd.dy());
+      }
       // mid irreps merged by l (sorted), see tp.h
       Irreps mid;
       for (int l3 = 0; l3 <= lmax_out; ++l3) {
@@ -787,7 +843,8 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
       const size_t n2 = numel(p + "_convolution.weight_nn.layer2.weight");
       const float* w2 = get(p + "_convolution.weight_nn.layer2.weight");
       const int W = (int)(n2 / 64);
-      const int Wexp = t == 0 ? LayerFirst::W : (last ? LayerLast::W : LayerMid::W);
+      int kdx = 0, Wexp = 0, kdm = 0;
+      fused_kind_dims(m->kcode(t), &kdx, &Wexp, &kdm);
       if (W != Wexp) throw std::runtime_error("radial weight width mismatch");
       m->W.push_back(W);
       auto scaled = [](const float* a, int r, int c, double s, bool tr) {
@@ -877,9 +934,7 @@ e3gnn_model* e3gnn_load(const char* weights_path, const char* manifest_path, int
         }
         // the kernels' visiting order of the 16-column blocks (input irrep,
         // channel block, path): pairs of consecutive blocks
-        const std::vector<int> cols = t == 0 ? bwd_w_block_cols<LayerFirst>()
-                                             : (last ? bwd_w_block_cols<LayerLast>()
-                                                     : bwd_w_block_cols<LayerMid>());
+        const std::vector<int> cols = bwd_w_block_cols(m->kcode(t));
         if ((int)cols.size() * 16 != W || cols.size() % 2)
           throw std::runtime_error("dE/dw block order does not cover the weights");
         // w2d (MlpW::w2d): element t of lane (g, c) for hidden block bh is
@@ -947,6 +1002,11 @@ int e3gnn_model_info(const e3gnn_model* m, int* num_species, float* cutoff, int*
   return E3GNN_OK;
 }
 
+int e3gnn_model_family(const e3gnn_model* m) {
+  if (!m) return fail(E3GNN_ERR_ARG, "null model"), -1;
+  return m->gen ? -1 : m->family;
+}
+
 e3gnn_ctx* e3gnn_ctx_create(e3gnn_model* m) {
   if (!m) {
     fail(E3GNN_ERR_ARG, "null model");
@@ -991,10 +1051,13 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   if (n_local + n_ghost > (1LL << 30) || n_edges > (1LL << 31) - 1)
     return fail(E3GNN_ERR_ARG, "graph too large for int32 indices");
   // the fused kernels gather node-feature rows through one 32-bit buffer
-  // descriptor (n x 480 fp32 < 2 GiB; the last block's dE/dagg rows, nl x 224,
-  // fit whenever these do)
-  if (!c->gen && (n_local + n_ghost) * 480LL * 4 > 0x7fffffffLL)
-    return fail(E3GNN_ERR_ARG, "more than 1.1M atoms (owned + ghost) per device: shard the system");
+  // descriptor (n x DX fp32 < 2 GiB: 1.1M atoms at SevenNet-0's 480; the last
+  // block's dE/dagg rows fit whenever these do)
+  if (!c->gen && (n_local + n_ghost) * (int64_t)c->m->max_dx * 4 > 0x7fffffffLL)
+    return fail(E3GNN_ERR_ARG, "more than " + std::to_string(0x7fffffffLL / (4LL * c->m->max_dx)) +
+                                   " atoms (owned + ghost) per device for this model: shard the system");
+  if (!c->gen && c->impl == 1 && c->m->family != 0)
+    return fail(E3GNN_ERR_ARG, "the v1 (unfused) kernels serve SevenNet-0's channel family only");
   if ((n_local + n_ghost > 0 && !type) || (n_edges > 0 && (!edge_center || !edge_nbr || !edge_vec)))
     return fail(E3GNN_ERR_ARG, "null input array");
   e3gnn_model* m = c->m;
@@ -1054,9 +1117,9 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
     HIPCHK(c->grad[m->nlayer].ensure(std::max<int64_t>(n, 1) * dlast * F));
     HIPCHK(c->agg.ensure(nl * maxDM * F));
     if (v1) HIPCHK(c->dw.ensure(E * maxW * F));
-    HIPCHK(c->dxc.ensure(E * 480 * F));
-    HIPCHK(c->dy.ensure(nl * 576 * F));
-    HIPCHK(c->dh.ensure(n * 480 * F));
+    HIPCHK(c->dxc.ensure(E * m->max_dx * F));
+    HIPCHK(c->dy.ensure(nl * m->max_dg * F));
+    HIPCHK(c->dh.ensure(n * m->max_dx * F));
     HIPCHK(c->eat.ensure(std::max<int64_t>(nl, 1) * F));
     HIPCHK(c->part.ensure((sum_blocks(nl) + 1) * F));
     HIPCHK(c->vpart.ensure((edge_force_blocks(E) + 1) * 6 * F));
@@ -1079,8 +1142,9 @@ int e3gnn_graph_set(e3gnn_ctx* c, int64_t n_local, int64_t n_ghost, int64_t n_ed
   if (c->gen) {
     HIPCHK(gen_graph_set(c->gen, m->gen, gen_graph(c), s));
   } else {
-    Region r(c, s, C_EMBED_NODE, 0, (double)n * 128 * 4);
-    HIPCHK(launch_embed((int)n, c->type.i(), m->nsp, m->embed.f(), c->x[0].f(), c->err.i(), s));
+    const int d0 = irreps_dim(m->irreps[0]);
+    Region r(c, s, C_EMBED_NODE, 0, (double)n * d0 * 4);
+    HIPCHK(launch_embed((int)n, d0, c->type.i(), m->nsp, m->embed.f(), c->x[0].f(), c->err.i(), s));
   }
   int err = 0, e_int = 0;
   HIPCHK(hipMemcpyAsync(&err, c->err.p, 4, hipMemcpyDeviceToHost, s));
@@ -1135,13 +1199,14 @@ int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
   const int dx = irreps_dim(m->irreps[t]), dg = irreps_dim(m->gin[t]);
   const int dm = irreps_dim(m->mid[t]), W = m->W[t];
   const bool last = t == m->nlayer - 1;
-  const int kind = t == 0 ? 0 : (last ? 2 : 1);
+  const int kind = t == 0 ? 0 : (last ? 2 : 1);   // block kind (timing class, v1 kernels)
+  const int code = m->kcode(t);                    // fused kernel kind code
   const bool fused = c->graph_impl == 0;
   const int64_t n_int = fused ? c->n_int : 0;
   auto conv_fwd = [&](int64_t c0, int64_t c1, double e_share) -> int {
     if (c1 <= c0) return E3GNN_OK;
     Region r(c, s, C_CONV_FWD + kind,
-             e_share * (tp_flops_per_edge(kind) + 2.0 * (8 * 64 + 64 * 64 + 64 * W)),
+             e_share * (tp_flops_per_edge(code) + 2.0 * (8 * 64 + 64 * 64 + 64 * W)),
              e_share * 4 * (8 + 9 + 2 + dx) + (c1 - c0) * 4.0 * dm);
     FusedArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -1157,7 +1222,7 @@ int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     a.denom = m->denom[t];
     a.c_begin = (int)c0;
     a.c_end = (int)c1;
-    HIPCHK(launch_conv_fwd(kind, a, s));
+    HIPCHK(launch_conv_fwd(code, a, s));
     return E3GNN_OK;
   };
   if (part == 0) {
@@ -1217,7 +1282,7 @@ int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
   }
   // tensor product + segmented neighbour sum
   {
-    Region r(c, s, C_TP_FWD, tp_flops_per_edge(kind) * E,
+    Region r(c, s, C_TP_FWD, tp_flops_per_edge(code) * E,
              (double)E * 4 * (W + 9 + dx + 2) + nl * 4.0 * dm);
     TpArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -1276,7 +1341,7 @@ int e3gnn_layer_forward_part(e3gnn_ctx* c, int t, int part, void* stream) {
   }
   {
     Region r(c, s, C_GATE_FWD, 0, nl * 4.0 * (dg + irreps_dim(m->irreps[t + 1])));
-    HIPCHK(launch_gate_fwd((int)nl, last, c->y[t].f(), c->x[t + 1].f(), s));
+    HIPCHK(launch_gate_fwd((int)nl, last, m->gdims[t], c->y[t].f(), c->x[t + 1].f(), s));
   }
   return E3GNN_OK;
 }
@@ -1299,13 +1364,14 @@ int e3gnn_readout(e3gnn_ctx* c, float* energy, float* atomic_energy, void* strea
   const int64_t nl = c->nl;
   const int L = m->nlayer;
   {
-    Region r(c, s, C_READOUT, 2.0 * nl * 128, nl * 4.0 * 130);
-    HIPCHK(launch_readout((int)nl, c->x[L].f(), m->readout_v.f(), c->type.i(), m->scale.f(),
+    const int dl = irreps_dim(m->irreps[L]);
+    Region r(c, s, C_READOUT, 2.0 * nl * dl, nl * 4.0 * (dl + 2));
+    HIPCHK(launch_readout((int)nl, dl, c->x[L].f(), m->readout_v.f(), c->type.i(), m->scale.f(),
                           m->shift.f(), c->eat.f(), s));
     HIPCHK(launch_sum(nl, c->eat.f(), c->part.f(), energy ? energy : c->scratch6.f(), s));
     if (atomic_energy && nl > 0)
       HIPCHK(hipMemcpyAsync(atomic_energy, c->eat.p, nl * 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(launch_readout_bwd((int)nl, m->readout_v.f(), c->type.i(), m->scale.f(),
+    HIPCHK(launch_readout_bwd((int)nl, dl, m->readout_v.f(), c->type.i(), m->scale.f(),
                               c->grad[L].f(), s));
   }
   c->readout_done = 1;
@@ -1334,14 +1400,15 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
   const int dx = irreps_dim(m->irreps[t]), dg = irreps_dim(m->gin[t]);
   const int dm = irreps_dim(m->mid[t]), W = m->W[t];
   const bool last = t == m->nlayer - 1;
-  const int kind = t == 0 ? 0 : (last ? 2 : 1);
+  const int kind = t == 0 ? 0 : (last ? 2 : 1);   // block kind (timing class, v1 kernels)
+  const int code = m->kcode(t);                    // fused kernel kind code
   const bool fused = c->graph_impl == 0;
   if (!fused && part == 1) return E3GNN_OK;
   const int64_t n_int = c->n_int, e_int = c->e_int;
   if (part == 0) {
     {
       Region r(c, s, C_GATE_BWD, 0, nl * 4.0 * (2 * dg + irreps_dim(m->irreps[t + 1])));
-      HIPCHK(launch_gate_bwd((int)nl, last, c->y[t].f(), c->grad[t + 1].f(), c->dy.f(), s));
+      HIPCHK(launch_gate_bwd((int)nl, last, m->gdims[t], c->y[t].f(), c->grad[t + 1].f(), c->dy.f(), s));
     }
     {
       Region r(c, s, C_LINEAR, lin_flops(*m->si2[t], nl));
@@ -1393,14 +1460,14 @@ int e3gnn_layer_backward_part(e3gnn_ctx* c, int t, int part, void* stream) {
     if (last ? a.node_end > a.node_begin : a.c_end > a.c_begin) {
       // algorithmic FLOP (the forward radial MLP the kernel recomputes is not
       // counted): dE/dx + dE/dY = 2 x TP; dE/dw = TP, dH2 = dw W2^T, MLP chain
-      const double xf = 3.0 * tp_flops_per_edge(kind) + 2.0 * (64 * W + 64 * 64 + 8 * 64);
+      const double xf = 3.0 * tp_flops_per_edge(code) + 2.0 * (64 * W + 64 * 64 + 8 * 64);
       Region r(c, s, C_CONV_BWD_X + kind, xf * ef,
                ef * 4 * (8 + 9 + 2 + 3 + 8) + (a.c_end - a.c_begin) * 4.0 * dm);
-      HIPCHK(last ? launch_conv_bwd_nbr_last(a, s) : launch_conv_bwd_ls(kind, a, s));
+      HIPCHK(last ? launch_conv_bwd_nbr_last(code, a, s) : launch_conv_bwd_ls(code, a, s));
     }
   } else {
   {
-    Region r(c, s, C_TP_BWD, 3.0 * tp_flops_per_edge(kind) * E,
+    Region r(c, s, C_TP_BWD, 3.0 * tp_flops_per_edge(code) * E,
              (double)E * 4 * (2 * W + 2 * 9 + dx + (t > 0 ? dx : 0) + 2) + nl * 4.0 * dm);
     TpArgs a;
     std::memset(&a, 0, sizeof(a));

@@ -60,6 +60,7 @@ struct FusedArgs {
   int c_begin, c_end, node_begin, node_end;
 };
 
+// `kind` is a kind code of tp.h (3 * channel family + block kind)
 hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s);
 // backward of a first / middle block: the lock-step kernel (4 centres per
 // workgroup, W2 operands staged per block pair in LDS, dH2 on bf16x6), per-edge
@@ -67,6 +68,6 @@ hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s);
 hipError_t launch_conv_bwd_ls(int kind, const FusedArgs& a, hipStream_t s);
 // backward of the last block, one wave per neighbour node: dE/dx to dh, dE/du,
 // dE/dw -> dE/demb
-hipError_t launch_conv_bwd_nbr_last(const FusedArgs& a, hipStream_t s);
+hipError_t launch_conv_bwd_nbr_last(int kind, const FusedArgs& a, hipStream_t s);
 
 }  // namespace e3gnn

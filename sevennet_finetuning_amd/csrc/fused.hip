@@ -40,6 +40,13 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int N, int I = 0, class F>
+constexpr void sfor_host(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor_host<N, I + 1>(f);
+  }
+}
+template <int N, int I = 0, class F>
 __device__ __forceinline__ void sfor(F&& f) {
   if constexpr (I < N) {
     f(std::integral_constant<int, I>{});
@@ -55,6 +62,38 @@ __device__ __forceinline__ constexpr int KH(int s) { return 16 * (s >> 2) + (s &
 // the MFMA chain of one column block and the tensor product of another, which
 // otherwise multiplies live registers and halves occupancy.
 __device__ __forceinline__ void phase() { __builtin_amdgcn_sched_barrier(0); }
+
+// Diagnostic build only (-DE3GNN_STAMPS, never the shipped library): per-wave
+// s_memtime totals of the middle backward's phases, written by lane 0 to a
+// buffer of their own (e3gnn_debug_stamps) that no other code reads.
+#ifdef E3GNN_STAMPS
+__device__ unsigned long long* g_stamp_buf = nullptr;
+#define STAMP_N 8
+#define STAMP_DECL                               \
+  unsigned long long st_acc[STAMP_N] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  unsigned long long st_t = __builtin_amdgcn_s_memtime(), st_t0 = st_t;
+#define STAMP(k)                                          \
+  do {                                                    \
+    const unsigned long long st_now = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += st_now - st_t;                           \
+    st_t = st_now;                                        \
+  } while (0)
+#define STAMP_FLUSH(wave)                                                   \
+  do {                                                                      \
+    if (g_stamp_buf && lane == 0) {                                         \
+      st_acc[7] = __builtin_amdgcn_s_memtime() - st_t0;                     \
+      for (int k_ = 0; k_ < STAMP_N; ++k_) g_stamp_buf[(int64_t)(wave) * STAMP_N + k_] = st_acc[k_]; \
+    }                                                                       \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#define STAMP_FLUSH(wave) \
+  do {                    \
+  } while (0)
+#endif
 
 // materialise a value here: stops the compiler from sinking an accumulation
 // chain past later paths (which keeps every partial product live)
@@ -519,7 +558,7 @@ __device__ __forceinline__ void load_tile_edges(const int* __restrict__ nbr,
 // block (128 input channels) fits three, the others two
 template <class L>
 struct Fwd2Waves {
-  static constexpr int v = std::is_same<L, LayerFirst>::value ? 3 : 2;
+  static constexpr int v = L::KIND == 0 ? 3 : 2;
 };
 template <class L>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Fwd2Waves<L>::v, Fwd2Waves<L>::v))) void k_conv_fwd(
@@ -948,8 +987,32 @@ __device__ __forceinline__ void lds_op3(Op3& o, const char* blk, int lane) {
 // dH2^T += W2[:, pair] dw^T on bf16x6 (K = 32: element t of lane (g, c) is
 // channel 4g + t of the pair's first block (t < 4) or 4g + t - 4 of its second,
 // the w2d order); A = the W2 pieces (LDS), B = dw split in three pieces
+#ifndef E3GNN_DH2_X3
+#define E3GNN_DH2_X3 0   // A/B experiment only: 3 piece products (bf16x3) instead of 6
+#endif
 __device__ __forceinline__ void dh2_pair(f32x4 (&dh2)[4], const float (&da)[4], const float (&db)[4],
                                          const char* pimg, int lane) {
+  if constexpr (E3GNN_DH2_X3) {
+    bf16x8 d[2];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      float v = t < 4 ? da[t] : db[t - 4];
+      const __bf16 b0 = (__bf16)v;
+      d[0][t] = b0;
+      d[1][t] = (__bf16)(v - (float)b0);
+    }
+#pragma unroll
+    for (int bh = 0; bh < 4; ++bh) {
+      bf16x8 a[2];
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc)
+        a[pc] = *reinterpret_cast<const bf16x8*>(pimg + ((pc * 4 + bh) * 64 + lane) * 16);
+      dh2[bh] = mfma16(a[1], d[0], dh2[bh]);
+      dh2[bh] = mfma16(a[0], d[1], dh2[bh]);
+      dh2[bh] = mfma16(a[0], d[0], dh2[bh]);
+    }
+    return;
+  }
   bf16x8 d[3];
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
@@ -1000,7 +1063,7 @@ __device__ __forceinline__ int ls_tiles(const int* __restrict__ row_ptr, int cb,
 // their 75 KB of LDS allows no more)
 template <class L>
 struct BwdLsWaves {
-  static constexpr int v = std::is_same<L, LayerFirst>::value ? 3 : 2;
+  static constexpr int v = L::KIND == 0 ? 3 : 2;
 };
 // centres (waves) per workgroup: 4; E3GNN_BWD_WPG = 8 (A/B) gives the middle
 // block one 8-wave workgroup per CU sharing each staged W2 pair (124 KB LDS)
@@ -1009,7 +1072,7 @@ struct BwdLsWaves {
 #endif
 template <class L>
 struct BwdWpg {
-  static constexpr int v = std::is_same<L, LayerMid>::value ? E3GNN_BWD_WPG : 4;
+  static constexpr int v = L::KIND == 1 ? E3GNN_BWD_WPG : 4;
 };
 template <class L>
 __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_eu(BwdLsWaves<L>::v, BwdLsWaves<L>::v))) void k_conv_bwd_ls(
@@ -1062,8 +1125,11 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
     for (int i = 0; i < NST; ++i) *reinterpret_cast<f32x4*>(img + (tid + NT * i) * 16) = st[i];
     __syncthreads();
   };
+  constexpr bool STAMPED = std::is_same<L, LayerMid>::value;   // SevenNet-0's
+  STAMP_DECL
   issue(0);
   for (int t = 0; t < T; ++t) {
+    if constexpr (STAMPED) STAMP(0);
     const int q0 = beg + 16 * t;
     const bool act = q0 < end;   // wave-uniform
     const int er = (act && q0 + col < end) ? q0 + col : -1;
@@ -1102,6 +1168,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
         for (int r = 0; r < 4; ++r) h2[bb][r] = act_fwd(m.a2[bb][r]);
       split_h2(h2, hq);
     }
+    if constexpr (STAMPED) STAMP(1);   // tile setup: edge loads, MLP chain, H2 split
     f32x4 dh2[4] = {zero4(), zero4(), zero4(), zero4()};
     float dYa[9];
 #pragma unroll
@@ -1140,8 +1207,10 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                 constexpr int ODD = (NB0 + hh * NPI + path_rank<L>(pi)) & 1;
                 const int nb = NB0 + jj * NPI + path_rank<L>(pi);
                 if constexpr (!ODD) {   // pair start: stage it, fetch the next one
+                  if constexpr (STAMPED) STAMP(5);
                   commit();
                   issue((nb >> 1) + 1 < NPAIR ? (nb >> 1) + 1 : 0);
+                  if constexpr (STAMPED) STAMP(2);   // barriers + staging
                   if (act) {
                     __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
                     Op3 wq;
@@ -1151,6 +1220,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                     wv1 = w2_block<false>(hq, wq);
                     __builtin_amdgcn_s_setprio(0);
                   }
+                  if constexpr (STAMPED) STAMP(3);   // w recompute
                 }
                 if (act) {
                   const f32x4 wv = ODD ? wv1 : wv0;
@@ -1161,12 +1231,14 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                   float dwr[4];
                   // padded slots: y = 0, so dE/dx = dE/dw = 0 there
                   tp_bwd_xw4<p.l1, p.l2, p.l3>(x, y + yoff(p.l2), wv, gm, dx, dYa + yoff(p.l2), dwr);
-                  if constexpr (!std::is_same<L, LayerFirst>::value) pin<4 * D1>(dx);
+                  if constexpr (L::KIND != 0) pin<4 * D1>(dx);
                   pin<8>(dYa + 1);
                   if constexpr (ODD) {
+                    if constexpr (STAMPED) STAMP(5);   // tensor product (+ stores)
                     __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
                     dh2_pair(dh2, dwp, dwr, img + LS_PAIR_W, lane);
                     __builtin_amdgcn_s_setprio(0);
+                    if constexpr (STAMPED) STAMP(4);   // dH2 (split + MFMA)
                   } else {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) dwp[r] = dwr[r];
@@ -1178,7 +1250,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
             // embedding, whose gradient no output needs: no stores at all (a
             // store to an empty descriptor still costs its issue and its
             // trip through the texture unit), and dx itself is dead code there
-            if constexpr (!std::is_same<L, LayerFirst>::value)
+            if constexpr (L::KIND != 0)
               stv<4 * D1>(Rd, vd + 4 * g * D1 * 4, (XOFF + 16 * jj * D1) * 4, dx);
           });
         }
@@ -1202,28 +1274,22 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
         o[1] += gy;
         o[2] += gz;
       }
+      if constexpr (STAMPED) STAMP(5);
       mlp_bwd_chain(R, emb, q0, end, lane, dh2, demb);
     }
+    if constexpr (STAMPED) STAMP(6);   // tile end: dE/dY sums, MLP chain backward
   }
+  if constexpr (STAMPED) STAMP_FLUSH(blockIdx.x * WPG + wid);
 }
 
 }  // namespace
 
-hipError_t launch_conv_bwd_ls(int kind, const FusedArgs& a, hipStream_t s) {
+template <class L>
+static hipError_t bwd_ls_impl(const FusedArgs& a, hipStream_t s) {
+  constexpr int WPG = BwdWpg<L>::v;
   const int nc = a.c_end - a.c_begin;
-  if (nc <= 0 || a.n_nodes <= 0) return hipSuccess;
-  const dim3 grid((nc + 3) / 4), block(256);
-  constexpr int WM = BwdWpg<LayerMid>::v;
-  switch (kind) {
-    case 0: hipLaunchKernelGGL(k_conv_bwd_ls<LayerFirst>, grid, block, 0, s, a.row_ptr, a.nbr, a.emb, a.Y,
-                               a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb, a.c_begin, a.c_end, a.n_nodes);
-      break;
-    case 1: hipLaunchKernelGGL(k_conv_bwd_ls<LayerMid>, dim3((nc + WM - 1) / WM), dim3(64 * WM), 0, s,
-                               a.row_ptr, a.nbr, a.emb, a.Y, a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb,
-                               a.c_begin, a.c_end, a.n_nodes);
-      break;
-    default: return hipErrorInvalidValue;  // the last block: launch_conv_bwd_nbr_last
-  }
+  hipLaunchKernelGGL(k_conv_bwd_ls<L>, dim3((nc + WPG - 1) / WPG), dim3(64 * WPG), 0, s, a.row_ptr, a.nbr,
+                     a.emb, a.Y, a.h, a.gagg, a.W, a.dxc, a.dgu, a.demb, a.c_begin, a.c_end, a.n_nodes);
   return hipGetLastError();
 }
 
@@ -1236,20 +1302,130 @@ static hipError_t fwd_impl(const FusedArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s) {
-  switch (kind) {
-    case 0: return fwd_impl<LayerFirst>(a, s);
-    case 1: return fwd_impl<LayerMid>(a, s);
-    default: return fwd_impl<LayerLast>(a, s);
-  }
-}
-hipError_t launch_conv_bwd_nbr_last(const FusedArgs& a, hipStream_t s) {
+template <class L>
+static hipError_t bwd_nbr_impl(const FusedArgs& a, hipStream_t s) {
   const int nn = a.node_end - a.node_begin;
-  if (nn <= 0 || a.n_nodes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_conv_bwd_nbr<LayerLast>, dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr,
-                     a.src_perm, a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu, a.n_centers,
-                     a.node_begin, a.node_end, a.demb);
+  hipLaunchKernelGGL(k_conv_bwd_nbr<L>, dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr, a.src_perm,
+                     a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu, a.n_centers, a.node_begin,
+                     a.node_end, a.demb);
   return hipGetLastError();
 }
 
+// kind code -> family (tp.h)
+#define E3GNN_FAMILY_SWITCH(code, F_FIRST, F_MID, F_LAST)       \
+  switch (code) {                                               \
+    case 0: F_FIRST(0); case 1: F_MID(0); case 2: F_LAST(0);    \
+    case 3: F_FIRST(1); case 4: F_MID(1); case 5: F_LAST(1);    \
+    case 6: F_FIRST(2); case 7: F_MID(2); case 8: F_LAST(2);    \
+    default: return hipErrorInvalidValue;                       \
+  }
+
+hipError_t launch_conv_bwd_ls(int kind, const FusedArgs& a, hipStream_t s) {
+  const int nc = a.c_end - a.c_begin;
+  if (nc <= 0 || a.n_nodes <= 0) return hipSuccess;
+#define FIRST_(f) return bwd_ls_impl<Family<f>::First>(a, s)
+#define MID_(f) return bwd_ls_impl<Family<f>::Mid>(a, s)
+#define LAST_(f) return hipErrorInvalidValue   // the last block: launch_conv_bwd_nbr_last
+  E3GNN_FAMILY_SWITCH(kind, FIRST_, MID_, LAST_)
+#undef FIRST_
+#undef MID_
+#undef LAST_
+}
+
+hipError_t launch_conv_fwd(int kind, const FusedArgs& a, hipStream_t s) {
+#define FIRST_(f) return fwd_impl<Family<f>::First>(a, s)
+#define MID_(f) return fwd_impl<Family<f>::Mid>(a, s)
+#define LAST_(f) return fwd_impl<Family<f>::Last>(a, s)
+  E3GNN_FAMILY_SWITCH(kind, FIRST_, MID_, LAST_)
+#undef FIRST_
+#undef MID_
+#undef LAST_
+}
+
+hipError_t launch_conv_bwd_nbr_last(int kind, const FusedArgs& a, hipStream_t s) {
+  const int nn = a.node_end - a.node_begin;
+  if (nn <= 0 || a.n_nodes <= 0) return hipSuccess;
+#define FIRST_(f) return hipErrorInvalidValue
+#define MID_(f) return hipErrorInvalidValue
+#define LAST_(f) return bwd_nbr_impl<Family<f>::Last>(a, s)
+  E3GNN_FAMILY_SWITCH(kind, FIRST_, MID_, LAST_)
+#undef FIRST_
+#undef MID_
+#undef LAST_
+}
+
+template <class L>
+static void kind_dims(int* dx, int* w, int* dm) {
+  *dx = L::DX;
+  *w = L::W;
+  *dm = L::DM;
+}
+bool fused_kind_dims(int code, int* dx, int* w, int* dm) {
+  auto f = [&]() -> hipError_t {
+#define FIRST_(f) return kind_dims<Family<f>::First>(dx, w, dm), hipSuccess
+#define MID_(f) return kind_dims<Family<f>::Mid>(dx, w, dm), hipSuccess
+#define LAST_(f) return kind_dims<Family<f>::Last>(dx, w, dm), hipSuccess
+    E3GNN_FAMILY_SWITCH(code, FIRST_, MID_, LAST_)
+#undef FIRST_
+#undef MID_
+#undef LAST_
+  };
+  return f() == hipSuccess;
+}
+
+// algorithmic FLOP of one TP forward per edge: per path and channel 2 per CG
+// entry + 1 per output component (SURVEY.md 8d's 3,456 / 16,832 / 1,184 for
+// SevenNet-0's first / middle / last block)
+template <class L>
+constexpr double kind_tp_flops() {
+  double f = 0;
+  sfor_host<L::NP>([&](auto pi) {
+    constexpr PathDef p = L::P[pi];
+    f += (double)p.mul * (2 * CG<p.l1, p.l2, p.l3>::n + 2 * p.l3 + 1);
+  });
+  return f;
+}
+static_assert(kind_tp_flops<LayerFirst>() == 3456.0 && kind_tp_flops<LayerMid>() == 16832.0 &&
+                  kind_tp_flops<LayerLast>() == 1184.0,
+              "SURVEY.md 8d per-edge TP FLOP");
+double fused_kind_tp_flops(int code) {
+  switch (code) {
+#define K_(c, f, T) \
+  case c:           \
+    return kind_tp_flops<Family<f>::T>();
+    K_(0, 0, First) K_(1, 0, Mid) K_(2, 0, Last) K_(3, 1, First) K_(4, 1, Mid) K_(5, 1, Last)
+    K_(6, 2, First) K_(7, 2, Mid) K_(8, 2, Last)
+#undef K_
+    default: return 0.0;
+  }
+}
+
+template <class L>
+static int kind_paths(PathDef* out, int max) {
+  for (int p = 0; p < L::NP && p < max; ++p) out[p] = L::P[p];
+  return L::NP;
+}
+int fused_kind_paths(int code, PathDef* out, int max) {
+  auto f = [&]() -> int {
+    switch (code) {
+#define K_(c, f, T) \
+  case c:           \
+    return kind_paths<Family<f>::T>(out, max);
+      K_(0, 0, First) K_(1, 0, Mid) K_(2, 0, Last) K_(3, 1, First) K_(4, 1, Mid) K_(5, 1, Last)
+      K_(6, 2, First) K_(7, 2, Mid) K_(8, 2, Last)
+#undef K_
+      default: return 0;
+    }
+  };
+  return f();
+}
+
 }  // namespace e3gnn
+
+#ifdef E3GNN_STAMPS
+// diagnostic builds only: the device buffer the middle backward's phase
+// stamps go to ([waves][8] u64; null disables)
+extern "C" int e3gnn_debug_stamps(void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(e3gnn::g_stamp_buf), &p, sizeof(p));
+}
+#endif

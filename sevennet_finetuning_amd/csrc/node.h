@@ -23,14 +23,22 @@ hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, con
 hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* center,
                               const int* nbr, int* row_ptr, int* src_ptr, int* src_perm, int* cnt,
                               int* err, hipStream_t s, int n_interior = 0);
-hipError_t launch_embed(int n, const int* type, int nsp, const float* W, float* x, int* err,
+hipError_t launch_embed(int n, int D, const int* type, int nsp, const float* W, float* x, int* err,
                         hipStream_t s);
-hipError_t launch_gate_fwd(int n, bool last, const float* y, float* x, hipStream_t s);
-hipError_t launch_gate_bwd(int n, bool last, const float* y, const float* dx, float* dy,
+// e3nn Gate of the SevenNet-0-shaped family: y = [ns scalars | g1 + g2 gates |
+// g1 x 1e | g2 x 2e] -> x = [ns x 0e | g1 x 1e | g2 x 2e]; the last block
+// (scalars only) uses ns alone
+struct GateDims {
+  int ns, g1, g2;
+  __host__ __device__ int dx() const { return ns + 3 * g1 + 5 * g2; }
+  __host__ __device__ int dy() const { return ns + 4 * g1 + 6 * g2; }
+};
+hipError_t launch_gate_fwd(int n, bool last, GateDims d, const float* y, float* x, hipStream_t s);
+hipError_t launch_gate_bwd(int n, bool last, GateDims d, const float* y, const float* dx, float* dy,
                            hipStream_t s);
-hipError_t launch_readout(int n, const float* x, const float* v, const int* type,
+hipError_t launch_readout(int n, int D, const float* x, const float* v, const int* type,
                           const float* scale, const float* shift, float* eat, hipStream_t s);
-hipError_t launch_readout_bwd(int n, const float* v, const int* type, const float* scale,
+hipError_t launch_readout_bwd(int n, int D, const float* v, const int* type, const float* scale,
                               float* dx, hipStream_t s);
 int sum_blocks(int64_t n);
 hipError_t launch_sum(int64_t n, const float* a, float* part, float* out, hipStream_t s);

@@ -434,81 +434,88 @@ __global__ __launch_bounds__(256) void k_sort_segments(int n, const int* __restr
 
 // ------------------------------------------------------------ node ops
 // OnehotEmbedding + IrrepsLinear(is_embed) (node_embedding.py:39-48,
-// linear.py:37-44): row lookup of the pre-scaled embedding matrix.
-__global__ void k_embed(int n, const int* __restrict__ type, int nsp, const float* __restrict__ W,
+// linear.py:37-44): row lookup of the pre-scaled embedding matrix (D columns).
+__global__ void k_embed(int n, int D, const int* __restrict__ type, int nsp, const float* __restrict__ W,
                         float* __restrict__ x, int* __restrict__ err) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)n * 128) return;
-  const int i = (int)(idx >> 7), c = (int)(idx & 127);
+  if (idx >= (int64_t)n * D) return;
+  const int i = (int)(idx / D), c = (int)(idx - (int64_t)i * D);
   const int t = type[i];
   if (t < 0 || t >= nsp) {
     if (c == 0) atomicOr(err, 8);
     x[idx] = 0.f;
     return;
   }
-  x[idx] = W[t * 128 + c];
+  x[idx] = W[t * D + c];
 }
 
-// e3nn Gate (equivariant_gate.py:13-61; serial_code.py:256-347).
-// y: [224x0e (128 scalars | 96 gates) | 64x1e | 32x2e] -> x: [128x0e | 64x1e | 32x2e]
-__global__ void k_gate_fwd(int n, const float* __restrict__ y, float* __restrict__ x) {
+// e3nn Gate (equivariant_gate.py:13-61; serial_code.py:256-347) of the
+// SevenNet-0-shaped family, dims GateDims (node.h):
+// y: [ns scalars | g1 + g2 gates | g1 x 1e | g2 x 2e] -> x: [ns x 0e | g1 x 1e | g2 x 2e]
+// (SevenNet-0: ns 128, g1 64, g2 32: y 576, x 480)
+__global__ void k_gate_fwd(int n, GateDims d, const float* __restrict__ y, float* __restrict__ x) {
+  const int DX = d.dx(), DY = d.dy();
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)n * 480) return;
-  const int64_t i = idx / 480;
-  const int c = (int)(idx - i * 480);
-  const float* yr = y + i * 576;
+  if (idx >= (int64_t)n * DX) return;
+  const int64_t i = idx / DX;
+  const int c = (int)(idx - i * DX);
+  const float* yr = y + i * DY;
+  const int ns = d.ns, o1 = ns + 3 * d.g1;           // x offsets of the 2e block
+  const int yg = ns, yv = ns + d.g1 + d.g2;          // y offsets: gates, gated values
   float v;
-  if (c < 128) v = act_fwd(yr[c]);
-  else if (c < 320) v = act_fwd(yr[128 + (c - 128) / 3]) * yr[224 + (c - 128)];
-  else v = act_fwd(yr[192 + (c - 320) / 5]) * yr[416 + (c - 320)];
+  if (c < ns) v = act_fwd(yr[c]);
+  else if (c < o1) v = act_fwd(yr[yg + (c - ns) / 3]) * yr[yv + (c - ns)];
+  else v = act_fwd(yr[yg + d.g1 + (c - o1) / 5]) * yr[yv + (c - ns)];
   x[idx] = v;
 }
-// Gate backward, one wave per node: the y (576) and dE/dx (480) rows staged
-// in LDS with float4 loads, 9 outputs per lane, coalesced stores.
-__global__ __launch_bounds__(256) void k_gate_bwd_rows(int n, const float* __restrict__ y,
+// Gate backward, one wave per node: the y (DY) and dE/dx (DX) rows staged in
+// LDS with float4 loads (dynamic LDS: 4 x (DY + DX) floats), coalesced stores.
+__global__ __launch_bounds__(256) void k_gate_bwd_rows(int n, GateDims d, const float* __restrict__ y,
                                                        const float* __restrict__ dx,
                                                        float* __restrict__ dy) {
-  __shared__ float4 sh[4][(576 + 480) / 4];
+  extern __shared__ float4 shg[];
+  const int DX = d.dx(), DY = d.dy();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = blockIdx.x * 4 + w;
   if (i >= n) return;  // whole wave: no block-level barrier below
-  float4* yr4 = sh[w];
-  float4* dr4 = sh[w] + 576 / 4;
-  const float4* yg = reinterpret_cast<const float4*>(y + (int64_t)i * 576);
-  const float4* dg = reinterpret_cast<const float4*>(dx + (int64_t)i * 480);
-  for (int k = lane; k < 144; k += 64) yr4[k] = yg[k];
-  for (int k = lane; k < 120; k += 64) dr4[k] = dg[k];
+  float4* yr4 = shg + w * ((DY + DX) / 4);
+  float4* dr4 = yr4 + DY / 4;
+  const float4* yg4 = reinterpret_cast<const float4*>(y + (int64_t)i * DY);
+  const float4* dg4 = reinterpret_cast<const float4*>(dx + (int64_t)i * DX);
+  for (int k = lane; k < DY / 4; k += 64) yr4[k] = yg4[k];
+  for (int k = lane; k < DX / 4; k += 64) dr4[k] = dg4[k];
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const float* yr = reinterpret_cast<const float*>(yr4);
   const float* dr = reinterpret_cast<const float*>(dr4);
-  float* out = dy + (int64_t)i * 576;
-#pragma unroll
-  for (int q = 0; q < 9; ++q) {
-    const int c = lane + 64 * q;
+  float* out = dy + (int64_t)i * DY;
+  const int ns = d.ns, g1 = d.g1, g2 = d.g2;
+  const int yg = ns, yv = ns + g1 + g2, yv2 = yv + 3 * g1;   // y: gates, 1e values, 2e values
+  const int x1 = ns, x2 = ns + 3 * g1;                         // x: 1e, 2e
+  for (int c = lane; c < DY; c += 64) {
     float v;
-    if (c < 128) {
+    if (c < ns) {
       v = dr[c] * act_grad(yr[c]);
-    } else if (c < 192) {
-      const int u = c - 128;
-      const float s = dr[128 + 3 * u] * yr[224 + 3 * u] + dr[129 + 3 * u] * yr[225 + 3 * u] +
-                      dr[130 + 3 * u] * yr[226 + 3 * u];
+    } else if (c < yg + g1) {
+      const int u = c - yg;
+      const float s = dr[x1 + 3 * u] * yr[yv + 3 * u] + dr[x1 + 3 * u + 1] * yr[yv + 3 * u + 1] +
+                      dr[x1 + 3 * u + 2] * yr[yv + 3 * u + 2];
       v = s * act_grad(yr[c]);
-    } else if (c < 224) {
-      const int u = c - 192;
+    } else if (c < yv) {
+      const int u = c - yg - g1;
       float s = 0.f;
 #pragma unroll
-      for (int m = 0; m < 5; ++m) s += dr[320 + 5 * u + m] * yr[416 + 5 * u + m];
+      for (int m = 0; m < 5; ++m) s += dr[x2 + 5 * u + m] * yr[yv2 + 5 * u + m];
       v = s * act_grad(yr[c]);
-    } else if (c < 416) {
-      v = dr[128 + (c - 224)] * act_fwd(yr[128 + (c - 224) / 3]);
+    } else if (c < yv2) {
+      v = dr[x1 + (c - yv)] * act_fwd(yr[yg + (c - yv) / 3]);
     } else {
-      v = dr[320 + (c - 416)] * act_fwd(yr[192 + (c - 416) / 5]);
+      v = dr[x2 + (c - yv2)] * act_fwd(yr[yg + g1 + (c - yv2) / 5]);
     }
     out[c] = v;
   }
 }
-// last layer: 128 scalars, all activated
+// last layer: scalars only, all activated
 __global__ void k_act_fwd(int64_t n, const float* __restrict__ y, float* __restrict__ x) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = act_fwd(y[i]);
@@ -520,25 +527,29 @@ __global__ void k_act_bwd(int64_t n, const float* __restrict__ y, const float* _
 }
 
 // readout (model_build.py:374-408) + SpeciesWiseRescale (scale.py:67-73):
-// E_i = scale[t] * <x_i, v> + shift[t], v = W_hidden @ W_energy (path weights folded)
-__global__ void k_readout(int n, const float* __restrict__ x, const float* __restrict__ v,
+// E_i = scale[t] * <x_i, v> + shift[t], v = W_hidden @ W_energy (path weights
+// folded), x_i of D scalars (one wave per atom, lane-strided, fixed order)
+__global__ void k_readout(int n, int D, const float* __restrict__ x, const float* __restrict__ v,
                           const int* __restrict__ type, const float* __restrict__ scale,
                           const float* __restrict__ shift, float* __restrict__ eat) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= n) return;
-  const float* xr = x + (int64_t)i * 128;
-  const float s = wave_sum(xr[lane] * v[lane] + xr[lane + 64] * v[lane + 64]);
+  const float* xr = x + (int64_t)i * D;
+  float a = 0.f;
+  for (int c = lane; c < D; c += 64) a += xr[c] * v[c];
+  const float s = wave_sum(a);
   if (lane == 0) {
     const int t = type[i];
     eat[i] = s * scale[t] + shift[t];
   }
 }
-__global__ void k_readout_bwd(int n, const float* __restrict__ v, const int* __restrict__ type,
+__global__ void k_readout_bwd(int n, int D, const float* __restrict__ v, const int* __restrict__ type,
                               const float* __restrict__ scale, float* __restrict__ dx) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)n * 128) return;
-  dx[idx] = scale[type[idx >> 7]] * v[idx & 127];
+  if (idx >= (int64_t)n * D) return;
+  const int64_t i = idx / D;
+  dx[idx] = scale[type[i]] * v[idx - i * D];
 }
 
 // per-block partial sums of a [n, stride] array's column `col` (fixed tree)
@@ -722,33 +733,36 @@ hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* 
     hipLaunchKernelGGL(k_sort_segments, dim3((n_nodes + 3) / 4), dim3(256), 0, s, n_nodes, src_ptr, src_perm);
   return hipGetLastError();
 }
-hipError_t launch_embed(int n, const int* type, int nsp, const float* W, float* x, int* err,
+hipError_t launch_embed(int n, int D, const int* type, int nsp, const float* W, float* x, int* err,
                         hipStream_t s) {
-  LAUNCH(k_embed, nblk((int64_t)n * 128), n, type, nsp, W, x, err);
+  LAUNCH(k_embed, nblk((int64_t)n * D), n, D, type, nsp, W, x, err);
   return hipGetLastError();
 }
-hipError_t launch_gate_fwd(int n, bool last, const float* y, float* x, hipStream_t s) {
-  if (last) LAUNCH(k_act_fwd, nblk((int64_t)n * 128), (int64_t)n * 128, y, x);
-  else LAUNCH(k_gate_fwd, nblk((int64_t)n * 480), n, y, x);
+hipError_t launch_gate_fwd(int n, bool last, GateDims d, const float* y, float* x, hipStream_t s) {
+  if (last) LAUNCH(k_act_fwd, nblk((int64_t)n * d.ns), (int64_t)n * d.ns, y, x);
+  else LAUNCH(k_gate_fwd, nblk((int64_t)n * d.dx()), n, d, y, x);
   return hipGetLastError();
 }
-hipError_t launch_gate_bwd(int n, bool last, const float* y, const float* dx, float* dy,
+hipError_t launch_gate_bwd(int n, bool last, GateDims d, const float* y, const float* dx, float* dy,
                            hipStream_t s) {
-  if (last) LAUNCH(k_act_bwd, nblk((int64_t)n * 128), (int64_t)n * 128, y, dx, dy);
-  else if (n > 0)
-    hipLaunchKernelGGL(k_gate_bwd_rows, dim3((n + 3) / 4), dim3(256), 0, s, n, y, dx, dy);
+  if (last) LAUNCH(k_act_bwd, nblk((int64_t)n * d.ns), (int64_t)n * d.ns, y, dx, dy);
+  else if (n > 0) {
+    if (d.dy() % 4 || d.dx() % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_gate_bwd_rows, dim3((n + 3) / 4), dim3(256), 4 * (d.dy() + d.dx()) * sizeof(float),
+                       s, n, d, y, dx, dy);
+  }
   return hipGetLastError();
 }
-hipError_t launch_readout(int n, const float* x, const float* v, const int* type,
+hipError_t launch_readout(int n, int D, const float* x, const float* v, const int* type,
                           const float* scale, const float* shift, float* eat, hipStream_t s) {
   if (n > 0)
-    hipLaunchKernelGGL(k_readout, dim3((n + 3) / 4), dim3(256), 0, s, n, x, v, type, scale, shift,
+    hipLaunchKernelGGL(k_readout, dim3((n + 3) / 4), dim3(256), 0, s, n, D, x, v, type, scale, shift,
                        eat);
   return hipGetLastError();
 }
-hipError_t launch_readout_bwd(int n, const float* v, const int* type, const float* scale,
+hipError_t launch_readout_bwd(int n, int D, const float* v, const int* type, const float* scale,
                               float* dx, hipStream_t s) {
-  LAUNCH(k_readout_bwd, nblk((int64_t)n * 128), n, v, type, scale, dx);
+  LAUNCH(k_readout_bwd, nblk((int64_t)n * D), n, D, v, type, scale, dx);
   return hipGetLastError();
 }
 int sum_blocks(int64_t n) { return nblk(n); }

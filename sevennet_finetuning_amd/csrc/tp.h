@@ -16,31 +16,97 @@ struct PathDef {
   int l1, l2, l3, mul, xoff, woff, moff;
 };
 
-// layer 0: x = 128x0e -> mid 128x0e+128x1e+128x2e
-struct LayerFirst {
-  static constexpr int DX = 128, W = 384, DM = 1152, NP = 3;
-  static constexpr PathDef P[NP] = {{0, 0, 0, 128, 0, 0, 0},
-                                    {0, 1, 1, 128, 0, 128, 128},
-                                    {0, 2, 2, 128, 0, 256, 512}};
+// The three block kinds of the SevenNet-0-shaped family (lmax 2, even
+// parity), templated on the channel multiplicities: the first block's input
+// A x0e; the middle blocks' input and output C0x0e+C1x1e+C2x2e; the last
+// block's input the same, output l3 = 0 only.  Instruction order (woff) and the
+// stable-by-l3 mid slots (moff) follow convolution.py:72-95 / :82-87.
+// KIND: 0 first, 1 middle, 2 last.
+template <int A>
+struct LayerFirstT {
+  static constexpr int KIND = 0, C0 = A;
+  static constexpr int DX = A, W = 3 * A, DM = 9 * A, NP = 3;
+  static constexpr PathDef P[NP] = {{0, 0, 0, A, 0, 0, 0}, {0, 1, 1, A, 0, A, A}, {0, 2, 2, A, 0, 2 * A, 4 * A}};
 };
 
-// layers 1..3: x = 128x0e+64x1e+32x2e -> mid 224x0e+384x1e+352x2e
-struct LayerMid {
-  static constexpr int DX = 480, W = 960, DM = 3136, NP = 15;
+template <int C0_, int C1, int C2>
+struct LayerMidT {
+  static constexpr int KIND = 1, C0 = C0_;
+  static constexpr int X1 = C0_, X2 = C0_ + 3 * C1;            // x offsets of 1e, 2e
+  static constexpr int DX = C0_ + 3 * C1 + 5 * C2;
+  static constexpr int W = 3 * C0_ + 6 * C1 + 6 * C2;
+  static constexpr int M0 = C0_ + C1 + C2;                      // 0e mid channels
+  static constexpr int B1 = M0, B2 = M0 + 3 * (C0_ + 3 * C1 + 2 * C2);  // 1e / 2e mid bases
+  static constexpr int DM = B2 + 5 * (C0_ + 2 * C1 + 3 * C2);
+  static constexpr int NP = 15;
+  static constexpr int V = 3 * C0_ + 6 * C1;                    // woff of the first l1 = 2 path
   static constexpr PathDef P[NP] = {
-      {0, 0, 0, 128, 0, 0, 0},      {0, 1, 1, 128, 0, 128, 224},  {0, 2, 2, 128, 0, 256, 1376},
-      {1, 0, 1, 64, 128, 384, 608}, {1, 1, 0, 64, 128, 448, 128}, {1, 1, 1, 64, 128, 512, 800},
-      {1, 1, 2, 64, 128, 576, 2016}, {1, 2, 1, 64, 128, 640, 992}, {1, 2, 2, 64, 128, 704, 2336},
-      {2, 0, 2, 32, 320, 768, 2656}, {2, 1, 1, 32, 320, 800, 1184}, {2, 1, 2, 32, 320, 832, 2816},
-      {2, 2, 0, 32, 320, 864, 192}, {2, 2, 1, 32, 320, 896, 1280}, {2, 2, 2, 32, 320, 928, 2976}};
+      {0, 0, 0, C0_, 0, 0, 0},
+      {0, 1, 1, C0_, 0, C0_, B1},
+      {0, 2, 2, C0_, 0, 2 * C0_, B2},
+      {1, 0, 1, C1, X1, 3 * C0_, B1 + 3 * C0_},
+      {1, 1, 0, C1, X1, 3 * C0_ + C1, C0_},
+      {1, 1, 1, C1, X1, 3 * C0_ + 2 * C1, B1 + 3 * C0_ + 3 * C1},
+      {1, 1, 2, C1, X1, 3 * C0_ + 3 * C1, B2 + 5 * C0_},
+      {1, 2, 1, C1, X1, 3 * C0_ + 4 * C1, B1 + 3 * C0_ + 6 * C1},
+      {1, 2, 2, C1, X1, 3 * C0_ + 5 * C1, B2 + 5 * C0_ + 5 * C1},
+      {2, 0, 2, C2, X2, V, B2 + 5 * C0_ + 10 * C1},
+      {2, 1, 1, C2, X2, V + C2, B1 + 3 * C0_ + 9 * C1},
+      {2, 1, 2, C2, X2, V + 2 * C2, B2 + 5 * C0_ + 10 * C1 + 5 * C2},
+      {2, 2, 0, C2, X2, V + 3 * C2, C0_ + C1},
+      {2, 2, 1, C2, X2, V + 4 * C2, B1 + 3 * C0_ + 9 * C1 + 3 * C2},
+      {2, 2, 2, C2, X2, V + 5 * C2, B2 + 5 * C0_ + 10 * C1 + 10 * C2}};
 };
 
-// layer 4: x = 128x0e+64x1e+32x2e -> mid 224x0e (lmax_out = 0)
-struct LayerLast {
-  static constexpr int DX = 480, W = 224, DM = 224, NP = 3;
+template <int C0_, int C1, int C2>
+struct LayerLastT {
+  static constexpr int KIND = 2, C0 = C0_;
+  static constexpr int DX = C0_ + 3 * C1 + 5 * C2, W = C0_ + C1 + C2, DM = W, NP = 3;
   static constexpr PathDef P[NP] = {
-      {0, 0, 0, 128, 0, 0, 0}, {1, 1, 0, 64, 128, 128, 128}, {2, 2, 0, 32, 320, 192, 192}};
+      {0, 0, 0, C0_, 0, 0, 0}, {1, 1, 0, C1, C0_, C0_, C0_}, {2, 2, 0, C2, C0_ + 3 * C1, C0_ + C1, C0_ + C1}};
 };
+
+// Compiled channel families.  A kernel KIND CODE is 3 * family + KIND.
+//   0: SevenNet-0 (128x0e -> 128x0e+64x1e+32x2e -> ... -> 128x0e)
+//   1: uniform 64 (model_build channel 64: 64x0e -> 64x0e+64x1e+64x2e -> ... -> 64x0e)
+//   2: uniform 32 (channel 32, the reference's base preset width)
+template <int F>
+struct Family;
+template <>
+struct Family<0> {
+  using First = LayerFirstT<128>;
+  using Mid = LayerMidT<128, 64, 32>;
+  using Last = LayerLastT<128, 64, 32>;
+};
+template <>
+struct Family<1> {
+  using First = LayerFirstT<64>;
+  using Mid = LayerMidT<64, 64, 64>;
+  using Last = LayerLastT<64, 64, 64>;
+};
+template <>
+struct Family<2> {
+  using First = LayerFirstT<32>;
+  using Mid = LayerMidT<32, 32, 32>;
+  using Last = LayerLastT<32, 32, 32>;
+};
+constexpr int N_FAMILIES = 3;
+
+// SevenNet-0's kinds (the training ops and the v1 kernels serve these only)
+using LayerFirst = Family<0>::First;
+using LayerMid = Family<0>::Mid;
+using LayerLast = Family<0>::Last;
+static_assert(LayerMid::DX == 480 && LayerMid::W == 960 && LayerMid::DM == 3136, "SevenNet-0 middle block");
+static_assert(LayerMid::P[8].moff == 2336 && LayerMid::P[13].moff == 1280 && LayerMid::P[14].woff == 928,
+              "SevenNet-0 path table");
+static_assert(LayerFirst::DM == 1152 && LayerLast::W == 224 && LayerLast::P[2].xoff == 320, "SevenNet-0 kinds");
+
+// dimensions of a kind code (host; false if unknown)
+bool fused_kind_dims(int code, int* dx, int* w, int* dm);
+// the kind's path table (l1, l2, l3, mul, xoff, woff, moff) per path; empty if unknown
+int fused_kind_paths(int code, PathDef* out, int max);
+// algorithmic FLOP of one TP forward per edge of the kind (0 if unknown)
+double fused_kind_tp_flops(int code);
 
 struct TpArgs {
   const int* row_ptr;  // [n_centers + 1] CSR over edges sorted by centre

@@ -56,6 +56,8 @@ class E3GNNModel:
         co = _lib.ctypes.c_float()
         _lib.check(self.lib.e3gnn_model_info(h, ns, co, nl, cs))
         self.num_species, self.num_layers, self.comm_size = ns.value, nl.value, cs.value
+        # >= 0: the fused-kernel channel family serving it; -1: the generic engine
+        self.family = int(self.lib.e3gnn_model_family(h))
         self.is_batch_data = False
         # outputs are device tensors on torch's current stream: return once the
         # evaluation is enqueued (stream order, like a torch module) rather than

@@ -491,3 +491,41 @@ def deploy(model, out_dir):
 
 
 deploy_parallel = deploy  # one deployment serves the segment API (comm_size in the manifest)
+
+
+def deploy_config(config, out_dir, seed=0):
+    """A config straight to a deployment (weights.bin + manifest.json) with
+    e3nn's initialisation (``init_weights``), without building the trainable
+    model: what ``deploy(build_E3_equivariant_model(config))`` writes, for
+    hosts and benchmarks that only serve the model (no GPU needed to write it)."""
+    cfg = resolve_config(config)
+    man = model_manifest(cfg)
+    _check_kernel_support(man)
+    flat = init_weights(man, cfg, seed).astype('<f4')
+    irreps = [_parse(s) for s in man['irreps_manual']]
+    man['comm_size'] = max(_dim(ir) for ir in irreps[1:-1]) if len(irreps) > 2 else _dim(irreps[0])
+    man['deploy_time'] = datetime.datetime.now().strftime('%Y-%m-%d')
+    man['deployed_by'] = BUILD_VERSION
+    os.makedirs(out_dir, exist_ok=True)
+    tmp = os.path.join(out_dir, 'weights.bin.tmp')
+    flat.tofile(tmp)
+    os.replace(tmp, os.path.join(out_dir, 'weights.bin'))
+    with open(os.path.join(out_dir, 'manifest.json'), 'w') as f:
+        json.dump(man, f, indent=1)
+    return out_dir
+
+
+def sevennet_shaped_config(channel, num_convolution_layer, species=None, avg_num_neigh=28.0):
+    """The SevenNet-0 preset (sevenn/presets/sevennet-0.yaml: lmax 2, even
+    parity, XPLOR 4.5-5.0 A, 8 Bessel functions, a 64-64 radial MLP, linear
+    self-connection) without its irreps_manual: ``channel`` x (0e+1e+2e) per
+    block, ``num_convolution_layer`` blocks (model_build.py:196-372)."""
+    return {'chemical_species': species or ['Cl', 'Li', 'P', 'S', 'Si'], 'cutoff': 5.0,
+            'channel': channel, 'is_parity': False, 'lmax': 2,
+            'num_convolution_layer': num_convolution_layer,
+            'weight_nn_hidden_neurons': [64, 64],
+            'radial_basis': {'radial_basis_name': 'bessel', 'bessel_basis_num': 8},
+            'cutoff_function': {'cutoff_function_name': 'XPLOR', 'cutoff_on': 4.5},
+            'act_gate': {'e': 'silu', 'o': 'tanh'}, 'act_scalar': {'e': 'silu', 'o': 'tanh'},
+            'conv_denominator': float(avg_num_neigh), 'self_connection_type': 'linear',
+            'train_shift_scale': False, 'train_denominator': False}

@@ -79,6 +79,8 @@ for s in "$@"; do
     testsv_*) v=${s#testsv_}; step tests_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -m pytest tests -m gpu -x -q ;;
     bench2self) step bench2self 600 python bench.py --gpus 2 --same-device --steps 2 --warmup 1 --cells 11 --no-cpu-baseline ;;
     paritydef) step paritydef 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
+    stamps_*) v=${s#stamps_}; step stamps_$v 300 python tools/stamps.py sevennet_finetuning_amd/variants/$v.so ;;
+    reportv_*) v=${s#reportv_}; step report_$v 300 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python tools/parity_report.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
