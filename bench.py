@@ -133,6 +133,44 @@ def rocprof_name(cls):
     return cls
 
 
+PEAK_BF16_TFLOPS = 16 * 157.3   # dense bf16 MFMA (MI355X_MICROARCH.md: 1/16 ratio to f32)
+
+
+def pmc_entry(kernel, cells):
+    """The committed PMC summary entry (profiles/pmc_traffic.json) of `kernel`."""
+    path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if d.get('cells') != cells:
+        return None
+    for k, v in d.get('kernels', {}).items():
+        if kernel in k:
+            return v
+    return None
+
+
+def mfma_fracs(kernel, cells, ms_per_launch):
+    """Matrix-core rate of `kernel` by the precision its MFMA work runs in:
+    executed FLOP per launch (SQ_INSTS_VALU_MFMA_MOPS_* x 512, committed PMC
+    pass) / the launch time measured in this run, against that precision's
+    dense peak.  The fused kernels run the radial MLP's products on bf16x6
+    (six bf16 MFMAs per f32-grade product), so this counts the bf16 work the
+    matrix cores did, not the algorithmic FLOP of `achieved`."""
+    e = pmc_entry(kernel, cells)
+    if not e or 'mfma_flop_bf16' not in e or not ms_per_launch:
+        return None
+    out = {}
+    for prec, peak in (('bf16', PEAK_BF16_TFLOPS), ('f32', PEAK_FP32_TFLOPS)):
+        f = e.get(f'mfma_flop_{prec}', 0)
+        ach = f / (ms_per_launch * 1e9)
+        out[prec] = {'flop_per_launch': f, 'achieved': round(ach, 2), 'peak': round(peak, 1),
+                     'unit': 'TFLOP/s', 'frac': round(ach / peak, 4)}
+    out['source'] = 'profiles/pmc_traffic.json (rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_*)'
+    return out
+
+
 def pmc_traffic(kernel, cells):
     """HBM bytes per launch of `kernel` from the committed PMC summary
     (tools/pmc_traffic.py: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE,
@@ -492,6 +530,7 @@ def main():
         roofline['step_tflops'] = round(tot_flops / (ms * 1e9), 3)
         roofline['rocprof_kernel'] = rp_name
         roofline['traffic'] = pmc_traffic(rp_name, cells)
+        roofline['mfma_by_precision'] = mfma_fracs(rp_name, cells, roofline['ms_per_launch'])
 
     distributed = None
     if world > 1:

@@ -206,20 +206,47 @@ __device__ __forceinline__ void load_w2b(Op3& o, __amdgpu_buffer_rsrc_t w2b, int
       o.v[pc][m] = __builtin_bit_cast(
           bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2b, lane * 16, ((col0 / 16 * 3 + pc) * 2 + m) * 1024, 0));
 }
+// Eight floats as three bf16 pieces (v = p0 + p1 + p2, each piece the
+// round-to-nearest-even bf16 of the remaining residual), two values per
+// v_cvt_pk_bf16_f32: the packed pair is both the MFMA operand word and, widened
+// by a shift / mask, what the residual subtracts (5.5 VALU per value instead of
+// the 7.5 of per-value conversions re-packed afterwards; same bits)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void split3x8(const float (&v)[8], bf16x8 (&d)[3]) {
+  u32x4 w[3];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x2 r;
+    r[0] = v[2 * q];
+    r[1] = v[2 * q + 1];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+      const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
+      w[pc][q] = u;
+      if (pc < 2) {
+        r[0] -= __builtin_bit_cast(float, u << 16);
+        r[1] -= __builtin_bit_cast(float, u & 0xffff0000u);
+      }
+    }
+  }
+#pragma unroll
+  for (int pc = 0; pc < 3; ++pc) d[pc] = __builtin_bit_cast(bf16x8, w[pc]);
+}
+
 // the lane's 16 H2 values (units 16 bh + 4g + r) as three bf16 pieces
 __device__ __forceinline__ void split_h2(const f32x4 (&h2)[4], Op3& o) {
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < 2; ++m) {
+    float v[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      float x = h2[2 * m + (t >> 2)][t & 3];
+    for (int t = 0; t < 8; ++t) v[t] = h2[2 * m + (t >> 2)][t & 3];
+    bf16x8 d[3];
+    split3x8(v, d);
 #pragma unroll
-      for (int pc = 0; pc < 3; ++pc) {
-        const __bf16 b = (__bf16)x;
-        o.v[pc][m][t] = b;
-        x -= (float)b;
-      }
-    }
+    for (int pc = 0; pc < 3; ++pc) o.v[pc][m] = d[pc];
+  }
 }
 // HA: H2 is the A operand (rows = edges: forward); else W2^T is (rows = channels)
 template <bool HA>
@@ -796,6 +823,38 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
 // pass per node): every W2 operand block (w recompute and dH2) feeds both
 // tiles, and dE/dx[j] of both tiles is summed in registers before the
 // per-block DPP row sum.  The second tile is skipped when it has no edge.
+constexpr int LS_BLK = 6144;            // bytes of one w2v column block (3 pieces x 2 halves x 1 KB)
+constexpr int LS_PAIR_W = 2 * LS_BLK;   // the pair's two w-recompute operand blocks
+constexpr int LS_PAIR_D = 12288;        // the pair's dH2 operand (w2d: 3 pieces x 4 bh x 1 KB)
+
+// the same product with the pair's W2 pieces read from global memory (L2: every
+// wave of the launch reads the same operand; w2d order, MlpW::w2d): per hidden
+// block the three pieces are loaded right before its six MFMAs
+__device__ __forceinline__ void dh2_pair_g(f32x4 (&dh2)[4], const float (&da)[4], const float (&db)[4],
+                                           __amdgpu_buffer_rsrc_t w2d, int pair, int lane) {
+  bf16x8 d[3];
+  {
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = t < 4 ? da[t] : db[t - 4];
+    split3x8(v, d);
+  }
+  constexpr int I[6] = {2, 1, 0, 1, 0, 0}, J[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+  for (int bh = 0; bh < 4; ++bh) {
+    bf16x8 a[3];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+      a[pc] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2d, lane * 16, pair * LS_PAIR_D + (pc * 4 + bh) * 1024, 0));
+#pragma unroll
+    for (int q = 0; q < 6; ++q) dh2[bh] = mfma16(a[I[q]], d[J[q]], dh2[bh]);
+  }
+}
+
+#ifndef E3GNN_NBR_DH2_BF16
+#define E3GNN_NBR_DH2_BF16 0
+#endif
 template <class L>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_bwd_nbr(
     const int* __restrict__ src_ptr, const int* __restrict__ src_perm, const int* __restrict__ center,
@@ -847,6 +906,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int bb = 0; bb < 4; ++bb) dh2[u][bb] = zero4();
+#if E3GNN_NBR_DH2_BF16
+    float dwp[2][4];   // dE/dw of the block pair's first block, per tile
+#endif
     int nb = 0;
     constexpr int NBLK = L::W / 16;
     f32x4 wcur[2], wnxt[2] = {zero4(), zero4()};
@@ -878,8 +940,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
               float gm[2][4 * D3];
               load_gm<L, pi>(gm[0], Rg, vg[0], g, jj);
               load_gm<L, pi>(gm[1], Rg, vg[1], g, jj);
+#if !E3GNN_NBR_DH2_BF16
               f32x4 bq[4];
               load_w2q(bq, R.w2r, lane, p.woff + 16 * jj);
+#endif
               f32x4 wv[2] = {wcur[0], wcur[1]};
               if (nb + 1 < NBLK) {
                 wnxt[0] = w2_block<false>(hq[0], wq);
@@ -906,11 +970,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                   pin<D1>(dx + r * D1);
                   pin<8>(dYa[u] + 1);
                 }
+#if E3GNN_NBR_DH2_BF16
+                // dH2^T += W2[:, pair] dw^T on bf16x6 over the block pair (K = 32
+                // channels: the pair's first block is held in dwp)
+                if (nb & 1) {
+                  dh2_pair_g(dh2[u], dwp[u], dwr, R.w2d, nb >> 1, lane);
+                } else {
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) dwp[u][r] = dwr[r];
+                }
+#else
                 // dH2^T += W2[:, block] dw^T: k = lane group g, channel 4g + r
 #pragma unroll
                 for (int bh = 0; bh < 4; ++bh)
 #pragma unroll
                   for (int r = 0; r < 4; ++r) dh2[u][bh] = mfma(bq[bh][r], dwr[r], dh2[u][bh]);
+#endif
               }
               pin<4 * D1>(dx);
               wcur[0] = wnxt[0];
@@ -972,9 +1047,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // on bf16x6 MFMA over the pair (K = 32 channels): 24 x 16 MFMA cycles instead of
 // 2 x 16 x 32 on f32 MFMA.  Middle blocks: two workgroups per CU (LDS), 2 waves
 // per SIMD; the first block: 3 waves per SIMD.
-constexpr int LS_BLK = 6144;            // bytes of one w2v column block (3 pieces x 2 halves x 1 KB)
-constexpr int LS_PAIR_W = 2 * LS_BLK;   // the pair's two w-recompute operand blocks
-constexpr int LS_PAIR_D = 12288;        // the pair's dH2 operand (w2d: 3 pieces x 4 bh x 1 KB)
 
 __device__ __forceinline__ void lds_op3(Op3& o, const char* blk, int lane) {
 #pragma unroll
@@ -1014,15 +1086,11 @@ __device__ __forceinline__ void dh2_pair(f32x4 (&dh2)[4], const float (&da)[4], 
     return;
   }
   bf16x8 d[3];
+  {
+    float v[8];
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    float v = t < 4 ? da[t] : db[t - 4];
-#pragma unroll
-    for (int pc = 0; pc < 3; ++pc) {
-      const __bf16 b = (__bf16)v;
-      d[pc][t] = b;
-      v -= (float)b;
-    }
+    for (int t = 0; t < 8; ++t) v[t] = t < 4 ? da[t] : db[t - 4];
+    split3x8(v, d);
   }
   constexpr int I[6] = {2, 1, 0, 1, 0, 0}, J[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll

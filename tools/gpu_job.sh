@@ -59,6 +59,7 @@ for s in "$@"; do
     mdpar) step mdpar 300 native/e3gnn_md_parallel sevennet_finetuning_amd/assets/sevennet0/weights.bin sevennet_finetuning_amd/assets/sevennet0/manifest.json 23 2 2 2 3 ;;
     prof10k) step prof10k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof10k -o run --output-format csv -- python bench.py --cells 11 --steps 3 --warmup 1 --profile-only ;;
     pmcf) step pmcf 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
+    pmcmops) step pmcmops 900 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU --kernel-trace --output-format csv -d gpurun_out/pmc_mops -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     pmcw) step pmcw 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     slp) step slp_build 600 env E3GNN_FUSED_FLAGS=" " python -c "import sevennet_finetuning_amd.build_lib as b; b.build(force=True)" && step benchslp 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     ptest) step ptest 600 python -m pytest tests/test_parallel.py -q ;;
