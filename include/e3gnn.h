@@ -83,6 +83,30 @@ void e3gnn_free(e3gnn_model* m);
  * comm_size (features exchanged per ghost atom between layers). */
 int e3gnn_model_info(const e3gnn_model* m, int* num_species, float* cutoff, int* num_layers,
                      int* comm_size);
+/* Grouped f32 GEMM on the library's matrix-core kernel (tgemm.hip), the dense
+ * products of the fine-tune step (train_explicit.py) instead of a vendor BLAS:
+ *   C = beta C + alpha (op(A) op(B) + op(A2) op(B2))      beta 0 or 1
+ * op(X) = X^T when trans_* is set; row-major storage with leading dimensions
+ * ld*; k2 = 0: no second operand pair (A2/B2 ignored).  Up to 8 independent
+ * problems per call (their outputs must not overlap); long-K problems are split
+ * over K into `workspace` (e3gnn_gemm_workspace_floats floats) and reduced in a
+ * fixed order: deterministic, no atomics. */
+typedef struct e3gnn_gemm_desc {
+  const float* a;
+  const float* b;
+  const float* a2;
+  const float* b2;
+  float* c;
+  int64_t lda, ldb, lda2, ldb2, ldc;
+  int32_t m, n, k, k2;
+  int32_t trans_a, trans_b, trans_a2, trans_b2;
+  float alpha;
+  int32_t beta;
+} e3gnn_gemm_desc;
+int64_t e3gnn_gemm_workspace_floats(int n, const e3gnn_gemm_desc* d);
+int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,
+                       void* stream);
+
 /* Which engine serves the deployment: the channel family of the fused
  * radial-MLP + tensor-product kernels (>= 0: 0 SevenNet-0's 128x0e+64x1e+32x2e,
  * 1 uniform 64, 2 uniform 32 channels; lmax 2, even parity, XPLOR, linear

@@ -26,6 +26,8 @@ SIGNATURES = {
     'e3gnn_free': (None, [_vp]),
     'e3gnn_model_info': (_c_int, [_vp, _P(_c_int), _P(_c_f), _P(_c_int), _P(_c_int)]),
     'e3gnn_model_family': (_c_int, [_vp]),
+    'e3gnn_gemm_workspace_floats': (_c_i64, [_c_int, _vp]),
+    'e3gnn_gemm_grouped': (_c_int, [_c_int, _vp, _vp, _c_i64, _vp]),
     'e3gnn_ctx_create': (_vp, [_vp]),
     'e3gnn_ctx_free': (None, [_vp]),
     'e3gnn_energy_forces': (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -90,6 +92,16 @@ SIGNATURES = {
     'e3gnn_workspace_bytes': (_c_i64, [_vp]),
     'e3gnn_debug_ptr': (_vp, [_vp, _cp, _c_int, _P(_c_i64)]),
 }
+
+
+class GemmDesc(ctypes.Structure):
+    """e3gnn_gemm_desc (include/e3gnn.h)"""
+    _fields_ = [('a', _vp), ('b', _vp), ('a2', _vp), ('b2', _vp), ('c', _vp),
+                ('lda', _c_i64), ('ldb', _c_i64), ('lda2', _c_i64), ('ldb2', _c_i64),
+                ('ldc', _c_i64), ('m', ctypes.c_int32), ('n', ctypes.c_int32),
+                ('k', ctypes.c_int32), ('k2', ctypes.c_int32), ('trans_a', ctypes.c_int32),
+                ('trans_b', ctypes.c_int32), ('trans_a2', ctypes.c_int32),
+                ('trans_b2', ctypes.c_int32), ('alpha', ctypes.c_float), ('beta', ctypes.c_int32)]
 
 
 class E3GNNError(RuntimeError):

@@ -16,7 +16,7 @@ INCLUDE = os.path.join(os.path.dirname(HERE), 'include')
 LIB = os.path.join(HERE, 'libe3gnn_hip.so')
 OBJDIR = os.path.join(HERE, 'csrc', 'build')
 SOURCES = ['api.cpp', 'generic.cpp', 'gemm.hip', 'tp.hip', 'node.hip', 'fused.hip', 'neighbor.hip', 'd3.hip',
-           'train_ops.hip', 'gtp.hip', 'generic.hip', 'mlp_train.hip']
+           'train_ops.hip', 'gtp.hip', 'generic.hip', 'mlp_train.hip', 'tgemm.hip']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', f'-I{INCLUDE}',
          '-Wall', '-Wno-unused-function']

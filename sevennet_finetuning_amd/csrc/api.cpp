@@ -35,6 +35,7 @@
 #include "minijson.h"
 #include "node.h"
 #include "neighbor.h"
+#include "tgemm.h"
 #include "tp.h"
 
 using namespace e3gnn;
@@ -999,6 +1000,48 @@ int e3gnn_model_info(const e3gnn_model* m, int* num_species, float* cutoff, int*
       *comm_size = irreps_dim(m->irreps[1]);
     }
   }
+  return E3GNN_OK;
+}
+
+int64_t e3gnn_gemm_workspace_floats(int n, const e3gnn_gemm_desc* d) {
+  if (n < 0 || (n > 0 && !d)) return -1;
+  int64_t w = 0;
+  for (int i = 0; i < n; ++i) {
+    const int sp = tg_splits(d[i].m, d[i].n, (int64_t)d[i].k + d[i].k2);
+    if (sp > 1) w += (int64_t)sp * d[i].m * d[i].n;
+  }
+  return w;
+}
+
+int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,
+                       void* stream) {
+  if (n < 0 || n > TG_MAX_PROBS || (n > 0 && !d))
+    return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: 0..8 problems");
+  TgBatch b;
+  int64_t used = 0;
+  for (int i = 0; i < n; ++i) {
+    const e3gnn_gemm_desc& q = d[i];
+    if (q.m < 0 || q.n < 0 || q.k < 0 || q.k2 < 0 || (q.m > 0 && q.n > 0 && (!q.c || (q.k > 0 && (!q.a || !q.b)) ||
+                                                                        (q.k2 > 0 && (!q.a2 || !q.b2)))))
+      return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: bad problem " + std::to_string(i));
+    if (q.beta != 0 && q.beta != 1) return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: beta must be 0 or 1");
+    TgProb p{};
+    p.A1 = q.a; p.B1 = q.b; p.A2 = q.a2; p.B2 = q.b2; p.C = q.c;
+    p.lda1 = q.lda; p.ldb1 = q.ldb; p.lda2 = q.lda2; p.ldb2 = q.ldb2; p.ldc = q.ldc;
+    p.M = q.m; p.N = q.n; p.K1 = q.k; p.K2 = q.k2;
+    p.ta1 = q.trans_a; p.tb1 = q.trans_b; p.ta2 = q.trans_a2; p.tb2 = q.trans_b2;
+    p.alpha = q.alpha; p.beta = q.beta;
+    p.splits = tg_splits(q.m, q.n, (int64_t)q.k + q.k2);
+    if (p.splits > 1) {
+      const int64_t need = (int64_t)p.splits * q.m * q.n;
+      if (!workspace || used + need > workspace_floats)
+        return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: workspace too small (e3gnn_gemm_workspace_floats)");
+      p.ws = workspace + used;
+      used += need;
+    }
+    if (!tg_add(b, p)) return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: problem " + std::to_string(i));
+  }
+  HIPCHK(launch_tgemm(b, (hipStream_t)stream));
   return E3GNN_OK;
 }
 

@@ -1,0 +1,39 @@
+// Grouped f32 GEMM of the fine-tune step (tgemm.hip); C ABI e3gnn_gemm_grouped.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+namespace e3gnn {
+
+// C = beta C + alpha (op(A1) op(B1) + op(A2) op(B2)); op(X) = X^T when t* is set
+// (row-major storage, leading dimensions ld*); K2 = 0: no second pair
+struct TgProb {
+  const float *A1, *B1, *A2, *B2;
+  float* C;
+  float* ws;  // split-K partial slabs [splits][M][N] (splits > 1)
+  int64_t lda1, ldb1, lda2, ldb2, ldc;
+  int M, N, K1, K2;
+  int ta1, tb1, ta2, tb2;
+  float alpha;
+  int beta;
+  int splits;  // requested (tg_add settles it)
+  // set by tg_add
+  int va1, vb1, va2, vb2;
+  int tiles_n, tiles_mn, ksteps, tile_begin;
+  int64_t red_begin;
+};
+constexpr int TG_MAX_PROBS = 8;
+struct TgBatch {
+  TgProb p[TG_MAX_PROBS];
+  int nprob = 0;
+  int total_tiles = 0;
+  int64_t red_total = 0;
+};
+// split count the kernel would choose for an (M x N) output with K summed rows
+int tg_splits(int64_t M, int64_t N, int64_t K);
+bool tg_add(TgBatch& b, TgProb p);
+hipError_t launch_tgemm(const TgBatch& b, hipStream_t s);
+
+}  // namespace e3gnn

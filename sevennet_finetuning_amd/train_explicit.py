@@ -112,6 +112,86 @@ class _Prims:
         return _put(out0, g * d1 + gd * d2 * xd), _put(out1, gd * d1)
 
 
+class _Gemms:
+    """Dense products of the step, ``C = beta C + alpha (A B [+ A2 B2])``, on the
+    library's grouped matrix-core GEMM (e3gnn_gemm_grouped, csrc/tgemm.hip) for
+    float32 device tensors -- independent products queued with ``add`` go out as
+    ONE launch (plus one fixed-order split-K reduction) at ``flush`` -- and as
+    torch GEMMs otherwise (CPU tests, float64).  Operands are 2-D views; a
+    transposed view (``W.t()``) is passed as op(X) = X^T of its storage."""
+
+    def __init__(self, model):
+        self.lib = model._act_lib() if model.flat.is_cuda else None
+        self.q = []
+        self.ws = None
+
+    def _hip(self, *ts):
+        return self.lib is not None and all(t.is_cuda and t.dtype == torch.float32 for t in ts)
+
+    @staticmethod
+    def _op(x):
+        """(ptr, ld, trans) of a 2-D view (r x k): row-major storage X[r][ld]
+        (trans 0) or a transposed view of X[k][ld] (trans 1)"""
+        r, k = x.shape
+        s0, s1 = x.stride()
+        if s1 == 1 or k == 1:
+            return x.data_ptr(), (s0 if r > 1 else max(k, 1)), 0
+        if s0 == 1 or r == 1:
+            return x.data_ptr(), (s1 if k > 1 else max(r, 1)), 1
+        return None
+
+    def add(self, C, A, B, alpha=1.0, beta=0, A2=None, B2=None):
+        if not self._hip(C, A, B, *(t for t in (A2, B2) if t is not None)):
+            v = torch.mm(A, B)
+            if A2 is not None:
+                v = v + torch.mm(A2, B2)
+            if beta:
+                C.add_(v, alpha=alpha)
+            else:
+                torch.mul(v, alpha, out=C) if alpha != 1.0 else C.copy_(v)
+            return C
+        ops = [self._op(A), self._op(B)] + ([self._op(A2), self._op(B2)] if A2 is not None else [])
+        if any(o is None for o in ops) or C.stride(1) != 1:
+            A, B = A.contiguous(), B.contiguous()
+            A2 = A2.contiguous() if A2 is not None else None
+            B2 = B2.contiguous() if B2 is not None else None
+            ops = [self._op(A), self._op(B)] + ([self._op(A2), self._op(B2)] if A2 is not None else [])
+            if C.stride(1) != 1:
+                raise ValueError('GEMM output must be row-major')
+        if len(self.q) == 8:
+            self.flush()
+        self.q.append((C, A, B, A2, B2, ops, float(alpha), int(bool(beta))))
+        return C
+
+    def flush(self):
+        if not self.q:
+            return
+        from . import _lib
+        n = len(self.q)
+        descs = (_lib.GemmDesc * n)()
+        keep = []
+        for i, (C, A, B, A2, B2, ops, alpha, beta) in enumerate(self.q):
+            d = descs[i]
+            d.a, d.lda, d.trans_a = ops[0]
+            d.b, d.ldb, d.trans_b = ops[1]
+            if A2 is not None:
+                d.a2, d.lda2, d.trans_a2 = ops[2]
+                d.b2, d.ldb2, d.trans_b2 = ops[3]
+                d.k2 = int(A2.shape[1])
+            d.c, d.ldc = C.data_ptr(), C.stride(0)
+            d.m, d.n, d.k = int(C.shape[0]), int(C.shape[1]), int(A.shape[1])
+            d.alpha, d.beta = alpha, beta
+            keep.append((C, A, B, A2, B2))
+        need = int(self.lib.e3gnn_gemm_workspace_floats(n, descs))
+        dev = self.q[0][0].device
+        if need > 0 and (self.ws is None or self.ws.numel() < need):
+            self.ws = torch.empty(max(need, 1 << 20), device=dev)
+        ws = self.ws.data_ptr() if self.ws is not None else None
+        _lib.check(self.lib.e3gnn_gemm_grouped(n, descs, ws, self.ws.numel() if self.ws is not None else 0,
+                                               torch.cuda.current_stream(dev).cuda_stream))
+        self.q = []
+
+
 def _put(out, v):
     if out is None:
         return v
@@ -539,6 +619,7 @@ class ExplicitStep:
             raise ValueError('the explicit fine-tune derivatives cover SevenNet-0\'s architecture only')
         self.m = model
         self.p = _Prims(model)
+        self.gm = _Gemms(model)
         self.geo = _Geometry(model, self.p)
         self.gates = [_Gate(b['gate'], self.p) for b in model.blocks]
         ent = []
@@ -571,6 +652,7 @@ class ExplicitStep:
             if pos < lin.in_off[-1]:
                 gaps.append((pos, lin.in_off[-1]))
             self.si2_blocks.append((bl, gaps))
+        self.dense_si2 = dense_si2
         # frozen convolution denominators (the default) are folded into si2:
         # agg / den W = agg (W / den), and the si2 gradient divided by den in
         # the flush -- no division launches on the activations
@@ -607,6 +689,12 @@ class ExplicitStep:
     def _P(self, name):
         return self.m.param(name)
 
+    def _mm(self, C, A, B, alpha=1.0, beta=0, A2=None, B2=None):
+        """one product now (its result is needed next)"""
+        self.gm.add(C, A, B, alpha, beta, A2, B2)
+        self.gm.flush()
+        return C
+
     # ---- si2 products over its instruction blocks (views, no copies)
     def _si2_fwd(self, t, A, Dm, out):
         """out += A Dm (the gate-input rows)"""
@@ -615,6 +703,9 @@ class ExplicitStep:
 
     def _si2_t(self, t, A, Dm):
         """A Dm^T (cotangent rows of the mid irreps)"""
+        if self.dense_si2:
+            return self._mm(torch.empty(A.shape[0], Dm.shape[0], device=A.device, dtype=A.dtype),
+                            A, Dm.t())
         bl, gaps = self.si2_blocks[t]
         out = torch.empty(A.shape[0], Dm.shape[0], device=A.device, dtype=A.dtype)
         seen = set()
@@ -755,7 +846,7 @@ class ExplicitStep:
             W0, W1, W2 = MW[t]
             x = X[:n]
             H = new(2 * n, D[f'si1{t}'].shape[1])
-            torch.mm(x, D[f'si1{t}'], out=H[:n])
+            self._mm(H[:n], x, D[f'si1{t}'])
             A1, H1 = new(2 * E, W0.shape[1]), new(2 * E, W0.shape[1])
             A2, H2 = new(2 * E, W1.shape[1]), new(2 * E, W1.shape[1])
             WT = new(2 * E, W2.shape[1])
@@ -766,8 +857,11 @@ class ExplicitStep:
             if not self.fold_den:            # (folded: D[si2] is si2 / den)
                 AGG[:n].div_(den)
             Yg = new(2 * n, D[f'si2{t}'].shape[1])
-            torch.mm(x, D[f'sc{t}'], out=Yg[:n])          # (GEMM into the output, then
-            self._si2_fwd(t, AGG[:n], D[f'si2{t}'], Yg[:n])  # accumulate: no bias copy)
+            if self.dense_si2:                              # x sc + agg si2: one product
+                self._mm(Yg[:n], x, D[f'sc{t}'], A2=AGG[:n], B2=D[f'si2{t}'])
+            else:
+                self._mm(Yg[:n], x, D[f'sc{t}'])            # (GEMM into the output, then
+                self._si2_fwd(t, AGG[:n], D[f'si2{t}'], Yg[:n])  # accumulate: no bias copy)
             Xn = new(2 * n, self.gates[t].dims[3] if self.gates[t].ng else Yg.shape[1])
             self.gates[t].fwd(Yg[:n], out=Xn[:n])
             blocks.append({'X': X, 'H': H, 'A1': A1, 'H1': H1, 'A2': A2, 'H2': H2, 'WT': WT,
@@ -775,15 +869,16 @@ class ExplicitStep:
             X = Xn
         S['blocks'] = blocks
         S['XL'] = X
-        hid = X[:n] @ D['r1']
-        e = (hid @ D['r2'])[:, 0]
+        hid = self._mm(new(n, D['r1'].shape[1]), X[:n], D['r1'])
+        e = self._mm(new(n, 1), hid, D['r2'])[:, 0]
         scale = P('rescale_atomic_energy.scale')[types]
         atomic = e * scale + P('rescale_atomic_energy.shift')[types]
         S.update(hid=hid, e=e, scale=scale)
         energy = torch.zeros(nb, device=dev, dtype=atomic.dtype).index_add(0, batch, atomic)
 
         # ---- first reverse: dE/dr per edge (seed dE/d atomic = 1)
-        xb = (scale.unsqueeze(-1) * D['r2'][:, 0].unsqueeze(0)) @ D['r1'].t()
+        xb = self._mm(new(n, D['r1'].shape[0]), scale.unsqueeze(-1) * D['r2'][:, 0].unsqueeze(0),
+                      D['r1'].t())
         Yb = torch.empty_like(g['Y'])         # the last block's launch assigns, the others add
         embb = torch.zeros_like(g['emb'])
         for t in range(len(blocks) - 1, -1, -1):
@@ -797,7 +892,7 @@ class ExplicitStep:
                                     acc=ACC_DY if t < len(blocks) - 1 else 0)
             self._mlp_rev(wb, b['W'], b['A1'][:E], b['A2'][:E], embb)
             if t > 0:
-                xb = (hb @ D[f'si1{t}'].t()).addmm_(yb, D[f'sc{t}'].t())
+                xb = self._mm(new(n, hb.shape[1]), hb, D[f'si1{t}'].t(), A2=yb, B2=D[f'sc{t}'].t())
         fij = self.geo.vjp(g, Yb, embb)                    # dE/dr_e, centre-sorted order
         S['fij'] = fij
         aux = graph.aux
@@ -854,7 +949,7 @@ class ExplicitStep:
             aggd = AGG[n:]                       # C(h, Y', w) + C(h, Y, w') + C(h', Y, w)
             X = b['X']
             if t > 0:
-                torch.mm(X[n:], D[f'si1{t}'], out=b['H'][n:])
+                self._mm(b['H'][n:], X[n:], D[f'si1{t}'])
             hd = b['H'][n:] if t > 0 else None   # x0' = 0: no h' term
             if fused:
                 be.tangent_forward(k, graph, h, hd, Y, Yd, w, WT[E:], out=aggd)
@@ -865,16 +960,22 @@ class ExplicitStep:
                     be.forward(k, graph, hd, Y, w, out=aggd, acc=True)
             if not self.fold_den:
                 aggd.div_(b['den'])
-            if t > 0:
-                torch.mm(X[n:], D[f'sc{t}'], out=Yg[n:])
+            if self.dense_si2:
+                if t > 0:
+                    self._mm(Yg[n:], X[n:], D[f'sc{t}'], A2=AGG[n:], B2=D[f'si2{t}'])
+                else:                            # x0' = 0
+                    self._mm(Yg[n:], AGG[n:], D[f'si2{t}'])
             else:
-                Yg[n:].zero_()
-            self._si2_fwd(t, AGG[n:], D[f'si2{t}'], Yg[n:])
+                if t > 0:
+                    self._mm(Yg[n:], X[n:], D[f'sc{t}'])
+                else:
+                    Yg[n:].zero_()
+                self._si2_fwd(t, AGG[n:], D[f'si2{t}'], Yg[n:])
             Xn = blocks[t + 1]['X'] if t + 1 < len(blocks) else S['XL']
             self.gates[t].jvp(Yg[:n], Yg[n:], out=Xn[n:])
         XL = S['XL']
-        hidd = XL[n:] @ D['r1']
-        ed = (hidd @ D['r2'])[:, 0]
+        hidd = self._mm(torch.empty(n, D['r1'].shape[1], device=dev, dtype=dt), XL[n:], D['r1'])
+        ed = self._mm(torch.empty(n, 1, device=dev, dtype=dt), hidd, D['r2'])[:, 0]
 
         # ---- one reverse sweep over (primal, tangent); seeds cE on E, 1 on E'
         G = self.bank.grads()
@@ -889,10 +990,12 @@ class ExplicitStep:
         # [e-bar; e'-bar] = [cE scale; scale]
         EB = torch.cat([atb * scale, scale]).unsqueeze(-1)
         HID = torch.cat([S['hid'], hidd])
-        G['r2'].addmm_(HID.t(), EB)
         HIDB = EB * D['r2'][:, 0].unsqueeze(0)
-        G['r1'].addmm_(XL.t(), HIDB)
-        XB = HIDB @ D['r1'].t()               # [x-bar; x'-bar] of the last block's output
+        XB = torch.empty(2 * n, D['r1'].shape[0], device=dev, dtype=dt)
+        self.gm.add(G['r2'], HID.t(), EB, beta=1)
+        self.gm.add(G['r1'], XL.t(), HIDB, beta=1)
+        self.gm.add(XB, HIDB, D['r1'].t())    # [x-bar; x'-bar] of the last block's output
+        self.gm.flush()
         EMBB = torch.zeros(2 * E, 8, device=dev, dtype=dt)
         new = lambda *shape: torch.empty(*shape, device=dev, dtype=dt)   # noqa: E731
         dYs = new(E, 9)                       # scratch for the unused dY outputs
@@ -903,8 +1006,18 @@ class ExplicitStep:
             Yg, AGG, X, H = b['Y'], b['AGG'], b['X'], b['H']
             YB = new(2 * n, Yg.shape[1])
             self.gates[t].dual_vjp(Yg[:n], Yg[n:], XB[:n], XB[n:], out0=YB[:n], out1=YB[n:])
-            self._si2_wgrad(t, G[f'si2{t}'], AGG, YB)
-            AGGB = self._si2_t(t, YB, D[f'si2{t}'])
+            if self.dense_si2:
+                # independent products of y-bar, one launch: si2's and sc's weight
+                # gradients and agg-bar
+                AGGB = new(2 * n, D[f'si2{t}'].shape[0])
+                self.gm.add(G[f'si2{t}'], AGG.t(), YB, beta=1)
+                self.gm.add(AGGB, YB, D[f'si2{t}'].t())
+                self.gm.add(G[f'sc{t}'], X.t(), YB, beta=1)
+                self.gm.flush()
+            else:
+                self._si2_wgrad(t, G[f'si2{t}'], AGG, YB)
+                AGGB = self._si2_t(t, YB, D[f'si2{t}'])
+                self._mm(G[f'sc{t}'], X.t(), YB, beta=1)
             gden = self._G(f'{pre}.denominator')
             if gden is not None:
                 gden.sub_(torch.dot(AGGB.view(-1), AGG.view(-1)) / b['den'])
@@ -934,21 +1047,19 @@ class ExplicitStep:
                 HB[n:].zero_()                # x0' = 0: no h' (its rows meet zero rows of X)
             # radial MLP, primal and tangent rows together
             W0, W1, W2 = b['W']
-            gw2 = self._G(f'{pre}.weight_nn.layer2.weight')
-            if gw2 is not None:
-                _wgrad(gw2, b['H2'], WB, 1.0 / math.sqrt(W2.shape[0]))
             A2B, A1B = new(2 * E, W1.shape[1]), new(2 * E, W0.shape[1])
             self._mlp_dual(WB, b['W'], b['A1'], b['A2'], A2B, A1B, EMBB)
-            gw1 = self._G(f'{pre}.weight_nn.layer1.weight')
-            if gw1 is not None:
-                _wgrad(gw1, b['H1'], A2B, 1.0 / math.sqrt(W1.shape[0]))
-            gw0 = self._G(f'{pre}.weight_nn.layer0.weight')
-            if gw0 is not None:
-                _wgrad(gw0, EMB, A1B, 1.0 / math.sqrt(W0.shape[0]))
-            # self-interaction 1 and self-connection (sc-bar = y-bar)
-            G[f'si1{t}'].addmm_(X.t(), HB)
-            G[f'sc{t}'].addmm_(X.t(), YB)
-            XB = (HB @ D[f'si1{t}'].t()).addmm_(YB, D[f'sc{t}'].t())
+            # the block's remaining products are independent: one launch (+ the
+            # split-K reduction of the edge-summed weight gradients, K = 2E)
+            for li, (rows, cot, Wl) in enumerate(((EMB, A1B, W0), (b['H1'], A2B, W1), (b['H2'], WB, W2))):
+                gw = self._G(f'{pre}.weight_nn.layer{li}.weight')
+                if gw is not None:
+                    self.gm.add(gw, rows.t(), cot, 1.0 / math.sqrt(Wl.shape[0]), beta=1)
+            # self-interaction 1 (sc-bar = y-bar, added above) and the input cotangent
+            self.gm.add(G[f'si1{t}'], X.t(), HB, beta=1)
+            XB = new(2 * n, D[f'si1{t}'].shape[0])
+            self.gm.add(XB, HB, D[f'si1{t}'].t(), A2=YB, B2=D[f'sc{t}'].t())
+            self.gm.flush()
         # embedding (x0 = W[types] / sqrt(nsp)) and the radial basis coefficients
         gemb = self._G('onehot_to_feature_x.linear.weight')
         if gemb is not None:
