@@ -107,6 +107,23 @@ int64_t e3gnn_gemm_workspace_floats(int n, const e3gnn_gemm_desc* d);
 int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,
                        void* stream);
 
+/* The fine-tune loss of the hand-scheduled step in one launch (train.py
+ * LossDefinition, loss.py:8-206): criterion 0 MSELoss, 1 HuberLoss(delta), mean
+ * over the labelled (non-NaN) entries of each term -- energy per atom
+ * (e_pred / natoms, nb graphs), forces (n x 3), stress (nb x 6, times s_scale =
+ * eV/A^3 -> kbar; s_pred null: no stress term) -- weighted by w_*.  Writes the
+ * weighted term values terms[3] and the cotangents dL/dE[nb], dL/dF[n*3],
+ * dL/dS[nb*6].  Deterministic fixed-order sums. */
+int e3gnn_loss_efs(int criterion, float delta, int64_t nb, int64_t n, const float* e_pred,
+                   const float* e_ref, const int64_t* natoms, const float* f_pred, const float* f_ref,
+                   const float* s_pred, const float* s_ref, float w_e, float w_f, float w_s,
+                   float s_scale, float* terms, float* ce, float* cf, float* cs, void* stream);
+/* EWC over the flat parameter buffer (loss.py:209-252): value[0] = sum f (theta
+ * - o)^2 (fixed-order sum; `part`: n + n / 256 + 1 floats of scratch), grad += lam f_train
+ * (theta - o) (grad nullable). */
+int e3gnn_ewc_flat(int64_t n, const float* theta, const float* f, const float* o, const float* f_train,
+                   float lam, float* grad, float* part, float* value, void* stream);
+
 /* Which engine serves the deployment: the channel family of the fused
  * radial-MLP + tensor-product kernels (>= 0: 0 SevenNet-0's 128x0e+64x1e+32x2e,
  * 1 uniform 64, 2 uniform 32 channels; lmax 2, even parity, XPLOR, linear

@@ -28,6 +28,9 @@ SIGNATURES = {
     'e3gnn_model_family': (_c_int, [_vp]),
     'e3gnn_gemm_workspace_floats': (_c_i64, [_c_int, _vp]),
     'e3gnn_gemm_grouped': (_c_int, [_c_int, _vp, _vp, _c_i64, _vp]),
+    'e3gnn_loss_efs': (_c_int, [_c_int, _c_f, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                _c_f, _c_f, _c_f, _c_f, _vp, _vp, _vp, _vp, _vp]),
+    'e3gnn_ewc_flat': (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _c_f, _vp, _vp, _vp, _vp]),
     'e3gnn_ctx_create': (_vp, [_vp]),
     'e3gnn_ctx_free': (None, [_vp]),
     'e3gnn_energy_forces': (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -1045,6 +1045,31 @@ int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_
   return E3GNN_OK;
 }
 
+int e3gnn_loss_efs(int criterion, float delta, int64_t nb, int64_t n, const float* e_pred,
+                   const float* e_ref, const int64_t* natoms, const float* f_pred, const float* f_ref,
+                   const float* s_pred, const float* s_ref, float w_e, float w_f, float w_s,
+                   float s_scale, float* terms, float* ce, float* cf, float* cs, void* stream) {
+  if (criterion != 0 && criterion != 1) return fail(E3GNN_ERR_ARG, "loss criterion must be 0 (mse) or 1 (huber)");
+  if (nb < 0 || n < 0 || !terms || (nb > 0 && (!e_pred || !e_ref || !natoms || !ce)) ||
+      (n > 0 && (!f_pred || !f_ref || !cf)) || (s_pred && (!s_ref || !cs)))
+    return fail(E3GNN_ERR_ARG, "null loss operand");
+  LossArgs a{criterion, delta, nb, n, e_pred, e_ref, natoms, f_pred, f_ref, s_pred, s_ref,
+             w_e, w_f, w_s, s_scale, terms, ce, cf, cs};
+  HIPCHK(launch_loss_efs(a, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
+int e3gnn_ewc_flat(int64_t n, const float* theta, const float* f, const float* o, const float* f_train,
+                   float lam, float* grad, float* part, float* value, void* stream) {
+  if (n < 0 || (n > 0 && (!theta || !f || !o || !part || (grad && !f_train))) || !value)
+    return fail(E3GNN_ERR_ARG, "null EWC operand");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(launch_ewc_flat(n, theta, f, o, f_train, lam, grad, part, s));
+  // fixed-order block sums into part[n ...], then their sum (node.hip launch_sum)
+  HIPCHK(launch_sum(n, part, part + n, value, s));
+  return E3GNN_OK;
+}
+
 int e3gnn_model_family(const e3gnn_model* m) {
   if (!m) return fail(E3GNN_ERR_ARG, "null model"), -1;
   return m->gen ? -1 : m->family;

@@ -31,4 +31,19 @@ hipError_t launch_mlp_bwd(int E, int W, const float* WB, const float* W0, const 
                           const float* W2, const float* A1, const float* A2, const float* A1d,
                           const float* A2d, float* A2B, float* A1B, float* EB, float c,
                           hipStream_t s);
+// the explicit step's loss (MSE / Huber, mean over labelled entries) and its
+// cotangents: terms[0..2] = weighted energy-per-atom / force / stress terms
+struct LossArgs {
+  int criterion;  // 0 MSELoss, 1 HuberLoss(delta)
+  float delta;
+  int64_t nb, n;
+  const float *e_pred, *e_ref;
+  const int64_t* natoms;
+  const float *f_pred, *f_ref, *s_pred, *s_ref;  // s_* null: no stress term
+  float w_e, w_f, w_s, s_scale;
+  float *terms, *ce, *cf, *cs;
+};
+hipError_t launch_loss_efs(const LossArgs& a, hipStream_t s);
+hipError_t launch_ewc_flat(int64_t n, const float* th, const float* f, const float* o, const float* ft,
+                           float lam, float* grad, float* part, hipStream_t s);
 }  // namespace e3gnn

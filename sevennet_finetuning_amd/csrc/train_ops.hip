@@ -315,3 +315,113 @@ hipError_t launch_gate(int op, int64_t n, const int* dims, const float* y, const
 }
 
 }  // namespace e3gnn
+
+// ------------------------------------------------------------------ loss
+// The explicit fine-tune step's loss (train.py LossDefinition: loss.py:8-206)
+// and its cotangents in one launch: block 0 the per-atom energy term, block 1
+// the force term, block 2 the stress term (kbar); criterion 0 MSELoss, 1
+// HuberLoss(delta), mean over the labelled entries (NaN labels excluded, the
+// reference's delete_unlabled); every sum a fixed-order tree (deterministic).
+namespace e3gnn {
+namespace {
+
+__device__ __forceinline__ float crit(int c, float delta, float x, float* g) {
+  if (c == 0) {
+    *g = 2.f * x;
+    return x * x;
+  }
+  const float a = fabsf(x);
+  if (a < delta) {
+    *g = x;
+    return 0.5f * x * x;
+  }
+  *g = x > 0.f ? delta : -delta;
+  return delta * (a - 0.5f * delta);
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) red[t] += red[t + s];
+    __syncthreads();
+  }
+  const float r = red[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_loss_efs(LossArgs a) {
+  __shared__ float red[256];
+  const int term = blockIdx.x;
+  const int64_t cnt_all = term == 0 ? a.nb : (term == 1 ? 3LL * a.n : 6LL * a.nb);
+  const float* pred = term == 0 ? a.e_pred : (term == 1 ? a.f_pred : a.s_pred);
+  const float* ref = term == 0 ? a.e_ref : (term == 1 ? a.f_ref : a.s_ref);
+  float* cot = term == 0 ? a.ce : (term == 1 ? a.cf : a.cs);
+  const float w = term == 0 ? a.w_e : (term == 1 ? a.w_f : a.w_s);
+  if (!pred) {   // no stress term
+    if (threadIdx.x == 0) a.terms[term] = 0.f;
+    return;
+  }
+  auto x_of = [&](int64_t i, bool* ok) {
+    const float r = ref[i];
+    *ok = !(r != r);
+    float x = pred[i] - (*ok ? r : 0.f);
+    if (term == 0) x /= (float)a.natoms[i];
+    if (term == 2) x *= a.s_scale;
+    return x;
+  };
+  float s = 0.f, c = 0.f;
+  for (int64_t i = threadIdx.x; i < cnt_all; i += 256) {
+    bool ok;
+    const float x = x_of(i, &ok);
+    float g;
+    if (ok) {
+      s += crit(a.criterion, a.delta, x, &g);
+      c += 1.f;
+    }
+  }
+  const float sum = block_sum(s, red), cnt = block_sum(c, red);
+  const float inv = cnt > 0.f ? w / cnt : 0.f;
+  if (threadIdx.x == 0) a.terms[term] = sum * inv;
+  for (int64_t i = threadIdx.x; i < cnt_all; i += 256) {
+    bool ok;
+    const float x = x_of(i, &ok);
+    float g = 0.f;
+    if (ok) crit(a.criterion, a.delta, x, &g);
+    float v = ok ? g * inv : 0.f;
+    if (term == 0) v /= (float)a.natoms[i];
+    if (term == 2) v *= a.s_scale;
+    cot[i] = v;
+  }
+}
+
+// EWC over the flat parameters (train.py _FlatEWC, loss.py:209-252):
+// part[i] = f (theta - o)^2 (summed by launch_sum), grad[i] += lam f_train (theta - o)
+__global__ void k_ewc_flat(int64_t n, const float* __restrict__ th, const float* __restrict__ f,
+                           const float* __restrict__ o, const float* __restrict__ ft, float lam,
+                           float* __restrict__ grad, float* __restrict__ part) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float d = th[i] - o[i];
+  part[i] = f[i] * d * d;
+  if (grad) grad[i] += lam * ft[i] * d;
+}
+
+}  // namespace
+
+hipError_t launch_loss_efs(const LossArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_loss_efs, dim3(3), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ewc_flat(int64_t n, const float* th, const float* f, const float* o, const float* ft,
+                           float lam, float* grad, float* part, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ewc_flat, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, th, f, o, ft, lam,
+                     grad, part);
+  return hipGetLastError();
+}
+
+}  // namespace e3gnn

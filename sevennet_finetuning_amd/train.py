@@ -496,6 +496,7 @@ class Trainer:
                 self.explicit = train_explicit.ExplicitStep(self.model)
         self._graphed = GraphedRehearsalStep(self, config.get('hip_graph_max', 16)) \
             if self.hip_graph else None
+        self._fused_loss = self._fused_loss_plan() if self.explicit is not None else None
 
     # ---- the pieces of one step
     def zero_grad(self):
@@ -522,6 +523,9 @@ class Trainer:
             output = self.model(batch, graph=graph)
             loss = self.total_loss(output)
             loss.backward()
+        elif self._fused_loss is not None:
+            output = self.explicit.forward(batch, graph)
+            loss = self._fused_loss_backward(output, batch)
         else:
             output = self.explicit.forward(batch, graph)
             loss = self.total_loss(output)
@@ -532,6 +536,82 @@ class Trainer:
         if reduce and self.distributed:
             self.all_reduce_grad()
         return loss, output
+
+    def _fused_loss_plan(self):
+        """The loss terms the library computes in one launch with their
+        cotangents (e3gnn_loss_efs: MSE / Huber, mean over labelled entries of
+        the energy-per-atom, force and stress terms) and the flat EWC term
+        (e3gnn_ewc_flat), or None when the configuration needs autograd
+        (weighted data, another criterion, non-standard keys, CPU / float64)."""
+        if self.device.type != 'cuda' or self.model.dtype != torch.float32:
+            return None
+        plan = {'w': [0.0, 0.0, 0.0], 'stress': False, 'ewc': None, 'crit': None}
+        std = {PerAtomEnergyLoss: (0, KEY.PRED_TOTAL_ENERGY, KEY.ENERGY),
+               ForceLoss: (1, KEY.PRED_FORCE, KEY.FORCE),
+               StressLoss: (2, KEY.PRED_STRESS, KEY.STRESS)}
+        for f, w in self.loss_functions:
+            if isinstance(f, EWCLoss):
+                if plan['ewc'] is not None:
+                    return None
+                plan['ewc'] = (f, float(w))
+                continue
+            if type(f) not in std or f.use_weight or not f.delete_unlabeled:
+                return None
+            term, pk, rk = std[type(f)]
+            if (f.pred_key, f.ref_key) != (pk, rk) or plan['w'][term]:
+                return None
+            c = f.criterion
+            if isinstance(c, torch.nn.HuberLoss) and c.reduction == 'mean':
+                crit = (1, float(c.delta))
+            elif isinstance(c, torch.nn.MSELoss) and c.reduction == 'mean':
+                crit = (0, 0.0)
+            else:
+                return None
+            if plan['crit'] not in (None, crit):
+                return None
+            plan['crit'] = crit
+            plan['w'][term] = float(w)
+            plan['stress'] |= term == 2
+        if plan['crit'] is None or not plan['w'][0] or not plan['w'][1]:
+            return None
+        from . import _lib
+        plan['lib'] = _lib.load()
+        plan['terms'] = torch.zeros(3, device=self.device)
+        plan['ewc_val'] = torch.zeros(1, device=self.device)
+        n = self.model.flat.numel()
+        plan['part'] = torch.empty(n + n // 256 + 2, device=self.device)
+        return plan
+
+    def _fused_loss_backward(self, output, batch):
+        """loss + cotangents in one launch (+ EWC value and its gradient into
+        the flat gradient buffer), then the explicit step's reverse sweep"""
+        from . import _lib
+        P, lib = self._fused_loss, self._fused_loss['lib']
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        E, F = output[KEY.PRED_TOTAL_ENERGY].detach(), output[KEY.PRED_FORCE].detach()
+        S = output.get(KEY.PRED_STRESS) if P['stress'] else None
+        S = S.detach().contiguous() if S is not None else None
+        nb, n = int(E.numel()), int(F.shape[0])
+        ref = lambda k, like: batch[k].to(like.device, like.dtype).contiguous()   # noqa: E731
+        cE, cF = torch.empty_like(E), torch.empty_like(F)
+        cS = torch.empty_like(S) if S is not None else None
+        natoms = batch[KEY.NUM_ATOMS].to(E.device, torch.long).contiguous()
+        p = lambda t: t.data_ptr() if t is not None else None   # noqa: E731
+        _lib.check(lib.e3gnn_loss_efs(
+            P['crit'][0], P['crit'][1], nb, n, p(E), p(ref(KEY.ENERGY, E)), p(natoms), p(F),
+            p(ref(KEY.FORCE, F)), p(S), p(ref(KEY.STRESS, S)) if S is not None else None,
+            P['w'][0], P['w'][1], P['w'][2], StressLoss.TO_KB, p(P['terms']), p(cE), p(cF),
+            p(cS), st))
+        loss = P['terms'].sum().view(1)
+        if P['ewc'] is not None:
+            f_def, w = P['ewc']
+            f, o, f_train = f_def._flat_terms(self.model)
+            m = self.model
+            _lib.check(lib.e3gnn_ewc_flat(m.flat.numel(), p(m.flat), p(f), p(o), p(f_train),
+                                          2.0 * w, p(m.flat_grad), p(P['part']), p(P['ewc_val']), st))
+            loss = loss + w * P['ewc_val']
+        self.explicit.backward(cE, cF, cS)
+        return loss
 
     def all_reduce_grad(self):
         """DDP's gradient average (one all-reduce of the flat gradient buffer)."""
