@@ -1142,6 +1142,12 @@ template <class L>
 struct BwdWpg {
   static constexpr int v = L::KIND == 1 ? E3GNN_BWD_WPG : 4;
 };
+#ifndef E3GNN_ABL_NOBAR
+#define E3GNN_ABL_NOBAR 0
+#endif
+#ifndef E3GNN_ABL_NOSTAGE
+#define E3GNN_ABL_NOSTAGE 0
+#endif
 template <class L>
 __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_eu(BwdLsWaves<L>::v, BwdLsWaves<L>::v))) void k_conv_bwd_ls(
     const int* __restrict__ row_ptr, const int* __restrict__ nbr, const float* __restrict__ emb,
@@ -1172,6 +1178,9 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
   const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
   f32x4 st[NST];
   auto issue = [&](int P) {
+#if E3GNN_ABL_NOSTAGE
+    return;
+#endif
     if constexpr (NWP % NT == 0) {  // (4 waves: each thread's pieces all W, then all D)
       constexpr int NW = NWP / NT;
 #pragma unroll
@@ -1187,11 +1196,18 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
       }
     }
   };
+  // E3GNN_ABL_*: timing-only ablations (results wrong; never the shipped build)
   auto commit = [&]() {
+#if !E3GNN_ABL_NOBAR
     __syncthreads();
+#endif
+#if !E3GNN_ABL_NOSTAGE
 #pragma unroll
     for (int i = 0; i < NST; ++i) *reinterpret_cast<f32x4*>(img + (tid + NT * i) * 16) = st[i];
+#endif
+#if !E3GNN_ABL_NOBAR
     __syncthreads();
+#endif
   };
   constexpr bool STAMPED = std::is_same<L, LayerMid>::value;   // SevenNet-0's
   STAMP_DECL

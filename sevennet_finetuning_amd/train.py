@@ -496,7 +496,9 @@ class Trainer:
                 self.explicit = train_explicit.ExplicitStep(self.model)
         self._graphed = GraphedRehearsalStep(self, config.get('hip_graph_max', 16)) \
             if self.hip_graph else None
-        self._fused_loss = self._fused_loss_plan() if self.explicit is not None else None
+        # E3GNN_TRAIN_FUSED_LOSS=0: the loss by autograd over its torch expression (A/B)
+        self._fused_loss = self._fused_loss_plan() if (
+            self.explicit is not None and os.environ.get('E3GNN_TRAIN_FUSED_LOSS', '1') != '0') else None
 
     # ---- the pieces of one step
     def zero_grad(self):

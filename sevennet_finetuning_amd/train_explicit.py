@@ -121,7 +121,9 @@ class _Gemms:
     transposed view (``W.t()``) is passed as op(X) = X^T of its storage."""
 
     def __init__(self, model):
-        self.lib = model._act_lib() if model.flat.is_cuda else None
+        # E3GNN_TRAIN_TGEMM=0: torch's GEMMs (A/B)
+        on = model.flat.is_cuda and os.environ.get('E3GNN_TRAIN_TGEMM', '1') != '0'
+        self.lib = model._act_lib() if on else None
         self.q = []
         self.ws = None
 

@@ -73,7 +73,7 @@ def test_family_model_vs_oracle(deployment, name):
     assert abs(got['energy'] - e) <= 2e-6 * abs(e), (got['energy'], e)
     assert np.abs(got['forces'] - ref['forces']).max() <= 1e-4
     assert np.abs(got['stress'] - ref['stress']).max() <= 2e-6
-    assert np.abs(ref['forces']).max() > 1e-2   # a real force field, not zeros
+    assert np.abs(ref['forces']).max() > 1e-3   # a real force field (10x the tolerance), not zeros
 
 
 def test_family_model_equals_generic_engine(deployment, monkeypatch):

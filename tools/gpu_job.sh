@@ -82,6 +82,10 @@ for s in "$@"; do
     paritydef) step paritydef 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
     stamps_*) v=${s#stamps_}; step stamps_$v 300 python tools/stamps.py sevennet_finetuning_amd/variants/$v.so ;;
     reportv_*) v=${s#reportv_}; step report_$v 300 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python tools/parity_report.py ;;
+    benchtrain_notg) step benchtrain_notg 300 env E3GNN_TRAIN_TGEMM=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    benchtrain_nofl) step benchtrain_nofl 300 env E3GNN_TRAIN_FUSED_LOSS=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    benchtrain_none) step benchtrain_none 300 env E3GNN_TRAIN_FUSED_LOSS=0 E3GNN_TRAIN_TGEMM=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    proftrain2) step proftrain2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train2 -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
