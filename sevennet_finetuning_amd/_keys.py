@@ -31,3 +31,7 @@ SELF_CONNECTION_TEMP = 'self_cont_tmp'
 INFO = 'data_info'
 # this build: dE/dedge_vec per edge (ForceStressOutputFromEdge's intermediate)
 EDGE_GRAD = 'edge_grad'
+# this build: 0-dim bool tensor set by train.collate when edge_index is sorted
+# by centre (stable, on the host); the captured fine-tune step then skips its
+# device sort
+EDGE_SORTED = 'edge_index_centre_sorted'

@@ -132,10 +132,17 @@ struct Linear {
 // same block; `W` holds [K1 + K2 x N] per block (16-byte aligned).
 struct PairBlock {
   int l, N, out_off, K1, off1, K2, off2, w_off;
+  int64_t wb_off;  // byte offset of the block's bf16 pieces in LinPair::Wb
 };
 struct LinPair {
   std::vector<PairBlock> blocks;
   DBuf W;
+  // W as three bf16 pieces (W = p0 + p1 + p2 exactly) in the 16x16x32 MFMA
+  // B-operand order of k_nodelin_b (gemm.hip): per block [16-column block cb]
+  // [32-row chunk kc (K1's chunks, then K2's)][piece][lane][8], element t of
+  // lane l = W[k][16 cb + l % 16] with k = 32 kc' + 8 (l / 16) + t inside its
+  // part (0 past the part's rows / the block's columns)
+  DBuf Wb;
   bool ok = false;
 };
 
@@ -421,6 +428,7 @@ bool nl_batch(NlBatch& b, LinPair& P, const float* A, int64_t lda, const float* 
     q.K1 = k.K1;
     q.K = k.K1 + k.K2;
     q.B = P.W.f() + k.w_off;
+    q.Bb = P.Wb.p ? static_cast<const char*>(P.Wb.p) + k.wb_off : nullptr;
     q.C = C;
     q.ldc = ldc;
     q.c_off = k.out_off;
@@ -509,6 +517,33 @@ int build_pair(LinPair& P, const Linear& a, bool ta, const Linear* b, bool tb) {
   }
   if (b && matched != b->blocks.size()) return 0;
   if (upload(P.W, W) != hipSuccess) return -2;
+  // the bf16x6 operand image (k_nodelin_b)
+  std::vector<float> Wb;   // bf16 pairs packed in floats (1 KB per piece image)
+  for (auto& pb : P.blocks) {
+    pb.wb_off = (int64_t)Wb.size() * 4;
+    const int ncb = (pb.N + 15) / 16, nk1 = (pb.K1 + 31) / 32, nk2 = (pb.K2 + 31) / 32;
+    const size_t base = Wb.size();
+    Wb.resize(base + (size_t)ncb * (nk1 + nk2) * 3 * 256, 0.f);
+    uint16_t* o = reinterpret_cast<uint16_t*>(Wb.data() + base);
+    const float* w = W.data() + pb.w_off;   // [K1 + K2][N]
+    for (int cb = 0; cb < ncb; ++cb)
+      for (int kc = 0; kc < nk1 + nk2; ++kc)
+        for (int l = 0; l < 64; ++l)
+          for (int t = 0; t < 8; ++t) {
+            const bool second = kc >= nk1;
+            const int kk = 32 * (second ? kc - nk1 : kc) + 8 * (l / 16) + t;
+            const int col = 16 * cb + l % 16;
+            float v = 0.f;
+            if (col < pb.N && kk < (second ? pb.K2 : pb.K1))
+              v = w[(size_t)(second ? pb.K1 + kk : kk) * pb.N + col];
+            for (int pc = 0; pc < 3; ++pc) {
+              const uint16_t hb = bf16_rne(v);
+              o[(((size_t)cb * (nk1 + nk2) + kc) * 3 + pc) * 512 + l * 8 + t] = hb;
+              v -= bf16_to_f32(hb);
+            }
+          }
+  }
+  if (upload(P.Wb, Wb) != hipSuccess) return -2;
   P.ok = true;
   return 0;
 }

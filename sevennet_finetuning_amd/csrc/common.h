@@ -99,6 +99,8 @@ struct NlProb {
   const float* A;
   const float* A2;
   const float* B;
+  const void* Bb;  // B as bf16 pieces (LinPair::Wb order): k_nodelin_b; null: k_nodelin
+
   float* C;
   float* xo;
   int64_t lda, lda2, ldc, ldxo;
@@ -106,6 +108,7 @@ struct NlProb {
   int K1, K, N, R, nodes;
   int epi, n_act, gate_off;
   int wn, ns, tpn, tile_begin, tiles_n;  // set by add_nl
+  int kind;  // set by add_nl: 0 k_nodelin (f32), 1 k_nodelin_b, 2 k_nodelin_s (bf16x6)
 };
 constexpr int NL_MAX_PROBS = 4;
 struct NlBatch {

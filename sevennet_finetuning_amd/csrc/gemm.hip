@@ -15,6 +15,7 @@
 // (lane l: A[row l&31][k l>>5], B[k l>>5][col l&31]) are unit-stride.
 #include "common.h"
 
+#include <cstdlib>
 #include <cstring>
 
 namespace e3gnn {
@@ -252,24 +253,17 @@ __device__ __forceinline__ void nl_epilogue(const NlProb& P, const f32x16& acc, 
 #ifndef E3GNN_NL_RUNS
 #define E3GNN_NL_RUNS 1
 #endif
-template <int WN, int R>
-__device__ __forceinline__ void nl_epilogue_runs(const NlProb& P, const f32x16& acc, int node0,
-                                                 int n0, float* lds) {
-  constexpr int BM = 128 / WN, CW = 32 * WN;
-  constexpr int T = BM / R, ROWS = T * R;
+// stage(lds, LDR) writes the accumulators as lds[nl * LDR + c * R + m] (the
+// tile's node nl, column c of the chunk, component m): the f32 (32x32) and
+// bf16x6 (16x16) accumulator layouts share the copy-out.
+template <int BM, int CW, int R, int LDSF, class Stage>
+__device__ __forceinline__ void nl_epi_runs(const NlProb& P, int node0, int n0, float* lds, Stage stage) {
+  constexpr int T = BM / R;
   constexpr int RUN = CW * R, LDR = RUN + 4;  // 16-byte aligned node runs
-  static_assert(T * LDR <= NL_LDS, "C runs must fit the LDS stages");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave / WN, wc = wave % WN;
+  static_assert(T * LDR <= LDSF, "C runs must fit the LDS stages");
+  const int tid = threadIdx.x;
   __syncthreads();
-  const int cR = (wc * 32 + (lane & 31)) * R;
-  const int rbase = wr * 32 + 4 * (lane >> 5);
-#pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int row = rbase + (reg & 3) + 8 * (reg >> 2);
-    const int nl = row / R, m = row - nl * R;
-    if (row < ROWS) lds[nl * LDR + cR + m] = acc[reg];
-  }
+  stage(lds, LDR);
   __syncthreads();
   const int ncol = P.N - n0 < CW ? P.N - n0 : CW;  // a multiple of 4 (add_nl)
   if (ncol <= 0) return;
@@ -292,6 +286,27 @@ __device__ __forceinline__ void nl_epilogue_runs(const NlProb& P, const f32x16& 
     *cp = v;
   }
 }
+// the f32 kernel's 32 x 32 accumulator (wave (wr, wc) of WN columns) into runs
+template <int WN, int R>
+__device__ __forceinline__ void nl_stage32(const f32x16& acc, float* L, int LDR) {
+  constexpr int BM = 128 / WN, ROWS = (BM / R) * R;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const int cR = (wc * 32 + (lane & 31)) * R;
+  const int rbase = wr * 32 + 4 * (lane >> 5);
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = rbase + (reg & 3) + 8 * (reg >> 2);
+    const int nl = row / R, m = row - nl * R;
+    if (row < ROWS) L[nl * LDR + cR + m] = acc[reg];
+  }
+}
+template <int WN, int R>
+__device__ __forceinline__ void nl_epilogue_runs(const NlProb& P, const f32x16& acc, int node0,
+                                                 int n0, float* lds) {
+  nl_epi_runs<128 / WN, 32 * WN, R, NL_LDS>(P, node0, n0, lds,
+                                             [&](float* L, int LDR) { nl_stage32<WN, R>(acc, L, LDR); });
+}
 
 // The gate epilogues (epi 2 / 3) in the same run form.  epi 2 (the 0e block,
 // R = 1): C = the pre-activations, xo = act(scalars) for columns < n_act.
@@ -305,27 +320,17 @@ __device__ __forceinline__ void nl_epilogue_runs(const NlProb& P, const f32x16& 
 #ifndef E3GNN_NL_GATE_RUNS
 #define E3GNN_NL_GATE_RUNS 1
 #endif
-template <int WN, int R>
-__device__ __forceinline__ void nl_epilogue_gate(const NlProb& P, const f32x16& acc, int node0,
-                                                 int n0, float* lds) {
-  constexpr int BM = 128 / WN, CW = 32 * WN;
-  constexpr int T = BM / R, ROWS = T * R;
+template <int BM, int CW, int R, int LDSF, class Stage>
+__device__ __forceinline__ void nl_epi_gate(const NlProb& P, int node0, int n0, float* lds, Stage stage) {
+  constexpr int T = BM / R;
   constexpr int RUN = CW * R, LDR = RUN + 4;
   constexpr int GS = R > 1 ? T * CW : 0, NG = (GS + 255) / 256;
-  static_assert(T * LDR + GS <= NL_LDS, "C runs and gate factors must fit the LDS stages");
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave / WN, wc = wave % WN;
+  static_assert(T * LDR + GS <= LDSF, "C runs and gate factors must fit the LDS stages");
+  const int tid = threadIdx.x;
   const int ncol = P.N - n0 < CW ? P.N - n0 : CW;  // a multiple of 4 (add_nl)
   const int vn = min(T, P.nodes - node0);
   __syncthreads();
-  const int cR = (wc * 32 + (lane & 31)) * R;
-  const int rbase = wr * 32 + 4 * (lane >> 5);
-#pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int row = rbase + (reg & 3) + 8 * (reg >> 2);
-    const int nl = row / R, m = row - nl * R;
-    if (row < ROWS) lds[nl * LDR + cR + m] = acc[reg];
-  }
+  stage(lds, LDR);
   float* gl = lds + T * LDR;
   if constexpr (GS > 0) {
     float gv[NG];
@@ -370,6 +375,12 @@ __device__ __forceinline__ void nl_epilogue_gate(const NlProb& P, const f32x16& 
                                                    gn[(j + 2) / R] * v.z, gn[(j + 3) / R] * v.w);
     }
   }
+}
+template <int WN, int R>
+__device__ __forceinline__ void nl_epilogue_gate(const NlProb& P, const f32x16& acc, int node0,
+                                                 int n0, float* lds) {
+  nl_epi_gate<128 / WN, 32 * WN, R, NL_LDS>(P, node0, n0, lds,
+                                             [&](float* L, int LDR) { nl_stage32<WN, R>(acc, L, LDR); });
 }
 
 // Operand loads through buffer descriptors based at the tile (a 32-bit lane
@@ -596,12 +607,435 @@ k_nodelin(NlBatch batch) {
     }
   }
 }
+// ------------------------------------------------- node linears on bf16x6 MFMA
+// k_nodelin_b: the same problems as k_nodelin (node-aligned tiles, the run /
+// gate epilogues) on v_mfma_f32_16x16x32_bf16 with both operands as three bf16
+// pieces (x = p0 + p1 + p2 exactly: 24 significant bits) and the six piece
+// products with i + j <= 2 accumulated in f32, smallest first -- f32-grade
+// results (dropped terms below 2^-24 relative) at 6 x 16 = 96 MFMA cycles per
+// 16 x 16 x 32 block instead of the 256 of the f32 MFMA (the si2^T launches
+// were MFMA-bound: 0.31 of their 0.51 ms with loads and epilogue removed).
+// The weights are split once at load (LinPair::Wb, already in B-operand lane
+// order: one b128 per lane, piece and 16-column block, from L2); the node rows
+// are split while staging: thread unit (row = node * R + m, k quad) -> 4
+// values, 3 pieces, one ds_write_b64 per piece into k-contiguous bf16 planes
+// [piece][row][k] (80-byte rows: the b128 fragment reads are conflict-free).
+// Tile 64 rows (T = 64 / R nodes) x BN columns, BK = 32, 4 waves:
+//   SH 0: BN 32, waves 4 x 1, each 16 rows x 32 columns (N <= 32)
+//   SH 1: BN 64, waves 2 x 2, each 32 x 32
+constexpr int NB_BM = 64, NB_BK = 32, NB_ALD = 40;
+constexpr int NB_PLANE = NB_BM * NB_ALD;        // bf16 per piece plane
+constexpr int NB_STAGE = 3 * NB_PLANE * 2;      // bytes per LDS stage
+constexpr int NB_LDSF = 2 * NB_STAGE / 4;       // floats (two stages; the epilogue reuses them)
+typedef __bf16 nbf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned nu32x2 __attribute__((ext_vector_type(2)));
+typedef float nf32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+typedef __bf16 nbf16x2 __attribute__((ext_vector_type(2)));
+template <int SH>
+struct NbShape {
+  static constexpr int WC = SH == 0 ? 1 : 2, WR = 4 / WC;
+  static constexpr int BN = 32 * WC, RB = NB_BM / WR / 16, CB = 2;
+};
+// four floats as three bf16 pieces, two values per v_cvt_pk_bf16_f32 (the
+// packed word is both the operand and, widened, what the residual subtracts)
+__device__ __forceinline__ void nb_split4(const float (&v)[4], nu32x2 (&d)[3]) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    nf32x2 r;
+    r[0] = v[2 * q];
+    r[1] = v[2 * q + 1];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+      const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(r, nbf16x2));
+      d[pc][q] = u;
+      if (pc < 2) {
+        r[0] -= __builtin_bit_cast(float, u << 16);
+        r[1] -= __builtin_bit_cast(float, u & 0xffff0000u);
+      }
+    }
+  }
+}
+__device__ __forceinline__ float nl_ld1(__amdgpu_buffer_rsrc_t r, int vbytes, int sbytes) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vbytes, sbytes, 0));
+}
+
+template <int SH, int R>
+__device__ __forceinline__ void nl_tile_b(const NlProb& P, int local, float* lds) {
+  using S = NbShape<SH>;
+  constexpr int BM = NB_BM, BK = NB_BK, BN = S::BN, WC = S::WC, RB = S::RB, CB = S::CB;
+  constexpr int T = BM / R, ROWS = T * R;
+  constexpr int UNITS = ROWS * (BK / 4), NU = (UNITS + 255) / 256;
+  constexpr int OOB = 0x7ffffff0;   // outside every descriptor: reads 0
+  // (wave index wave-uniform for the compiler: the B fragment offsets are
+  // scalar offsets, not per-lane waterfall loops)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WC, wc = wave % WC;
+  const int tm = local / P.tiles_n, tn = local - tm * P.tiles_n;
+  const int node0 = tm * T, n0 = tn * BN;
+  const int vn = min(T, P.nodes - node0);
+  const int K2 = P.K - P.K1;
+  const int nkc1 = (P.K1 + BK - 1) / BK, nkc = nkc1 + (K2 + BK - 1) / BK;
+  const __amdgpu_buffer_rsrc_t RA =
+      nl_rsrc(P.A + (int64_t)node0 * P.lda + P.a_off, ((int64_t)(vn - 1) * P.lda + P.K1 * R) * 4);
+  const __amdgpu_buffer_rsrc_t RA2 =
+      K2 > 0 ? nl_rsrc(P.A2 + (int64_t)node0 * P.lda2 + P.a_off2, ((int64_t)(vn - 1) * P.lda2 + K2 * R) * 4)
+             : RA;
+  const int ncb = (P.N + 15) / 16;
+  const __amdgpu_buffer_rsrc_t RBb =
+      nl_rsrc(static_cast<const float*>(P.Bb), (int64_t)ncb * nkc * 3 * 1024);
+  // the thread's staging units: (row, k quad); rows past the tile's nodes and
+  // idle units read 0 (OOB offsets)
+  int uo[NU], uo2[NU], ukq[NU];
+#pragma unroll
+  for (int i = 0; i < NU; ++i) {
+    const int u = tid + 256 * i;
+    const int row = u >> 3, kq = u & 7;
+    const int nl = row / R, m = row - nl * R;
+    const bool ok = (UNITS % 256 == 0 || u < UNITS) && nl < vn;
+    uo[i] = ok ? (nl * (int)P.lda + 4 * kq * R + m) * 4 : OOB;
+    uo2[i] = ok ? (nl * (int)P.lda2 + 4 * kq * R + m) * 4 : OOB;
+    ukq[i] = kq;
+  }
+  // B fragments of the wave's column blocks: two register sets (step kc's in
+  // use while kc + 1's load)
+  const int cb0 = n0 / 16 + wc * CB;
+  nbf16x8 bq[2][CB][3];
+  // (steps past the end issue the same loads at OOB offsets: every step
+  // issues the same vector-memory instructions, so the compiler's wait counts
+  // stay exact and a step waits only for the previous step's loads)
+  auto load_b = [&](int kc, nbf16x8 (&d)[CB][3]) {
+#pragma unroll
+    for (int b = 0; b < CB; ++b)
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) {
+        const int cb = cb0 + b;
+        const int off = (cb < ncb && kc < nkc) ? ((cb * nkc + kc) * 3 + pc) * 1024 : OOB;
+        d[b][pc] = __builtin_bit_cast(nbf16x8, __builtin_amdgcn_raw_buffer_load_b128(RBb, lane * 16, off, 0));
+      }
+  };
+  float ra[NU][4];
+  auto load_a = [&](int kc) {
+    const bool second = kc >= nkc1;
+    const int kb = (second ? kc - nkc1 : kc) * BK, kend = second ? K2 : P.K1;
+    const int soff = kb * R * 4;
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      // K is a multiple of 4 (add_nl): a quad is in or out as a whole
+      const int o = (kc < nkc && kb + 4 * ukq[i] < kend) ? (second ? uo2[i] : uo[i]) : OOB;
+      const __amdgpu_buffer_rsrc_t Ra = second ? RA2 : RA;
+      if constexpr (R == 1) {
+        const float4 v = nl_ld4(Ra, o, soff);
+        ra[i][0] = v.x, ra[i][1] = v.y, ra[i][2] = v.z, ra[i][3] = v.w;
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) ra[i][t] = nl_ld1(Ra, o == OOB ? OOB : o + t * R * 4, soff);
+      }
+    }
+  };
+  auto store_a = [&](int buf) {
+    char* base = reinterpret_cast<char*>(lds) + buf * NB_STAGE;
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      const int u = tid + 256 * i;
+      if (UNITS % 256 != 0 && u >= UNITS) continue;
+      nu32x2 d[3];
+      nb_split4(ra[i], d);
+      const int row = u >> 3;
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+        *reinterpret_cast<nu32x2*>(base + ((pc * NB_PLANE + row * NB_ALD) + 4 * ukq[i]) * 2) = d[pc];
+    }
+  };
+  constexpr int I6[6] = {2, 1, 0, 1, 0, 0}, J6[6] = {0, 1, 2, 0, 1, 0};
+  auto compute = [&](int buf, const nbf16x8 (&bb)[CB][3], f32x4 (&c)[RB][CB]) {
+    const char* base = reinterpret_cast<const char*>(lds) + buf * NB_STAGE;
+#pragma unroll
+    for (int a = 0; a < RB; ++a) {
+      const int row = (wr * RB + a) * 16 + (lane & 15);
+      nbf16x8 af[3];
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+        af[pc] = *reinterpret_cast<const nbf16x8*>(base + ((pc * NB_PLANE + row * NB_ALD) + 8 * (lane >> 4)) * 2);
+#pragma unroll
+      for (int b = 0; b < CB; ++b)
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+          c[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[I6[q]], bb[b][J6[q]], c[a][b], 0, 0, 0);
+    }
+  };
+  f32x4 acc[RB][CB];
+#pragma unroll
+  for (int a = 0; a < RB; ++a)
+#pragma unroll
+    for (int b = 0; b < CB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[a][b][i] = 0.f;
+  load_a(0);
+  load_b(0, bq[0]);
+  store_a(0);
+  __syncthreads();
+  // step kc (B set and LDS stage SET = kc & 1, a compile-time constant: the
+  // loop runs two steps per iteration, an odd first step peeled): step kc +
+  // 1's node rows and B fragments load while its MFMAs run.  (The two linears
+  // of a split problem share the f32 accumulator: one K-concatenated sum.)
+  auto step = [&](int kc, auto SET) {
+    constexpr int CUR = decltype(SET)::value;
+    load_a(kc + 1);
+    load_b(kc + 1, bq[CUR ^ 1]);
+    compute(CUR, bq[CUR], acc);
+    store_a(CUR ^ 1);
+    __syncthreads();
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if (nkc & 1) {
+    step(0, S0{});
+#pragma unroll 1
+    for (int kc = 1; kc < nkc; kc += 2) {
+      step(kc, S1{});
+      step(kc + 1, S0{});
+    }
+  } else {
+#pragma unroll 1
+    for (int kc = 0; kc < nkc; kc += 2) {
+      step(kc, S0{});
+      step(kc + 1, S1{});
+    }
+  }
+  // D lane l, register i of block (a, b): row 16 (wr RB + a) + 4 (l / 16) + i,
+  // column 32 wc + 16 b + l % 16 of the tile
+  auto stage = [&](float* L, int LDR) {
+#pragma unroll
+    for (int a = 0; a < RB; ++a)
+#pragma unroll
+      for (int b = 0; b < CB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = (wr * RB + a) * 16 + 4 * (lane >> 4) + i;
+          const int col = wc * 32 + b * 16 + (lane & 15);
+          const int nl = row / R, m = row - nl * R;
+          if (row < ROWS) L[nl * LDR + col * R + m] = acc[a][b][i];
+        }
+  };
+  if (P.epi <= 1)
+    nl_epi_runs<BM, BN, R, NB_LDSF>(P, node0, n0, lds, stage);
+  else
+    nl_epi_gate<BM, BN, R, NB_LDSF>(P, node0, n0, lds, stage);
+}
+
+// ------------------------------------------------- skinny node linears
+// k_nodelin_s: a problem with K <= 64 (the si2^T / si1 l > 0 blocks: K = 64 /
+// 32 onto N = 320 / 352 mid channels) is output-bound, not MFMA-bound.  A
+// workgroup owns 64 rows (T = 64 / R nodes) and ALL N columns: its node rows
+// are loaded and split into the bf16 piece planes ONCE (both K chunks side by
+// side in the two LDS stages), then it walks N in 64-column chunks: the
+// chunk's bf16x6 MFMAs (B fragments from L2), the next chunk's B loads, the
+// chunk's accumulators staged as node runs and copied out with buffer stores.
+// Every chunk issues the same vector-memory instructions (masked lanes and
+// steps past the end use OOB offsets the hardware drops), so the compiler's
+// wait before a chunk's MFMAs covers that chunk's B loads only, and the
+// previous chunks' output stores drain under them.
+constexpr int NS_EPIF = 64 * 68;   // max over R of T x (64 R + 4) floats: one chunk's runs
+constexpr int NS_LDSF = NB_LDSF + NS_EPIF;
+
+template <int R>
+__device__ __forceinline__ void nl_tile_s(const NlProb& P, int local, float* lds) {
+  constexpr int BM = NB_BM, BK = NB_BK, CW = 64, WC = 2, RB = 2, CB = 2;
+  constexpr int T = BM / R, ROWS = T * R;
+  constexpr int UNITS = ROWS * (BK / 4), NU = (UNITS + 255) / 256;
+  constexpr int OOB = 0x7ffffff0;
+  constexpr int RUN = CW * R, LDR = RUN + 4, SEGC = RUN / 4, UC = T * SEGC, NC = (UC + 255) / 256;
+  static_assert(T * LDR <= NS_EPIF, "chunk runs must fit");
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WC, wc = wave % WC;
+  const int node0 = local * T;
+  const int vn = min(T, P.nodes - node0);
+  const int nkc = (P.K + BK - 1) / BK;   // 1 or 2
+  const __amdgpu_buffer_rsrc_t RA =
+      nl_rsrc(P.A + (int64_t)node0 * P.lda + P.a_off, ((int64_t)(vn - 1) * P.lda + P.K * R) * 4);
+  const int ncb = (P.N + 15) / 16;
+  const __amdgpu_buffer_rsrc_t RBb =
+      nl_rsrc(static_cast<const float*>(P.Bb), (int64_t)ncb * nkc * 3 * 1024);
+  const __amdgpu_buffer_rsrc_t RC =
+      nl_rsrc(P.C + (int64_t)node0 * P.ldc + P.c_off, ((int64_t)(vn - 1) * P.ldc + P.N * R) * 4);
+  // ---- the node rows of both K chunks, split into the piece planes
+  {
+    float ra[2][NU][4];
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        const int u = tid + 256 * i;
+        const int row = u >> 3, kq = u & 7;
+        const int nl = row / R, m = row - nl * R;
+        const bool ok = (UNITS % 256 == 0 || u < UNITS) && nl < vn && kc * BK + 4 * kq < P.K;
+        const int o = ok ? (nl * (int)P.lda + (kc * BK + 4 * kq) * R + m) * 4 : OOB;
+        if constexpr (R == 1) {
+          const float4 v = nl_ld4(RA, o, 0);
+          ra[kc][i][0] = v.x, ra[kc][i][1] = v.y, ra[kc][i][2] = v.z, ra[kc][i][3] = v.w;
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) ra[kc][i][t] = nl_ld1(RA, ok ? o + t * R * 4 : OOB, 0);
+        }
+      }
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      char* base = reinterpret_cast<char*>(lds) + kc * NB_STAGE;
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        const int u = tid + 256 * i;
+        if (UNITS % 256 != 0 && u >= UNITS) continue;
+        nu32x2 d[3];
+        nb_split4(ra[kc][i], d);
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc)
+          *reinterpret_cast<nu32x2*>(base + ((pc * NB_PLANE + (u >> 3) * NB_ALD) + 4 * (u & 7)) * 2) = d[pc];
+      }
+    }
+  }
+  // ---- B fragments of a chunk: [k chunk][column block][piece]
+  nbf16x8 bq[2][CB][3];
+  auto load_b = [&](int ch) {
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+      for (int b = 0; b < CB; ++b)
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc) {
+          const int cb = ch * 4 + wc * 2 + b;
+          const int off = (cb < ncb && kc < nkc) ? ((cb * nkc + kc) * 3 + pc) * 1024 : OOB;
+          bq[kc][b][pc] =
+              __builtin_bit_cast(nbf16x8, __builtin_amdgcn_raw_buffer_load_b128(RBb, lane * 16, off, 0));
+        }
+  };
+  load_b(0);
+  __syncthreads();
+  constexpr int I6[6] = {2, 1, 0, 1, 0, 0}, J6[6] = {0, 1, 2, 0, 1, 0};
+  float* ep = lds + NB_LDSF;
+  const int nch = (P.N + CW - 1) / CW;
+#pragma unroll 1
+  for (int ch = 0; ch < nch; ++ch) {
+    f32x4 acc[RB][CB];
+#pragma unroll
+    for (int a = 0; a < RB; ++a)
+#pragma unroll
+      for (int b = 0; b < CB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      if (kc < nkc) {
+        const char* base = reinterpret_cast<const char*>(lds) + kc * NB_STAGE;
+#pragma unroll
+        for (int a = 0; a < RB; ++a) {
+          const int row = (wr * RB + a) * 16 + (lane & 15);
+          nbf16x8 af[3];
+#pragma unroll
+          for (int pc = 0; pc < 3; ++pc)
+            af[pc] = *reinterpret_cast<const nbf16x8*>(base + ((pc * NB_PLANE + row * NB_ALD) + 8 * (lane >> 4)) * 2);
+#pragma unroll
+          for (int b = 0; b < CB; ++b)
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[I6[q]], bq[kc][b][J6[q]], acc[a][b], 0, 0, 0);
+        }
+      }
+    }
+    load_b(ch + 1);   // (past the last chunk: OOB, same instructions)
+    // the chunk's runs: lds ep[nl * LDR + c * R + m]
+    __syncthreads();   // the previous chunk's copy-out has read ep
+#pragma unroll
+    for (int a = 0; a < RB; ++a)
+#pragma unroll
+      for (int b = 0; b < CB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = (wr * RB + a) * 16 + 4 * (lane >> 4) + i;
+          const int col = wc * 32 + b * 16 + (lane & 15);
+          const int nl = row / R, m = row - nl * R;
+          if (row < ROWS) ep[nl * LDR + col * R + m] = acc[a][b][i];
+        }
+    __syncthreads();
+    const int len = min(CW, P.N - ch * CW) * R;   // a multiple of 4 (N % 4 == 0)
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int u = tid + 256 * i;
+      const int nl = u / SEGC, j = 4 * (u - nl * SEGC);
+      const bool ok = (UC % 256 == 0 || u < UC) && nl < vn && j < len;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(ep + (ok ? nl * LDR + j : 0));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), RC,
+                                             ok ? (nl * (int)P.ldc + ch * CW * R + j) * 4 : OOB, 0, 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void
+k_nodelin_s(NlBatch batch) {
+  __shared__ __attribute__((aligned(16))) float lds[NS_LDSF];
+  const int tile = blockIdx.x;
+  int pi = 0;
+#pragma unroll 1
+  for (int i = 1; i < batch.nprob; ++i)
+    if (tile >= batch.p[i].tile_begin) pi = i;
+  NlProb P = batch.p[0];
+  if (pi == 1) P = batch.p[1];
+  if (pi == 2) P = batch.p[2];
+  if (pi == 3) P = batch.p[3];
+  const int local = tile - P.tile_begin;
+  switch (P.R) {
+    case 1: nl_tile_s<1>(P, local, lds); break;
+    case 3: nl_tile_s<3>(P, local, lds); break;
+    default: nl_tile_s<5>(P, local, lds); break;
+  }
+}
+
+#ifndef E3GNN_NLB_WAVES
+#define E3GNN_NLB_WAVES 3
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E3GNN_NLB_WAVES, 8))) void
+k_nodelin_b(NlBatch batch) {
+  __shared__ __attribute__((aligned(16))) float lds[NB_LDSF];
+  const int tile = blockIdx.x;
+  int pi = 0;
+#pragma unroll 1
+  for (int i = 1; i < batch.nprob; ++i)
+    if (tile >= batch.p[i].tile_begin) pi = i;
+  NlProb P = batch.p[0];
+  if (pi == 1) P = batch.p[1];
+  if (pi == 2) P = batch.p[2];
+  if (pi == 3) P = batch.p[3];
+  const int local = tile - P.tile_begin;
+  if (P.wn == 1) {
+    switch (P.R) {
+      case 1: nl_tile_b<0, 1>(P, local, lds); break;
+      case 3: nl_tile_b<0, 3>(P, local, lds); break;
+      default: nl_tile_b<0, 5>(P, local, lds); break;
+    }
+  } else {
+    switch (P.R) {
+      case 1: nl_tile_b<1, 1>(P, local, lds); break;
+      case 3: nl_tile_b<1, 3>(P, local, lds); break;
+      default: nl_tile_b<1, 5>(P, local, lds); break;
+    }
+  }
+}
 }  // namespace
 
 hipError_t launch_gemm(const GemmBatch& b, hipStream_t s) {
   if (b.total_tiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_gemm, dim3(b.total_tiles), dim3(256), 0, s, b);
   return hipGetLastError();
+}
+
+// which kernel runs a node-linear problem (E3GNN_NL_BF16): 0 k_nodelin (f32
+// MFMA) for all; 1 (default) k_nodelin_s (skinny, bf16x6) where it applies,
+// k_nodelin otherwise; 2 k_nodelin_s where it applies, k_nodelin_b (bf16x6
+// tiles) otherwise; 3 k_nodelin_b for all
+static int nl_mode() {
+  static const int m = [] {
+    const char* v = std::getenv("E3GNN_NL_BF16");
+    return v ? std::atoi(v) : 1;
+  }();
+  return m;
 }
 
 bool add_nl(NlBatch& b, const NlProb& p) {
@@ -613,13 +1047,38 @@ bool add_nl(NlBatch& b, const NlProb& p) {
     return false;
   if (p.epi >= 2 && (!al(p.xo) || p.ldxo % 4 || p.xo_off % 4 || (p.epi == 2 && p.R != 1)))
     return false;
-  if (p.K > p.K1 && (!al(p.A2) || p.lda2 % 4 || p.a_off2 % 4 || p.K1 % NL_BK)) return false;
   NlProb q = p;
-  q.wn = p.N <= 32 ? 1 : 2;
-  q.ns = (E3GNN_NL_WIDE && q.wn == 2 && p.K == p.K1 && p.K <= E3GNN_NL_WIDE_KMAX && p.N >= 128) ? 2 : 1;
-  const int BM = 128 / q.wn, BN = 32 * q.wn * q.ns;
-  q.tpn = BM / p.R;
-  const int tm = (p.nodes + q.tpn - 1) / q.tpn, tn = (p.N + BN - 1) / BN;
+  const int mode = nl_mode();
+  // skinny: K <= 64 onto N >= 128 columns (si2^T l > 0: 345 vs ~400 us per
+  // launch on the f32 tiles; si1's N <= 64 blocks ran slower there: f32)
+  const bool skinny = p.Bb && mode >= 1 && mode <= 2 && p.K == p.K1 && p.K <= 64 && p.K % 4 == 0 &&
+                      p.N >= 128 && p.epi == 0;
+  const bool btile = p.Bb && mode >= 2 && !skinny && p.K1 % 4 == 0 && (p.K - p.K1) % 4 == 0;
+  int tm, tn;
+  if (skinny) {          // k_nodelin_s: 64-row tiles over all N
+    q.kind = 2;
+    q.wn = 2;
+    q.ns = 1;
+    q.tpn = NB_BM / p.R;
+    tm = (p.nodes + q.tpn - 1) / q.tpn;
+    tn = 1;
+  } else if (btile) {    // k_nodelin_b: 64-row tiles, BN 32 (N <= 32) or 64
+    q.kind = 1;
+    q.wn = p.N <= 32 ? 1 : 2;
+    q.ns = 1;
+    q.tpn = NB_BM / p.R;
+    tm = (p.nodes + q.tpn - 1) / q.tpn;
+    tn = (p.N + 32 * q.wn - 1) / (32 * q.wn);
+  } else {
+    if (p.K > p.K1 && (!al(p.A2) || p.lda2 % 4 || p.a_off2 % 4 || p.K1 % NL_BK)) return false;
+    q.kind = 0;
+    q.wn = p.N <= 32 ? 1 : 2;
+    q.ns = (E3GNN_NL_WIDE && q.wn == 2 && p.K == p.K1 && p.K <= E3GNN_NL_WIDE_KMAX && p.N >= 128) ? 2 : 1;
+    const int BM = 128 / q.wn, BN = 32 * q.wn * q.ns;
+    q.tpn = BM / p.R;
+    tm = (p.nodes + q.tpn - 1) / q.tpn;
+    tn = (p.N + BN - 1) / BN;
+  }
   if (tm <= 0 || tn <= 0) return true;
   q.tiles_n = tn;
   q.tile_begin = b.total_tiles;
@@ -628,9 +1087,28 @@ bool add_nl(NlBatch& b, const NlProb& p) {
   return true;
 }
 
+// one launch per kernel kind present in the batch (same stream, in order)
 hipError_t launch_nodelin(const NlBatch& b, hipStream_t s) {
   if (b.total_tiles <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_nodelin, dim3(b.total_tiles), dim3(256), 0, s, b);
+  for (int kind = 0; kind < 3; ++kind) {
+    NlBatch sb;
+    std::memset(&sb, 0, sizeof(sb));
+    for (int i = 0; i < b.nprob; ++i) {
+      if (b.p[i].kind != kind) continue;
+      const int end = i + 1 < b.nprob ? b.p[i + 1].tile_begin : b.total_tiles;
+      NlProb q = b.p[i];
+      q.tile_begin = sb.total_tiles;
+      sb.p[sb.nprob++] = q;
+      sb.total_tiles += end - b.p[i].tile_begin;
+    }
+    if (sb.total_tiles <= 0) continue;
+    if (kind == 0)
+      hipLaunchKernelGGL(k_nodelin, dim3(sb.total_tiles), dim3(256), 0, s, sb);
+    else if (kind == 1)
+      hipLaunchKernelGGL(k_nodelin_b, dim3(sb.total_tiles), dim3(256), 0, s, sb);
+    else
+      hipLaunchKernelGGL(k_nodelin_s, dim3(sb.total_tiles), dim3(256), 0, s, sb);
+  }
   return hipGetLastError();
 }
 

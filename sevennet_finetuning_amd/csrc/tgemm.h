@@ -20,7 +20,6 @@ struct TgProb {
   int beta;
   int splits;  // requested (tg_add settles it)
   // set by tg_add
-  int va1, vb1, va2, vb2;
   int tiles_n, tiles_mn, ksteps, tile_begin;
   int64_t red_begin;
 };

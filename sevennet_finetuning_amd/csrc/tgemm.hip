@@ -22,10 +22,16 @@
 #include "common.h"
 #include "tgemm.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace e3gnn {
 namespace {
 
 constexpr int TBM = 64, TBN = 64, TBK = 16, TPAD = 4;
+constexpr int TEL = TBK * TBM / 256;   // elements of one operand slab per thread
+constexpr int TLD = TBM + TPAD;        // LDS row (k) stride, floats
+constexpr int OOB = 0x7ffffff0;        // outside every descriptor: reads 0
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int tg_find(const TgBatch& b, int tile) {
@@ -36,55 +42,57 @@ __device__ __forceinline__ int tg_find(const TgBatch& b, int tile) {
   return p;
 }
 
-// op(X)(r, k) of a row-major X with leading dimension ld (trans: X[k][r])
-struct Opnd {
-  const float* X;
-  int64_t ld;
-  int trans, vec;  // vec: 16-byte loads along the contiguous dimension
-};
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t rfl(int64_t v) {
+  const uint64_t u = (uint64_t)v;
+  return (int64_t)(((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                   (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u));
+}
 
-// One 16 x 64 (k x r) slab of op(X): 256 threads x 4 elements.  Not
-// transposed (X[r][k]): thread -> (r = e / 4, k quad = e % 4), 4 consecutive k;
-// transposed (X[k][r]): thread -> (k = e / 16, r quad = e % 16), 4 consecutive r.
-__device__ __forceinline__ void tg_load(const Opnd& o, int r0, int rmax, int k0, int kmax, float (&v)[4]) {
+// One operand of the tile, op(X)(r, k) (row-major X, leading dimension ld;
+// trans: X[k][r]), read through a buffer descriptor based at the tile's first
+// row (column): the thread's TEL elements of a TBK x 64 slab, element
+// e = 256 i + tid walking the contiguous dimension fastest (not transposed:
+// k = e % TBK, r = e / TBK; transposed: r = e % 64, k = e / 64).  Their byte
+// offsets at k = 0 and LDS slots are fixed for the launch; a k step adds a
+// scalar offset -- no per-element 64-bit address arithmetic in the k loop.
+// Elements past the problem's rows (columns) or its K read 0 (OOB offset).
+struct OpB {
+  __amdgpu_buffer_rsrc_t R;
+  int vo[TEL];   // byte offset at k = 0, OOB past the rows
+  int kk[TEL];   // k within a step
+  int lo[TEL];   // LDS slot S[k][r]
+  int kstride;   // bytes per k
+};
+__device__ __forceinline__ void opb_init(OpB& o, const float* X, int64_t ld, int trans, int r0, int rmax,
+                                         int K) {
+  const float* base = trans ? X + r0 : X + (int64_t)r0 * ld;
+  int64_t bytes = trans ? ((int64_t)(K - 1) * ld + (rmax - r0)) * 4 : ((int64_t)(rmax - r0 - 1) * ld + K) * 4;
+  bytes = K <= 0 || rmax <= r0 ? 0 : (bytes > 0x7fffffff ? 0x7fffffff : bytes);
+  o.R = __builtin_amdgcn_make_buffer_rsrc((void*)(base ? base : X), (short)0, (int)bytes, 0x00020000);
   const int tid = threadIdx.x;
-  if (!o.trans) {
-    const int r = r0 + (tid >> 2), k = k0 + 4 * (tid & 3);
-    const float* p = o.X + (int64_t)r * o.ld + k;
-    if (r < rmax && o.vec && k + 3 < kmax) {
-      const float4 q = *reinterpret_cast<const float4*>(p);
-      v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
-    } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (r < rmax && k + i < kmax) ? p[i] : 0.f;
-    }
-  } else {
-    const int k = k0 + (tid >> 4), r = r0 + 4 * (tid & 15);
-    const float* p = o.X + (int64_t)k * o.ld + r;
-    if (k < kmax && o.vec && r + 3 < rmax) {
-      const float4 q = *reinterpret_cast<const float4*>(p);
-      v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (k < kmax && r + i < rmax) ? p[i] : 0.f;
-    }
+  for (int i = 0; i < TEL; ++i) {
+    const int e = 256 * i + tid;
+    const int r = trans ? (e & 63) : (e / TBK), k = trans ? (e >> 6) : (e % TBK);
+    o.vo[i] = r0 + r < rmax ? (int)(trans ? (int64_t)k * ld + r : (int64_t)r * ld + k) * 4 : OOB;
+    o.kk[i] = k;
+    o.lo[i] = k * TLD + r;
   }
+  o.kstride = trans ? (int)ld * 4 : 4;
 }
-__device__ __forceinline__ void tg_store(const Opnd& o, float (*S)[TBM + TPAD], const float (&v)[4]) {
-  const int tid = threadIdx.x;
-  if (!o.trans) {
-    const int r = tid >> 2, k = 4 * (tid & 3);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) S[k + i][r] = v[i];
-  } else {
-    const int k = tid >> 4, r = 4 * (tid & 15);
-    *reinterpret_cast<float4*>(&S[k][r]) = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
+
+// Main loop: LDS double buffer + a ring of NS register slots, so the loads of
+// k-step kt + NS - 1 are in flight while step kt computes (small GEMMs are
+// latency-bound).  The loop is unrolled by NS so every slot index is a
+// compile-time constant, and every iteration issues the same loads (past the
+// split's end at OOB offsets, the compute skipped), so the compiler's wait
+// counts are exact: a slot's consumer waits for that slot's loads only.
+constexpr int NS = 4;
 
 __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
-  __shared__ __attribute__((aligned(16))) float As[2][TBK][TBM + TPAD];
-  __shared__ __attribute__((aligned(16))) float Bs[2][TBK][TBN + TPAD];
+  __shared__ __attribute__((aligned(16))) float As[2][TBK * TLD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][TBK * TLD];
   const TgProb& P = batch.p[tg_find(batch, blockIdx.x)];
   const int local = blockIdx.x - P.tile_begin;
   const int s = local / P.tiles_mn, mn = local - s * P.tiles_mn;
@@ -92,73 +100,104 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
   const int m0 = tm * TBM, n0 = tn * TBN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
+  // the problem's scalars as values computed in registers (readfirstlane):
+  // the compiler would otherwise re-load them from the kernel arguments inside
+  // the k loop, and each such scalar load's wait also drains the outstanding
+  // LDS operations (one counter)
+  const int PM = rfl(P.M), PN = rfl(P.N), PK1 = rfl(P.K1), PK2 = rfl(P.K2);
   // this split's k steps over the concatenated K = K1 + K2 (each part padded
   // to whole k-steps)
-  const int nk1 = (P.K1 + TBK - 1) / TBK, nk = nk1 + (P.K2 + TBK - 1) / TBK;
-  const int kb = s * P.ksteps, ke = min(nk, kb + P.ksteps);
+  const int nk1 = (PK1 + TBK - 1) / TBK, nk = nk1 + (PK2 + TBK - 1) / TBK;
+  const int kb = rfl(s * P.ksteps), ke = min(nk, kb + rfl(P.ksteps));
   // op(A)(m, k) and op(B)(n, k): B enters as the (n x k) operand
-  const Opnd a1{P.A1, P.lda1, P.ta1, P.va1}, b1{P.B1, P.ldb1, !P.tb1, P.vb1};
-  const Opnd a2{P.A2, P.lda2, P.ta2, P.va2}, b2{P.B2, P.ldb2, !P.tb2, P.vb2};
-  float ra[4], rb[4];
-  auto load = [&](int kt) {
-    if (kt < nk1) {
-      tg_load(a1, m0, P.M, kt * TBK, P.K1, ra);
-      tg_load(b1, n0, P.N, kt * TBK, P.K1, rb);
-    } else {
-      tg_load(a2, m0, P.M, (kt - nk1) * TBK, P.K2, ra);
-      tg_load(b2, n0, P.N, (kt - nk1) * TBK, P.K2, rb);
+  OpB a1, b1, a2, b2;
+  opb_init(a1, P.A1, P.lda1, P.ta1, m0, PM, PK1);
+  opb_init(b1, P.B1, P.ldb1, !P.tb1, n0, PN, PK1);
+  opb_init(a2, P.A2, P.lda2, P.ta2, m0, PM, PK2);
+  opb_init(b2, P.B2, P.ldb2, !P.tb2, n0, PN, PK2);
+  float ra[NS][TEL], rb[NS][TEL];
+  // step kt's operands (kt >= ke: zeros, same instructions); the operand
+  // pair is selected arithmetically, not branched on
+  auto load1 = [&](const OpB& o1, const OpB& o2, bool first, bool live, int kl, int kmax, float (&x)[TEL]) {
+    const int soff = kl * (first ? o1.kstride : o2.kstride);
+#pragma unroll
+    for (int i = 0; i < TEL; ++i) {
+      const int vo = first ? o1.vo[i] : o2.vo[i];
+      const int kk = first ? o1.kk[i] : o2.kk[i];
+      const int v = (live && kl + kk < kmax) ? vo : OOB;
+      x[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(first ? o1.R : o2.R, v, soff, 0));
     }
   };
-  auto store = [&](int buf, int kt) {
-    if (kt < nk1) {
-      tg_store(a1, As[buf], ra);
-      tg_store(b1, Bs[buf], rb);
-    } else {
-      tg_store(a2, As[buf], ra);
-      tg_store(b2, Bs[buf], rb);
+  auto load = [&](int kt, float (&xa)[TEL], float (&xb)[TEL]) {
+    const bool live = kt < ke, first = kt < nk1;
+    const int kl = (first ? kt : kt - nk1) * TBK, kmax = first ? PK1 : PK2;
+    load1(a1, a2, first, live, kl, kmax, xa);
+    load1(b1, b2, first, live, kl, kmax, xb);
+  };
+  auto store = [&](int buf, int kt, const float (&xa)[TEL], const float (&xb)[TEL]) {
+    const bool first = kt < nk1;
+#pragma unroll
+    for (int i = 0; i < TEL; ++i) {
+      As[buf][first ? a1.lo[i] : a2.lo[i]] = xa[i];
+      Bs[buf][first ? b1.lo[i] : b2.lo[i]] = xb[i];
     }
   };
   f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   if (kb < ke) {
-    load(kb);
-    store(0, kb);
+#pragma unroll
+    for (int u = 0; u < NS - 1; ++u) load(kb + u, ra[u], rb[u]);
+    store(0, kb, ra[0], rb[0]);
     __syncthreads();
 #pragma unroll 1
-    for (int kt = kb; kt < ke; ++kt) {
-      const int buf = (kt - kb) & 1;
-      if (kt + 1 < ke) load(kt + 1);
+    for (int k0 = kb; k0 < ke; k0 += NS) {
 #pragma unroll
-      for (int kk = 0; kk < TBK; kk += 2) {
-        const float av = As[buf][kk + (lane >> 5)][wr * 32 + (lane & 31)];
-        const float bv = Bs[buf][kk + (lane >> 5)][wc * 32 + (lane & 31)];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      for (int u = 0; u < NS; ++u) {
+        const int kt = k0 + u;
+        // slot of step kt + NS - 1 is (u + NS - 1) % NS: the one step kt - 1 used
+        load(kt + NS - 1, ra[(u + NS - 1) % NS], rb[(u + NS - 1) % NS]);
+        if (kt < ke) {
+          const int buf = (kt - kb) & 1;
+#pragma unroll
+          for (int kk = 0; kk < TBK; kk += 2) {
+            const float av = As[buf][(kk + (lane >> 5)) * TLD + wr * 32 + (lane & 31)];
+            const float bv = Bs[buf][(kk + (lane >> 5)) * TLD + wc * 32 + (lane & 31)];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+          }
+        }
+        // step kt + 1 from its slot into the other LDS buffer
+        store((kt + 1 - kb) & 1, kt + 1, ra[(u + 1) % NS], rb[(u + 1) % NS]);
+        __syncthreads();
       }
-      if (kt + 1 < ke) store(buf ^ 1, kt + 1);
-      __syncthreads();
     }
   }
   const int col = n0 + wc * 32 + (lane & 31);
-  if (col >= P.N) return;
+  if (col >= PN) return;
   // D lane l, reg r: row 8 (r >> 2) + 4 (l >> 5) + (r & 3), column l & 31
-  if (P.splits > 1) {   // partial tile to this split's slab; k_tgemm_reduce finishes
-    float* w = P.ws + (int64_t)s * P.M * P.N;
+  auto row_of = [&](int r) { return m0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); };
+  typedef __attribute__((address_space(1))) float* gp;
+  if (rfl(P.splits) > 1) {   // partial tile to this split's slab; k_tgemm_reduce finishes
+    const gp w = (gp)(uintptr_t)rfl((int64_t)(uintptr_t)(P.ws + (int64_t)s * PM * PN));
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = m0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (row < P.M) w[(int64_t)row * P.N + col] = acc[r];
-    }
+    for (int r = 0; r < 16; ++r)
+      if (row_of(r) < PM) w[(int64_t)row_of(r) * PN + col] = acc[r];
     return;
   }
+  const gp C = (gp)(uintptr_t)rfl((int64_t)(uintptr_t)P.C);
+  const int64_t ldc = rfl(P.ldc);
+  const float alpha = __builtin_bit_cast(float, rfl(__builtin_bit_cast(int, P.alpha)));
+  float old[16];
+  if (rfl(P.beta)) {   // all 16 old values in flight at once
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = m0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row >= P.M) continue;
-    float* c = P.C + (int64_t)row * P.ldc + col;
-    const float v = P.alpha * acc[r];
-    *c = P.beta ? *c + v : v;
+    for (int r = 0; r < 16; ++r) old[r] = row_of(r) < PM ? C[(int64_t)row_of(r) * ldc + col] : 0.f;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) old[r] = 0.f;
   }
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if (row_of(r) < PM) C[(int64_t)row_of(r) * ldc + col] = old[r] + alpha * acc[r];
 }
 
 // C = beta C + alpha sum_s ws[s] over the split problems, s in order
@@ -181,24 +220,31 @@ __global__ __launch_bounds__(256) void k_tgemm_reduce(TgBatch batch) {
 
 }  // namespace
 
+// split-K policy (E3GNN_TG_SPLIT="min_ksteps,target_wgs,ksteps_per_split" for
+// A/B timing): split only a long K (the extra reduction launch costs ~5 us)
+static int tg_policy(int i) {
+  static int v[3] = {-1, -1, -1};
+  if (v[0] < 0) {
+    v[0] = 48, v[1] = 1024, v[2] = 16;
+    if (const char* e = std::getenv("E3GNN_TG_SPLIT")) std::sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]);
+  }
+  return v[i];
+}
 int tg_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
   const int64_t nk = (K + TBK - 1) / TBK;
-  // long K and few output tiles: split so the launch has ~512 tiles of >= 32
-  // k-steps each (the edge-summed weight gradients: K = 2E ~ 24k rows)
-  if (nk < 128 || tiles >= 256) return 1;
-  int64_t s = std::min<int64_t>(512 / std::max<int64_t>(tiles, 1), nk / 32);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 128));
+  // few output tiles and a long K (the edge-summed weight gradients: K = 2E
+  // ~ 24k rows onto 64 x 960 outputs): split K so the launch has ~target
+  // workgroups of >= ksteps_per_split k-steps each
+  if (tiles >= tg_policy(1) / 2 || nk < tg_policy(0)) return 1;
+  int64_t s = std::min<int64_t>((tg_policy(1) + tiles - 1) / tiles, nk / tg_policy(2));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 256));
 }
 
 bool tg_add(TgBatch& b, TgProb p) {
   if (b.nprob >= TG_MAX_PROBS || p.M < 0 || p.N < 0 || p.K1 < 0 || p.K2 < 0) return false;
   if (p.M == 0 || p.N == 0) return true;
-  auto al = [](const void* q, int64_t ld) { return ((uintptr_t)q & 15) == 0 && ld % 4 == 0; };
-  p.va1 = al(p.A1, p.lda1);
-  p.vb1 = al(p.B1, p.ldb1);
-  p.va2 = p.K2 > 0 ? al(p.A2, p.lda2) : 0;
-  p.vb2 = p.K2 > 0 ? al(p.B2, p.ldb2) : 0;
+  if (p.K2 == 0) p.A2 = p.A1, p.B2 = p.B1, p.lda2 = p.lda1, p.ldb2 = p.ldb1;  // never read
   const int nk = (p.K1 + TBK - 1) / TBK + (p.K2 + TBK - 1) / TBK;
   p.tiles_n = (p.N + TBN - 1) / TBN;
   p.tiles_mn = ((p.M + TBM - 1) / TBM) * p.tiles_n;

@@ -416,6 +416,17 @@ def collate(graphs, device=None, dtype=None):
     for k in (KEY.EDGE_VEC, KEY.CELL_SHIFT):
         if k in edges:
             out[k] = torch.cat(edges[k], 0)
+    # edges stably sorted by centre here, on the host (the neighbour lists
+    # already are: a no-op permutation then), so the captured step needs no
+    # device sort (GraphedStep._centre_sorted)
+    cen = out[KEY.EDGE_IDX][0].numpy()
+    if cen.size > 1 and (cen[1:] < cen[:-1]).any():
+        perm = torch.from_numpy(np.argsort(cen, kind='stable'))
+        out[KEY.EDGE_IDX] = out[KEY.EDGE_IDX][:, perm]
+        for k in (KEY.EDGE_VEC, KEY.CELL_SHIFT):
+            if k in out:
+                out[k] = out[k][perm]
+    out[KEY.EDGE_SORTED] = torch.tensor(True)
     for k, v in pg.items():
         if v:
             t = torch.cat(v, 0)
@@ -810,10 +821,11 @@ class GraphedRehearsalStep:
     @staticmethod
     def _centre_sorted(b):
         """The captured model takes a prebuilt ConvGraph, i.e. edges CSR-sorted
-        by centre (the eager model sorts them itself): stable device argsort
-        of the per-edge entries, no host sync."""
+        by centre (the eager model sorts them itself).  Batches from collate()
+        are sorted on the host already (EDGE_SORTED); anything else gets a
+        stable device argsort of the per-edge entries, no host sync."""
         ei = b.get(KEY.EDGE_IDX)
-        if ei is None or ei.shape[1] < 2:
+        if ei is None or ei.shape[1] < 2 or KEY.EDGE_SORTED in b:   # (collate sorted it)
             return b
         perm = torch.argsort(ei[0], stable=True)
         out = dict(b)

@@ -144,13 +144,10 @@ class _Gemms:
 
     def add(self, C, A, B, alpha=1.0, beta=0, A2=None, B2=None):
         if not self._hip(C, A, B, *(t for t in (A2, B2) if t is not None)):
-            v = torch.mm(A, B)
+            # straight into C (no temporaries / copy kernels)
+            torch.addmm(C, A, B, beta=1 if beta else 0, alpha=alpha, out=C)
             if A2 is not None:
-                v = v + torch.mm(A2, B2)
-            if beta:
-                C.add_(v, alpha=alpha)
-            else:
-                torch.mul(v, alpha, out=C) if alpha != 1.0 else C.copy_(v)
+                C.addmm_(A2, B2, alpha=alpha)
             return C
         ops = [self._op(A), self._op(B)] + ([self._op(A2), self._op(B2)] if A2 is not None else [])
         if any(o is None for o in ops) or C.stride(1) != 1:
@@ -820,7 +817,8 @@ class ExplicitStep:
         center, nbr = ei[0], ei[1]
         perm = None
         if graph is None:
-            if center.numel() > 1 and bool((center[1:] < center[:-1]).any()):
+            if (KEY.EDGE_SORTED not in data and center.numel() > 1
+                    and bool((center[1:] < center[:-1]).any())):
                 perm = torch.argsort(center, stable=True)
                 center, nbr = center[perm], nbr[perm]
             graph = conv_ops.ConvGraph(n, center, nbr, m.conv_backend)
