@@ -102,6 +102,13 @@ typedef struct e3gnn_gemm_desc {
   int32_t trans_a, trans_b, trans_a2, trans_b2;
   float alpha;
   int32_t beta;
+  /* optional block sparsity (nullable): per output tile (64 x 64; tile
+   * (tm, tn) reads entry tm * krange_stride_m + tn) four int32 -- the k
+   * ranges [lo1, hi1) of the first operand pair and [lo2, hi2) of the second
+   * that can be nonzero; the product skips the rest (a linear's dense matrix
+   * is block-diagonal by l).  krange_stride_m = 0: one entry per column tile. */
+  const int32_t* krange;
+  int32_t krange_stride_m;
 } e3gnn_gemm_desc;
 int64_t e3gnn_gemm_workspace_floats(int n, const e3gnn_gemm_desc* d);
 int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,

@@ -104,7 +104,8 @@ class GemmDesc(ctypes.Structure):
                 ('ldc', _c_i64), ('m', ctypes.c_int32), ('n', ctypes.c_int32),
                 ('k', ctypes.c_int32), ('k2', ctypes.c_int32), ('trans_a', ctypes.c_int32),
                 ('trans_b', ctypes.c_int32), ('trans_a2', ctypes.c_int32),
-                ('trans_b2', ctypes.c_int32), ('alpha', ctypes.c_float), ('beta', ctypes.c_int32)]
+                ('trans_b2', ctypes.c_int32), ('alpha', ctypes.c_float), ('beta', ctypes.c_int32),
+                ('krange', _vp), ('krange_stride_m', ctypes.c_int32)]
 
 
 class E3GNNError(RuntimeError):

@@ -1066,6 +1066,7 @@ int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_
     p.M = q.m; p.N = q.n; p.K1 = q.k; p.K2 = q.k2;
     p.ta1 = q.trans_a; p.tb1 = q.trans_b; p.ta2 = q.trans_a2; p.tb2 = q.trans_b2;
     p.alpha = q.alpha; p.beta = q.beta;
+    p.kr = q.krange; p.kr_sm = q.krange_stride_m;
     p.splits = tg_splits(q.m, q.n, (int64_t)q.k + q.k2);
     if (p.splits > 1) {
       const int64_t need = (int64_t)p.splits * q.m * q.n;

@@ -19,6 +19,8 @@ struct TgProb {
   float alpha;
   int beta;
   int splits;  // requested (tg_add settles it)
+  const int* kr;  // per-tile k ranges [lo1, hi1, lo2, hi2) (nullable; e3gnn_gemm_desc::krange)
+  int kr_sm;      // its row-tile stride (0: per column tile)
   // set by tg_add
   int tiles_n, tiles_mn, ksteps, tile_begin;
   int64_t red_begin;

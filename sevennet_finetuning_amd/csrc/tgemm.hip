@@ -108,7 +108,20 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
   // this split's k steps over the concatenated K = K1 + K2 (each part padded
   // to whole k-steps)
   const int nk1 = (PK1 + TBK - 1) / TBK, nk = nk1 + (PK2 + TBK - 1) / TBK;
-  const int kb = rfl(s * P.ksteps), ke = min(nk, kb + rfl(P.ksteps));
+  // the tile's k-step ranges (block sparsity): [kb1, ke1) of the first pair,
+  // [nk1 + kb2, nk1 + ke2) of the second; step j of the tile's sequence is
+  // kb1 + j (j < n1) or nk1 + kb2 + j - n1.  This split's slice of it:
+  // [jb, je) (a split past the tile's steps has none: zero partials)
+  int kb1 = 0, n1 = nk1, kb2 = 0, n2 = nk - nk1;
+  if (P.kr) {
+    const int* q = P.kr + 4 * (tm * P.kr_sm + tn);
+    kb1 = rfl(q[0] / TBK);
+    n1 = max(0, rfl((q[1] + TBK - 1) / TBK) - kb1);
+    kb2 = rfl(q[2] / TBK);
+    n2 = max(0, rfl((q[3] + TBK - 1) / TBK) - kb2);
+  }
+  const int jb = rfl(s * P.ksteps), je = min(n1 + n2, jb + rfl(P.ksteps));
+  auto kt_of = [&](int j) { return j < n1 ? kb1 + j : nk1 + kb2 + (j - n1); };
   // op(A)(m, k) and op(B)(n, k): B enters as the (n x k) operand
   OpB a1, b1, a2, b2;
   opb_init(a1, P.A1, P.lda1, P.ta1, m0, PM, PK1);
@@ -116,7 +129,7 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
   opb_init(a2, P.A2, P.lda2, P.ta2, m0, PM, PK2);
   opb_init(b2, P.B2, P.ldb2, !P.tb2, n0, PN, PK2);
   float ra[NS][TEL], rb[NS][TEL];
-  // step kt's operands (kt >= ke: zeros, same instructions); the operand
+  // step j's operands (j >= je: zeros, same instructions); the operand
   // pair is selected arithmetically, not branched on
   auto load1 = [&](const OpB& o1, const OpB& o2, bool first, bool live, int kl, int kmax, float (&x)[TEL]) {
     const int soff = kl * (first ? o1.kstride : o2.kstride);
@@ -128,14 +141,15 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
       x[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(first ? o1.R : o2.R, v, soff, 0));
     }
   };
-  auto load = [&](int kt, float (&xa)[TEL], float (&xb)[TEL]) {
-    const bool live = kt < ke, first = kt < nk1;
+  auto load = [&](int j, float (&xa)[TEL], float (&xb)[TEL]) {
+    const int kt = kt_of(j);
+    const bool live = j < je, first = kt < nk1;
     const int kl = (first ? kt : kt - nk1) * TBK, kmax = first ? PK1 : PK2;
     load1(a1, a2, first, live, kl, kmax, xa);
     load1(b1, b2, first, live, kl, kmax, xb);
   };
-  auto store = [&](int buf, int kt, const float (&xa)[TEL], const float (&xb)[TEL]) {
-    const bool first = kt < nk1;
+  auto store = [&](int buf, int j, const float (&xa)[TEL], const float (&xb)[TEL]) {
+    const bool first = kt_of(j) < nk1;
 #pragma unroll
     for (int i = 0; i < TEL; ++i) {
       As[buf][first ? a1.lo[i] : a2.lo[i]] = xa[i];
@@ -145,20 +159,20 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
   f32x16 acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  if (kb < ke) {
+  if (jb < je) {
 #pragma unroll
-    for (int u = 0; u < NS - 1; ++u) load(kb + u, ra[u], rb[u]);
-    store(0, kb, ra[0], rb[0]);
+    for (int u = 0; u < NS - 1; ++u) load(jb + u, ra[u], rb[u]);
+    store(0, jb, ra[0], rb[0]);
     __syncthreads();
 #pragma unroll 1
-    for (int k0 = kb; k0 < ke; k0 += NS) {
+    for (int j0 = jb; j0 < je; j0 += NS) {
 #pragma unroll
       for (int u = 0; u < NS; ++u) {
-        const int kt = k0 + u;
-        // slot of step kt + NS - 1 is (u + NS - 1) % NS: the one step kt - 1 used
-        load(kt + NS - 1, ra[(u + NS - 1) % NS], rb[(u + NS - 1) % NS]);
-        if (kt < ke) {
-          const int buf = (kt - kb) & 1;
+        const int j = j0 + u;
+        // slot of step j + NS - 1 is (u + NS - 1) % NS: the one step j - 1 used
+        load(j + NS - 1, ra[(u + NS - 1) % NS], rb[(u + NS - 1) % NS]);
+        if (j < je) {
+          const int buf = (j - jb) & 1;
 #pragma unroll
           for (int kk = 0; kk < TBK; kk += 2) {
             const float av = As[buf][(kk + (lane >> 5)) * TLD + wr * 32 + (lane & 31)];
@@ -166,11 +180,13 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
           }
         }
-        // step kt + 1 from its slot into the other LDS buffer
-        store((kt + 1 - kb) & 1, kt + 1, ra[(u + 1) % NS], rb[(u + 1) % NS]);
+        // step j + 1 from its slot into the other LDS buffer
+        store((j + 1 - jb) & 1, j + 1, ra[(u + 1) % NS], rb[(u + 1) % NS]);
         __syncthreads();
       }
     }
+  } else if (P.kr && rfl(P.beta) && rfl(P.splits) <= 1) {
+    return;   // nothing to add to this tile
   }
   const int col = n0 + wc * 32 + (lane & 31);
   if (col >= PN) return;
@@ -207,11 +223,23 @@ __global__ __launch_bounds__(256) void k_tgemm_reduce(TgBatch batch) {
   for (int p = 0; p < batch.nprob; ++p) {
     const TgProb& P = batch.p[p];
     if (P.splits <= 1 || i < P.red_begin || i >= P.red_begin + (int64_t)P.M * P.N) continue;
-    const int64_t e = i - P.red_begin;
+    const int64_t e = i - P.red_begin, mn = (int64_t)P.M * P.N;
     const int row = (int)(e / P.N), col = (int)(e - (int64_t)row * P.N);
+    // slabs 0, 1, 2, ... added in order; eight loads in flight at a time (a
+    // split count of ~70 read one dependent load at a time took ~70 latencies)
+    const float* w = P.ws + e;
     float sum = 0.f;
+    int s = 0;
 #pragma unroll 1
-    for (int s = 0; s < P.splits; ++s) sum += P.ws[(int64_t)s * P.M * P.N + e];
+    for (; s + 8 <= P.splits; s += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = w[(int64_t)(s + u) * mn];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += v[u];
+    }
+#pragma unroll 1
+    for (; s < P.splits; ++s) sum += w[(int64_t)s * mn];
     float* c = P.C + (int64_t)row * P.ldc + col;
     const float v = P.alpha * sum;
     *c = P.beta ? *c + v : v;

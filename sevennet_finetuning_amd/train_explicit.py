@@ -142,7 +142,9 @@ class _Gemms:
             return x.data_ptr(), (s1 if k > 1 else max(r, 1)), 1
         return None
 
-    def add(self, C, A, B, alpha=1.0, beta=0, A2=None, B2=None):
+    def add(self, C, A, B, alpha=1.0, beta=0, A2=None, B2=None, kr=None):
+        """kr: (int32 device tensor, row-tile stride) of per-tile k ranges (the
+        dense matrices' block sparsity, e3gnn_gemm_desc::krange) or None"""
         if not self._hip(C, A, B, *(t for t in (A2, B2) if t is not None)):
             # straight into C (no temporaries / copy kernels)
             torch.addmm(C, A, B, beta=1 if beta else 0, alpha=alpha, out=C)
@@ -159,7 +161,7 @@ class _Gemms:
                 raise ValueError('GEMM output must be row-major')
         if len(self.q) == 8:
             self.flush()
-        self.q.append((C, A, B, A2, B2, ops, float(alpha), int(bool(beta))))
+        self.q.append((C, A, B, A2, B2, ops, float(alpha), int(bool(beta)), kr))
         return C
 
     def flush(self):
@@ -169,7 +171,7 @@ class _Gemms:
         n = len(self.q)
         descs = (_lib.GemmDesc * n)()
         keep = []
-        for i, (C, A, B, A2, B2, ops, alpha, beta) in enumerate(self.q):
+        for i, (C, A, B, A2, B2, ops, alpha, beta, kr) in enumerate(self.q):
             d = descs[i]
             d.a, d.lda, d.trans_a = ops[0]
             d.b, d.ldb, d.trans_b = ops[1]
@@ -180,6 +182,8 @@ class _Gemms:
             d.c, d.ldc = C.data_ptr(), C.stride(0)
             d.m, d.n, d.k = int(C.shape[0]), int(C.shape[1]), int(A.shape[1])
             d.alpha, d.beta = alpha, beta
+            if kr is not None:
+                d.krange, d.krange_stride_m = kr[0].data_ptr(), kr[1]
             keep.append((C, A, B, A2, B2))
         need = int(self.lib.e3gnn_gemm_workspace_floats(n, descs))
         dev = self.q[0][0].device
@@ -659,6 +663,9 @@ class ExplicitStep:
         self.fold_den = not any(model.param(d).requires_grad for d in dens)
         self.bank = _DenseBank(model, ent, {f'si2{t}': d for t, d in enumerate(dens)}
                                if self.fold_den else None)
+        self._lins = {key: lin for key, lin, _ in ent}
+        self._dims = {key: (lin.in_off[-1], lin.out_off[-1]) for key, lin, _ in ent}
+        self._kr_cache = {}
         # the radial MLP weights of every block, scaled by 1/sqrt(fan-in)
         # (e3nn FullyConnectedNet), gathered into one buffer by one launch
         idx, scl, self.mlp_views = [], [], []
@@ -688,11 +695,64 @@ class ExplicitStep:
     def _P(self, name):
         return self.m.param(name)
 
-    def _mm(self, C, A, B, alpha=1.0, beta=0, A2=None, B2=None):
+    def _mm(self, C, A, B, alpha=1.0, beta=0, A2=None, B2=None, kr=None):
         """one product now (its result is needed next)"""
-        self.gm.add(C, A, B, alpha, beta, A2, B2)
+        self.gm.add(C, A, B, alpha, beta, A2, B2, kr=kr)
         self.gm.flush()
         return C
+
+    # ---- block sparsity of the dense linear matrices (e3gnn_gemm_desc::krange)
+    def _lin_blocks(self, key, trans=False):
+        """(row range, column range) of every nonzero block of key's dense
+        matrix (din x dout; trans: of its transpose)"""
+        lin = self._lins[key]
+        out = []
+        for i, j in lin.ins:
+            r = (lin.in_off[i], lin.in_off[i] + lin.irreps_in[i][0] * (2 * lin.irreps_in[i][1] + 1))
+            c = (lin.out_off[j], lin.out_off[j] + lin.irreps_out[j][0] * (2 * lin.irreps_out[j][1] + 1))
+            out.append((c, r) if trans else (r, c))
+        return out
+
+    def _kr(self, part1, part2=None, grad=None):
+        """per-tile k ranges of a product with the dense matrices on its right:
+        part1 / part2 = (key, trans) of C = A op(D) [+ A2 op(D2)] -- for each
+        64-column tile of C the hull of the k rows of op(D) that are nonzero in
+        it; grad = key: C = A^T B is key's dense gradient (din x dout), tiles
+        that meet no block get an empty range (nothing is added there).
+        (device int32 tensor, row-tile stride), cached."""
+        ck = (part1, part2, grad)
+        if ck in self._kr_cache:
+            return self._kr_cache[ck]
+        T = 64
+        if grad is not None:
+            bl = self._lin_blocks(grad)
+            din, dout = self._dims[grad]
+            tm, tn = -(-din // T), -(-dout // T)
+            tab = np.zeros((tm, tn, 4), dtype=np.int32)
+            for a in range(tm):
+                for b in range(tn):
+                    if any(r0 < (a + 1) * T and r1 > a * T and c0 < (b + 1) * T and c1 > b * T
+                           for (r0, r1), (c0, c1) in bl):
+                        tab[a, b, 1] = 1 << 30          # the whole K
+            res = (torch.as_tensor(tab.ravel(), device=self.m.flat.device), tn)
+        else:
+            def hull(key, trans, ncol):
+                bl = self._lin_blocks(key, trans)
+                out = np.zeros((-(-ncol // T), 2), dtype=np.int32)
+                for b in range(out.shape[0]):
+                    rows = [(r0, r1) for (r0, r1), (c0, c1) in bl if c0 < (b + 1) * T and c1 > b * T]
+                    if rows:
+                        out[b] = (min(r for r, _ in rows), max(r for _, r in rows))
+                return out
+            d1 = self._dims[part1[0]]
+            ncol = d1[0] if part1[1] else d1[1]
+            tab = np.zeros((-(-ncol // T), 4), dtype=np.int32)
+            tab[:, :2] = hull(part1[0], part1[1], ncol)
+            if part2 is not None:
+                tab[:, 2:] = hull(part2[0], part2[1], ncol)
+            res = (torch.as_tensor(tab.ravel(), device=self.m.flat.device), 0)
+        self._kr_cache[ck] = res
+        return res
 
     # ---- si2 products over its instruction blocks (views, no copies)
     def _si2_fwd(self, t, A, Dm, out):
@@ -704,7 +764,7 @@ class ExplicitStep:
         """A Dm^T (cotangent rows of the mid irreps)"""
         if self.dense_si2:
             return self._mm(torch.empty(A.shape[0], Dm.shape[0], device=A.device, dtype=A.dtype),
-                            A, Dm.t())
+                            A, Dm.t(), kr=self._kr((f'si2{t}', True)))
         bl, gaps = self.si2_blocks[t]
         out = torch.empty(A.shape[0], Dm.shape[0], device=A.device, dtype=A.dtype)
         seen = set()
@@ -846,7 +906,7 @@ class ExplicitStep:
             W0, W1, W2 = MW[t]
             x = X[:n]
             H = new(2 * n, D[f'si1{t}'].shape[1])
-            self._mm(H[:n], x, D[f'si1{t}'])
+            self._mm(H[:n], x, D[f'si1{t}'], kr=self._kr((f'si1{t}', False)))
             A1, H1 = new(2 * E, W0.shape[1]), new(2 * E, W0.shape[1])
             A2, H2 = new(2 * E, W1.shape[1]), new(2 * E, W1.shape[1])
             WT = new(2 * E, W2.shape[1])
@@ -858,7 +918,8 @@ class ExplicitStep:
                 AGG[:n].div_(den)
             Yg = new(2 * n, D[f'si2{t}'].shape[1])
             if self.dense_si2:                              # x sc + agg si2: one product
-                self._mm(Yg[:n], x, D[f'sc{t}'], A2=AGG[:n], B2=D[f'si2{t}'])
+                self._mm(Yg[:n], x, D[f'sc{t}'], A2=AGG[:n], B2=D[f'si2{t}'],
+                         kr=self._kr((f'sc{t}', False), (f'si2{t}', False)))
             else:
                 self._mm(Yg[:n], x, D[f'sc{t}'])            # (GEMM into the output, then
                 self._si2_fwd(t, AGG[:n], D[f'si2{t}'], Yg[:n])  # accumulate: no bias copy)
@@ -892,7 +953,8 @@ class ExplicitStep:
                                     acc=ACC_DY if t < len(blocks) - 1 else 0)
             self._mlp_rev(wb, b['W'], b['A1'][:E], b['A2'][:E], embb)
             if t > 0:
-                xb = self._mm(new(n, hb.shape[1]), hb, D[f'si1{t}'].t(), A2=yb, B2=D[f'sc{t}'].t())
+                xb = self._mm(new(n, hb.shape[1]), hb, D[f'si1{t}'].t(), A2=yb, B2=D[f'sc{t}'].t(),
+                              kr=self._kr((f'si1{t}', True), (f'sc{t}', True)))
         fij = self.geo.vjp(g, Yb, embb)                    # dE/dr_e, centre-sorted order
         S['fij'] = fij
         aux = graph.aux
@@ -949,7 +1011,7 @@ class ExplicitStep:
             aggd = AGG[n:]                       # C(h, Y', w) + C(h, Y, w') + C(h', Y, w)
             X = b['X']
             if t > 0:
-                self._mm(b['H'][n:], X[n:], D[f'si1{t}'])
+                self._mm(b['H'][n:], X[n:], D[f'si1{t}'], kr=self._kr((f'si1{t}', False)))
             hd = b['H'][n:] if t > 0 else None   # x0' = 0: no h' term
             if fused:
                 be.tangent_forward(k, graph, h, hd, Y, Yd, w, WT[E:], out=aggd)
@@ -962,9 +1024,10 @@ class ExplicitStep:
                 aggd.div_(b['den'])
             if self.dense_si2:
                 if t > 0:
-                    self._mm(Yg[n:], X[n:], D[f'sc{t}'], A2=AGG[n:], B2=D[f'si2{t}'])
+                    self._mm(Yg[n:], X[n:], D[f'sc{t}'], A2=AGG[n:], B2=D[f'si2{t}'],
+                             kr=self._kr((f'sc{t}', False), (f'si2{t}', False)))
                 else:                            # x0' = 0
-                    self._mm(Yg[n:], AGG[n:], D[f'si2{t}'])
+                    self._mm(Yg[n:], AGG[n:], D[f'si2{t}'], kr=self._kr((f'si2{t}', False)))
             else:
                 if t > 0:
                     self._mm(Yg[n:], X[n:], D[f'sc{t}'])
@@ -1010,9 +1073,9 @@ class ExplicitStep:
                 # independent products of y-bar, one launch: si2's and sc's weight
                 # gradients and agg-bar
                 AGGB = new(2 * n, D[f'si2{t}'].shape[0])
-                self.gm.add(G[f'si2{t}'], AGG.t(), YB, beta=1)
-                self.gm.add(AGGB, YB, D[f'si2{t}'].t())
-                self.gm.add(G[f'sc{t}'], X.t(), YB, beta=1)
+                self.gm.add(G[f'si2{t}'], AGG.t(), YB, beta=1, kr=self._kr(None, grad=f'si2{t}'))
+                self.gm.add(AGGB, YB, D[f'si2{t}'].t(), kr=self._kr((f'si2{t}', True)))
+                self.gm.add(G[f'sc{t}'], X.t(), YB, beta=1, kr=self._kr(None, grad=f'sc{t}'))
                 self.gm.flush()
             else:
                 self._si2_wgrad(t, G[f'si2{t}'], AGG, YB)
@@ -1056,9 +1119,10 @@ class ExplicitStep:
                 if gw is not None:
                     self.gm.add(gw, rows.t(), cot, 1.0 / math.sqrt(Wl.shape[0]), beta=1)
             # self-interaction 1 (sc-bar = y-bar, added above) and the input cotangent
-            self.gm.add(G[f'si1{t}'], X.t(), HB, beta=1)
+            self.gm.add(G[f'si1{t}'], X.t(), HB, beta=1, kr=self._kr(None, grad=f'si1{t}'))
             XB = new(2 * n, D[f'si1{t}'].shape[0])
-            self.gm.add(XB, HB, D[f'si1{t}'].t(), A2=YB, B2=D[f'sc{t}'].t())
+            self.gm.add(XB, HB, D[f'si1{t}'].t(), A2=YB, B2=D[f'sc{t}'].t(),
+                        kr=self._kr((f'si1{t}', True), (f'sc{t}', True)))
             self.gm.flush()
         # embedding (x0 = W[types] / sqrt(nsp)) and the radial basis coefficients
         gemb = self._G('onehot_to_feature_x.linear.weight')

@@ -46,8 +46,7 @@ def main():
 
     def flush(self):
         if self.q:
-            rec.append([(C, A, B, A2, B2, ops, alpha, beta)
-                        for (C, A, B, A2, B2, ops, alpha, beta) in self.q])
+            rec.append(list(self.q))
         return orig(self)
     train_explicit._Gemms.flush = flush
     tr.rehearsal_step(b[0], b[1])
@@ -75,7 +74,7 @@ def main():
         n = len(q)
         descs = (_lib.GemmDesc * n)()
         shapes = []
-        for j, (C, A, B, A2, B2, ops, alpha, beta) in enumerate(q):
+        for j, (C, A, B, A2, B2, ops, alpha, beta, kr) in enumerate(q):
             d = descs[j]
             d.a, d.lda, d.trans_a = ops[0]
             d.b, d.ldb, d.trans_b = ops[1]
@@ -86,6 +85,8 @@ def main():
             d.c, d.ldc = C.data_ptr(), C.stride(0)
             d.m, d.n, d.k = int(C.shape[0]), int(C.shape[1]), int(A.shape[1])
             d.alpha, d.beta = alpha, beta
+            if kr is not None:
+                d.krange, d.krange_stride_m = kr[0].data_ptr(), kr[1]
             shapes.append(f"{d.m}x{d.n}x{d.k}{'+' + str(d.k2) if d.k2 else ''}"
                           f"{'T' if d.trans_a else 'N'}{'T' if d.trans_b else 'N'}")
         stream = torch.cuda.current_stream(dev).cuda_stream
@@ -93,7 +94,7 @@ def main():
                                                              stream)))
 
         def tor():
-            for (C, A, B, A2, B2, ops, alpha, beta) in q:
+            for (C, A, B, A2, B2, ops, alpha, beta, kr) in q:
                 torch.addmm(C, A, B, beta=1 if beta else 0, alpha=alpha, out=C)
                 if A2 is not None:
                     C.addmm_(A2, B2, alpha=alpha)
