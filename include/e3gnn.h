@@ -91,6 +91,22 @@ int e3gnn_model_info(const e3gnn_model* m, int* num_species, float* cutoff, int*
  * problems per call (their outputs must not overlap); long-K problems are split
  * over K into `workspace` (e3gnn_gemm_workspace_floats floats) and reduced in a
  * fixed order: deterministic, no atomics. */
+/* General operand layout of a grouped-GEMM problem (e3gnn_gemm_desc::layout):
+ * element (i, k) of op(A) (i = row m) or of op(B)^T (i = column n) at
+ *   X[(i / rep) * ld + (i % rep) * rs + (k % ks) * kst + (k / ks) * sst]
+ * (X, K from the descriptor; K a whole number of ks-row segments) -- e.g. an
+ * e3nn irreps block [node][mul][2l+1] as rows (node, m) (rep = 2l + 1), or a
+ * linear's weight gradient summed over K = (m, node) segments.  C(m, n) at
+ * c[(m / crep) * ldc + (m % crep) * crs + n * cns]. */
+typedef struct e3gnn_gemm_layout {
+  int64_t ld, kst, sst;
+  int32_t rep, rs, ks;
+} e3gnn_gemm_layout;
+typedef struct e3gnn_gemm_layouts {
+  e3gnn_gemm_layout a, b, a2, b2;
+  int64_t ldc;
+  int32_t crep, crs, cns;
+} e3gnn_gemm_layouts;
 typedef struct e3gnn_gemm_desc {
   const float* a;
   const float* b;
@@ -109,6 +125,8 @@ typedef struct e3gnn_gemm_desc {
    * is block-diagonal by l).  krange_stride_m = 0: one entry per column tile. */
   const int32_t* krange;
   int32_t krange_stride_m;
+  /* nullable: the general layouts (then lda.. / trans_* / ldc are unused) */
+  const e3gnn_gemm_layouts* layout;
 } e3gnn_gemm_desc;
 int64_t e3gnn_gemm_workspace_floats(int n, const e3gnn_gemm_desc* d);
 int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,

@@ -97,6 +97,19 @@ SIGNATURES = {
 }
 
 
+class GemmLayout(ctypes.Structure):
+    """e3gnn_gemm_layout (include/e3gnn.h)"""
+    _fields_ = [('ld', _c_i64), ('kst', _c_i64), ('sst', _c_i64), ('rep', ctypes.c_int32),
+                ('rs', ctypes.c_int32), ('ks', ctypes.c_int32)]
+
+
+class GemmLayouts(ctypes.Structure):
+    """e3gnn_gemm_layouts (include/e3gnn.h)"""
+    _fields_ = [('a', GemmLayout), ('b', GemmLayout), ('a2', GemmLayout), ('b2', GemmLayout),
+                ('ldc', _c_i64), ('crep', ctypes.c_int32), ('crs', ctypes.c_int32),
+                ('cns', ctypes.c_int32)]
+
+
 class GemmDesc(ctypes.Structure):
     """e3gnn_gemm_desc (include/e3gnn.h)"""
     _fields_ = [('a', _vp), ('b', _vp), ('a2', _vp), ('b2', _vp), ('c', _vp),
@@ -105,7 +118,7 @@ class GemmDesc(ctypes.Structure):
                 ('k', ctypes.c_int32), ('k2', ctypes.c_int32), ('trans_a', ctypes.c_int32),
                 ('trans_b', ctypes.c_int32), ('trans_a2', ctypes.c_int32),
                 ('trans_b2', ctypes.c_int32), ('alpha', ctypes.c_float), ('beta', ctypes.c_int32),
-                ('krange', _vp), ('krange_stride_m', ctypes.c_int32)]
+                ('krange', _vp), ('krange_stride_m', ctypes.c_int32), ('layout', _vp)]
 
 
 class E3GNNError(RuntimeError):

@@ -1051,7 +1051,7 @@ int64_t e3gnn_gemm_workspace_floats(int n, const e3gnn_gemm_desc* d) {
 int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,
                        void* stream) {
   if (n < 0 || n > TG_MAX_PROBS || (n > 0 && !d))
-    return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: 0..8 problems");
+    return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: 0.." + std::to_string(TG_MAX_PROBS) + " problems");
   TgBatch b;
   int64_t used = 0;
   for (int i = 0; i < n; ++i) {
@@ -1061,10 +1061,27 @@ int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_
       return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: bad problem " + std::to_string(i));
     if (q.beta != 0 && q.beta != 1) return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: beta must be 0 or 1");
     TgProb p{};
-    p.A1 = q.a; p.B1 = q.b; p.A2 = q.a2; p.B2 = q.b2; p.C = q.c;
-    p.lda1 = q.lda; p.ldb1 = q.ldb; p.lda2 = q.lda2; p.ldb2 = q.ldb2; p.ldc = q.ldc;
+    // op(A)(m, k): X[m][k] (ld, k contiguous) or X[k][m]; op(B)(k, n) as
+    // element (n, k): B[k][n] or B[n][k]
+    auto lay = [](const float* X, int64_t ld, bool kfast, int K) {
+      return TgLay{X, kfast ? (int)ld : 1, kfast ? 1 : (int)ld, 0, 1, 0, K};
+    };
+    auto glay = [](const float* X, const e3gnn_gemm_layout& g) {
+      return TgLay{X, (int)g.ld, (int)g.kst, (int)g.sst, g.rep, g.rs, g.ks};
+    };
+    if (q.layout) {
+      const e3gnn_gemm_layouts& L = *q.layout;
+      p.A1 = glay(q.a, L.a); p.B1 = glay(q.b, L.b); p.A2 = glay(q.a2, L.a2); p.B2 = glay(q.b2, L.b2);
+      p.ldc = L.ldc; p.crep = L.crep; p.crs = L.crs; p.cns = L.cns;
+    } else {
+      p.A1 = lay(q.a, q.lda, !q.trans_a, q.k);
+      p.B1 = lay(q.b, q.ldb, q.trans_b, q.k);
+      p.A2 = lay(q.a2, q.lda2, !q.trans_a2, q.k2);
+      p.B2 = lay(q.b2, q.ldb2, q.trans_b2, q.k2);
+      p.ldc = q.ldc; p.crep = 1; p.crs = 0; p.cns = 1;
+    }
+    p.C = q.c;
     p.M = q.m; p.N = q.n; p.K1 = q.k; p.K2 = q.k2;
-    p.ta1 = q.trans_a; p.tb1 = q.trans_b; p.ta2 = q.trans_a2; p.tb2 = q.trans_b2;
     p.alpha = q.alpha; p.beta = q.beta;
     p.kr = q.krange; p.kr_sm = q.krange_stride_m;
     p.splits = tg_splits(q.m, q.n, (int64_t)q.k + q.k2);

@@ -9,13 +9,25 @@ namespace e3gnn {
 
 // C = beta C + alpha (op(A1) op(B1) + op(A2) op(B2)); op(X) = X^T when t* is set
 // (row-major storage, leading dimensions ld*); K2 = 0: no second pair
+// One operand of a pair in the general layout: element (i, k) of op(A)
+// (i = row m) or op(B)^T (i = column n) sits at
+//   X[(i / rep) * ld + (i % rep) * rs + (k % ks) * kst + (k / ks) * sst]
+// -- plain row-major / transposed matrices (rep 1, one segment), the e3nn
+// irreps layout ([node][mul][2l+1]: rows (node, m), rep = 2l + 1) and K
+// summed over (m, node) segments (a linear's weight gradient).
+struct TgLay {
+  const float* X;
+  int ld, kst, sst;  // element strides (byte offsets are 32-bit: < 2 GB per operand)
+  int rep, rs, ks;   // ks: rows of one K segment (the part's K: one segment)
+};
 struct TgProb {
-  const float *A1, *B1, *A2, *B2;
+  TgLay A1, B1, A2, B2;
   float* C;
   float* ws;  // split-K partial slabs [splits][M][N] (splits > 1)
-  int64_t lda1, ldb1, lda2, ldb2, ldc;
-  int M, N, K1, K2;
-  int ta1, tb1, ta2, tb2;
+  // C(m, n) = C[(m / crep) * ldc + (m % crep) * crs + n * cns]
+  int64_t ldc;
+  int crep, crs, cns;
+  int M, N, K1, K2;   // K1, K2: whole segments (segments x ks)
   float alpha;
   int beta;
   int splits;  // requested (tg_add settles it)
@@ -25,7 +37,7 @@ struct TgProb {
   int tiles_n, tiles_mn, ksteps, tile_begin;
   int64_t red_begin;
 };
-constexpr int TG_MAX_PROBS = 8;
+constexpr int TG_MAX_PROBS = 12;
 struct TgBatch {
   TgProb p[TG_MAX_PROBS];
   int nprob = 0;

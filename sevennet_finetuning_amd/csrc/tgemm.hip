@@ -49,37 +49,44 @@ __device__ __forceinline__ int64_t rfl(int64_t v) {
                    (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u));
 }
 
-// One operand of the tile, op(X)(r, k) (row-major X, leading dimension ld;
-// trans: X[k][r]), read through a buffer descriptor based at the tile's first
-// row (column): the thread's TEL elements of a TBK x 64 slab, element
-// e = 256 i + tid walking the contiguous dimension fastest (not transposed:
-// k = e % TBK, r = e / TBK; transposed: r = e % 64, k = e / 64).  Their byte
-// offsets at k = 0 and LDS slots are fixed for the launch; a k step adds a
-// scalar offset -- no per-element 64-bit address arithmetic in the k loop.
-// Elements past the problem's rows (columns) or its K read 0 (OOB offset).
+// One operand of the tile, element (r, k) in the TgLay layout, read through
+// a buffer descriptor at the operand's base: the thread's TEL elements of a
+// TBK x 64 slab, element e = 256 i + tid walking the contiguous dimension
+// fastest (k contiguous: k = e % TBK, r = e / TBK; else r = e % 64, k = e / 64).
+// Their byte offsets at the segment start and LDS slots are fixed for the
+// launch; a k step adds a scalar offset (k steps never straddle a segment: a
+// segment is padded to whole steps) -- no per-element address arithmetic in
+// the k loop.  Elements past the rows or a segment's ks read 0 (OOB offset).
+constexpr int TG_RECORDS = 0x7fff0000;
+constexpr int TG_MAX_SEG = 9;   // K segments of a part (2l + 1 <= 9: lmax 4)   // descriptor size: every real offset is below, OOB above
 struct OpB {
   __amdgpu_buffer_rsrc_t R;
-  int vo[TEL];   // byte offset at k = 0, OOB past the rows
+  int vo[TEL];   // byte offset at k = 0 of a segment, OOB past the rows
   int kk[TEL];   // k within a step
   int lo[TEL];   // LDS slot S[k][r]
-  int kstride;   // bytes per k
+  int kst4, sst4, ks, sps;   // bytes per k, per segment; segment rows; steps per segment
 };
-__device__ __forceinline__ void opb_init(OpB& o, const float* X, int64_t ld, int trans, int r0, int rmax,
-                                         int K) {
-  const float* base = trans ? X + r0 : X + (int64_t)r0 * ld;
-  int64_t bytes = trans ? ((int64_t)(K - 1) * ld + (rmax - r0)) * 4 : ((int64_t)(rmax - r0 - 1) * ld + K) * 4;
-  bytes = K <= 0 || rmax <= r0 ? 0 : (bytes > 0x7fffffff ? 0x7fffffff : bytes);
-  o.R = __builtin_amdgcn_make_buffer_rsrc((void*)(base ? base : X), (short)0, (int)bytes, 0x00020000);
+__device__ __forceinline__ void opb_init(OpB& o, const TgLay& L, int r0, int rmax) {
+  o.R = __builtin_amdgcn_make_buffer_rsrc((void*)L.X, (short)0, TG_RECORDS, 0x00020000);
+  const int rep = rfl(L.rep), rs = rfl(L.rs);
+  const int ld = rfl(L.ld), kst = rfl(L.kst);
+  const bool kfast = kst == 1;
+  const unsigned mag = rep > 1 ? 0xffffffffu / (unsigned)rep + 1u : 0u;
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < TEL; ++i) {
     const int e = 256 * i + tid;
-    const int r = trans ? (e & 63) : (e / TBK), k = trans ? (e >> 6) : (e % TBK);
-    o.vo[i] = r0 + r < rmax ? (int)(trans ? (int64_t)k * ld + r : (int64_t)r * ld + k) * 4 : OOB;
+    const int r = kfast ? (e / TBK) : (e & 63), k = kfast ? (e % TBK) : (e >> 6);
+    const int rr = r0 + r;
+    const int q = rep > 1 ? (int)__umulhi((unsigned)rr, mag) : rr;   // rr / rep (rep <= 9)
+    o.vo[i] = rr < rmax ? (q * ld + (rr - q * rep) * rs + k * kst) * 4 : OOB;
     o.kk[i] = k;
     o.lo[i] = k * TLD + r;
   }
-  o.kstride = trans ? (int)ld * 4 : 4;
+  o.kst4 = kst * 4;
+  o.sst4 = rfl(L.sst) * 4;
+  o.ks = rfl(L.ks);
+  o.sps = (o.ks + TBK - 1) / TBK;
 }
 
 // Main loop: LDS double buffer + a ring of NS register slots, so the loads of
@@ -105,9 +112,16 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
   // the k loop, and each such scalar load's wait also drains the outstanding
   // LDS operations (one counter)
   const int PM = rfl(P.M), PN = rfl(P.N), PK1 = rfl(P.K1), PK2 = rfl(P.K2);
-  // this split's k steps over the concatenated K = K1 + K2 (each part padded
-  // to whole k-steps)
-  const int nk1 = (PK1 + TBK - 1) / TBK, nk = nk1 + (PK2 + TBK - 1) / TBK;
+  // op(A)(m, k) and op(B)(n, k): B enters as the (n x k) operand
+  OpB a1, b1, a2, b2;
+  opb_init(a1, P.A1, m0, PM);
+  opb_init(b1, P.B1, n0, PN);
+  opb_init(a2, P.A2, m0, PM);
+  opb_init(b2, P.B2, n0, PN);
+  // the k steps over the concatenated K = K1 + K2: each part's segments
+  // padded to whole steps
+  const int nk1 = a1.ks > 0 ? (PK1 / a1.ks) * a1.sps : 0;
+  const int nk = nk1 + (a2.ks > 0 ? (PK2 / a2.ks) * a2.sps : 0);
   // the tile's k-step ranges (block sparsity): [kb1, ke1) of the first pair,
   // [nk1 + kb2, nk1 + ke2) of the second; step j of the tile's sequence is
   // kb1 + j (j < n1) or nk1 + kb2 + j - n1.  This split's slice of it:
@@ -122,34 +136,49 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
   }
   const int jb = rfl(s * P.ksteps), je = min(n1 + n2, jb + rfl(P.ksteps));
   auto kt_of = [&](int j) { return j < n1 ? kb1 + j : nk1 + kb2 + (j - n1); };
-  // op(A)(m, k) and op(B)(n, k): B enters as the (n x k) operand
-  OpB a1, b1, a2, b2;
-  opb_init(a1, P.A1, P.lda1, P.ta1, m0, PM, PK1);
-  opb_init(b1, P.B1, P.ldb1, !P.tb1, n0, PN, PK1);
-  opb_init(a2, P.A2, P.lda2, P.ta2, m0, PM, PK2);
-  opb_init(b2, P.B2, P.ldb2, !P.tb2, n0, PN, PK2);
   float ra[NS][TEL], rb[NS][TEL];
   // step j's operands (j >= je: zeros, same instructions); the operand
-  // pair is selected arithmetically, not branched on
-  auto load1 = [&](const OpB& o1, const OpB& o2, bool first, bool live, int kl, int kmax, float (&x)[TEL]) {
-    const int soff = kl * (first ? o1.kstride : o2.kstride);
+  // pair is selected arithmetically, not branched on.  Loads run in step
+  // order, so a cursor carries the next load's part, segment and row in it
+  // (scalar selects per load; the segment index of a part step t -- t / sps
+  // -- is found by compares only where the cursor starts or changes part)
+  auto seg_of = [&](int t, int sps, int& seg, int& kin) {
+    seg = 0;
+#pragma unroll
+    for (int c = 1; c < TG_MAX_SEG; ++c) seg += t >= c * sps;
+    kin = (t - seg * sps) * TBK;
+  };
+  int cj = jb, cseg, ckin;
+  bool cfirst = kt_of(jb) < nk1;
+  seg_of(cfirst ? kt_of(jb) : kt_of(jb) - nk1, cfirst ? a1.sps : a2.sps, cseg, ckin);
+  int seg2, kin2;   // where the second pair's range of this tile starts
+  seg_of(kb2, a2.sps, seg2, kin2);
+  auto load1 = [&](const OpB& o1, const OpB& o2, bool first, bool live, int seg, int kin, float (&x)[TEL]) {
+    const int soff = kin * (first ? o1.kst4 : o2.kst4) + seg * (first ? o1.sst4 : o2.sst4);
+    const int kmax = first ? o1.ks : o2.ks;
 #pragma unroll
     for (int i = 0; i < TEL; ++i) {
       const int vo = first ? o1.vo[i] : o2.vo[i];
       const int kk = first ? o1.kk[i] : o2.kk[i];
-      const int v = (live && kl + kk < kmax) ? vo : OOB;
+      const int v = (live && kin + kk < kmax) ? vo : OOB;
       x[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(first ? o1.R : o2.R, v, soff, 0));
     }
   };
-  auto load = [&](int j, float (&xa)[TEL], float (&xb)[TEL]) {
-    const int kt = kt_of(j);
-    const bool live = j < je, first = kt < nk1;
-    const int kl = (first ? kt : kt - nk1) * TBK, kmax = first ? PK1 : PK2;
-    load1(a1, a2, first, live, kl, kmax, xa);
-    load1(b1, b2, first, live, kl, kmax, xb);
+  auto load = [&](float (&xa)[TEL], float (&xb)[TEL]) {   // step cj, then advance
+    const bool live = cj < je;
+    load1(a1, a2, cfirst, live, cseg, ckin, xa);
+    load1(b1, b2, cfirst, live, cseg, ckin, xb);
+    ++cj;
+    const bool sw = cfirst && cj == n1;             // into the second pair's range
+    const int spsT = (cfirst ? a1.sps : a2.sps) * TBK;
+    const bool wrap = ckin + TBK >= spsT;
+    const int nkin = wrap ? 0 : ckin + TBK, nseg = wrap ? cseg + 1 : cseg;
+    ckin = sw ? kin2 : nkin;
+    cseg = sw ? seg2 : nseg;
+    cfirst = cfirst && !sw;
   };
   auto store = [&](int buf, int j, const float (&xa)[TEL], const float (&xb)[TEL]) {
-    const bool first = kt_of(j) < nk1;
+    const bool first = j < n1;
 #pragma unroll
     for (int i = 0; i < TEL; ++i) {
       As[buf][first ? a1.lo[i] : a2.lo[i]] = xa[i];
@@ -161,7 +190,7 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   if (jb < je) {
 #pragma unroll
-    for (int u = 0; u < NS - 1; ++u) load(jb + u, ra[u], rb[u]);
+    for (int u = 0; u < NS - 1; ++u) load(ra[u], rb[u]);
     store(0, jb, ra[0], rb[0]);
     __syncthreads();
 #pragma unroll 1
@@ -170,7 +199,7 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
       for (int u = 0; u < NS; ++u) {
         const int j = j0 + u;
         // slot of step j + NS - 1 is (u + NS - 1) % NS: the one step j - 1 used
-        load(j + NS - 1, ra[(u + NS - 1) % NS], rb[(u + NS - 1) % NS]);
+        load(ra[(u + NS - 1) % NS], rb[(u + NS - 1) % NS]);
         if (j < je) {
           const int buf = (j - jb) & 1;
 #pragma unroll
@@ -202,18 +231,27 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
   }
   const gp C = (gp)(uintptr_t)rfl((int64_t)(uintptr_t)P.C);
   const int64_t ldc = rfl(P.ldc);
+  const int crep = rfl(P.crep), crs = rfl(P.crs), cns = rfl(P.cns);
   const float alpha = __builtin_bit_cast(float, rfl(__builtin_bit_cast(int, P.alpha)));
+  // m / crep by a multiply-high (exact for crep <= 9, m < 2^28): an integer
+  // division per output element would cost ~30 vector instructions
+  const unsigned cmag = crep > 1 ? 0xffffffffu / (unsigned)crep + 1u : 0u;
+  auto at = [&](int r) {
+    const int m = row_of(r);
+    const int q = crep > 1 ? (int)__umulhi((unsigned)m, cmag) : m;
+    return (int64_t)q * ldc + (m - q * crep) * crs + (int64_t)col * cns;
+  };
   float old[16];
   if (rfl(P.beta)) {   // all 16 old values in flight at once
 #pragma unroll
-    for (int r = 0; r < 16; ++r) old[r] = row_of(r) < PM ? C[(int64_t)row_of(r) * ldc + col] : 0.f;
+    for (int r = 0; r < 16; ++r) old[r] = row_of(r) < PM ? C[at(r)] : 0.f;
   } else {
 #pragma unroll
     for (int r = 0; r < 16; ++r) old[r] = 0.f;
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r)
-    if (row_of(r) < PM) C[(int64_t)row_of(r) * ldc + col] = old[r] + alpha * acc[r];
+    if (row_of(r) < PM) C[at(r)] = old[r] + alpha * acc[r];
 }
 
 // C = beta C + alpha sum_s ws[s] over the split problems, s in order
@@ -240,7 +278,7 @@ __global__ __launch_bounds__(256) void k_tgemm_reduce(TgBatch batch) {
     }
 #pragma unroll 1
     for (; s < P.splits; ++s) sum += w[(int64_t)s * mn];
-    float* c = P.C + (int64_t)row * P.ldc + col;
+    float* c = P.C + (int64_t)(row / P.crep) * P.ldc + (row % P.crep) * P.crs + (int64_t)col * P.cns;
     const float v = P.alpha * sum;
     *c = P.beta ? *c + v : v;
   }
@@ -253,7 +291,7 @@ __global__ __launch_bounds__(256) void k_tgemm_reduce(TgBatch batch) {
 static int tg_policy(int i) {
   static int v[3] = {-1, -1, -1};
   if (v[0] < 0) {
-    v[0] = 48, v[1] = 1024, v[2] = 16;
+    v[0] = 32, v[1] = 1024, v[2] = 8;
     if (const char* e = std::getenv("E3GNN_TG_SPLIT")) std::sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]);
   }
   return v[i];
@@ -272,8 +310,17 @@ int tg_splits(int64_t M, int64_t N, int64_t K) {
 bool tg_add(TgBatch& b, TgProb p) {
   if (b.nprob >= TG_MAX_PROBS || p.M < 0 || p.N < 0 || p.K1 < 0 || p.K2 < 0) return false;
   if (p.M == 0 || p.N == 0) return true;
-  if (p.K2 == 0) p.A2 = p.A1, p.B2 = p.B1, p.lda2 = p.lda1, p.ldb2 = p.ldb1;  // never read
-  const int nk = (p.K1 + TBK - 1) / TBK + (p.K2 + TBK - 1) / TBK;
+  if (p.K2 == 0) p.A2 = p.A1, p.B2 = p.B1, p.A2.ks = p.B2.ks = 0;   // no second pair
+  auto steps = [](int K, const TgLay& a, const TgLay& b) {
+    if (K <= 0) return 0;
+    if (a.ks <= 0 || a.ks != b.ks || K % a.ks || K / a.ks > TG_MAX_SEG || a.rep < 1 || b.rep < 1 ||
+        a.rep > 9 || b.rep > 9)
+      return -1;
+    return (K / a.ks) * ((a.ks + TBK - 1) / TBK);
+  };
+  const int s1 = steps(p.K1, p.A1, p.B1), s2 = steps(p.K2, p.A2, p.B2);
+  if (s1 < 0 || s2 < 0 || p.crep < 1 || p.crep > 9 || (int64_t)p.M * 9 >= (1 << 28)) return false;
+  const int nk = s1 + s2;
   p.tiles_n = (p.N + TBN - 1) / TBN;
   p.tiles_mn = ((p.M + TBM - 1) / TBM) * p.tiles_n;
   if (p.splits < 1) p.splits = 1;

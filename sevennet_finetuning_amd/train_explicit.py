@@ -35,6 +35,7 @@ Scope: SevenNet-0's architecture (nn.sevennet0_kinds, linear
 self-connection, XPLOR cutoff, normalised or raw SH, silu gates); other
 members of the family keep the autograd path.
 """
+import ctypes
 import math
 import os
 
@@ -126,6 +127,7 @@ class _Gemms:
         self.lib = model._act_lib() if on else None
         self.q = []
         self.ws = None
+        self.max_probs = 12        # e3gnn_gemm_grouped's problems per launch
 
     def _hip(self, *ts):
         return self.lib is not None and all(t.is_cuda and t.dtype == torch.float32 for t in ts)
@@ -159,34 +161,49 @@ class _Gemms:
             ops = [self._op(A), self._op(B)] + ([self._op(A2), self._op(B2)] if A2 is not None else [])
             if C.stride(1) != 1:
                 raise ValueError('GEMM output must be row-major')
-        if len(self.q) == 8:
-            self.flush()
-        self.q.append((C, A, B, A2, B2, ops, float(alpha), int(bool(beta)), kr))
+        from . import _lib
+        d = _lib.GemmDesc()
+        d.a, d.lda, d.trans_a = ops[0]
+        d.b, d.ldb, d.trans_b = ops[1]
+        if A2 is not None:
+            d.a2, d.lda2, d.trans_a2 = ops[2]
+            d.b2, d.ldb2, d.trans_b2 = ops[3]
+            d.k2 = int(A2.shape[1])
+        d.c, d.ldc = C.data_ptr(), C.stride(0)
+        d.m, d.n, d.k = int(C.shape[0]), int(C.shape[1]), int(A.shape[1])
+        d.alpha, d.beta = float(alpha), int(bool(beta))
+        if kr is not None:
+            d.krange, d.krange_stride_m = kr[0].data_ptr(), kr[1]
+        self._push(d, (C, A, B, A2, B2, kr), C.device, (C, A, B, A2, B2, float(alpha), int(bool(beta))))
         return C
+
+    def add_lay(self, M, N, K, C, A, B, lay, A2=None, B2=None, K2=0, alpha=1.0, beta=0):
+        """one problem in the general layouts (e3gnn_gemm_layouts ``lay``); C, A,
+        B, A2, B2 = (tensor, element offset) of the operand bases"""
+        from . import _lib
+        d = _lib.GemmDesc()
+        ptr = lambda t: t[0].data_ptr() + 4 * t[1]   # noqa: E731 (float32)
+        d.a, d.b, d.c = ptr(A), ptr(B), ptr(C)
+        if K2:
+            d.a2, d.b2 = ptr(A2), ptr(B2)
+        d.m, d.n, d.k, d.k2 = int(M), int(N), int(K), int(K2)
+        d.alpha, d.beta = float(alpha), int(bool(beta))
+        d.layout = ctypes.addressof(lay)
+        self._push(d, (C[0], A[0], B[0], A2, B2, lay), C[0].device, None)
+
+    def _push(self, d, keep, dev, info):
+        if len(self.q) == self.max_probs:
+            self.flush()
+        self.q.append((d, keep, dev, info))
 
     def flush(self):
         if not self.q:
             return
         from . import _lib
         n = len(self.q)
-        descs = (_lib.GemmDesc * n)()
-        keep = []
-        for i, (C, A, B, A2, B2, ops, alpha, beta, kr) in enumerate(self.q):
-            d = descs[i]
-            d.a, d.lda, d.trans_a = ops[0]
-            d.b, d.ldb, d.trans_b = ops[1]
-            if A2 is not None:
-                d.a2, d.lda2, d.trans_a2 = ops[2]
-                d.b2, d.ldb2, d.trans_b2 = ops[3]
-                d.k2 = int(A2.shape[1])
-            d.c, d.ldc = C.data_ptr(), C.stride(0)
-            d.m, d.n, d.k = int(C.shape[0]), int(C.shape[1]), int(A.shape[1])
-            d.alpha, d.beta = alpha, beta
-            if kr is not None:
-                d.krange, d.krange_stride_m = kr[0].data_ptr(), kr[1]
-            keep.append((C, A, B, A2, B2))
+        descs = (_lib.GemmDesc * n)(*[e[0] for e in self.q])
         need = int(self.lib.e3gnn_gemm_workspace_floats(n, descs))
-        dev = self.q[0][0].device
+        dev = self.q[0][2]
         if need > 0 and (self.ws is None or self.ws.numel() < need):
             self.ws = torch.empty(max(need, 1 << 20), device=dev)
         ws = self.ws.data_ptr() if self.ws is not None else None
@@ -664,6 +681,9 @@ class ExplicitStep:
         self.bank = _DenseBank(model, ent, {f'si2{t}': d for t, d in enumerate(dens)}
                                if self.fold_den else None)
         self._lins = {key: lin for key, lin, _ in ent}
+        self._lb_cache = {}
+        # E3GNN_TRAIN_IRREPS=0: the dense products (zero-block ranges only)
+        self._irreps = os.environ.get('E3GNN_TRAIN_IRREPS', '1') != '0'
         self._dims = {key: (lin.in_off[-1], lin.out_off[-1]) for key, lin, _ in ent}
         self._kr_cache = {}
         # the radial MLP weights of every block, scaled by 1/sqrt(fan-in)
@@ -700,6 +720,99 @@ class ExplicitStep:
         self.gm.add(C, A, B, alpha, beta, A2, B2, kr=kr)
         self.gm.flush()
         return C
+
+    # ---- the linears per l-block in the e3nn irreps layout (e3gnn_gemm_layouts):
+    # rows (node, m) of [node][mul][2l+1] blocks against the m = 0 diagonal of
+    # the dense matrices -- no zero blocks and no zeros between the m copies
+    # (the dense products spent 2l + 1 times the work on those); weight
+    # gradients summed over K = (m, node) segments into the m = 0 diagonal of
+    # the dense gradient (the bank's flush sums the diagonal positions)
+    def _lblocks(self, key):
+        """[(l, d, in_lo, mul_in, out_lo, mul_out)] of key's linear, its input
+        and output irreps merged by l (sorted by l: consecutive)"""
+        if key in self._lb_cache:
+            return self._lb_cache[key]
+        lin = self._lins[key]
+        def merged(irreps, offs):
+            out = {}
+            for i, (mul, l, _) in enumerate(irreps):
+                d = 2 * l + 1
+                if l in out:
+                    lo, m0 = out[l]
+                    assert lo + m0 * d == offs[i], 'irreps of one l not contiguous'
+                    out[l] = (lo, m0 + mul)
+                else:
+                    out[l] = (offs[i], mul)
+            return out
+        ins = merged(lin.irreps_in, lin.in_off)
+        outs = merged(lin.irreps_out, lin.out_off)
+        ls = sorted({lin.irreps_in[i][1] for i, j in lin.ins})
+        res = [(l, 2 * l + 1, ins[l][0], ins[l][1], outs[l][0], outs[l][1]) for l in ls]
+        self._lb_cache[key] = res
+        return res
+
+    def _irr(self, *ts):
+        return self._irreps and self.gm._hip(*ts)
+
+    def _lin(self, C, A, key, A2=None, key2=None, trans=False, beta=0, flush=True):
+        """C = A op(D[key]) [+ A2 op(D[key2])], op = identity or transpose, one
+        problem per l-block (the dense product with its zero-block ranges on
+        other devices / dtypes)"""
+        D = self.S['D']
+        if not self._irr(C, A, *([A2] if A2 is not None else [])):
+            B = D[key].t() if trans else D[key]
+            B2 = None if key2 is None else (D[key2].t() if trans else D[key2])
+            kr = self._kr((key, trans), None if key2 is None else (key2, trans))
+            self.gm.add(C, A, B, beta=beta, A2=A2, B2=B2, kr=kr)
+            if flush:
+                self.gm.flush()
+            return C
+        from . import _lib
+        rows = int(A.shape[0])
+        outs = {}
+        for Ai, k in [(A, key)] + ([(A2, key2)] if A2 is not None else []):
+            Dk = D[k]
+            dout = int(Dk.shape[1])
+            for (l, d, in_lo, mi, out_lo, mo) in self._lblocks(k):
+                if trans:   # C[:, in] += A[:, out] D[in, out]^T: k over the output block
+                    ent = (Ai, out_lo, mo, Dk, in_lo * dout + out_lo, d * dout, d)
+                    outs.setdefault((l, in_lo, mi, d), []).append(ent)
+                else:
+                    ent = (Ai, in_lo, mi, Dk, in_lo * dout + out_lo, d, d * dout)
+                    outs.setdefault((l, out_lo, mo, d), []).append(ent)
+        for (l, c_lo, N, d), ps in outs.items():
+            assert len(ps) <= 2
+            lay = _lib.GemmLayouts()
+            ops = []
+            for (Ai, a_lo, K, Dk, b_off, b_ld, b_kst), La, Lb in zip(ps, (lay.a, lay.a2), (lay.b, lay.b2)):
+                La.ld, La.rep, La.rs, La.kst, La.ks, La.sst = Ai.stride(0), d, 1, d, K, 0
+                Lb.ld, Lb.rep, Lb.rs, Lb.kst, Lb.ks, Lb.sst = b_ld, 1, 0, b_kst, K, 0
+                ops.append(((Ai, a_lo), (Dk, b_off), K))
+            lay.ldc, lay.crep, lay.crs, lay.cns = C.stride(0), d, 1, d
+            extra = {}
+            if len(ops) > 1:
+                extra = dict(A2=ops[1][0], B2=ops[1][1], K2=ops[1][2])
+            self.gm.add_lay(rows * d, N, ops[0][2], (C, c_lo), ops[0][0], ops[0][1], lay, beta=beta, **extra)
+        if flush:
+            self.gm.flush()
+        return C
+
+    def _lin_grad(self, G, X, Y, key):
+        """G += X^T Y, G the dense gradient of key's matrix, on its l-blocks"""
+        if not self._irr(G, X, Y):
+            self.gm.add(G, X.t(), Y, beta=1, kr=self._kr(None, grad=key))
+            return
+        from . import _lib
+        rows = int(X.shape[0])
+        dout = int(G.shape[1])
+        for (l, d, in_lo, mi, out_lo, mo) in self._lblocks(key):
+            lay = _lib.GemmLayouts()
+            # element (u, (m, node)) = X[node][in_lo + u d + m]
+            lay.a.ld, lay.a.rep, lay.a.rs, lay.a.kst, lay.a.ks, lay.a.sst = d, 1, 0, X.stride(0), rows, 1
+            lay.b.ld, lay.b.rep, lay.b.rs, lay.b.kst, lay.b.ks, lay.b.sst = d, 1, 0, Y.stride(0), rows, 1
+            lay.ldc, lay.crep, lay.crs, lay.cns = d * dout, 1, 0, d
+            self.gm.add_lay(mi, mo, d * rows, (G, in_lo * dout + out_lo), (X, in_lo), (Y, out_lo), lay,
+                            beta=1)
 
     # ---- block sparsity of the dense linear matrices (e3gnn_gemm_desc::krange)
     def _lin_blocks(self, key, trans=False):
@@ -763,8 +876,8 @@ class ExplicitStep:
     def _si2_t(self, t, A, Dm):
         """A Dm^T (cotangent rows of the mid irreps)"""
         if self.dense_si2:
-            return self._mm(torch.empty(A.shape[0], Dm.shape[0], device=A.device, dtype=A.dtype),
-                            A, Dm.t(), kr=self._kr((f'si2{t}', True)))
+            return self._lin(torch.empty(A.shape[0], Dm.shape[0], device=A.device, dtype=A.dtype),
+                             A, f'si2{t}', trans=True)
         bl, gaps = self.si2_blocks[t]
         out = torch.empty(A.shape[0], Dm.shape[0], device=A.device, dtype=A.dtype)
         seen = set()
@@ -906,7 +1019,7 @@ class ExplicitStep:
             W0, W1, W2 = MW[t]
             x = X[:n]
             H = new(2 * n, D[f'si1{t}'].shape[1])
-            self._mm(H[:n], x, D[f'si1{t}'], kr=self._kr((f'si1{t}', False)))
+            self._lin(H[:n], x, f'si1{t}')
             A1, H1 = new(2 * E, W0.shape[1]), new(2 * E, W0.shape[1])
             A2, H2 = new(2 * E, W1.shape[1]), new(2 * E, W1.shape[1])
             WT = new(2 * E, W2.shape[1])
@@ -918,8 +1031,7 @@ class ExplicitStep:
                 AGG[:n].div_(den)
             Yg = new(2 * n, D[f'si2{t}'].shape[1])
             if self.dense_si2:                              # x sc + agg si2: one product
-                self._mm(Yg[:n], x, D[f'sc{t}'], A2=AGG[:n], B2=D[f'si2{t}'],
-                         kr=self._kr((f'sc{t}', False), (f'si2{t}', False)))
+                self._lin(Yg[:n], x, f'sc{t}', A2=AGG[:n], key2=f'si2{t}')
             else:
                 self._mm(Yg[:n], x, D[f'sc{t}'])            # (GEMM into the output, then
                 self._si2_fwd(t, AGG[:n], D[f'si2{t}'], Yg[:n])  # accumulate: no bias copy)
@@ -953,8 +1065,7 @@ class ExplicitStep:
                                     acc=ACC_DY if t < len(blocks) - 1 else 0)
             self._mlp_rev(wb, b['W'], b['A1'][:E], b['A2'][:E], embb)
             if t > 0:
-                xb = self._mm(new(n, hb.shape[1]), hb, D[f'si1{t}'].t(), A2=yb, B2=D[f'sc{t}'].t(),
-                              kr=self._kr((f'si1{t}', True), (f'sc{t}', True)))
+                xb = self._lin(new(n, hb.shape[1]), hb, f'si1{t}', A2=yb, key2=f'sc{t}', trans=True)
         fij = self.geo.vjp(g, Yb, embb)                    # dE/dr_e, centre-sorted order
         S['fij'] = fij
         aux = graph.aux
@@ -1011,7 +1122,7 @@ class ExplicitStep:
             aggd = AGG[n:]                       # C(h, Y', w) + C(h, Y, w') + C(h', Y, w)
             X = b['X']
             if t > 0:
-                self._mm(b['H'][n:], X[n:], D[f'si1{t}'], kr=self._kr((f'si1{t}', False)))
+                self._lin(b['H'][n:], X[n:], f'si1{t}')
             hd = b['H'][n:] if t > 0 else None   # x0' = 0: no h' term
             if fused:
                 be.tangent_forward(k, graph, h, hd, Y, Yd, w, WT[E:], out=aggd)
@@ -1024,10 +1135,9 @@ class ExplicitStep:
                 aggd.div_(b['den'])
             if self.dense_si2:
                 if t > 0:
-                    self._mm(Yg[n:], X[n:], D[f'sc{t}'], A2=AGG[n:], B2=D[f'si2{t}'],
-                             kr=self._kr((f'sc{t}', False), (f'si2{t}', False)))
+                    self._lin(Yg[n:], X[n:], f'sc{t}', A2=AGG[n:], key2=f'si2{t}')
                 else:                            # x0' = 0
-                    self._mm(Yg[n:], AGG[n:], D[f'si2{t}'], kr=self._kr((f'si2{t}', False)))
+                    self._lin(Yg[n:], AGG[n:], f'si2{t}')
             else:
                 if t > 0:
                     self._mm(Yg[n:], X[n:], D[f'sc{t}'])
@@ -1073,9 +1183,9 @@ class ExplicitStep:
                 # independent products of y-bar, one launch: si2's and sc's weight
                 # gradients and agg-bar
                 AGGB = new(2 * n, D[f'si2{t}'].shape[0])
-                self.gm.add(G[f'si2{t}'], AGG.t(), YB, beta=1, kr=self._kr(None, grad=f'si2{t}'))
-                self.gm.add(AGGB, YB, D[f'si2{t}'].t(), kr=self._kr((f'si2{t}', True)))
-                self.gm.add(G[f'sc{t}'], X.t(), YB, beta=1, kr=self._kr(None, grad=f'sc{t}'))
+                self._lin_grad(G[f'si2{t}'], AGG, YB, f'si2{t}')
+                self._lin(AGGB, YB, f'si2{t}', trans=True, flush=False)
+                self._lin_grad(G[f'sc{t}'], X, YB, f'sc{t}')
                 self.gm.flush()
             else:
                 self._si2_wgrad(t, G[f'si2{t}'], AGG, YB)
@@ -1119,10 +1229,9 @@ class ExplicitStep:
                 if gw is not None:
                     self.gm.add(gw, rows.t(), cot, 1.0 / math.sqrt(Wl.shape[0]), beta=1)
             # self-interaction 1 (sc-bar = y-bar, added above) and the input cotangent
-            self.gm.add(G[f'si1{t}'], X.t(), HB, beta=1, kr=self._kr(None, grad=f'si1{t}'))
+            self._lin_grad(G[f'si1{t}'], X, HB, f'si1{t}')
             XB = new(2 * n, D[f'si1{t}'].shape[0])
-            self.gm.add(XB, HB, D[f'si1{t}'].t(), A2=YB, B2=D[f'sc{t}'].t(),
-                        kr=self._kr((f'si1{t}', True), (f'sc{t}', True)))
+            self._lin(XB, HB, f'si1{t}', A2=YB, key2=f'sc{t}', trans=True, flush=False)
             self.gm.flush()
         # embedding (x0 = W[types] / sqrt(nsp)) and the radial basis coefficients
         gemb = self._G('onehot_to_feature_x.linear.weight')

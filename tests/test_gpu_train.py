@@ -856,3 +856,51 @@ def test_fused_loss_and_ewc_match_autograd(loss):
         assert float((a - r).abs().max()) <= 1e-6 * float(r.abs().max()) + 1e-12
     assert float(calls['c'][0][1]) == 0.0 and float(calls['c'][1][5, 1]) == 0.0
     assert float((m.flat_grad - g_ref).abs().max()) <= 1e-6 * float(g_ref.abs().max())
+
+
+def test_irreps_layout_linears_match_dense():
+    """The fine-tune step's linears in the irreps layout (one grouped-GEMM
+    problem per l-block, e3gnn_gemm_layouts: rows (node, m), the m = 0
+    diagonal of the dense matrix; weight gradients over K = (m, node)
+    segments) against the dense float64 products: C = A D, C = A D^T with two
+    operand pairs, and the gradient's diagonal sums."""
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    from sevennet_finetuning_amd.train_explicit import ExplicitStep
+    torch.manual_seed(0)
+    m = SevenNetTrainable(device=DEV)
+    st = ExplicitStep(m)
+    D = st.bank.build()
+    st.S = {'D': D}
+    rows = 77                                            # not a multiple of any tile
+    for t in range(len(m.blocks)):
+        for key, key2 in ((f'si1{t}', None), (f'sc{t}', f'si2{t}')):
+            din, dout = D[key].shape
+            A = torch.randn(rows, din, device=DEV)
+            A2 = torch.randn(rows, D[key2].shape[0], device=DEV) if key2 else None
+            C = torch.empty(rows, dout, device=DEV)
+            st._lin(C, A, key, A2=A2, key2=key2)
+            ref = A.double() @ D[key].double()
+            if key2:
+                ref += A2.double() @ D[key2].double()
+            assert (C.double() - ref).abs().max() <= 2e-5 * (1 + ref.abs().max()), (key, key2)
+            # transposed: C = A D^T (+ A2 D2^T) into the input space
+            if key2 is None or D[key2].shape[1] == dout:
+                At = torch.randn(rows, dout, device=DEV)
+                Ct = torch.empty(rows, din, device=DEV)
+                if key == f'si1{t}':
+                    st._lin(Ct, At, key, trans=True)
+                    reft = At.double() @ D[key].double().t()
+                    assert (Ct.double() - reft).abs().max() <= 2e-5 * (1 + reft.abs().max()), key
+        for key in (f'si1{t}', f'sc{t}', f'si2{t}'):
+            din, dout = D[key].shape
+            X, Y = torch.randn(rows, din, device=DEV), torch.randn(rows, dout, device=DEV)
+            G = torch.zeros(din, dout, device=DEV)
+            st._lin_grad(G, X, Y, key)
+            st.gm.flush()
+            full = X.double().t() @ Y.double()
+            for (l, d, in_lo, mi, out_lo, mo) in st._lblocks(key):
+                u = torch.arange(mi, device=DEV)[:, None]
+                v = torch.arange(mo, device=DEV)[None, :]
+                want = sum(full[in_lo + u * d + k, out_lo + v * d + k] for k in range(d))
+                got = G[in_lo + u * d, out_lo + v * d].double()
+                assert (got - want).abs().max() <= 2e-5 * (1 + want.abs().max()), (key, l)

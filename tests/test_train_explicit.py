@@ -146,3 +146,30 @@ def test_split_k_weight_gradient():
     ref = G + 0.5 * A.t() @ B
     _wgrad(G, A, B, 0.5)
     assert torch.allclose(G, ref, rtol=1e-12, atol=1e-10)
+
+
+def test_block_sparsity_tables_cover_every_nonzero(model):
+    """The per-tile k ranges the fine-tune GEMMs skip by (e3gnn_gemm_desc::
+    krange, ExplicitStep._kr) cover every nonzero of the dense linear matrices
+    (built from random weights, so no weight is zero by chance): C = A D and
+    C = A D^T read each output tile's nonzero rows only inside its range, the
+    gradient tables mark every tile that holds a nonzero."""
+    from sevennet_finetuning_amd.train_explicit import ExplicitStep
+    step = ExplicitStep(model)
+    D = step.bank.build()
+    T = 64
+    for key in [k for k in D if k[:2] in ('sc', 'si')]:
+        nz = (D[key] != 0).numpy()
+        for trans in (False, True):
+            m = nz.T if trans else nz              # op(D): k rows x output columns
+            tab = step._kr((key, trans))[0].cpu().numpy().reshape(-1, 4)
+            for b in range(tab.shape[0]):
+                rows = np.nonzero(m[:, b * T:(b + 1) * T].any(1))[0]
+                if rows.size:
+                    assert tab[b, 0] <= rows.min() and rows.max() < tab[b, 1], (key, trans, b)
+        tab, stride = step._kr(None, grad=key)
+        tab = tab.cpu().numpy().reshape(-1, stride, 4)
+        for a in range(tab.shape[0]):
+            for b in range(stride):
+                if nz[a * T:(a + 1) * T, b * T:(b + 1) * T].any():
+                    assert tab[a, b, 1] > 0, (key, a, b)

@@ -85,6 +85,8 @@ for s in "$@"; do
     benchtrain_notg) step benchtrain_notg 300 env E3GNN_TRAIN_TGEMM=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchtrain_nofl) step benchtrain_nofl 300 env E3GNN_TRAIN_FUSED_LOSS=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchtrain_none) step benchtrain_none 300 env E3GNN_TRAIN_FUSED_LOSS=0 E3GNN_TRAIN_TGEMM=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    btsplit_*) v=${s#btsplit_}; step btsplit_$v 300 env E3GNN_TG_SPLIT=${v//_/,} python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    btdense) step btdense 300 env E3GNN_TRAIN_IRREPS=0 python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     tgb) step tgb 300 python tools/tgemm_bench.py ;;
     benchmc_*) v=${s#benchmc_}; step benchmc_$v 600 python bench.py --model-config $v --steps 5 --warmup 2 --no-cpu-baseline ;;
     proftrain2) step proftrain2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train2 -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;

@@ -46,7 +46,7 @@ def main():
 
     def flush(self):
         if self.q:
-            rec.append(list(self.q))
+            rec.append(list(self.q))   # (desc, keep-alive, device, plain operands or None)
         return orig(self)
     train_explicit._Gemms.flush = flush
     tr.rehearsal_step(b[0], b[1])
@@ -69,38 +69,26 @@ def main():
         return ts[len(ts) // 2]
 
     tot_h = tot_t = 0.0
-    print(f"{'launch':>6} {'problems (M x N x K[+K2], tA tB)':60s} {'tgemm us':>9} {'torch us':>9}")
+    print(f"{'launch':>6} {'problems (M x N x K[+K2], tA tB; L: irreps layout)':60s} {'tgemm us':>9} {'torch us':>9}")
     for i, q in enumerate(rec):
         n = len(q)
-        descs = (_lib.GemmDesc * n)()
-        shapes = []
-        for j, (C, A, B, A2, B2, ops, alpha, beta, kr) in enumerate(q):
-            d = descs[j]
-            d.a, d.lda, d.trans_a = ops[0]
-            d.b, d.ldb, d.trans_b = ops[1]
-            if A2 is not None:
-                d.a2, d.lda2, d.trans_a2 = ops[2]
-                d.b2, d.ldb2, d.trans_b2 = ops[3]
-                d.k2 = int(A2.shape[1])
-            d.c, d.ldc = C.data_ptr(), C.stride(0)
-            d.m, d.n, d.k = int(C.shape[0]), int(C.shape[1]), int(A.shape[1])
-            d.alpha, d.beta = alpha, beta
-            if kr is not None:
-                d.krange, d.krange_stride_m = kr[0].data_ptr(), kr[1]
-            shapes.append(f"{d.m}x{d.n}x{d.k}{'+' + str(d.k2) if d.k2 else ''}"
-                          f"{'T' if d.trans_a else 'N'}{'T' if d.trans_b else 'N'}")
+        descs = (_lib.GemmDesc * n)(*[e[0] for e in q])
+        shapes = [f"{d.m}x{d.n}x{d.k}{'+' + str(d.k2) if d.k2 else ''}"
+                  f"{'L' if d.layout else ('T' if d.trans_a else 'N') + ('T' if d.trans_b else 'N')}"
+                  for d in descs]
         stream = torch.cuda.current_stream(dev).cuda_stream
         th = timed(lambda: _lib.check(lib.e3gnn_gemm_grouped(n, descs, ws.data_ptr(), ws.numel(),
                                                              stream)))
+        plain = [e[3] for e in q if e[3] is not None]
 
         def tor():
-            for (C, A, B, A2, B2, ops, alpha, beta, kr) in q:
+            for (C, A, B, A2, B2, alpha, beta) in plain:
                 torch.addmm(C, A, B, beta=1 if beta else 0, alpha=alpha, out=C)
                 if A2 is not None:
                     C.addmm_(A2, B2, alpha=alpha)
-        tt = timed(tor)
+        tt = timed(tor) if len(plain) == n else float('nan')
         tot_h += th
-        tot_t += tt
+        tot_t += tt if tt == tt else 0.0
         print(f"{i:6d} {' '.join(shapes)[:60]:60s} {th:9.1f} {tt:9.1f}")
     print(f"total (one rehearsal step's launches): tgemm {tot_h:.0f} us, torch {tot_t:.0f} us, "
           f"{len(rec)} launches")
