@@ -120,8 +120,15 @@ def device_nl_timing(box, device, reps=5):
             'edges': int(c.numel())}
 
 
-def rocprof_name(cls):
-    """Kernel symbol (as rocprofv3 prints it) of a fused timing class."""
+# template arguments of the fused kernels' layer structs per channel family
+# (csrc/tp.h Family<f>): rocprofv3 prints e.g. k_conv_bwd_ls<e3gnn::LayerMidT<128, 64, 32> >
+FAMILY_DIMS = {0: ('128', '128, 64, 32'), 1: ('64', '64, 64, 64'), 2: ('32', '32, 32, 32')}
+
+
+def rocprof_name(cls, family=0):
+    """Kernel symbol prefix (as rocprofv3 prints it) of a fused timing class
+    of the given channel family (so PMC entries of another family's kernels
+    never match)."""
     kinds = {'first': 'LayerFirst', 'mid': 'LayerMid', 'last': 'LayerLast'}
     if '.' in cls:  # template prefix
         k, kind = cls.split('.')
@@ -129,7 +136,8 @@ def rocprof_name(cls):
             # first / middle blocks: the lock-step kernel; the last block: one
             # wave per neighbour node
             k = 'conv_bwd_nbr' if kind == 'last' else 'conv_bwd_ls'
-        return f'k_{k}<e3gnn::{kinds[kind]}'
+        first, rest = FAMILY_DIMS.get(family, FAMILY_DIMS[0])
+        return f'k_{k}<e3gnn::{kinds[kind]}T<{first if kind == "first" else rest}>'
     return cls
 
 
@@ -512,7 +520,7 @@ def main():
                    for k, v in stats.items() if v['launches']}
         dom = max(stats, key=lambda k: stats[k]['ms'])
         d = stats[dom]
-        rp_name = rocprof_name(dom)
+        rp_name = rocprof_name(dom, max(getattr(model, 'family', 0), 0))
         if d['flops'] > 0:
             ach = d['flops'] / (d['ms'] * 1e9)
             roofline = {'bound': 'mfma', 'kernel': dom, 'achieved': round(ach, 3),
