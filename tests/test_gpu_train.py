@@ -337,12 +337,17 @@ def test_force_loss_parameter_gradients_vs_fp64(models):
     assert float(g64.abs().max()) > 0
     assert float((g32 - g64).norm() / g64.norm()) < 1e-4
     # per tensor, relative to each tensor's own scale
+    worst = []
     for name, (off, n, _) in m64.slices.items():
         ref = g64[off:off + n]
         if float(ref.abs().max()) == 0.0:
             assert float(g32[off:off + n].abs().max()) == 0.0, name
             continue
-        assert float((g32[off:off + n] - ref).norm() / ref.norm()) < 1e-3, name
+        worst.append((float((g32[off:off + n] - ref).norm() / ref.norm()), name))
+    worst.sort(reverse=True)
+    print('autograd-path per-tensor relative gradient errors, worst five:', worst[:5])
+    for err, name in worst:
+        assert err < 2e-4, name
 
 
 def test_explicit_step_gradients_vs_fp64(models):
@@ -373,12 +378,17 @@ def test_explicit_step_gradients_vs_fp64(models):
     g64 = m64.flat_grad.detach().clone()
     assert float((out[KEY.PRED_FORCE].detach().cpu().double() - o64[KEY.PRED_FORCE]).abs().max()) < 1e-4
     assert float((g32 - g64).norm() / g64.norm()) < 1e-4
+    worst = []
     for name, (off, n, _) in m64.slices.items():
         ref = g64[off:off + n]
         if float(ref.abs().max()) == 0.0:
             assert float(g32[off:off + n].abs().max()) == 0.0, name
             continue
-        assert float((g32[off:off + n] - ref).norm() / ref.norm()) < 1e-3, name
+        worst.append((float((g32[off:off + n] - ref).norm() / ref.norm()), name))
+    worst.sort(reverse=True)
+    print('explicit-step per-tensor relative gradient errors, worst five:', worst[:5])
+    for err, name in worst:   # measured ~2e-6 at worst (round 5)
+        assert err < 2e-4, name
     # the dual kernels against the torch forms of the same module
     torch.manual_seed(0)
     p = _Prims(m32)
