@@ -1027,9 +1027,9 @@ hipError_t launch_gemm(const GemmBatch& b, hipStream_t s) {
 }
 
 // which kernel runs a node-linear problem (E3GNN_NL_BF16): 0 k_nodelin (f32
-// MFMA) for all; 1 (default) k_nodelin_s (skinny, bf16x6) where it applies,
-// k_nodelin otherwise; 2 k_nodelin_s where it applies, k_nodelin_b (bf16x6
-// tiles) otherwise; 3 k_nodelin_b for all
+// MFMA) for all; 1 (default) k_nodelin_s (skinny, bf16x6) and k_nodelin_b
+// (bf16x6 tiles) where they measured faster, k_nodelin otherwise; 2
+// k_nodelin_s where it applies, k_nodelin_b otherwise; 3 k_nodelin_b for all
 static int nl_mode() {
   static const int m = [] {
     const char* v = std::getenv("E3GNN_NL_BF16");
@@ -1051,9 +1051,14 @@ bool add_nl(NlBatch& b, const NlProb& p) {
   const int mode = nl_mode();
   // skinny: K <= 64 onto N >= 128 columns (si2^T l > 0: 345 vs ~400 us per
   // launch on the f32 tiles; si1's N <= 64 blocks ran slower there: f32)
-  const bool skinny = p.Bb && mode >= 1 && mode <= 2 && p.K == p.K1 && p.K <= 64 && p.K % 4 == 0 &&
-                      p.N >= 128 && p.epi == 0;
-  const bool btile = p.Bb && mode >= 2 && !skinny && p.K1 % 4 == 0 && (p.K - p.K1) % 4 == 0;
+  const bool skinny = p.Bb && (mode == 1 || mode == 2) && p.K == p.K1 && p.K <= 64 &&
+                      p.K % 4 == 0 && p.N >= 128 && p.epi == 0;
+  // bf16x6 tiles (default, mode 1) for the wide scalar blocks: l = 0, K and N
+  // >= 224 -- the 0e gate launch (K 352, N 224) and si2^T's 0e block (224 x
+  // 224) are MFMA-bound on the f32 tiles (139 vs 185 us and 75 vs ~105 us per
+  // launch); si1's and si1^T + sc^T's 0e blocks (N 128) are not (+5 to +8 us)
+  const bool btile = p.Bb && !skinny && p.K1 % 4 == 0 && (p.K - p.K1) % 4 == 0 &&
+                     (mode == 2 || mode == 3 || (mode == 1 && p.R == 1 && p.K >= 224 && p.N >= 224));
   int tm, tn;
   if (skinny) {          // k_nodelin_s: 64-row tiles over all N
     q.kind = 2;
