@@ -235,6 +235,25 @@ __device__ __forceinline__ void split3x8(const float (&v)[8], bf16x8 (&d)[3]) {
   for (int pc = 0; pc < 3; ++pc) d[pc] = __builtin_bit_cast(bf16x8, w[pc]);
 }
 
+// the same in two pieces (v = p0 + p1 + O(2^-16 |v|)): the operand of the
+// three-product (bf16x3) dH2 form below
+__device__ __forceinline__ void split2x8(const float (&v)[8], bf16x8 (&d)[2]) {
+  u32x4 w[2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x2 r;
+    r[0] = v[2 * q];
+    r[1] = v[2 * q + 1];
+    const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
+    w[0][q] = u;
+    r[0] -= __builtin_bit_cast(float, u << 16);
+    r[1] -= __builtin_bit_cast(float, u & 0xffff0000u);
+    w[1][q] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
+  }
+  d[0] = __builtin_bit_cast(bf16x8, w[0]);
+  d[1] = __builtin_bit_cast(bf16x8, w[1]);
+}
+
 // the lane's 16 H2 values (units 16 bh + 4g + r) as three bf16 pieces
 __device__ __forceinline__ void split_h2(const f32x4 (&h2)[4], Op3& o) {
 #pragma unroll
@@ -823,6 +842,17 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
 // pass per node): every W2 operand block (w recompute and dH2) feeds both
 // tiles, and dE/dx[j] of both tiles is summed in registers before the
 // per-block DPP row sum.  The second tile is skipped when it has no edge.
+// dH2 = dw W2^T (the gradient of the radial MLP's hidden layer; the
+// forward-consistent w = H2 W2 stays on six products) on three bf16 products
+// by default: dw in two pieces (16 significant bits), W2's first two pieces,
+// products p1 q0 + p0 q1 + p0 q0 (dropped terms ~2^-16 of dH2).  Measured on
+// the reference KAT systems: the force errors against the reference are the
+// six-product build's (2.9e-6 .. 2.1e-5 vs 3.1e-6 .. 1.9e-5 eV/A, both
+// dominated by the fp32 path elsewhere; tolerance 1e-4), the middle backward
+// 12 % faster (fewer MFMAs and split instructions).  E3GNN_DH2_X3=0: six.
+#ifndef E3GNN_DH2_X3
+#define E3GNN_DH2_X3 1
+#endif
 constexpr int LS_BLK = 6144;            // bytes of one w2v column block (3 pieces x 2 halves x 1 KB)
 constexpr int LS_PAIR_W = 2 * LS_BLK;   // the pair's two w-recompute operand blocks
 constexpr int LS_PAIR_D = 12288;        // the pair's dH2 operand (w2d: 3 pieces x 4 bh x 1 KB)
@@ -832,6 +862,27 @@ constexpr int LS_PAIR_D = 12288;        // the pair's dH2 operand (w2d: 3 pieces
 // block the three pieces are loaded right before its six MFMAs
 __device__ __forceinline__ void dh2_pair_g(f32x4 (&dh2)[4], const float (&da)[4], const float (&db)[4],
                                            __amdgpu_buffer_rsrc_t w2d, int pair, int lane) {
+  if constexpr (E3GNN_DH2_X3) {   // three products (see dh2_pair)
+    bf16x8 d[2];
+    {
+      float v[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = t < 4 ? da[t] : db[t - 4];
+      split2x8(v, d);
+    }
+#pragma unroll
+    for (int bh = 0; bh < 4; ++bh) {
+      bf16x8 a[2];
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc)
+        a[pc] = __builtin_bit_cast(
+            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2d, lane * 16, pair * LS_PAIR_D + (pc * 4 + bh) * 1024, 0));
+      dh2[bh] = mfma16(a[1], d[0], dh2[bh]);
+      dh2[bh] = mfma16(a[0], d[1], dh2[bh]);
+      dh2[bh] = mfma16(a[0], d[0], dh2[bh]);
+    }
+    return;
+  }
   bf16x8 d[3];
   {
     float v[8];
@@ -852,8 +903,12 @@ __device__ __forceinline__ void dh2_pair_g(f32x4 (&dh2)[4], const float (&da)[4]
   }
 }
 
+// the last block's dH2 on bf16 MFMA from global (L2) W2 pieces: with the
+// three-product form its operand traffic equals the f32 form's (two pieces x 4
+// hidden blocks per pair) and the MFMA cycles drop ~5x (2.60 -> 2.41 ms, same
+// box); the six-product form (E3GNN_DH2_X3=0) measured slower than f32
 #ifndef E3GNN_NBR_DH2_BF16
-#define E3GNN_NBR_DH2_BF16 0
+#define E3GNN_NBR_DH2_BF16 E3GNN_DH2_X3
 #endif
 template <class L>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_bwd_nbr(
@@ -1056,22 +1111,19 @@ __device__ __forceinline__ void lds_op3(Op3& o, const char* blk, int lane) {
       o.v[pc][m] = *reinterpret_cast<const bf16x8*>(blk + ((pc * 2 + m) * 64 + lane) * 16);
 }
 
-// dH2^T += W2[:, pair] dw^T on bf16x6 (K = 32: element t of lane (g, c) is
+// dH2^T += W2[:, pair] dw^T on bf16 MFMA (K = 32: element t of lane (g, c) is
 // channel 4g + t of the pair's first block (t < 4) or 4g + t - 4 of its second,
-// the w2d order); A = the W2 pieces (LDS), B = dw split in three pieces
-#ifndef E3GNN_DH2_X3
-#define E3GNN_DH2_X3 0   // A/B experiment only: 3 piece products (bf16x3) instead of 6
-#endif
+// the w2d order); A = the W2 pieces (LDS), B = dw split in pieces (three
+// products by default, six with E3GNN_DH2_X3=0)
 __device__ __forceinline__ void dh2_pair(f32x4 (&dh2)[4], const float (&da)[4], const float (&db)[4],
                                          const char* pimg, int lane) {
   if constexpr (E3GNN_DH2_X3) {
     bf16x8 d[2];
+    {
+      float v[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      float v = t < 4 ? da[t] : db[t - 4];
-      const __bf16 b0 = (__bf16)v;
-      d[0][t] = b0;
-      d[1][t] = (__bf16)(v - (float)b0);
+      for (int t = 0; t < 8; ++t) v[t] = t < 4 ? da[t] : db[t - 4];
+      split2x8(v, d);
     }
 #pragma unroll
     for (int bh = 0; bh < 4; ++bh) {

@@ -92,6 +92,7 @@ for s in "$@"; do
     btmlp_*) v=${s#btmlp_}; cg=${v%_*}; wt=${v#*_}; step btmlp_$v 600 env E3GNN_MLP_FWD_CG=$cg E3GNN_MLP_W2T=$wt rocprofv3 --kernel-trace --stats -d gpurun_out/prof_mlp_$v -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     proftracenl_*) v=${s#proftracenl_}; step proftracenl_$v 600 env E3GNN_NL_BF16=$v rocprofv3 --kernel-trace --output-format csv -d gpurun_out/proftracenl_$v -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     benchnlm_*) v=${s#benchnlm_}; step benchnlm_$v 600 env E3GNN_NL_BF16=$v python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
+    fullv_*) v=${s#fullv_}; step full_$v 900 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v --timeout 600 --timeout-method thread ;;
     tgb) step tgb 300 python tools/tgemm_bench.py ;;
     benchmc_*) v=${s#benchmc_}; step benchmc_$v 600 python bench.py --model-config $v --steps 5 --warmup 2 --no-cpu-baseline ;;
     proftrain2) step proftrain2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train2 -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
