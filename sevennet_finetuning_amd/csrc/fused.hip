@@ -280,6 +280,32 @@ __device__ __forceinline__ f32x4 w2_block(const Op3& h, const Op3& w) {
   return acc;
 }
 
+// the same block from the first two pieces only (three products): the
+// backward kernels' w recompute (default; E3GNN_BWD_W_X3=0: six).  The energy
+// keeps the forward's six-product w; the recomputed w differs from it by
+// ~2^-16 relative, and the force errors against the reference KATs did not
+// move (max 1.91e-5 -> 1.89e-5 eV/A over the five systems; 97k / 778k
+// full-size checks green); middle backward -5.5 %, first block -11 %
+template <bool HA>
+__device__ __forceinline__ f32x4 w2_block3(const Op3& h, const Op3& w) {
+  f32x4 acc = zero4();
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    acc = HA ? mfma16(h.v[1][m], w.v[0][m], acc) : mfma16(w.v[0][m], h.v[1][m], acc);
+    acc = HA ? mfma16(h.v[0][m], w.v[1][m], acc) : mfma16(w.v[1][m], h.v[0][m], acc);
+    acc = HA ? mfma16(h.v[0][m], w.v[0][m], acc) : mfma16(w.v[0][m], h.v[0][m], acc);
+  }
+  return acc;
+}
+#ifndef E3GNN_BWD_W_X3
+#define E3GNN_BWD_W_X3 1
+#endif
+template <bool HA>
+__device__ __forceinline__ f32x4 w2_block_bwd(const Op3& h, const Op3& w) {
+  if constexpr (E3GNN_BWD_W_X3) return w2_block3<HA>(h, w);
+  else return w2_block<HA>(h, w);
+}
+
 // ---------------------------------------------------------------- radial MLP
 // Tile of 16 edge slots [e0, e0+16) (slots >= e1 are zero rows).
 // a1/a2: pre-activations of the two hidden layers, transposed (4 blocks of 16 units).
@@ -967,8 +993,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     int nb = 0;
     constexpr int NBLK = L::W / 16;
     f32x4 wcur[2], wnxt[2] = {zero4(), zero4()};
-    wcur[0] = w2_block<false>(hq[0], wq);
-    wcur[1] = two ? w2_block<false>(hq[1], wq) : zero4();
+    wcur[0] = w2_block_bwd<false>(hq[0], wq);
+    wcur[1] = two ? w2_block_bwd<false>(hq[1], wq) : zero4();
     if (NBLK > 1) load_w2b(wq, R.w2v, lane, 16);
     float dYa[2][9];
 #pragma unroll
@@ -1001,8 +1027,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #endif
               f32x4 wv[2] = {wcur[0], wcur[1]};
               if (nb + 1 < NBLK) {
-                wnxt[0] = w2_block<false>(hq[0], wq);
-                wnxt[1] = two ? w2_block<false>(hq[1], wq) : zero4();
+                wnxt[0] = w2_block_bwd<false>(hq[0], wq);
+                wnxt[1] = two ? w2_block_bwd<false>(hq[1], wq) : zero4();
               }
               if (nb + 2 < NBLK) load_w2b(wq, R.w2v, lane, 16 * (nb + 2));
 #pragma unroll
@@ -1351,9 +1377,9 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                     __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
                     Op3 wq;
                     lds_op3(wq, img, lane);
-                    wv0 = w2_block<false>(hq, wq);
+                    wv0 = w2_block_bwd<false>(hq, wq);
                     lds_op3(wq, img + LS_BLK, lane);
-                    wv1 = w2_block<false>(hq, wq);
+                    wv1 = w2_block_bwd<false>(hq, wq);
                     __builtin_amdgcn_s_setprio(0);
                   }
                   if constexpr (STAMPED) STAMP(3);   // w recompute
