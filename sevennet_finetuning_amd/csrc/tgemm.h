@@ -34,15 +34,23 @@ struct TgProb {
   const int* kr;  // per-tile k ranges [lo1, hi1, lo2, hi2) (nullable; e3gnn_gemm_desc::krange)
   int kr_sm;      // its row-tile stride (0: per column tile)
   // set by tg_add
+  int mode;   // tile shape: 0 = 64 x 64 x 16, 1 = 32 x 32 x 32 with the waves over k
   int tiles_n, tiles_mn, ksteps, tile_begin;
   int64_t red_begin;
 };
 constexpr int TG_MAX_PROBS = 12;
+// The kernel argument.  Every workgroup first finds its problem: the
+// problems' first tiles (and reduction ranges) sit in compact arrays at the
+// front, read with a few wide scalar loads at once -- a loop over the
+// problems' own fields (240 bytes apart) read them one dependent load at a
+// time, ~5 us of kernel-argument latency per launch.
 struct TgBatch {
-  TgProb p[TG_MAX_PROBS];
+  int tile_begin[TG_MAX_PROBS] = {};
+  int64_t red_lo[TG_MAX_PROBS] = {}, red_hi[TG_MAX_PROBS] = {};   // [lo, hi): the problem's outputs in the reduction grid
   int nprob = 0;
   int total_tiles = 0;
   int64_t red_total = 0;
+  TgProb p[TG_MAX_PROBS];
 };
 // split count the kernel would choose for an (M x N) output with K summed rows
 int tg_splits(int64_t M, int64_t N, int64_t K);

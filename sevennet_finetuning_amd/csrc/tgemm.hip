@@ -14,11 +14,15 @@
 // calls torch made for these products (trainer.py:155-222 under
 // force_output.py:158-215's create_graph).
 //
-// Tile 64x64x16, 256 threads = 4 waves, each wave one 32x32 accumulator;
-// operands staged k-major through LDS (As[k][m], Bs[k][n]) so the MFMA operand
-// reads are unit-stride; the next k-step's loads are issued before the
-// current step's MFMAs.  Vector (16-byte) loads along the contiguous dimension
-// when the operand's base and leading dimension allow it.
+// Two tile shapes, chosen per problem (TgProb::mode): 64x64x16 -- 256
+// threads = 4 waves, each wave one 32x32 accumulator -- for problems with
+// enough output tiles to fill the chip, and 32x32x32 with the four waves
+// splitting each k step (8 k each) for the small ones (the fine-tune batch's
+// linears: M ~ 400-2000 rows, ~100 tiles of 64x64 = one wave on a tenth of
+// the SIMDs); the four partial accumulators are summed through LDS in wave
+// order (deterministic).  Operands staged k-major through LDS (As[k][m],
+// Bs[k][n]) so the MFMA operand reads are unit-stride; the next k-steps'
+// loads are in flight during the current step's MFMAs.
 #include "common.h"
 #include "tgemm.h"
 
@@ -28,17 +32,34 @@
 namespace e3gnn {
 namespace {
 
-constexpr int TBM = 64, TBN = 64, TBK = 16, TPAD = 4;
-constexpr int TEL = TBK * TBM / 256;   // elements of one operand slab per thread
-constexpr int TLD = TBM + TPAD;        // LDS row (k) stride, floats
+// tile shapes: MODE 0 = 64x64x16 (waves 2 x 2 over the tile), MODE 1 =
+// 32x32xTG_M1_BK (waves over k); NS = register ring depth in k steps
+#ifndef TG_M1_BK
+#define TG_M1_BK 32
+#endif
+#ifndef TG_NS0
+#define TG_NS0 4
+#endif
+#ifndef TG_NS1
+#define TG_NS1 4
+#endif
+template <int MODE> struct TgShape {
+  static constexpr int BM = MODE ? 32 : 64;         // tile rows = columns
+  static constexpr int BK = MODE ? TG_M1_BK : 16;   // k per step
+  static constexpr int NS = MODE ? TG_NS1 : TG_NS0;
+  static constexpr int TEL = BK * BM / 256;         // elements of one operand slab per thread
+  static constexpr int TLD = BM + 4;                // LDS row (k) stride, floats
+  static constexpr int SLAB = BK * TLD;             // one LDS buffer of one operand
+};
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+// staging (2 operands x 2 buffers) of either shape, and MODE 1's 4 x 16 x 64 partials
+constexpr int LDS_FLOATS = cmax(cmax(4 * TgShape<0>::SLAB, 4 * TgShape<1>::SLAB), 4 * 16 * 64);
 constexpr int OOB = 0x7ffffff0;        // outside every descriptor: reads 0
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-
 __device__ __forceinline__ int tg_find(const TgBatch& b, int tile) {
   int p = 0;
-#pragma unroll 1
-  for (int i = 1; i < b.nprob; ++i)
-    if (tile >= b.p[i].tile_begin) p = i;
+#pragma unroll
+  for (int i = 1; i < TG_MAX_PROBS; ++i) p += (i < b.nprob && tile >= b.tile_begin[i]) ? 1 : 0;
   return p;
 }
 
@@ -51,14 +72,15 @@ __device__ __forceinline__ int64_t rfl(int64_t v) {
 
 // One operand of the tile, element (r, k) in the TgLay layout, read through
 // a buffer descriptor at the operand's base: the thread's TEL elements of a
-// TBK x 64 slab, element e = 256 i + tid walking the contiguous dimension
-// fastest (k contiguous: k = e % TBK, r = e / TBK; else r = e % 64, k = e / 64).
+// BK x BM slab, element e = 256 i + tid walking the contiguous dimension
+// fastest (k contiguous: k = e % BK, r = e / BK; else r = e % BM, k = e / BM).
 // Their byte offsets at the segment start and LDS slots are fixed for the
 // launch; a k step adds a scalar offset (k steps never straddle a segment: a
 // segment is padded to whole steps) -- no per-element address arithmetic in
 // the k loop.  Elements past the rows or a segment's ks read 0 (OOB offset).
 constexpr int TG_RECORDS = 0x7fff0000;
 constexpr int TG_MAX_SEG = 9;   // K segments of a part (2l + 1 <= 9: lmax 4)   // descriptor size: every real offset is below, OOB above
+template <int TEL>
 struct OpB {
   __amdgpu_buffer_rsrc_t R;
   int vo[TEL];   // byte offset at k = 0 of a segment, OOB past the rows
@@ -66,7 +88,10 @@ struct OpB {
   int lo[TEL];   // LDS slot S[k][r]
   int kst4, sst4, ks, sps;   // bytes per k, per segment; segment rows; steps per segment
 };
-__device__ __forceinline__ void opb_init(OpB& o, const TgLay& L, int r0, int rmax) {
+template <int MODE>
+__device__ __forceinline__ void opb_init(OpB<TgShape<MODE>::TEL>& o, const TgLay& L, int r0, int rmax) {
+  using Sh = TgShape<MODE>;
+  constexpr int BM = Sh::BM, BK = Sh::BK, TEL = Sh::TEL;
   o.R = __builtin_amdgcn_make_buffer_rsrc((void*)L.X, (short)0, TG_RECORDS, 0x00020000);
   const int rep = rfl(L.rep), rs = rfl(L.rs);
   const int ld = rfl(L.ld), kst = rfl(L.kst);
@@ -76,17 +101,17 @@ __device__ __forceinline__ void opb_init(OpB& o, const TgLay& L, int r0, int rma
 #pragma unroll
   for (int i = 0; i < TEL; ++i) {
     const int e = 256 * i + tid;
-    const int r = kfast ? (e / TBK) : (e & 63), k = kfast ? (e % TBK) : (e >> 6);
+    const int r = kfast ? (e / BK) : (e % BM), k = kfast ? (e % BK) : (e / BM);
     const int rr = r0 + r;
     const int q = rep > 1 ? (int)__umulhi((unsigned)rr, mag) : rr;   // rr / rep (rep <= 9)
     o.vo[i] = rr < rmax ? (q * ld + (rr - q * rep) * rs + k * kst) * 4 : OOB;
     o.kk[i] = k;
-    o.lo[i] = k * TLD + r;
+    o.lo[i] = k * Sh::TLD + r;
   }
   o.kst4 = kst * 4;
   o.sst4 = rfl(L.sst) * 4;
   o.ks = rfl(L.ks);
-  o.sps = (o.ks + TBK - 1) / TBK;
+  o.sps = (o.ks + BK - 1) / BK;
 }
 
 // Main loop: LDS double buffer + a ring of NS register slots, so the loads of
@@ -95,29 +120,29 @@ __device__ __forceinline__ void opb_init(OpB& o, const TgLay& L, int r0, int rma
 // compile-time constant, and every iteration issues the same loads (past the
 // split's end at OOB offsets, the compute skipped), so the compiler's wait
 // counts are exact: a slot's consumer waits for that slot's loads only.
-constexpr int NS = 4;
 
-__global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
-  __shared__ __attribute__((aligned(16))) float As[2][TBK * TLD];
-  __shared__ __attribute__((aligned(16))) float Bs[2][TBK * TLD];
-  const TgProb& P = batch.p[tg_find(batch, blockIdx.x)];
-  const int local = blockIdx.x - P.tile_begin;
+template <int MODE>
+__device__ __forceinline__ void tg_tile(const TgProb& P, int local, float* lds) {
+  using Sh = TgShape<MODE>;
+  constexpr int BM = Sh::BM, BK = Sh::BK, TLD = Sh::TLD, SLAB = Sh::SLAB, NS = Sh::NS, TEL = Sh::TEL;
+  float* As = lds;              // [2][BK][TLD]
+  float* Bs = lds + 2 * SLAB;   // [2][BK][TLD]
   const int s = local / P.tiles_mn, mn = local - s * P.tiles_mn;
   const int tm = mn / P.tiles_n, tn = mn - tm * P.tiles_n;
-  const int m0 = tm * TBM, n0 = tn * TBN;
+  const int m0 = tm * BM, n0 = tn * BM;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = MODE ? 0 : wave >> 1, wc = MODE ? 0 : wave & 1;
   // the problem's scalars as values computed in registers (readfirstlane):
   // the compiler would otherwise re-load them from the kernel arguments inside
   // the k loop, and each such scalar load's wait also drains the outstanding
   // LDS operations (one counter)
   const int PM = rfl(P.M), PN = rfl(P.N), PK1 = rfl(P.K1), PK2 = rfl(P.K2);
   // op(A)(m, k) and op(B)(n, k): B enters as the (n x k) operand
-  OpB a1, b1, a2, b2;
-  opb_init(a1, P.A1, m0, PM);
-  opb_init(b1, P.B1, n0, PN);
-  opb_init(a2, P.A2, m0, PM);
-  opb_init(b2, P.B2, n0, PN);
+  OpB<TEL> a1, b1, a2, b2;
+  opb_init<MODE>(a1, P.A1, m0, PM);
+  opb_init<MODE>(b1, P.B1, n0, PN);
+  opb_init<MODE>(a2, P.A2, m0, PM);
+  opb_init<MODE>(b2, P.B2, n0, PN);
   // the k steps over the concatenated K = K1 + K2: each part's segments
   // padded to whole steps
   const int nk1 = a1.ks > 0 ? (PK1 / a1.ks) * a1.sps : 0;
@@ -127,12 +152,12 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
   // kb1 + j (j < n1) or nk1 + kb2 + j - n1.  This split's slice of it:
   // [jb, je) (a split past the tile's steps has none: zero partials)
   int kb1 = 0, n1 = nk1, kb2 = 0, n2 = nk - nk1;
-  if (P.kr) {
-    const int* q = P.kr + 4 * (tm * P.kr_sm + tn);
-    kb1 = rfl(q[0] / TBK);
-    n1 = max(0, rfl((q[1] + TBK - 1) / TBK) - kb1);
-    kb2 = rfl(q[2] / TBK);
-    n2 = max(0, rfl((q[3] + TBK - 1) / TBK) - kb2);
+  if (P.kr) {   // the table is per 64 x 64 tile: a 32 x 32 tile takes its hull's range
+    const int* q = P.kr + 4 * ((MODE ? tm >> 1 : tm) * P.kr_sm + (MODE ? tn >> 1 : tn));
+    kb1 = rfl(q[0] / BK);
+    n1 = max(0, rfl((q[1] + BK - 1) / BK) - kb1);
+    kb2 = rfl(q[2] / BK);
+    n2 = max(0, rfl((q[3] + BK - 1) / BK) - kb2);
   }
   const int jb = rfl(s * P.ksteps), je = min(n1 + n2, jb + rfl(P.ksteps));
   auto kt_of = [&](int j) { return j < n1 ? kb1 + j : nk1 + kb2 + (j - n1); };
@@ -146,14 +171,14 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
     seg = 0;
 #pragma unroll
     for (int c = 1; c < TG_MAX_SEG; ++c) seg += t >= c * sps;
-    kin = (t - seg * sps) * TBK;
+    kin = (t - seg * sps) * BK;
   };
   int cj = jb, cseg, ckin;
   bool cfirst = kt_of(jb) < nk1;
   seg_of(cfirst ? kt_of(jb) : kt_of(jb) - nk1, cfirst ? a1.sps : a2.sps, cseg, ckin);
   int seg2, kin2;   // where the second pair's range of this tile starts
   seg_of(kb2, a2.sps, seg2, kin2);
-  auto load1 = [&](const OpB& o1, const OpB& o2, bool first, bool live, int seg, int kin, float (&x)[TEL]) {
+  auto load1 = [&](const OpB<TEL>& o1, const OpB<TEL>& o2, bool first, bool live, int seg, int kin, float (&x)[TEL]) {
     const int soff = kin * (first ? o1.kst4 : o2.kst4) + seg * (first ? o1.sst4 : o2.sst4);
     const int kmax = first ? o1.ks : o2.ks;
 #pragma unroll
@@ -170,9 +195,9 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
     load1(b1, b2, cfirst, live, cseg, ckin, xb);
     ++cj;
     const bool sw = cfirst && cj == n1;             // into the second pair's range
-    const int spsT = (cfirst ? a1.sps : a2.sps) * TBK;
-    const bool wrap = ckin + TBK >= spsT;
-    const int nkin = wrap ? 0 : ckin + TBK, nseg = wrap ? cseg + 1 : cseg;
+    const int spsT = (cfirst ? a1.sps : a2.sps) * BK;
+    const bool wrap = ckin + BK >= spsT;
+    const int nkin = wrap ? 0 : ckin + BK, nseg = wrap ? cseg + 1 : cseg;
     ckin = sw ? kin2 : nkin;
     cseg = sw ? seg2 : nseg;
     cfirst = cfirst && !sw;
@@ -181,8 +206,8 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
     const bool first = j < n1;
 #pragma unroll
     for (int i = 0; i < TEL; ++i) {
-      As[buf][first ? a1.lo[i] : a2.lo[i]] = xa[i];
-      Bs[buf][first ? b1.lo[i] : b2.lo[i]] = xb[i];
+      As[buf * SLAB + (first ? a1.lo[i] : a2.lo[i])] = xa[i];
+      Bs[buf * SLAB + (first ? b1.lo[i] : b2.lo[i])] = xb[i];
     }
   };
   f32x16 acc;
@@ -202,10 +227,14 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
         load(ra[(u + NS - 1) % NS], rb[(u + NS - 1) % NS]);
         if (j < je) {
           const int buf = (j - jb) & 1;
+          // MODE 0: the step's 16 k on the wave's 32 x 32 quarter; MODE 1:
+          // the wave's 8 of the step's 32 k on the whole 32 x 32 tile
+          constexpr int KW = MODE ? BK / 4 : BK;
+          const int kw0 = MODE ? wave * KW : 0;
 #pragma unroll
-          for (int kk = 0; kk < TBK; kk += 2) {
-            const float av = As[buf][(kk + (lane >> 5)) * TLD + wr * 32 + (lane & 31)];
-            const float bv = Bs[buf][(kk + (lane >> 5)) * TLD + wc * 32 + (lane & 31)];
+          for (int kk = 0; kk < KW; kk += 2) {
+            const float av = As[buf * SLAB + (kw0 + kk + (lane >> 5)) * TLD + wr * 32 + (lane & 31)];
+            const float bv = Bs[buf * SLAB + (kw0 + kk + (lane >> 5)) * TLD + wc * 32 + (lane & 31)];
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
           }
         }
@@ -215,18 +244,42 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
       }
     }
   } else if (P.kr && rfl(P.beta) && rfl(P.splits) <= 1) {
-    return;   // nothing to add to this tile
+    return;   // nothing to add to this tile (uniform over the workgroup)
+  }
+  // the tile's values this wave finishes: MODE 0 its own 16 accumulator
+  // registers; MODE 1 registers 4 wave .. 4 wave + 3 of the sum of the four
+  // waves' partial accumulators (LDS, added in wave order)
+  constexpr int RN = MODE ? 4 : 16;
+  const int r0 = MODE ? 4 * wave : 0;
+  float v[RN];
+  if (MODE) {
+    // every wave is past the loop's last barrier: the staging buffers are free
+#pragma unroll
+    for (int r = 0; r < 16; ++r) lds[(wave * 16 + r) * 64 + lane] = acc[r];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int r = r0 + j;
+      v[j] = ((lds[r * 64 + lane] + lds[(16 + r) * 64 + lane]) + lds[(32 + r) * 64 + lane]) +
+             lds[(48 + r) * 64 + lane];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < RN; ++j) v[j] = acc[j];
   }
   const int col = n0 + wc * 32 + (lane & 31);
   if (col >= PN) return;
   // D lane l, reg r: row 8 (r >> 2) + 4 (l >> 5) + (r & 3), column l & 31
-  auto row_of = [&](int r) { return m0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); };
+  auto row_of = [&](int j) {
+    const int r = r0 + j;
+    return m0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+  };
   typedef __attribute__((address_space(1))) float* gp;
   if (rfl(P.splits) > 1) {   // partial tile to this split's slab; k_tgemm_reduce finishes
     const gp w = (gp)(uintptr_t)rfl((int64_t)(uintptr_t)(P.ws + (int64_t)s * PM * PN));
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if (row_of(r) < PM) w[(int64_t)row_of(r) * PN + col] = acc[r];
+    for (int j = 0; j < RN; ++j)
+      if (row_of(j) < PM) w[(int64_t)row_of(j) * PN + col] = v[j];
     return;
   }
   const gp C = (gp)(uintptr_t)rfl((int64_t)(uintptr_t)P.C);
@@ -236,69 +289,93 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
   // m / crep by a multiply-high (exact for crep <= 9, m < 2^28): an integer
   // division per output element would cost ~30 vector instructions
   const unsigned cmag = crep > 1 ? 0xffffffffu / (unsigned)crep + 1u : 0u;
-  auto at = [&](int r) {
-    const int m = row_of(r);
+  auto at = [&](int j) {
+    const int m = row_of(j);
     const int q = crep > 1 ? (int)__umulhi((unsigned)m, cmag) : m;
     return (int64_t)q * ldc + (m - q * crep) * crs + (int64_t)col * cns;
   };
-  float old[16];
-  if (rfl(P.beta)) {   // all 16 old values in flight at once
+  float old[RN];
+  if (rfl(P.beta)) {   // all old values in flight at once
 #pragma unroll
-    for (int r = 0; r < 16; ++r) old[r] = row_of(r) < PM ? C[at(r)] : 0.f;
+    for (int j = 0; j < RN; ++j) old[j] = row_of(j) < PM ? C[at(j)] : 0.f;
   } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) old[r] = 0.f;
+    for (int j = 0; j < RN; ++j) old[j] = 0.f;
   }
 #pragma unroll
-  for (int r = 0; r < 16; ++r)
-    if (row_of(r) < PM) C[at(r)] = old[r] + alpha * acc[r];
+  for (int j = 0; j < RN; ++j)
+    if (row_of(j) < PM) C[at(j)] = old[j] + alpha * v[j];
+}
+
+__global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
+  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+  const TgProb& P = batch.p[tg_find(batch, blockIdx.x)];
+  const int local = blockIdx.x - P.tile_begin;
+  if (rfl(P.mode))
+    tg_tile<1>(P, local, lds);
+  else
+    tg_tile<0>(P, local, lds);
 }
 
 // C = beta C + alpha sum_s ws[s] over the split problems, s in order
 __global__ __launch_bounds__(256) void k_tgemm_reduce(TgBatch batch) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-#pragma unroll 1
-  for (int p = 0; p < batch.nprob; ++p) {
-    const TgProb& P = batch.p[p];
-    if (P.splits <= 1 || i < P.red_begin || i >= P.red_begin + (int64_t)P.M * P.N) continue;
-    const int64_t e = i - P.red_begin, mn = (int64_t)P.M * P.N;
-    const int row = (int)(e / P.N), col = (int)(e - (int64_t)row * P.N);
-    // slabs 0, 1, 2, ... added in order; eight loads in flight at a time (a
-    // split count of ~70 read one dependent load at a time took ~70 latencies)
-    const float* w = P.ws + e;
-    float sum = 0.f;
-    int s = 0;
-#pragma unroll 1
-    for (; s + 8 <= P.splits; s += 8) {
-      float v[8];
+  int p = -1;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = w[(int64_t)(s + u) * mn];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sum += v[u];
-    }
+  for (int q = 0; q < TG_MAX_PROBS; ++q)
+    if (q < batch.nprob && i >= batch.red_lo[q] && i < batch.red_hi[q]) p = q;
+  if (p < 0) return;
+  const TgProb& P = batch.p[p];
+  const int64_t e = i - batch.red_lo[p], mn = (int64_t)P.M * P.N;
+  const int row = (int)(e / P.N), col = (int)(e - (int64_t)row * P.N);
+  // slabs 0, 1, 2, ... added in order; sixteen loads in flight at a time
+  // (a split count of ~70 read one dependent load at a time took ~70
+  // latencies)
+  const float* w = P.ws + e;
+  float sum = 0.f;
+  int s = 0;
 #pragma unroll 1
-    for (; s < P.splits; ++s) sum += w[(int64_t)s * mn];
-    float* c = P.C + (int64_t)(row / P.crep) * P.ldc + (row % P.crep) * P.crs + (int64_t)col * P.cns;
-    const float v = P.alpha * sum;
-    *c = P.beta ? *c + v : v;
+  for (; s + 16 <= P.splits; s += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = w[(int64_t)(s + u) * mn];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) sum += v[u];
   }
+#pragma unroll 1
+  for (; s + 4 <= P.splits; s += 4) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = w[(int64_t)(s + u) * mn];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sum += v[u];
+  }
+#pragma unroll 1
+  for (; s < P.splits; ++s) sum += w[(int64_t)s * mn];
+  float* c = P.C + (int64_t)(row / P.crep) * P.ldc + (row % P.crep) * P.crs + (int64_t)col * P.cns;
+  const float v = P.alpha * sum;
+  *c = P.beta ? *c + v : v;
 }
 
 }  // namespace
 
 // split-K policy (E3GNN_TG_SPLIT="min_ksteps,target_wgs,ksteps_per_split" for
-// A/B timing): split only a long K (the extra reduction launch costs ~5 us)
+// A/B timing, in 64 x 64 x 16 tile steps): split only a long K (the extra
+// reduction launch costs ~5 us).  E3GNN_TG_SMALL: problems with fewer
+// (64 x 64 tiles x splits) than this take the 32 x 32 x 32 k-split tiles
 static int tg_policy(int i) {
-  static int v[3] = {-1, -1, -1};
+  static int v[5] = {-1, -1, -1, -1, -1};
   if (v[0] < 0) {
-    v[0] = 32, v[1] = 1024, v[2] = 8;
+    v[0] = 32, v[1] = 1024, v[2] = 8, v[3] = 256, v[4] = 0;
     if (const char* e = std::getenv("E3GNN_TG_SPLIT")) std::sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]);
+    if (const char* e = std::getenv("E3GNN_TG_SMALL")) v[3] = std::atoi(e);
+    if (const char* e = std::getenv("E3GNN_TG_SMALL_SPLIT")) v[4] = std::atoi(e);
   }
   return v[i];
 }
 int tg_splits(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
-  const int64_t nk = (K + TBK - 1) / TBK;
+  const int64_t tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  const int64_t nk = (K + 15) / 16;
   // few output tiles and a long K (the edge-summed weight gradients: K = 2E
   // ~ 24k rows onto 64 x 960 outputs): split K so the launch has ~target
   // workgroups of >= ksteps_per_split k-steps each
@@ -311,26 +388,32 @@ bool tg_add(TgBatch& b, TgProb p) {
   if (b.nprob >= TG_MAX_PROBS || p.M < 0 || p.N < 0 || p.K1 < 0 || p.K2 < 0) return false;
   if (p.M == 0 || p.N == 0) return true;
   if (p.K2 == 0) p.A2 = p.A1, p.B2 = p.B1, p.A2.ks = p.B2.ks = 0;   // no second pair
-  auto steps = [](int K, const TgLay& a, const TgLay& b) {
+  if (p.splits < 1) p.splits = 1;
+  p.mode = ((int64_t)((p.M + 63) / 64) * ((p.N + 63) / 64) * p.splits < tg_policy(3) &&
+            (p.splits == 1 || tg_policy(4))) ? 1 : 0;
+  const int BM = p.mode ? 32 : 64, BK = p.mode ? TG_M1_BK : 16;
+  auto steps = [BK](int K, const TgLay& a, const TgLay& b) {
     if (K <= 0) return 0;
     if (a.ks <= 0 || a.ks != b.ks || K % a.ks || K / a.ks > TG_MAX_SEG || a.rep < 1 || b.rep < 1 ||
         a.rep > 9 || b.rep > 9)
       return -1;
-    return (K / a.ks) * ((a.ks + TBK - 1) / TBK);
+    return (K / a.ks) * ((a.ks + BK - 1) / BK);
   };
   const int s1 = steps(p.K1, p.A1, p.B1), s2 = steps(p.K2, p.A2, p.B2);
   if (s1 < 0 || s2 < 0 || p.crep < 1 || p.crep > 9 || (int64_t)p.M * 9 >= (1 << 28)) return false;
   const int nk = s1 + s2;
-  p.tiles_n = (p.N + TBN - 1) / TBN;
-  p.tiles_mn = ((p.M + TBM - 1) / TBM) * p.tiles_n;
-  if (p.splits < 1) p.splits = 1;
+  p.tiles_n = (p.N + BM - 1) / BM;
+  p.tiles_mn = ((p.M + BM - 1) / BM) * p.tiles_n;
   p.ksteps = std::max(1, (nk + p.splits - 1) / p.splits);
-  p.splits = std::max(1, (nk + p.ksteps - 1) / p.ksteps);
+  p.splits = std::max(1, (nk + p.ksteps - 1) / p.ksteps);   // never above the request: the workspace holds it
   p.tile_begin = b.total_tiles;
+  b.tile_begin[b.nprob] = p.tile_begin;
   b.total_tiles += p.tiles_mn * p.splits;
+  b.red_lo[b.nprob] = b.red_hi[b.nprob] = b.red_total;
   if (p.splits > 1) {
     p.red_begin = b.red_total;
     b.red_total += (int64_t)p.M * p.N;
+    b.red_hi[b.nprob] = b.red_total;
   }
   b.p[b.nprob++] = p;
   return true;

@@ -773,7 +773,8 @@ def test_grouped_gemm_matches_fp64():
     op(A) op(B) [+ op(A2) op(B2)] with every transpose combination, alpha /
     beta, ragged tails, a split-K weight gradient (K = 24,192 rows, the
     stacked edge count) and a K-concatenated pair, several problems in one
-    launch -- against float64 torch (f32 MFMA accumulation: 2e-6 relative to
+    launch, both tile shapes (64 x 64 for the 1100 x 1000 and the split-K
+    products, 32 x 32 with the waves over k for the small ones) -- against float64 torch (f32 MFMA accumulation: 2e-6 relative to
     the output's scale); deterministic bitwise on repetition."""
     from sevennet_finetuning_amd.train_explicit import _Gemms
 
@@ -790,7 +791,7 @@ def test_grouped_gemm_matches_fp64():
     cases = []
     for (m, n, k, ta, tb) in [(432, 480, 576, 0, 0), (433, 97, 61, 1, 0), (64, 960, 24192, 1, 0),
                               (221, 64, 130, 0, 1), (37, 29, 17, 1, 1), (1, 64, 128, 0, 0),
-                              (864, 1, 64, 0, 0)]:
+                              (864, 1, 64, 0, 0), (1100, 1000, 96, 0, 1)]:
         A = rnd(k, m).t() if ta else rnd(m, k)
         B = rnd(n, k).t() if tb else rnd(k, n)
         cases.append((A, B))

@@ -93,7 +93,17 @@ for s in "$@"; do
     proftracenl_*) v=${s#proftracenl_}; step proftracenl_$v 600 env E3GNN_NL_BF16=$v rocprofv3 --kernel-trace --output-format csv -d gpurun_out/proftracenl_$v -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     benchnlm_*) v=${s#benchnlm_}; step benchnlm_$v 600 env E3GNN_NL_BF16=$v python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     fullv_*) v=${s#fullv_}; step full_$v 900 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v --timeout 600 --timeout-method thread ;;
-    tgb) step tgb 300 python tools/tgemm_bench.py ;;
+    tgb) step tgb 300 python tools/tgemm_bench.py --full ;;
+    tgbs_*) v=${s#tgbs_}; step tgbs_$v 300 env E3GNN_TG_SMALL=$v python tools/tgemm_bench.py ;;
+    btsmall_*) v=${s#btsmall_}; step btsmall_$v 300 env E3GNN_TG_SMALL=$v python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    btss_*) v=${s#btss_}; step btss_$v 300 env E3GNN_TG_SMALL_SPLIT=$v python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    tgbss_*) v=${s#tgbss_}; step tgbss_$v 300 env E3GNN_TG_SMALL_SPLIT=$v python tools/tgemm_bench.py ;;
+    proftgb) step proftgb 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_tgb -o run -- python tools/tgemm_bench.py --reps 3 --full ;;
+    tgbv_*) v=${s#tgbv_}; step tgbv_$v 300 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python tools/tgemm_bench.py ;;
+    btv_*) v=${s#btv_}; step btv_$v 300 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    btkarg_*) v=${s#btkarg_}; step btkarg_$v 300 env HIP_FORCE_DEV_KERNARG=$v python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    tgbkarg_*) v=${s#tgbkarg_}; step tgbkarg_$v 300 env HIP_FORCE_DEV_KERNARG=$v python tools/tgemm_bench.py ;;
+    gtrain) step gtrain 600 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread ;;
     benchmc_*) v=${s#benchmc_}; step benchmc_$v 600 python bench.py --model-config $v --steps 5 --warmup 2 --no-cpu-baseline ;;
     proftrain2) step proftrain2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train2 -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -3,7 +3,7 @@ against torch's (rocBLAS) products of the same shapes.
 
 Runs one eager explicit fine-tune step of the bench_train workload, records
 every e3gnn_gemm_grouped launch (its problem descriptors), then replays each
-recorded launch alone (HIP events, median of 20) and the same problems as
+recorded launch alone (HIP events over 20 back-to-back calls, median of 5) and the same problems as
 torch.addmm calls.  GPU only.
 
 usage: python tools/tgemm_bench.py [--reps 20]
@@ -22,6 +22,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reps', type=int, default=20)
+    ap.add_argument('--full', action='store_true', help='print every problem of a long launch')
     a = ap.parse_args()
     from sevennet_finetuning_amd import _lib, train, train_explicit
     from sevennet_finetuning_amd.nn import SevenNetTrainable
@@ -56,17 +57,19 @@ def main():
     ws = torch.empty(1 << 26, device=dev)
 
     def timed(fn):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.reps)]
+        """per-call time of reps back-to-back calls (the launches queue as in
+        the step's graph), median of 5 such runs"""
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(10)]
         fn()
         torch.cuda.synchronize()
-        ts = []
-        for r in range(a.reps):
+        for r in range(5):
             ev[2 * r].record()
-            fn()
+            for _ in range(a.reps):
+                fn()
             ev[2 * r + 1].record()
         torch.cuda.synchronize()
-        ts = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e3 for r in range(a.reps))
-        return ts[len(ts) // 2]
+        ts = sorted(ev[2 * r].elapsed_time(ev[2 * r + 1]) * 1e3 / a.reps for r in range(5))
+        return ts[2]
 
     tot_h = tot_t = 0.0
     print(f"{'launch':>6} {'problems (M x N x K[+K2], tA tB; L: irreps layout)':60s} {'tgemm us':>9} {'torch us':>9}")
@@ -90,6 +93,8 @@ def main():
         tot_h += th
         tot_t += tt if tt == tt else 0.0
         print(f"{i:6d} {' '.join(shapes)[:60]:60s} {th:9.1f} {tt:9.1f}")
+        if a.full and len(' '.join(shapes)) > 60:
+            print(f"{'':6s}   {' '.join(shapes)}")
     print(f"total (one rehearsal step's launches): tgemm {tot_h:.0f} us, torch {tot_t:.0f} us, "
           f"{len(rec)} launches")
 
