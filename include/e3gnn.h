@@ -87,7 +87,7 @@ int e3gnn_model_info(const e3gnn_model* m, int* num_species, float* cutoff, int*
  * products of the fine-tune step (train_explicit.py) instead of a vendor BLAS:
  *   C = beta C + alpha (op(A) op(B) + op(A2) op(B2))      beta 0 or 1
  * op(X) = X^T when trans_* is set; row-major storage with leading dimensions
- * ld*; k2 = 0: no second operand pair (A2/B2 ignored).  Up to 8 independent
+ * ld*; k2 = 0: no second operand pair (A2/B2 ignored).  Up to 12 independent
  * problems per call (their outputs must not overlap); long-K problems are split
  * over K into `workspace` (e3gnn_gemm_workspace_floats floats) and reduced in a
  * fixed order: deterministic, no atomics. */
@@ -131,6 +131,18 @@ typedef struct e3gnn_gemm_desc {
 int64_t e3gnn_gemm_workspace_floats(int n, const e3gnn_gemm_desc* d);
 int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,
                        void* stream);
+/* flags E3GNN_GEMM_DEFER_REDUCE: the split problems' partial slabs stay in
+ * `workspace` (not reused until reduced) and their outputs are written later
+ * by e3gnn_gemm_reduce -- the fine-tune step reduces all its weight
+ * gradients in one launch at the end of the reverse sweep. */
+#define E3GNN_GEMM_DEFER_REDUCE 1
+int e3gnn_gemm_grouped_ex(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,
+                          int flags, void* stream);
+/* The deferred reductions of problems d[0..n) (the descriptors of their
+ * launches, in order; workspaces[i] = the workspace pointer their launch got
+ * plus the floats of the split problems before it in that launch); problems
+ * that were not split are skipped.  Same sums, same order as undeferred. */
+int e3gnn_gemm_reduce(int n, const e3gnn_gemm_desc* d, float* const* workspaces, void* stream);
 
 /* The fine-tune loss of the hand-scheduled step in one launch (train.py
  * LossDefinition, loss.py:8-206): criterion 0 MSELoss, 1 HuberLoss(delta), mean
@@ -246,6 +258,15 @@ int e3gnn_conv_dims(int kind, int* h_dim, int* w_dim, int* agg_dim);
 int e3gnn_conv_graph(int64_t n_nodes, int64_t n_edges, const int32_t* edge_center,
                      const int32_t* edge_nbr, int32_t* row_ptr, int32_t* src_ptr,
                      int32_t* src_perm, int32_t* scratch, void* stream);
+/* The same build from int64 edge indices (a batch's edge_index rows), also
+ * writing their int32 copies center_out / nbr_out [E]; graphs of at most
+ * e3gnn_conv_graph_small_max_nodes() nodes (one workgroup, one launch -- the
+ * per-step rebuild of a captured fine-tune step). */
+int e3gnn_conv_graph_i64(int64_t n_nodes, int64_t n_edges, const int64_t* edge_center,
+                         const int64_t* edge_nbr, int32_t* center_out, int32_t* nbr_out,
+                         int32_t* row_ptr, int32_t* src_ptr, int32_t* src_perm, int32_t* scratch,
+                         void* stream);
+int e3gnn_conv_graph_small_max_nodes(void);
 /* agg[n_nodes x agg_dim] = segmented sum of TP(h[nbr], Y, w); Y [E x 9],
  * w [E x w_dim], h [n_nodes x h_dim]. */
 int e3gnn_conv_forward(int kind, int64_t n_nodes, const int32_t* row_ptr, const int32_t* edge_nbr,

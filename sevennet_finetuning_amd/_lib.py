@@ -28,6 +28,8 @@ SIGNATURES = {
     'e3gnn_model_family': (_c_int, [_vp]),
     'e3gnn_gemm_workspace_floats': (_c_i64, [_c_int, _vp]),
     'e3gnn_gemm_grouped': (_c_int, [_c_int, _vp, _vp, _c_i64, _vp]),
+    'e3gnn_gemm_grouped_ex': (_c_int, [_c_int, _vp, _vp, _c_i64, _c_int, _vp]),
+    'e3gnn_gemm_reduce': (_c_int, [_c_int, _vp, _vp, _vp]),
     'e3gnn_loss_efs': (_c_int, [_c_int, _c_f, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                 _c_f, _c_f, _c_f, _c_f, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_ewc_flat': (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _c_f, _vp, _vp, _vp, _vp]),
@@ -50,6 +52,8 @@ SIGNATURES = {
     'e3gnn_halo_unpack': (_c_int, [_vp, _c_i64, _c_int, _vp, _vp, _c_i64, _c_int, _vp]),
     'e3gnn_conv_dims': (_c_int, [_c_int, _P(_c_int), _P(_c_int), _P(_c_int)]),
     'e3gnn_conv_graph': (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'e3gnn_conv_graph_i64': (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'e3gnn_conv_graph_small_max_nodes': (_c_int, []),
     'e3gnn_conv_forward': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_conv_backward': (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -61,6 +61,7 @@ class HipConvBackend:
 
     def __init__(self):
         self.lib = _lib.load()
+        self.small_max = int(self.lib.e3gnn_conv_graph_small_max_nodes())
         self.dims = {}
         for kind in (0, 1, 2):
             a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
@@ -85,8 +86,17 @@ class HipConvBackend:
                    'scratch': torch.empty(n + 1, dtype=torch.int32, device=dev)}
         else:
             aux = into
-            aux['center'].copy_(g.edge_center)
-            aux['nbr'].copy_(g.edge_nbr)
+            c, j = g.edge_center, g.edge_nbr
+            if (c.dtype == torch.int64 and j.dtype == torch.int64 and c.is_contiguous() and j.is_contiguous()
+                    and c.device == dev and n <= self.small_max):
+                # one launch: the int32 copies, the CSRs and the validation
+                _lib.check(self.lib.e3gnn_conv_graph_i64(
+                    n, E, c.data_ptr(), j.data_ptr(), aux['center'].data_ptr(), aux['nbr'].data_ptr(),
+                    aux['row_ptr'].data_ptr(), aux['src_ptr'].data_ptr(), aux['src_perm'].data_ptr(),
+                    aux['scratch'].data_ptr(), self._stream(aux['center'])))
+                return aux
+            aux['center'].copy_(c)
+            aux['nbr'].copy_(j)
         _lib.check(self.lib.e3gnn_conv_graph(
             n, E, aux['center'].data_ptr(), aux['nbr'].data_ptr(), aux['row_ptr'].data_ptr(),
             aux['src_ptr'].data_ptr(), aux['src_perm'].data_ptr(), aux['scratch'].data_ptr(),

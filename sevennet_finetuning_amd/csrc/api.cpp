@@ -1048,45 +1048,50 @@ int64_t e3gnn_gemm_workspace_floats(int n, const e3gnn_gemm_desc* d) {
   return w;
 }
 
-int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,
-                       void* stream) {
+static int gemm_prob(const e3gnn_gemm_desc& q, int i, TgProb& p) {
+  if (q.m < 0 || q.n < 0 || q.k < 0 || q.k2 < 0 || (q.m > 0 && q.n > 0 && (!q.c || (q.k > 0 && (!q.a || !q.b)) ||
+                                                                      (q.k2 > 0 && (!q.a2 || !q.b2)))))
+    return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: bad problem " + std::to_string(i));
+  if (q.beta != 0 && q.beta != 1) return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: beta must be 0 or 1");
+  p = TgProb{};
+  // op(A)(m, k): X[m][k] (ld, k contiguous) or X[k][m]; op(B)(k, n) as
+  // element (n, k): B[k][n] or B[n][k]
+  auto lay = [](const float* X, int64_t ld, bool kfast, int K) {
+    return TgLay{X, kfast ? (int)ld : 1, kfast ? 1 : (int)ld, 0, 1, 0, K};
+  };
+  auto glay = [](const float* X, const e3gnn_gemm_layout& g) {
+    return TgLay{X, (int)g.ld, (int)g.kst, (int)g.sst, g.rep, g.rs, g.ks};
+  };
+  if (q.layout) {
+    const e3gnn_gemm_layouts& L = *q.layout;
+    p.A1 = glay(q.a, L.a); p.B1 = glay(q.b, L.b); p.A2 = glay(q.a2, L.a2); p.B2 = glay(q.b2, L.b2);
+    p.ldc = L.ldc; p.crep = L.crep; p.crs = L.crs; p.cns = L.cns;
+  } else {
+    p.A1 = lay(q.a, q.lda, !q.trans_a, q.k);
+    p.B1 = lay(q.b, q.ldb, q.trans_b, q.k);
+    p.A2 = lay(q.a2, q.lda2, !q.trans_a2, q.k2);
+    p.B2 = lay(q.b2, q.ldb2, q.trans_b2, q.k2);
+    p.ldc = q.ldc; p.crep = 1; p.crs = 0; p.cns = 1;
+  }
+  p.C = q.c;
+  p.M = q.m; p.N = q.n; p.K1 = q.k; p.K2 = q.k2;
+  p.alpha = q.alpha; p.beta = q.beta;
+  p.kr = q.krange; p.kr_sm = q.krange_stride_m;
+  p.splits = tg_splits(q.m, q.n, (int64_t)q.k + q.k2);
+  return E3GNN_OK;
+}
+
+int e3gnn_gemm_grouped_ex(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,
+                          int flags, void* stream) {
   if (n < 0 || n > TG_MAX_PROBS || (n > 0 && !d))
     return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: 0.." + std::to_string(TG_MAX_PROBS) + " problems");
   TgBatch b;
   int64_t used = 0;
   for (int i = 0; i < n; ++i) {
-    const e3gnn_gemm_desc& q = d[i];
-    if (q.m < 0 || q.n < 0 || q.k < 0 || q.k2 < 0 || (q.m > 0 && q.n > 0 && (!q.c || (q.k > 0 && (!q.a || !q.b)) ||
-                                                                        (q.k2 > 0 && (!q.a2 || !q.b2)))))
-      return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: bad problem " + std::to_string(i));
-    if (q.beta != 0 && q.beta != 1) return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: beta must be 0 or 1");
-    TgProb p{};
-    // op(A)(m, k): X[m][k] (ld, k contiguous) or X[k][m]; op(B)(k, n) as
-    // element (n, k): B[k][n] or B[n][k]
-    auto lay = [](const float* X, int64_t ld, bool kfast, int K) {
-      return TgLay{X, kfast ? (int)ld : 1, kfast ? 1 : (int)ld, 0, 1, 0, K};
-    };
-    auto glay = [](const float* X, const e3gnn_gemm_layout& g) {
-      return TgLay{X, (int)g.ld, (int)g.kst, (int)g.sst, g.rep, g.rs, g.ks};
-    };
-    if (q.layout) {
-      const e3gnn_gemm_layouts& L = *q.layout;
-      p.A1 = glay(q.a, L.a); p.B1 = glay(q.b, L.b); p.A2 = glay(q.a2, L.a2); p.B2 = glay(q.b2, L.b2);
-      p.ldc = L.ldc; p.crep = L.crep; p.crs = L.crs; p.cns = L.cns;
-    } else {
-      p.A1 = lay(q.a, q.lda, !q.trans_a, q.k);
-      p.B1 = lay(q.b, q.ldb, q.trans_b, q.k);
-      p.A2 = lay(q.a2, q.lda2, !q.trans_a2, q.k2);
-      p.B2 = lay(q.b2, q.ldb2, q.trans_b2, q.k2);
-      p.ldc = q.ldc; p.crep = 1; p.crs = 0; p.cns = 1;
-    }
-    p.C = q.c;
-    p.M = q.m; p.N = q.n; p.K1 = q.k; p.K2 = q.k2;
-    p.alpha = q.alpha; p.beta = q.beta;
-    p.kr = q.krange; p.kr_sm = q.krange_stride_m;
-    p.splits = tg_splits(q.m, q.n, (int64_t)q.k + q.k2);
+    TgProb p;
+    if (int rc = gemm_prob(d[i], i, p)) return rc;
     if (p.splits > 1) {
-      const int64_t need = (int64_t)p.splits * q.m * q.n;
+      const int64_t need = (int64_t)p.splits * d[i].m * d[i].n;
       if (!workspace || used + need > workspace_floats)
         return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: workspace too small (e3gnn_gemm_workspace_floats)");
       p.ws = workspace + used;
@@ -1094,7 +1099,36 @@ int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_
     }
     if (!tg_add(b, p)) return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: problem " + std::to_string(i));
   }
-  HIPCHK(launch_tgemm(b, (hipStream_t)stream));
+  HIPCHK(launch_tgemm(b, (hipStream_t)stream, !(flags & E3GNN_GEMM_DEFER_REDUCE)));
+  return E3GNN_OK;
+}
+
+int e3gnn_gemm_grouped(int n, const e3gnn_gemm_desc* d, float* workspace, int64_t workspace_floats,
+                       void* stream) {
+  return e3gnn_gemm_grouped_ex(n, d, workspace, workspace_floats, 0, stream);
+}
+
+int e3gnn_gemm_reduce(int n, const e3gnn_gemm_desc* d, float* const* workspaces, void* stream) {
+  if (n < 0 || (n > 0 && (!d || !workspaces))) return fail(E3GNN_ERR_ARG, "e3gnn_gemm_reduce: bad arguments");
+  TgRedBatch r;
+  for (int i = 0; i < n; ++i) {
+    TgProb p;
+    if (int rc = gemm_prob(d[i], i, p)) return rc;
+    if (p.splits <= 1 || p.M == 0 || p.N == 0) continue;   // reduced (or written) by its own launch
+    {   // the split count its launch settled on (tg_add: whole k-step slices per split)
+      TgBatch one;
+      if (!tg_add(one, p)) return fail(E3GNN_ERR_ARG, "e3gnn_gemm_reduce: problem " + std::to_string(i));
+      p = one.p[0];
+      if (p.splits <= 1) continue;
+    }
+    if (!workspaces[i]) return fail(E3GNN_ERR_ARG, "e3gnn_gemm_reduce: problem " + std::to_string(i) + " has no slabs");
+    if (r.n == TG_MAX_RED) {   // launches of TG_MAX_RED problems, in order
+      HIPCHK(launch_tgemm_reduce(r, (hipStream_t)stream));
+      r = TgRedBatch{};
+    }
+    tg_red_add(r, TgRed{workspaces[i], p.C, p.ldc, p.crep, p.crs, p.cns, p.M, p.N, p.splits, p.alpha, p.beta});
+  }
+  HIPCHK(launch_tgemm_reduce(r, (hipStream_t)stream));
   return E3GNN_OK;
 }
 
@@ -1758,6 +1792,8 @@ int e3gnn_conv_dims(int kind, int* dx, int* w, int* dm) {
   return E3GNN_OK;
 }
 
+static int graph_check(int* err_d, hipStream_t s);   // reads the build's error bits (synchronises)
+
 int e3gnn_conv_graph(int64_t n_nodes, int64_t n_edges, const int32_t* edge_center,
                      const int32_t* edge_nbr, int32_t* row_ptr, int32_t* src_ptr,
                      int32_t* src_perm, int32_t* scratch, void* stream) {
@@ -1767,9 +1803,38 @@ int e3gnn_conv_graph(int64_t n_nodes, int64_t n_edges, const int32_t* edge_cente
     return fail(E3GNN_ERR_ARG, "null conv graph buffer");
   hipStream_t s = (hipStream_t)stream;
   int* err_d = scratch + n_nodes;
-  HIPCHK(hipMemsetAsync(err_d, 0, 4, s));
-  HIPCHK(launch_build_graph(n_edges, (int)n_nodes, (int)n_nodes, edge_center, edge_nbr, row_ptr,
-                            src_ptr, src_perm, scratch, err_d, s));
+  if (n_nodes <= graph_small_max_nodes()) {   // one workgroup, one launch
+    HIPCHK(launch_build_graph_small(n_edges, (int)n_nodes, edge_center, edge_nbr, nullptr, nullptr, nullptr,
+                                    nullptr, row_ptr, src_ptr, src_perm, err_d, s));
+  } else {
+    HIPCHK(hipMemsetAsync(err_d, 0, 4, s));
+    HIPCHK(launch_build_graph(n_edges, (int)n_nodes, (int)n_nodes, edge_center, edge_nbr, row_ptr,
+                              src_ptr, src_perm, scratch, err_d, s));
+  }
+  return graph_check(err_d, s);
+}
+
+int e3gnn_conv_graph_i64(int64_t n_nodes, int64_t n_edges, const int64_t* edge_center,
+                         const int64_t* edge_nbr, int32_t* center_out, int32_t* nbr_out, int32_t* row_ptr,
+                         int32_t* src_ptr, int32_t* src_perm, int32_t* scratch, void* stream) {
+  if (n_nodes < 0 || n_edges < 0 || n_nodes >= (int64_t)1 << 31 || n_edges >= (int64_t)1 << 31)
+    return fail(E3GNN_ERR_ARG, "conv graph size out of int32 range");
+  if (n_nodes > graph_small_max_nodes())
+    return fail(E3GNN_ERR_ARG, "e3gnn_conv_graph_i64: more than " + std::to_string(graph_small_max_nodes()) +
+                                   " nodes (convert the indices and use e3gnn_conv_graph)");
+  if (!row_ptr || !src_ptr || !scratch ||
+      (n_edges > 0 && (!edge_center || !edge_nbr || !center_out || !nbr_out || !src_perm)))
+    return fail(E3GNN_ERR_ARG, "null conv graph buffer");
+  hipStream_t s = (hipStream_t)stream;
+  int* err_d = scratch + n_nodes;
+  HIPCHK(launch_build_graph_small(n_edges, (int)n_nodes, nullptr, nullptr, edge_center, edge_nbr, center_out,
+                                  nbr_out, row_ptr, src_ptr, src_perm, err_d, s));
+  return graph_check(err_d, s);
+}
+
+int e3gnn_conv_graph_small_max_nodes(void) { return graph_small_max_nodes(); }
+
+static int graph_check(int* err_d, hipStream_t s) {
   int err = 0;
   HIPCHK(hipMemcpyAsync(&err, err_d, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -2003,8 +2068,10 @@ int e3gnn_conv_dual_backward(int kind, int64_t n_nodes, int64_t n_edges, const i
   a.dxcd = dhd ? dxc + n_edges * dx : nullptr;
   a.n_centers = (int)n_nodes;
   HIPCHK(launch_tp_bwd_dual(kind, a, s));
-  HIPCHK(launch_gather_rows((int)n_nodes, dx, src_ptr, src_perm, dxc, dh, s, 0));
-  if (dhd) HIPCHK(launch_gather_rows((int)n_nodes, dx, src_ptr, src_perm, a.dxcd, dhd, s, 0));
+  if (dhd)
+    HIPCHK(launch_gather_rows2((int)n_nodes, dx, src_ptr, src_perm, dxc, dh, a.dxcd, dhd, s));
+  else
+    HIPCHK(launch_gather_rows((int)n_nodes, dx, src_ptr, src_perm, dxc, dh, s, 0));
   return E3GNN_OK;
 }
 

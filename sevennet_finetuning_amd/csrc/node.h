@@ -23,6 +23,13 @@ hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, con
 hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* center,
                               const int* nbr, int* row_ptr, int* src_ptr, int* src_perm, int* cnt,
                               int* err, hipStream_t s, int n_interior = 0);
+// the whole build in one workgroup (n <= graph_small_max_nodes()); int64
+// indices (c64 / j64, converted into cout / jout) or int32 ones (c32 / j32);
+// writes *err (no memset needed)
+hipError_t launch_build_graph_small(int64_t E, int n, const int* c32, const int* j32, const int64_t* c64,
+                                    const int64_t* j64, int* cout, int* jout, int* row_ptr, int* src_ptr,
+                                    int* src_perm, int* err, hipStream_t s);
+int graph_small_max_nodes();
 hipError_t launch_embed(int n, int D, const int* type, int nsp, const float* W, float* x, int* err,
                         hipStream_t s);
 // e3nn Gate of the SevenNet-0-shaped family: y = [ns scalars | g1 + g2 gates |
@@ -45,6 +52,9 @@ hipError_t launch_sum(int64_t n, const float* a, float* part, float* out, hipStr
 hipError_t launch_final_sum(int nb, int k, const float* part, float* out, hipStream_t s);
 hipError_t launch_zero(float* p, int64_t n, hipStream_t s);
 // acc: dst += the sums instead of dst = (the explicit fine-tune derivatives)
+// two gathers over the same transposed CSR in one launch (src -> dst, src2 -> dst2)
+hipError_t launch_gather_rows2(int n, int D, const int* ptr, const int* perm, const float* src,
+                               float* dst, const float* src2, float* dst2, hipStream_t s);
 hipError_t launch_gather_rows(int n, int D, const int* ptr, const int* perm, const float* src,
                               float* dst, hipStream_t s, int acc = 0);
 // the same over neighbour nodes [j_begin, j_end) only

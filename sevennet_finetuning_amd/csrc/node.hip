@@ -432,6 +432,102 @@ __global__ __launch_bounds__(256) void k_sort_segments(int n, const int* __restr
   }
 }
 
+// The whole graph build in ONE workgroup for small graphs (a fine-tune batch:
+// ~10^3 nodes, ~10^4 edges), the per-neighbour counts and offsets in LDS:
+// validation + row_ptr, counts, exclusive scan, scatter and the segment sort
+// of the launches above (eleven launches and a memset, each mostly launch
+// latency at this size).  Optionally converts int64 edge indices (the
+// batch's edge_index rows) into the int32 copies the kernels read.
+constexpr int GRAPH_SMALL_N = 6144;
+template <typename T>
+__global__ __launch_bounds__(1024) void k_build_graph_small(int E, int n, const T* __restrict__ cin,
+                                                            const T* __restrict__ jin, int* __restrict__ cout,
+                                                            int* __restrict__ jout, int* __restrict__ row_ptr,
+                                                            int* __restrict__ src_ptr, int* __restrict__ perm,
+                                                            int* __restrict__ err) {
+  __shared__ int cnt[GRAPH_SMALL_N];
+  __shared__ int ptr[GRAPH_SMALL_N + 1];
+  __shared__ int wsum[16];
+  __shared__ int errl;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int i = t; i < n; i += 1024) cnt[i] = 0;
+  for (int i = t; i <= n; i += 1024) row_ptr[i] = 0;
+  if (t == 0) errl = 0;
+  __syncthreads();
+  // validation, row_ptr (as k_row_ptr) and the per-neighbour counts
+  for (int e = t; e < E; e += 1024) {
+    const int c = (int)cin[e], j = (int)jin[e];
+    if (cout) cout[e] = c;
+    if (jout) jout[e] = j;
+    if (j < 0 || j >= n) atomicOr(&errl, 4);
+    else atomicAdd(&cnt[j], 1);
+    if (c < 0 || c >= n) {
+      atomicOr(&errl, 2);
+      continue;
+    }
+    const int prev = e ? (int)cin[e - 1] : -1;
+    if (c < prev) {
+      atomicOr(&errl, 1);
+      continue;
+    }
+    for (int q = prev + 1; q <= c; ++q) row_ptr[q] = e;
+    if (e == E - 1)
+      for (int q = c + 1; q <= n; ++q) row_ptr[q] = E;
+  }
+  __syncthreads();
+  // exclusive scan of the counts: chunks of consecutive nodes per thread
+  constexpr int CH = (GRAPH_SMALL_N + 1023) / 1024;
+  const int b0 = t * CH;
+  int tot = 0;
+#pragma unroll
+  for (int q = 0; q < CH; ++q) tot += b0 + q < n ? cnt[b0 + q] : 0;
+  const int incl = wave_incl_scan(tot, lane);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int run = incl - tot;
+  for (int q = 0; q < w; ++q) run += wsum[q];
+#pragma unroll
+  for (int q = 0; q < CH; ++q)
+    if (b0 + q < n) {
+      ptr[b0 + q] = run;
+      run += cnt[b0 + q];
+    }
+  if (t == 1023) ptr[n] = run;   // the last thread's running sum is the total
+  __syncthreads();
+  for (int i = t; i <= n; i += 1024) src_ptr[i] = ptr[i];
+  for (int i = t; i < n; i += 1024) cnt[i] = 0;
+  __syncthreads();
+  for (int e = t; e < E; e += 1024) {
+    const int j = (int)jin[e];
+    if (j < 0 || j >= n) continue;
+    perm[ptr[j] + atomicAdd(&cnt[j], 1)] = e;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // each neighbour's edges ascending (as k_sort_segments; one wave per node)
+  for (int j = w; j < n; j += 16) {
+    const int b = ptr[j], len = ptr[j + 1] - b;
+    if (len <= 1) continue;
+    if (len <= 64) {
+      const int v = lane < len ? perm[b + lane] : INT_MAX;
+      int rank = 0;
+      for (int k = 0; k < len; ++k) rank += __shfl(v, k) < v;
+      if (lane < len) perm[b + rank] = v;
+    } else if (lane == 0) {
+      for (int i = b + 1; i < b + len; ++i) {
+        const int v = perm[i];
+        int k = i - 1;
+        while (k >= b && perm[k] > v) {
+          perm[k + 1] = perm[k];
+          --k;
+        }
+        perm[k + 1] = v;
+      }
+    }
+  }
+  if (t == 0) *err = errl;
+}
+
 // ------------------------------------------------------------ node ops
 // OnehotEmbedding + IrrepsLinear(is_embed) (node_embedding.py:39-48,
 // linear.py:37-44): row lookup of the pre-scaled embedding matrix (D columns).
@@ -608,10 +704,16 @@ __global__ void k_gather_rows(int j_begin, int n, int D, const int* __restrict__
 #ifndef E3GNN_GATHER_U
 #define E3GNN_GATHER_U 4
 #endif
+// blockIdx.y = 1: the second (src, dst) pair of launch_gather_rows2
 __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict__ ptr,
                                const int* __restrict__ perm, const float4* __restrict__ src,
-                               float4* __restrict__ dst, int acc) {
+                               float4* __restrict__ dst, int acc, const float4* __restrict__ src2,
+                               float4* __restrict__ dst2) {
   constexpr int U = E3GNN_GATHER_U;
+  if (blockIdx.y) {
+    src = src2;
+    dst = dst2;
+  }
   const int j = j_begin + xcd_block() * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (j >= n) return;
@@ -733,6 +835,19 @@ hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* 
     hipLaunchKernelGGL(k_sort_segments, dim3((n_nodes + 3) / 4), dim3(256), 0, s, n_nodes, src_ptr, src_perm);
   return hipGetLastError();
 }
+hipError_t launch_build_graph_small(int64_t E, int n, const int* c32, const int* j32, const int64_t* c64,
+                                    const int64_t* j64, int* cout, int* jout, int* row_ptr, int* src_ptr,
+                                    int* src_perm, int* err, hipStream_t s) {
+  if (n < 0 || n > GRAPH_SMALL_N || E < 0 || E >= ((int64_t)1 << 30)) return hipErrorInvalidValue;
+  if (c64)
+    hipLaunchKernelGGL(k_build_graph_small<int64_t>, dim3(1), dim3(1024), 0, s, (int)E, n, c64, j64, cout,
+                       jout, row_ptr, src_ptr, src_perm, err);
+  else
+    hipLaunchKernelGGL(k_build_graph_small<int>, dim3(1), dim3(1024), 0, s, (int)E, n, c32, j32, cout, jout,
+                       row_ptr, src_ptr, src_perm, err);
+  return hipGetLastError();
+}
+int graph_small_max_nodes() { return GRAPH_SMALL_N; }
 hipError_t launch_embed(int n, int D, const int* type, int nsp, const float* W, float* x, int* err,
                         hipStream_t s) {
   LAUNCH(k_embed, nblk((int64_t)n * D), n, D, type, nsp, W, x, err);
@@ -792,11 +907,22 @@ hipError_t launch_gather_rows_range(int j_begin, int j_end, int D, const int* pt
   if (n <= 0) return hipGetLastError();
   if (D % 4 == 0) {
     hipLaunchKernelGGL(k_gather_rows4, dim3((n + 3) / 4), dim3(256), 0, s, j_begin, j_end, D / 4,
-                       ptr, perm, (const float4*)src, (float4*)dst, acc);
+                       ptr, perm, (const float4*)src, (float4*)dst, acc, nullptr, nullptr);
   } else {
     hipLaunchKernelGGL(k_gather_rows, dim3((n + 3) / 4), dim3(256), 0, s, j_begin, j_end, D, ptr,
                        perm, src, dst, acc);
   }
+  return hipGetLastError();
+}
+hipError_t launch_gather_rows2(int n, int D, const int* ptr, const int* perm, const float* src,
+                               float* dst, const float* src2, float* dst2, hipStream_t s) {
+  if (n <= 0) return hipGetLastError();
+  if (D % 4) {
+    const hipError_t e = launch_gather_rows_range(0, n, D, ptr, perm, src, dst, s, 0);
+    return e != hipSuccess ? e : launch_gather_rows_range(0, n, D, ptr, perm, src2, dst2, s, 0);
+  }
+  hipLaunchKernelGGL(k_gather_rows4, dim3((n + 3) / 4, 2), dim3(256), 0, s, 0, n, D / 4, ptr, perm,
+                     (const float4*)src, (float4*)dst, 0, (const float4*)src2, (float4*)dst2);
   return hipGetLastError();
 }
 hipError_t launch_pack(int64_t n, int dim, const int* idx, const float* src, int64_t ss, float* dst,

@@ -46,15 +46,37 @@ constexpr int TG_MAX_PROBS = 12;
 // time, ~5 us of kernel-argument latency per launch.
 struct TgBatch {
   int tile_begin[TG_MAX_PROBS] = {};
-  int64_t red_lo[TG_MAX_PROBS] = {}, red_hi[TG_MAX_PROBS] = {};   // [lo, hi): the problem's outputs in the reduction grid
   int nprob = 0;
   int total_tiles = 0;
   int64_t red_total = 0;
   TgProb p[TG_MAX_PROBS];
 };
+// The fixed-order split-K reduction C = beta C + alpha sum_s ws[s] of split
+// problems -- right after their GEMM launch, or deferred and batched: the
+// fine-tune step's weight gradients are read only at the step's end, so one
+// launch reduces all of them (k_tgemm_reduce)
+struct TgRed {
+  const float* ws;   // [splits][M][N]
+  float* C;
+  int64_t ldc;
+  int crep, crs, cns;
+  int M, N, splits;
+  float alpha;
+  int beta;
+};
+constexpr int TG_MAX_RED = 32;
+struct TgRedBatch {
+  int64_t lo[TG_MAX_RED] = {}, hi[TG_MAX_RED] = {};   // [lo, hi): the problem's outputs in the launch's grid
+  int n = 0;
+  int64_t total = 0;
+  TgRed p[TG_MAX_RED];
+};
 // split count the kernel would choose for an (M x N) output with K summed rows
 int tg_splits(int64_t M, int64_t N, int64_t K);
 bool tg_add(TgBatch& b, TgProb p);
-hipError_t launch_tgemm(const TgBatch& b, hipStream_t s);
+// reduce = false: the split problems' slabs are left for launch_tgemm_reduce
+hipError_t launch_tgemm(const TgBatch& b, hipStream_t s, bool reduce = true);
+bool tg_red_add(TgRedBatch& r, const TgRed& q);
+hipError_t launch_tgemm_reduce(const TgRedBatch& r, hipStream_t s);
 
 }  // namespace e3gnn

@@ -318,15 +318,15 @@ __global__ __launch_bounds__(256) void k_tgemm(TgBatch batch) {
 }
 
 // C = beta C + alpha sum_s ws[s] over the split problems, s in order
-__global__ __launch_bounds__(256) void k_tgemm_reduce(TgBatch batch) {
+__global__ __launch_bounds__(256) void k_tgemm_reduce(TgRedBatch batch) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int p = -1;
 #pragma unroll
-  for (int q = 0; q < TG_MAX_PROBS; ++q)
-    if (q < batch.nprob && i >= batch.red_lo[q] && i < batch.red_hi[q]) p = q;
+  for (int q = 0; q < TG_MAX_RED; ++q)
+    if (q < batch.n && i >= batch.lo[q] && i < batch.hi[q]) p = q;
   if (p < 0) return;
-  const TgProb& P = batch.p[p];
-  const int64_t e = i - batch.red_lo[p], mn = (int64_t)P.M * P.N;
+  const TgRed& P = batch.p[p];
+  const int64_t e = i - batch.lo[p], mn = (int64_t)P.M * P.N;
   const int row = (int)(e / P.N), col = (int)(e - (int64_t)row * P.N);
   // slabs 0, 1, 2, ... added in order; sixteen loads in flight at a time
   // (a split count of ~70 read one dependent load at a time took ~70
@@ -409,21 +409,41 @@ bool tg_add(TgBatch& b, TgProb p) {
   p.tile_begin = b.total_tiles;
   b.tile_begin[b.nprob] = p.tile_begin;
   b.total_tiles += p.tiles_mn * p.splits;
-  b.red_lo[b.nprob] = b.red_hi[b.nprob] = b.red_total;
   if (p.splits > 1) {
     p.red_begin = b.red_total;
     b.red_total += (int64_t)p.M * p.N;
-    b.red_hi[b.nprob] = b.red_total;
   }
   b.p[b.nprob++] = p;
   return true;
 }
 
-hipError_t launch_tgemm(const TgBatch& b, hipStream_t s) {
+bool tg_red_add(TgRedBatch& r, const TgRed& q) {
+  if (r.n >= TG_MAX_RED || q.splits <= 1 || q.M <= 0 || q.N <= 0) return false;
+  r.lo[r.n] = r.total;
+  r.total += (int64_t)q.M * q.N;
+  r.hi[r.n] = r.total;
+  r.p[r.n++] = q;
+  return true;
+}
+
+hipError_t launch_tgemm_reduce(const TgRedBatch& r, hipStream_t s) {
+  if (r.total > 0)
+    hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)((r.total + 255) / 256)), dim3(256), 0, s, r);
+  return hipGetLastError();
+}
+
+hipError_t launch_tgemm(const TgBatch& b, hipStream_t s, bool reduce) {
   if (b.total_tiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_tgemm, dim3(b.total_tiles), dim3(256), 0, s, b);
-  if (b.red_total > 0)
-    hipLaunchKernelGGL(k_tgemm_reduce, dim3((unsigned)((b.red_total + 255) / 256)), dim3(256), 0, s, b);
+  if (reduce && b.red_total > 0) {
+    TgRedBatch r;
+    for (int i = 0; i < b.nprob; ++i) {
+      const TgProb& p = b.p[i];
+      if (p.splits > 1)
+        tg_red_add(r, TgRed{p.ws, p.C, p.ldc, p.crep, p.crs, p.cns, p.M, p.N, p.splits, p.alpha, p.beta});
+    }
+    return launch_tgemm_reduce(r, s);
+  }
   return hipGetLastError();
 }
 

@@ -128,6 +128,12 @@ class _Gemms:
         self.q = []
         self.ws = None
         self.max_probs = 12        # e3gnn_gemm_grouped's problems per launch
+        # deferred split-K reductions (begin_defer .. finish_defer): the
+        # slabs of every flush in their own workspace region, all reduced
+        # by one e3gnn_gemm_reduce launch
+        self.defer = None
+        self.dws = []              # workspace chunks (one after the first step)
+        self.dws_total = 0
 
     def _hip(self, *ts):
         return self.lib is not None and all(t.is_cuda and t.dtype == torch.float32 for t in ts)
@@ -144,9 +150,11 @@ class _Gemms:
             return x.data_ptr(), (s1 if k > 1 else max(r, 1)), 1
         return None
 
-    def add(self, C, A, B, alpha=1.0, beta=0, A2=None, B2=None, kr=None):
+    def add(self, C, A, B, alpha=1.0, beta=0, A2=None, B2=None, kr=None, wgrad=False):
         """kr: (int32 device tensor, row-tile stride) of per-tile k ranges (the
-        dense matrices' block sparsity, e3gnn_gemm_desc::krange) or None"""
+        dense matrices' block sparsity, e3gnn_gemm_desc::krange) or None;
+        wgrad: C is a weight gradient read only after finish_defer (its split-K
+        reduction may be deferred)"""
         if not self._hip(C, A, B, *(t for t in (A2, B2) if t is not None)):
             # straight into C (no temporaries / copy kernels)
             torch.addmm(C, A, B, beta=1 if beta else 0, alpha=alpha, out=C)
@@ -174,10 +182,11 @@ class _Gemms:
         d.alpha, d.beta = float(alpha), int(bool(beta))
         if kr is not None:
             d.krange, d.krange_stride_m = kr[0].data_ptr(), kr[1]
-        self._push(d, (C, A, B, A2, B2, kr), C.device, (C, A, B, A2, B2, float(alpha), int(bool(beta))))
+        self._push(d, (C, A, B, A2, B2, kr), C.device, (C, A, B, A2, B2, float(alpha), int(bool(beta))),
+                   wgrad)
         return C
 
-    def add_lay(self, M, N, K, C, A, B, lay, A2=None, B2=None, K2=0, alpha=1.0, beta=0):
+    def add_lay(self, M, N, K, C, A, B, lay, A2=None, B2=None, K2=0, alpha=1.0, beta=0, wgrad=False):
         """one problem in the general layouts (e3gnn_gemm_layouts ``lay``); C, A,
         B, A2, B2 = (tensor, element offset) of the operand bases"""
         from . import _lib
@@ -189,12 +198,12 @@ class _Gemms:
         d.m, d.n, d.k, d.k2 = int(M), int(N), int(K), int(K2)
         d.alpha, d.beta = float(alpha), int(bool(beta))
         d.layout = ctypes.addressof(lay)
-        self._push(d, (C[0], A[0], B[0], A2, B2, lay), C[0].device, None)
+        self._push(d, (C[0], A[0], B[0], A2, B2, lay), C[0].device, None, wgrad)
 
-    def _push(self, d, keep, dev, info):
+    def _push(self, d, keep, dev, info, wgrad=False):
         if len(self.q) == self.max_probs:
             self.flush()
-        self.q.append((d, keep, dev, info))
+        self.q.append((d, keep, dev, info, wgrad))
 
     def flush(self):
         if not self.q:
@@ -204,12 +213,63 @@ class _Gemms:
         descs = (_lib.GemmDesc * n)(*[e[0] for e in self.q])
         need = int(self.lib.e3gnn_gemm_workspace_floats(n, descs))
         dev = self.q[0][2]
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        split = [int(self.lib.e3gnn_gemm_workspace_floats(1, ctypes.byref(descs[i]))) for i in range(n)]
+        # deferred only when every split problem of the launch is a weight
+        # gradient (any other output is read by the next launches)
+        if self.defer is not None and need > 0 and all(e[4] for e, w in zip(self.q, split) if w > 0):
+            base = self._dws_take(need, dev)
+            _lib.check(self.lib.e3gnn_gemm_grouped_ex(n, descs, base, need, 1, stream))
+            off = 0
+            for i, (e, w) in enumerate(zip(self.q, split)):
+                if w > 0:
+                    self.defer.append((descs[i], e[1], base + 4 * off))
+                off += w
+            self.q = []
+            return
         if need > 0 and (self.ws is None or self.ws.numel() < need):
             self.ws = torch.empty(max(need, 1 << 20), device=dev)
         ws = self.ws.data_ptr() if self.ws is not None else None
         _lib.check(self.lib.e3gnn_gemm_grouped(n, descs, ws, self.ws.numel() if self.ws is not None else 0,
-                                               torch.cuda.current_stream(dev).cuda_stream))
+                                               stream))
         self.q = []
+
+    def _dws_take(self, need, dev):
+        """the device address of `need` floats of deferred workspace (a new
+        chunk when the current one is full; one chunk of the whole step's
+        size from the next begin_defer on)"""
+        buf, used = self.dws[-1] if self.dws else (None, 0)
+        if buf is None or used + need > buf.numel():
+            buf, used = torch.empty(max(need, self.dws_total, 1 << 20), device=dev), 0
+            self.dws.append([buf, 0])
+        self.dws[-1][1] = used + need
+        return buf.data_ptr() + 4 * used
+
+    def begin_defer(self):
+        if self.lib is None:
+            return
+        self.flush()
+        if len(self.dws) > 1:     # last step needed several chunks: one of the total
+            self.dws_total = sum(u for _, u in self.dws)
+            self.dws = []
+        for c in self.dws:
+            c[1] = 0
+        self.defer = []
+
+    def finish_defer(self):
+        """the deferred split-K reductions, one launch (per 32 problems)"""
+        if self.defer is None:
+            return
+        self.flush()
+        pend, self.defer = self.defer, None
+        if not pend:
+            return
+        from . import _lib
+        n = len(pend)
+        descs = (_lib.GemmDesc * n)(*[p[0] for p in pend])
+        wss = (ctypes.c_void_p * n)(*[p[2] for p in pend])
+        dev = pend[0][1][0].device
+        _lib.check(self.lib.e3gnn_gemm_reduce(n, descs, wss, torch.cuda.current_stream(dev).cuda_stream))
 
 
 def _put(out, v):
@@ -800,7 +860,7 @@ class ExplicitStep:
     def _lin_grad(self, G, X, Y, key):
         """G += X^T Y, G the dense gradient of key's matrix, on its l-blocks"""
         if not self._irr(G, X, Y):
-            self.gm.add(G, X.t(), Y, beta=1, kr=self._kr(None, grad=key))
+            self.gm.add(G, X.t(), Y, beta=1, kr=self._kr(None, grad=key), wgrad=True)
             return
         from . import _lib
         rows = int(X.shape[0])
@@ -812,7 +872,7 @@ class ExplicitStep:
             lay.b.ld, lay.b.rep, lay.b.rs, lay.b.kst, lay.b.ks, lay.b.sst = d, 1, 0, Y.stride(0), rows, 1
             lay.ldc, lay.crep, lay.crs, lay.cns = d * dout, 1, 0, d
             self.gm.add_lay(mi, mo, d * rows, (G, in_lo * dout + out_lo), (X, in_lo), (Y, out_lo), lay,
-                            beta=1)
+                            beta=1, wgrad=True)
 
     # ---- block sparsity of the dense linear matrices (e3gnn_gemm_desc::krange)
     def _lin_blocks(self, key, trans=False):
@@ -1152,6 +1212,9 @@ class ExplicitStep:
 
         # ---- one reverse sweep over (primal, tangent); seeds cE on E, 1 on E'
         G = self.bank.grads()
+        # the weight gradients (G, read only by the bank's flush below) take
+        # their split-K reductions in one launch at the end of the sweep
+        self.gm.begin_defer()
         scale = S['scale']
         atb = cE[batch]                       # d L / d atomic
         gsc = self._G('rescale_atomic_energy.scale')
@@ -1165,8 +1228,8 @@ class ExplicitStep:
         HID = torch.cat([S['hid'], hidd])
         HIDB = EB * D['r2'][:, 0].unsqueeze(0)
         XB = torch.empty(2 * n, D['r1'].shape[0], device=dev, dtype=dt)
-        self.gm.add(G['r2'], HID.t(), EB, beta=1)
-        self.gm.add(G['r1'], XL.t(), HIDB, beta=1)
+        self.gm.add(G['r2'], HID.t(), EB, beta=1, wgrad=True)
+        self.gm.add(G['r1'], XL.t(), HIDB, beta=1, wgrad=True)
         self.gm.add(XB, HIDB, D['r1'].t())    # [x-bar; x'-bar] of the last block's output
         self.gm.flush()
         EMBB = torch.zeros(2 * E, 8, device=dev, dtype=dt)
@@ -1227,7 +1290,7 @@ class ExplicitStep:
             for li, (rows, cot, Wl) in enumerate(((EMB, A1B, W0), (b['H1'], A2B, W1), (b['H2'], WB, W2))):
                 gw = self._G(f'{pre}.weight_nn.layer{li}.weight')
                 if gw is not None:
-                    self.gm.add(gw, rows.t(), cot, 1.0 / math.sqrt(Wl.shape[0]), beta=1)
+                    self.gm.add(gw, rows.t(), cot, 1.0 / math.sqrt(Wl.shape[0]), beta=1, wgrad=True)
             # self-interaction 1 (sc-bar = y-bar, added above) and the input cotangent
             self._lin_grad(G[f'si1{t}'], X, HB, f'si1{t}')
             XB = new(2 * n, D[f'si1{t}'].shape[0])
@@ -1241,4 +1304,5 @@ class ExplicitStep:
         if gco is not None:
             coeffs = self._P('edge_embedding.basis_function.coeffs').detach()
             gco.add_(self.geo.coeff_grad(g, EMBB[:E], EMBB[E:], rd, coeffs))
+        self.gm.finish_defer()
         self.bank.flush(m.flat_grad)

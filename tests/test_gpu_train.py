@@ -269,6 +269,18 @@ def test_conv_graph_csr_matches_numpy(hip_backend, n, mean_deg, hub):
     assert np.array_equal(aux['row_ptr'].cpu().numpy(), row_ptr)
     assert np.array_equal(aux['src_ptr'].cpu().numpy(), src_ptr)
     assert np.array_equal(aux['src_perm'].cpu().numpy()[:len(center)], src_perm)
+    # the in-place rebuild of a captured step from int64 edge_index rows (one
+    # launch up to e3gnn_conv_graph_small_max_nodes(), the int32 copies +
+    # multi-launch build beyond): new neighbours, same edge count
+    nbr2 = rng.permutation(nbr)
+    ei = torch.tensor(np.stack([center, nbr2]), device=DEV, dtype=torch.int64)
+    g.rebuild(ei[0], ei[1])
+    cnt2 = np.bincount(nbr2, minlength=n)
+    assert np.array_equal(aux['center'].cpu().numpy(), center)
+    assert np.array_equal(aux['nbr'].cpu().numpy(), nbr2)
+    assert np.array_equal(aux['row_ptr'].cpu().numpy(), row_ptr)
+    assert np.array_equal(aux['src_ptr'].cpu().numpy(), np.concatenate([[0], np.cumsum(cnt2)]))
+    assert np.array_equal(aux['src_perm'].cpu().numpy()[:len(center)], np.argsort(nbr2, kind='stable'))
 
 
 def test_conv_graph_rejects_unsorted(hip_backend):
@@ -279,6 +291,12 @@ def test_conv_graph_rejects_unsorted(hip_backend):
     with pytest.raises(E3GNNError, match='out of'):
         conv_ops.ConvGraph(4, torch.tensor([0, 1, 2], device=DEV),
                            torch.tensor([1, 9, 1], device=DEV), hip_backend)
+    g = conv_ops.ConvGraph(4, torch.tensor([0, 1, 2], device=DEV), torch.tensor([1, 2, 1], device=DEV),
+                           hip_backend)
+    with pytest.raises(E3GNNError, match='not sorted'):   # the int64 one-launch rebuild validates too
+        g.rebuild(torch.tensor([0, 2, 1], device=DEV), torch.tensor([1, 1, 1], device=DEV))
+    with pytest.raises(E3GNNError, match='out of'):
+        g.rebuild(torch.tensor([0, 1, 2], device=DEV), torch.tensor([1, -1, 1], device=DEV))
 
 
 @pytest.fixture(scope='module')
@@ -820,6 +838,25 @@ def test_grouped_gemm_matches_fp64():
     gm.add(r2, A, B)
     gm.flush()
     assert torch.equal(r1, r2)
+    # deferred split-K reductions (E3GNN_GEMM_DEFER_REDUCE + e3gnn_gemm_reduce,
+    # the fine-tune sweep's weight gradients): bitwise the immediate result,
+    # over several launches, beta 0 / 1, split and unsplit problems mixed
+    outs = []
+    for defer in (False, True):
+        Cs = [torch.ones(64, 960, device=DEV), torch.ones(433, 97, device=DEV), torch.ones(64, 960, device=DEV)]
+        if defer:
+            gm.begin_defer()
+        gm.add(Cs[0], A, B, alpha=0.5, beta=1, wgrad=True)
+        gm.add(Cs[1], *cases[1], wgrad=True)
+        gm.flush()
+        gm.add(Cs[2], A, B, beta=0, wgrad=True)
+        gm.flush()
+        if defer:
+            assert gm.defer and len(gm.defer) == 2    # the two split problems wait
+            gm.finish_defer()
+        outs.append(Cs)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize('loss', ['mse', 'huber'])

@@ -103,6 +103,7 @@ for s in "$@"; do
     btv_*) v=${s#btv_}; step btv_$v 300 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     btkarg_*) v=${s#btkarg_}; step btkarg_$v 300 env HIP_FORCE_DEV_KERNARG=$v python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     tgbkarg_*) v=${s#tgbkarg_}; step tgbkarg_$v 300 env HIP_FORCE_DEV_KERNARG=$v python tools/tgemm_bench.py ;;
+    proftraint) step proftraint 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_traint -o run -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     gtrain) step gtrain 600 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread ;;
     benchmc_*) v=${s#benchmc_}; step benchmc_$v 600 python bench.py --model-config $v --steps 5 --warmup 2 --no-cpu-baseline ;;
     proftrain2) step proftrain2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train2 -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;

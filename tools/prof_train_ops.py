@@ -11,7 +11,7 @@ fisher = {n: torch.full_like(p, 1e-3) for n, p in m.named_parameters()}
 opt = {n: p.detach().clone() for n, p in m.named_parameters()}
 cfg = {'loss': 'huber', 'loss_param': {'delta': 0.01}, 'force_loss_weight': 1.0, 'stress_loss_weight': 0.01,
        'is_train_stress': True, 'optimizer': 'adam', 'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
-       'scheduler_param': {'gamma': 0.99}, 'device': dev, 'hip_graph': False,
+       'scheduler_param': {'gamma': 0.99}, 'device': dev, 'hip_graph': False, 'explicit_grad': True,
        'continue': {'fisher_information': fisher, 'opt_params': opt, 'ewc_lambda': 1e5}}
 tr = train.Trainer(m, cfg)
 bs = bt.make_batches(0, 2, 8, m.chemical_symbols)
@@ -27,7 +27,15 @@ for e in prof.events():
     if e.name.startswith('aten::') and e.stack and e.device_time_total > 0:
         fr = [s for s in e.stack if 'sevennet_finetuning_amd' in s]
         by_src[(e.name, fr[0] if fr else '?')] += 1
-for (name, src), c in by_src.most_common(40):
+# library kernels and runtime copies (no aten op of their own)
+kern = collections.Counter()
+for e in prof.events():
+    if e.device_type == torch.autograd.DeviceType.CUDA:
+        kern[e.name[:80]] += 1
+print('device kernels:', sum(kern.values()))
+for k, c in kern.most_common(60):
+    print('  ', c, k)
+for (name, src), c in by_src.most_common(60):
     print(c, name, src)
 rows = []
 for e in prof.key_averages():

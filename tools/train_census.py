@@ -1,9 +1,10 @@
-"""Per-step kernel census of the fine-tune bench (bench_train.py under
-rocprofv3 --kernel-trace --stats, tools/gpu_job.sh proftrain2): launches and
-GPU time per step by kernel, grouped into the library's kernels and torch's.
+"""Per-step kernel census of the fine-tune bench from a rocprofv3 kernel trace
+of bench_train.py (tools/gpu_job.sh proftraint): the kernels of one
+steady-state rehearsal step (two batches) -- between the k_loss_efs launches
+that open the last two reverse sweeps but one -- by count and GPU time,
+grouped into the library's kernels and torch's / the runtime's.
 
-usage: python tools/train_census.py [stats.csv] [--steps 16]
-(16 = 3 warmup + 10 timed + the 3 capture / first-call steps of bench_train)
+usage: python tools/train_census.py [run_kernel_trace.csv]
 """
 import argparse
 import collections
@@ -23,32 +24,34 @@ def short(name):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('stats', nargs='?', default=os.path.join(ROOT, 'gpurun_out/prof_train2/run_kernel_stats.csv'))
-    ap.add_argument('--steps', type=int, default=16)
+    ap.add_argument('trace', nargs='?', default=os.path.join(ROOT, 'gpurun_out/prof_traint/run_kernel_trace.csv'))
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.stats)))
+    rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r['Start_Timestamp']))
+    marks = [i for i, r in enumerate(rows) if 'k_loss_efs' in r['Kernel_Name']]
+    if len(marks) < 4:
+        raise SystemExit('need at least two steady-state steps in the trace')
+    seg = rows[marks[-4]:marks[-2]]        # one rehearsal step: two batches' sweeps
+    dur = lambda r: (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3   # noqa: E731 (us)
+    busy = sum(dur(r) for r in seg)
+    span = (int(seg[-1]['End_Timestamp']) - int(seg[0]['Start_Timestamp'])) / 1e3
     groups = collections.defaultdict(lambda: [0, 0.0])
     per = collections.defaultdict(lambda: [0, 0.0])
-    for r in rows:
-        calls, ns = int(r['Calls']), float(r['TotalDurationNs'])
-        name = r['Name']
+    for r in seg:
+        name = r['Kernel_Name']
         g = ('library GEMM (tgemm)' if 'k_tgemm' in name else
              'library (other)' if 'e3gnn::' in name else
-             'copies / fills (runtime)' if '__amd_rocclr' in name else
-             'rocprim' if 'rocprim' in name else 'torch')
-        groups[g][0] += calls
-        groups[g][1] += ns
-        per[short(name)][0] += calls
-        per[short(name)][1] += ns
-    S = a.steps
-    tot_c = sum(v[0] for v in groups.values()) / S
-    tot_t = sum(v[1] for v in groups.values()) / S / 1e6
-    print(f'per step: {tot_c:.0f} kernels, {tot_t:.3f} ms of kernel time ({a.stats}, {S} steps)')
+             'copies / fills (runtime)' if '__amd_rocclr' in name else 'torch')
+        groups[g][0] += 1
+        groups[g][1] += dur(r)
+        per[short(name)][0] += 1
+        per[short(name)][1] += dur(r)
+    print(f'one rehearsal step: {len(seg)} kernels, {busy / 1e3:.3f} ms of kernel time, '
+          f'{span / 1e3:.3f} ms span ({a.trace})')
     for g, (c, t) in sorted(groups.items(), key=lambda x: -x[1][1]):
-        print(f'  {g:28s} {c / S:7.1f} launches {t / S / 1e6:7.3f} ms')
-    print('top kernels:')
-    for n, (c, t) in sorted(per.items(), key=lambda x: -x[1][1])[:40]:
-        print(f'  {c / S:7.1f} x {t / max(c, 1) / 1e3:7.1f} us = {t / S / 1e6:6.3f} ms  {n}')
+        print(f'  {g:28s} {c:5d} launches {t / 1e3:7.3f} ms')
+    print('kernels by time:')
+    for n, (c, t) in sorted(per.items(), key=lambda x: -x[1][1])[:45]:
+        print(f'  {c:4d} x {t / c:7.1f} us = {t / 1e3:6.3f} ms  {n}')
 
 
 if __name__ == '__main__':
