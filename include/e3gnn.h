@@ -308,6 +308,19 @@ int e3gnn_radial_mlp_forward(int64_t n_rows, int width, const float* emb, const 
                              const float* W1, const float* W2, const float* a1_primal,
                              const float* a2_primal, float* a1, float* h1, float* a2, float* h2,
                              float* w, float act_scale, void* stream);
+/* The forward / tangent chain with layer 2 on bf16 matrix cores at f32-grade
+ * accuracy (bf16x6: three bf16 pieces per operand, the six products above
+ * 2^-24): w2_pieces = W2's piece image from e3gnn_radial_mlp_w2_pieces
+ * (e3gnn_radial_mlp_w2_piece_bytes(width) bytes, 16-byte aligned; rebuilt
+ * whenever W2 changes); null: the f32 form above. */
+int e3gnn_radial_mlp_forward_p(int64_t n_rows, int width, const float* emb, const float* W0,
+                               const float* W1, const float* W2, const void* w2_pieces,
+                               const float* a1_primal, const float* a2_primal, float* a1, float* h1,
+                               float* a2, float* h2, float* w, float act_scale, void* stream);
+int64_t e3gnn_radial_mlp_w2_piece_bytes(int width);
+/* piece images of n (<= 8) W2 matrices [64, widths[i]] in one launch */
+int e3gnn_radial_mlp_w2_pieces(int n, const float* const* W2, const int32_t* widths, void* const* images,
+                               void* stream);
 int e3gnn_radial_mlp_backward(int64_t n_rows, int width, const float* wb, const float* W0,
                               const float* W1, const float* W2, const float* a1, const float* a2,
                               const float* a1_tangent, const float* a2_tangent, float* a2b,

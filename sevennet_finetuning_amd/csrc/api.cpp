@@ -1937,6 +1937,38 @@ int e3gnn_radial_mlp_forward(int64_t n_rows, int width, const float* emb, const 
   return E3GNN_OK;
 }
 
+int e3gnn_radial_mlp_forward_p(int64_t n_rows, int width, const float* emb, const float* W0,
+                               const float* W1, const float* W2, const void* w2_pieces,
+                               const float* a1_primal, const float* a2_primal, float* a1, float* h1,
+                               float* a2, float* h2, float* w, float act_scale, void* stream) {
+  if (n_rows <= 0) return E3GNN_OK;
+  if (n_rows > INT32_MAX || width <= 0 || width % 16)
+    return fail(E3GNN_ERR_ARG, "radial MLP: width must be a positive multiple of 16");
+  if (!emb || !W0 || !W1 || !W2 || !a1 || !h1 || !a2 || !h2 || !w ||
+      ((a1_primal == nullptr) != (a2_primal == nullptr)))
+    return fail(E3GNN_ERR_ARG, "null radial MLP operand");
+  if (w2_pieces && reinterpret_cast<uintptr_t>(w2_pieces) % 16)
+    return fail(E3GNN_ERR_ARG, "radial MLP: the W2 piece image must be 16-byte aligned");
+  HIPCHK(launch_mlp_fwd((int)n_rows, width, emb, W0, W1, W2, a1_primal, a2_primal, a1, h1, a2, h2, w,
+                        act_scale, (hipStream_t)stream, w2_pieces));
+  return E3GNN_OK;
+}
+
+int64_t e3gnn_radial_mlp_w2_piece_bytes(int width) {
+  return (width > 0 && width % 16 == 0) ? mlp_w2_piece_bytes(width) : -1;
+}
+
+int e3gnn_radial_mlp_w2_pieces(int n, const float* const* W2, const int32_t* widths, void* const* images,
+                               void* stream) {
+  if (n < 0 || n > 8 || (n > 0 && (!W2 || !widths || !images)))
+    return fail(E3GNN_ERR_ARG, "e3gnn_radial_mlp_w2_pieces: 0..8 matrices");
+  for (int i = 0; i < n; ++i)
+    if (!W2[i] || !images[i] || widths[i] <= 0 || widths[i] % 16 || reinterpret_cast<uintptr_t>(images[i]) % 16)
+      return fail(E3GNN_ERR_ARG, "e3gnn_radial_mlp_w2_pieces: matrix " + std::to_string(i));
+  HIPCHK(launch_mlp_w2_pieces(n, W2, widths, images, (hipStream_t)stream));
+  return E3GNN_OK;
+}
+
 int e3gnn_radial_mlp_backward(int64_t n_rows, int width, const float* wb, const float* W0,
                               const float* W1, const float* W2, const float* a1, const float* a2,
                               const float* a1_tangent, const float* a2_tangent, float* a2b,

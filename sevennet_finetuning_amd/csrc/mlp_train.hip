@@ -50,6 +50,67 @@ __device__ __forceinline__ float ddphi(float x, float c) {
 constexpr int H = 64;        // hidden width
 constexpr int LDH = H + 1;   // LDS row stride of the 16 x 64 hidden tiles
 
+// ---- layer 2 on bf16 matrix cores, f32-grade (bf16x6): each f32 operand as
+// three bf16 pieces (x = p0 + p1 + p2, 24 significant bits), the six piece
+// products with i + j <= 2 accumulated in f32 smallest first (dropped terms
+// below 2^-24 relative).  v_mfma_f32_16x16x32_bf16: A lane l = A[l & 15][k =
+// 8 (l >> 4) + t], B lane l = B[k = 8 (l >> 4) + t][l & 15], t < 8; D as the f32
+// form's.  12 MFMAs (192 cycles) per 16 x 16 x 64 block instead of 16 x 32 = 512.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// eight floats as three bf16 pieces (each the round-to-nearest-even bf16 of
+// the remaining residual; two values per packed conversion)
+__device__ __forceinline__ void split3(const float (&v)[8], bf16x8 (&d)[3]) {
+  u32x4 w[3];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x2 r;
+    r[0] = v[2 * q];
+    r[1] = v[2 * q + 1];
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+      const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf16x2));
+      w[pc][q] = u;
+      if (pc < 2) {
+        r[0] -= __builtin_bit_cast(float, u << 16);
+        r[1] -= __builtin_bit_cast(float, u & 0xffff0000u);
+      }
+    }
+  }
+#pragma unroll
+  for (int pc = 0; pc < 3; ++pc) d[pc] = __builtin_bit_cast(bf16x8, w[pc]);
+}
+// the piece image of W2 [64][W]: per 16-column block b, k-half kb (32 hidden
+// units) and piece p, 64 lanes x 16 bytes at ((b * 2 + kb) * 3 + p) * 1024
+struct W2Pieces {
+  const float* W2[8];
+  bf16x8* img[8];
+  int W[8];
+  int begin[9];   // thread ranges (64 per (block, k-half))
+  int n;
+};
+__global__ __launch_bounds__(256) void k_w2_pieces(W2Pieces a) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  int m = 0;
+#pragma unroll
+  for (int i = 1; i < 8; ++i) m += (i < a.n && t >= a.begin[i]) ? 1 : 0;
+  if (t >= a.begin[a.n]) return;
+  const int local = t - a.begin[m], lane = local & 63, bk = local >> 6;   // bk = b * 2 + kb
+  const int b = bk >> 1, kb = bk & 1, g = lane >> 4, cl = lane & 15, W = a.W[m];
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = a.W2[m][(int64_t)(32 * kb + 8 * g + i) * W + 16 * b + cl];
+  bf16x8 d[3];
+  split3(v, d);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) a.img[m][(bk * 3 + p) * 64 + lane] = d[p];
+}
+
 // forward (TAN = false) / tangent (TAN = true) chain; one workgroup per
 // 16-row tile; wave w owns hidden columns 16w..16w+15 of layers 0 / 1 and the
 // output column blocks w, w + 4, ... of layer 2 (its A operand, the tile's h2
@@ -63,7 +124,8 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __re
                                                  const float* __restrict__ A2p,
                                                  float* __restrict__ A1, float* __restrict__ H1,
                                                  float* __restrict__ A2, float* __restrict__ H2,
-                                                 float* __restrict__ WT, float c) {
+                                                 float* __restrict__ WT, float c,
+                                                 const bf16x8* __restrict__ W2p) {
   __shared__ float hs[2][16 * LDH];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
   const int r0 = blockIdx.x * 16;
@@ -77,7 +139,7 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __re
 #pragma unroll
     for (int s = 0; s < 16; ++s) o[s] = W2[(int64_t)(4 * s + g) * W + n];
   };
-  load_b2(w, b2[0]);
+  if (!W2p) load_b2(w, b2[0]);
   // primal pre-activations at this lane's D positions (tangent chain)
   float p1[4], p2[4];
   if (TAN) {
@@ -122,12 +184,6 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __re
     }
   }
   __syncthreads();
-  // layer 2: the tile's h2 rows as A operands, column blocks w, w + 4, ...
-  float a2[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) a2[s] = hs[1][cl * LDH + 4 * s + g];
-  // two column blocks at a time (independent accumulator chains), the next
-  // pair's W2 operands loaded while this pair is multiplied
   auto store = [&](int blk, const f32x4& o) __attribute__((always_inline)) {
     const int n = 16 * blk + cl;
 #pragma unroll
@@ -136,6 +192,47 @@ __global__ __launch_bounds__(256) void k_mlp_fwd(int E, int W, const float* __re
       if (row < E) WT[(int64_t)row * W + n] = o[r];
     }
   };
+  if (W2p) {   // layer 2 on bf16x6 (wave-uniform)
+    bf16x8 ap[2][3];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      float v[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) v[t] = hs[1][cl * LDH + 32 * kb + 8 * g + t];
+      split3(v, ap[kb]);
+    }
+    auto load_p = [&](int blk, bf16x8 (&o)[2][3]) __attribute__((always_inline)) {
+      const int b = blk < NB ? blk : 0;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) o[kb][p] = W2p[((b * 2 + kb) * 3 + p) * 64 + lane];
+    };
+    constexpr int I[6] = {2, 1, 0, 1, 0, 0}, J[6] = {0, 1, 2, 0, 1, 0};
+    bf16x8 bp[2][2][3];
+    load_p(w, bp[0]);
+    for (int blk = w; blk < NB; blk += 8) {
+      load_p(blk + 4, bp[1]);
+      f32x4 o0 = zero4(), o1 = zero4();
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          o0 = mfma16(ap[kb][I[q]], bp[0][kb][J[q]], o0);
+          o1 = mfma16(ap[kb][I[q]], bp[1][kb][J[q]], o1);
+        }
+      load_p(blk + 8, bp[0]);
+      store(blk, o0);
+      if (blk + 4 < NB) store(blk + 4, o1);
+    }
+    return;
+  }
+  // layer 2: the tile's h2 rows as A operands, column blocks w, w + 4, ...
+  float a2[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) a2[s] = hs[1][cl * LDH + 4 * s + g];
+  // two column blocks at a time (independent accumulator chains), the next
+  // pair's W2 operands loaded while this pair is multiplied
   for (int blk = w; blk < NB; blk += 8) {
     load_b2(blk + 4, b2[1]);
     f32x4 o0 = zero4(), o1 = zero4();
@@ -319,15 +416,33 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int E, int W, const float* __re
 // Tangent chain when A1p / A2p (the primal pre-activations) are given.
 hipError_t launch_mlp_fwd(int E, int W, const float* emb, const float* W0, const float* W1,
                           const float* W2, const float* A1p, const float* A2p, float* A1, float* H1,
-                          float* A2, float* H2, float* WT, float c, hipStream_t s) {
+                          float* A2, float* H2, float* WT, float c, hipStream_t s, const void* W2p) {
   if (E <= 0) return hipSuccess;
   const dim3 grid((E + 15) / 16);
+  const bf16x8* p = reinterpret_cast<const bf16x8*>(W2p);
   if (A1p)
     hipLaunchKernelGGL(k_mlp_fwd<true>, grid, dim3(256), 0, s, E, W, emb, W0, W1, W2, A1p, A2p, A1, H1,
-                       A2, H2, WT, c);
+                       A2, H2, WT, c, p);
   else
     hipLaunchKernelGGL(k_mlp_fwd<false>, grid, dim3(256), 0, s, E, W, emb, W0, W1, W2, A1p, A2p, A1,
-                       H1, A2, H2, WT, c);
+                       H1, A2, H2, WT, c, p);
+  return hipGetLastError();
+}
+int64_t mlp_w2_piece_bytes(int W) { return (int64_t)(W / 16) * 6 * 1024; }
+hipError_t launch_mlp_w2_pieces(int n, const float* const* W2, const int* W, void* const* img, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (n > 8) return hipErrorInvalidValue;
+  W2Pieces a{};
+  a.n = n;
+  a.begin[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    if (W[i] <= 0 || W[i] % 16) return hipErrorInvalidValue;
+    a.W2[i] = W2[i];
+    a.img[i] = reinterpret_cast<bf16x8*>(img[i]);
+    a.W[i] = W[i];
+    a.begin[i + 1] = a.begin[i] + (W[i] / 16) * 2 * 64;
+  }
+  hipLaunchKernelGGL(k_w2_pieces, dim3((a.begin[n] + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 // W % 16 == 0; dual when A1d / A2d (tangent pre-activations) are given: WB,

@@ -26,7 +26,10 @@ hipError_t launch_gate_dual(int op, int64_t n, const int* dims, const float* y, 
 // pre-activations; 2E rows) of e -> W0 -> phi -> W1 -> phi -> W2
 hipError_t launch_mlp_fwd(int E, int W, const float* emb, const float* W0, const float* W1,
                           const float* W2, const float* A1p, const float* A2p, float* A1, float* H1,
-                          float* A2, float* H2, float* WT, float c, hipStream_t s);
+                          float* A2, float* H2, float* WT, float c, hipStream_t s,
+                          const void* W2p = nullptr);   // W2p: W2's piece image (layer 2 on bf16x6)
+int64_t mlp_w2_piece_bytes(int W);
+hipError_t launch_mlp_w2_pieces(int n, const float* const* W2, const int* W, void* const* img, hipStream_t s);
 hipError_t launch_mlp_bwd(int E, int W, const float* WB, const float* W0, const float* W1,
                           const float* W2, const float* A1, const float* A2, const float* A1d,
                           const float* A2d, float* A2B, float* A1B, float* EB, float c,

@@ -763,14 +763,38 @@ class ExplicitStep:
         self.mlp_idx = torch.as_tensor(np.concatenate(idx), device=dev)
         self.mlp_scl = torch.as_tensor(np.concatenate(scl), device=dev, dtype=dt)
         self.mlp_buf = torch.empty(off, device=dev, dtype=dt)
+        # layer 2 of the forward / tangent chains on bf16x6 matrix cores
+        # (e3gnn_radial_mlp_forward_p): the W2 piece images, rebuilt by one
+        # launch with the weights (E3GNN_TRAIN_MLP_BF16=0: the f32 chains)
+        self.w2p = None
+        self._w2p_of = {}
+        widths = [views[2][1][1] for views in self.mlp_views]
+        if (self.p._hip(self.mlp_buf) and os.environ.get('E3GNN_TRAIN_MLP_BF16', '1') != '0'
+                and all(w % 16 == 0 for w in widths) and len(widths) <= 8):
+            lib = self.p.lib
+            nb = [int(lib.e3gnn_radial_mlp_w2_piece_bytes(w)) for w in widths]
+            offs = np.concatenate([[0], np.cumsum(nb)]).astype(np.int64)
+            self.w2p_buf = torch.empty(int(offs[-1]), device=dev, dtype=torch.uint8)
+            self.w2p = [self.w2p_buf.data_ptr() + int(o) for o in offs[:-1]]
+            self.w2p_widths = (ctypes.c_int32 * len(widths))(*widths)
 
     def _mlp_weights(self):
         """[(W0, W1, W2) per block], each scaled by 1/sqrt(fan-in), views of one
         buffer filled by one gather-multiply (16-byte aligned when the counts
         are multiples of 4)"""
         torch.mul(self.m.flat.detach()[self.mlp_idx], self.mlp_scl, out=self.mlp_buf)
-        return [tuple(self.mlp_buf[o:o + int(np.prod(sh))].view(*sh) for o, sh in views)
-                for views in self.mlp_views]
+        Ws = [tuple(self.mlp_buf[o:o + int(np.prod(sh))].view(*sh) for o, sh in views)
+              for views in self.mlp_views]
+        self._w2p_of = {}
+        if self.w2p is not None:
+            from . import _lib
+            n = len(Ws)
+            srcs = (ctypes.c_void_p * n)(*[W[2].data_ptr() for W in Ws])
+            imgs = (ctypes.c_void_p * n)(*self.w2p)
+            _lib.check(self.p.lib.e3gnn_radial_mlp_w2_pieces(n, srcs, self.w2p_widths, imgs,
+                                                             self._stream(self.mlp_buf)))
+            self._w2p_of = {W[2].data_ptr(): q for W, q in zip(Ws, self.w2p)}
+        return Ws
 
     def _P(self, name):
         return self.m.param(name)
@@ -970,10 +994,10 @@ class ExplicitStep:
         if self._mlp_hip(e) and W2.shape[1] % 16 == 0:
             from . import _lib
             ptr = lambda t: t.data_ptr() if t is not None else None   # noqa: E731
-            _lib.check(self.p.lib.e3gnn_radial_mlp_forward(
+            _lib.check(self.p.lib.e3gnn_radial_mlp_forward_p(
                 int(e.shape[0]), int(W2.shape[1]), e.data_ptr(), W0.data_ptr(), W1.data_ptr(),
-                W2.data_ptr(), ptr(a1p), ptr(a2p), A1.data_ptr(), H1.data_ptr(), A2.data_ptr(),
-                H2.data_ptr(), WT.data_ptr(), self.p.c, self._stream(e)))
+                W2.data_ptr(), self._w2p_of.get(W2.data_ptr()), ptr(a1p), ptr(a2p), A1.data_ptr(),
+                H1.data_ptr(), A2.data_ptr(), H2.data_ptr(), WT.data_ptr(), self.p.c, self._stream(e)))
             return
         torch.mm(e, W0, out=A1)
         if a1p is None:

@@ -7,6 +7,8 @@ second derivatives 2e-5 relative to the output's max magnitude; model forces
 1e-4 eV/A (north_star), energies 2e-6 relative; parameter gradients of the
 force loss (double backward, create_graph=True) 1e-4 relative in norm.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -197,12 +199,15 @@ def test_edge_geometry_kernels_vs_fp64(hip_backend, normalize):
     assert _rel(F, ref) < 1e-5
 
 
+@pytest.mark.parametrize('pieces', [False, True])
 @pytest.mark.parametrize('width', [384, 960, 224])
-def test_radial_mlp_chain_kernels_vs_fp64(width):
+def test_radial_mlp_chain_kernels_vs_fp64(width, pieces):
     """e3gnn_radial_mlp_forward / _backward (whole chains per 16-row tile) vs
     the same chains as float64 GEMMs + element-wise steps (train_explicit's
     torch path): forward, tangent, first reverse and dual reverse; a row
-    count that is not a multiple of 16; the three block widths."""
+    count that is not a multiple of 16; the three block widths; pieces: layer
+    2 of the forward / tangent chains on bf16x6 (e3gnn_radial_mlp_forward_p
+    with e3gnn_radial_mlp_w2_pieces' image) -- the same f32-grade bound."""
     from sevennet_finetuning_amd import _lib
     from sevennet_finetuning_amd.train_explicit import ExplicitStep, _Prims
 
@@ -233,6 +238,14 @@ def test_radial_mlp_chain_kernels_vs_fp64(width):
         z = lambda *sh: torch.zeros(*sh, dtype=dt, device=dev)        # noqa: E731
         h = host(dev)
         Ws = tuple(T(w) for w in Wn)
+        h._w2p_of = {}
+        if pieces and dev != 'cpu':
+            lib = _lib.load()
+            img = torch.empty(int(lib.e3gnn_radial_mlp_w2_piece_bytes(width)), dtype=torch.uint8, device=dev)
+            _lib.check(lib.e3gnn_radial_mlp_w2_pieces(
+                1, (ctypes.c_void_p * 1)(Ws[2].data_ptr()), (ctypes.c_int32 * 1)(width),
+                (ctypes.c_void_p * 1)(img.data_ptr()), torch.cuda.current_stream().cuda_stream))
+            h._w2p_of = {Ws[2].data_ptr(): img.data_ptr()}
         A1, H1, A2, H2, WT = z(2 * E, 64), z(2 * E, 64), z(2 * E, 64), z(2 * E, 64), z(2 * E, width)
         h._mlp_fwd(T(emb), Ws, None, None, A1[:E], H1[:E], A2[:E], H2[:E], WT[:E])
         h._mlp_fwd(T(embd), Ws, A1[:E], A2[:E], A1[E:], H1[E:], A2[E:], H2[E:], WT[E:])

@@ -105,6 +105,7 @@ for s in "$@"; do
     tgbkarg_*) v=${s#tgbkarg_}; step tgbkarg_$v 300 env HIP_FORCE_DEV_KERNARG=$v python tools/tgemm_bench.py ;;
     proftraint) step proftraint 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_traint -o run -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     benchdxc_*) v=${s#benchdxc_}; step benchdxc_$v 600 env E3GNN_DXC_SORTED=$v python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
+    btmlpbf_*) v=${s#btmlpbf_}; step btmlpbf_$v 300 env E3GNN_TRAIN_MLP_BF16=$v python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     gtrain) step gtrain 600 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread ;;
     benchmc_*) v=${s#benchmc_}; step benchmc_$v 600 python bench.py --model-config $v --steps 5 --warmup 2 --no-cpu-baseline ;;
     proftrain2) step proftrain2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train2 -o run --output-format csv -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
