@@ -317,6 +317,12 @@ int e3gnn_radial_mlp_forward_p(int64_t n_rows, int width, const float* emb, cons
                                const float* W1, const float* W2, const void* w2_pieces,
                                const float* a1_primal, const float* a2_primal, float* a1, float* h1,
                                float* a2, float* h2, float* w, float act_scale, void* stream);
+/* The reverse / dual chain with h2b = wb W2^T on bf16x6 (w2_pieces as above;
+ * width % 32 == 0, else the f32 form runs). */
+int e3gnn_radial_mlp_backward_p(int64_t n_rows, int width, const float* wb, const float* W0,
+                                const float* W1, const float* W2, const void* w2_pieces, const float* a1,
+                                const float* a2, const float* a1_tangent, const float* a2_tangent,
+                                float* a2b, float* a1b, float* embb, float act_scale, void* stream);
 int64_t e3gnn_radial_mlp_w2_piece_bytes(int width);
 /* piece images of n (<= 8) W2 matrices [64, widths[i]] in one launch */
 int e3gnn_radial_mlp_w2_pieces(int n, const float* const* W2, const int32_t* widths, void* const* images,

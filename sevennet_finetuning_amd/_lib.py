@@ -69,6 +69,7 @@ SIGNATURES = {
     'e3gnn_radial_mlp_w2_piece_bytes': (_c_i64, [_c_int]),
     'e3gnn_radial_mlp_w2_pieces': (_c_int, [_c_int, _vp, _vp, _vp, _vp]),
     'e3gnn_radial_mlp_backward': (_c_int, [_c_i64, _c_int] + [_vp] * 11 + [_c_f, _vp]),
+    'e3gnn_radial_mlp_backward_p': (_c_int, [_c_i64, _c_int] + [_vp] * 12 + [_c_f, _vp]),
     'e3gnn_edge_geometry': (_c_int, [_c_i64, _vp, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp]),
     'e3gnn_edge_geometry_jvp': (_c_int, [_c_i64, _vp, _vp, _c_f, _c_f, _c_int] + [_vp] * 10),
     'e3gnn_edge_geometry_vjp': (_c_int, [_c_i64, _vp, _vp, _c_f, _c_f, _c_int, _vp, _vp, _vp, _vp]),

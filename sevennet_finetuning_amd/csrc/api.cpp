@@ -1973,7 +1973,17 @@ int e3gnn_radial_mlp_backward(int64_t n_rows, int width, const float* wb, const 
                               const float* W1, const float* W2, const float* a1, const float* a2,
                               const float* a1_tangent, const float* a2_tangent, float* a2b,
                               float* a1b, float* embb, float act_scale, void* stream) {
+  return e3gnn_radial_mlp_backward_p(n_rows, width, wb, W0, W1, W2, nullptr, a1, a2, a1_tangent, a2_tangent,
+                                     a2b, a1b, embb, act_scale, stream);
+}
+
+int e3gnn_radial_mlp_backward_p(int64_t n_rows, int width, const float* wb, const float* W0,
+                                const float* W1, const float* W2, const void* w2_pieces, const float* a1,
+                                const float* a2, const float* a1_tangent, const float* a2_tangent,
+                                float* a2b, float* a1b, float* embb, float act_scale, void* stream) {
   if (n_rows <= 0) return E3GNN_OK;
+  if (w2_pieces && reinterpret_cast<uintptr_t>(w2_pieces) % 16)
+    return fail(E3GNN_ERR_ARG, "radial MLP backward: the W2 piece image must be 16-byte aligned");
   if (n_rows > INT32_MAX || width <= 0 || width % 16)
     return fail(E3GNN_ERR_ARG, "radial MLP backward: width must be a multiple of 16");
   if (!wb || !W0 || !W1 || !W2 || !a1 || !a2 || !embb ||
@@ -1983,7 +1993,7 @@ int e3gnn_radial_mlp_backward(int64_t n_rows, int width, const float* wb, const 
   if (!al(wb) || !al(W0) || !al(W1) || !al(W2))
     return fail(E3GNN_ERR_ARG, "radial MLP backward: wb / W0 / W1 / W2 must be 16-byte aligned");
   HIPCHK(launch_mlp_bwd((int)n_rows, width, wb, W0, W1, W2, a1, a2, a1_tangent, a2_tangent, a2b, a1b,
-                        embb, act_scale, (hipStream_t)stream));
+                        embb, act_scale, (hipStream_t)stream, w2_pieces));
   return E3GNN_OK;
 }
 

@@ -85,13 +85,19 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8 (&d)[3]) {
 #pragma unroll
   for (int pc = 0; pc < 3; ++pc) d[pc] = __builtin_bit_cast(bf16x8, w[pc]);
 }
-// the piece image of W2 [64][W]: per 16-column block b, k-half kb (32 hidden
-// units) and piece p, 64 lanes x 16 bytes at ((b * 2 + kb) * 3 + p) * 1024
+// the piece images of W2 [64][W], W * 384 bytes each:
+//   img  (layer 2, w = h2 W2): per 16-column block b, k-half kb (32 hidden
+//        units) and piece p, 64 lanes x 16 bytes at ((b * 2 + kb) * 3 + p) * 1024;
+//        lane l: W2[32 kb + 8 (l >> 4) + i][16 b + (l & 15)], i < 8
+//   imgT (the reverse chains' h2b = wb W2^T): per k group t (32 columns of W2),
+//        hidden block hb and piece p at ((t * 4 + hb) * 3 + p) * 1024; lane l:
+//        W2[16 hb + (l & 15)][32 t + 8 (l >> 4) + i]
 struct W2Pieces {
   const float* W2[8];
   bf16x8* img[8];
+  bf16x8* imgT[8];
   int W[8];
-  int begin[9];   // thread ranges (64 per (block, k-half))
+  int begin[9];   // thread ranges (64 per (block, k-half) = per (k group, hidden block))
   int n;
 };
 __global__ __launch_bounds__(256) void k_w2_pieces(W2Pieces a) {
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(256) void k_w2_pieces(W2Pieces a) {
 #pragma unroll
   for (int i = 1; i < 8; ++i) m += (i < a.n && t >= a.begin[i]) ? 1 : 0;
   if (t >= a.begin[a.n]) return;
-  const int local = t - a.begin[m], lane = local & 63, bk = local >> 6;   // bk = b * 2 + kb
+  const int local = t - a.begin[m], lane = local & 63, bk = local >> 6;   // bk = b * 2 + kb = tq * 4 + hb
   const int b = bk >> 1, kb = bk & 1, g = lane >> 4, cl = lane & 15, W = a.W[m];
   float v[8];
 #pragma unroll
@@ -109,6 +115,14 @@ __global__ __launch_bounds__(256) void k_w2_pieces(W2Pieces a) {
   split3(v, d);
 #pragma unroll
   for (int p = 0; p < 3; ++p) a.img[m][(bk * 3 + p) * 64 + lane] = d[p];
+  if (W % 32) return;   // (no transposed image: the reverse chains stay f32)
+  const int tq = bk >> 2, hb = bk & 3;
+  const float4* r = reinterpret_cast<const float4*>(a.W2[m] + (int64_t)(16 * hb + cl) * W + 32 * tq + 8 * g);
+  const float4 x0 = r[0], x1 = r[1];
+  const float u[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  split3(u, d);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) a.imgT[m][(bk * 3 + p) * 64 + lane] = d[p];
 }
 
 // forward (TAN = false) / tangent (TAN = true) chain; one workgroup per
@@ -261,7 +275,8 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int E, int W, const float* __re
                                                  const float* __restrict__ A1d,
                                                  const float* __restrict__ A2d,
                                                  float* __restrict__ A2B, float* __restrict__ A1B,
-                                                 float* __restrict__ EB, float c) {
+                                                 float* __restrict__ EB, float c,
+                                                 const bf16x8* __restrict__ W2pT) {
   constexpr int NS = DUAL ? 2 : 1;  // row sets: primal (and tangent)
   __shared__ float hs[NS][16 * LDH];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, cl = lane & 15;
@@ -307,6 +322,41 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int E, int W, const float* __re
         pacc[q][hb] = mfma4(a[q].w, b[hb].w, pacc[q][hb]);
       }
   };
+  if (W2pT) {   // bf16x6 (wave-uniform): k groups of 32 (W % 32 == 0), W2^T from the piece image
+    const int T32 = W / 32;
+    constexpr int I[6] = {2, 1, 0, 1, 0, 0}, J[6] = {0, 1, 2, 0, 1, 0};
+    auto lda = [&](int t, float4 (&a)[NS][2]) __attribute__((always_inline)) {
+      const bool ok = t < T32 && aok;
+#pragma unroll
+      for (int q = 0; q < NS; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          a[q][h] = ok ? reinterpret_cast<const float4*>(WB + ((int64_t)q * E + arow) * W + 32 * t + 8 * g)[h]
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    float4 ar[NS][2];
+    lda(w, ar);
+    for (int t = w; t < T32; t += 4) {
+      bf16x8 ap[NS][3];
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        const float v[8] = {ar[q][0].x, ar[q][0].y, ar[q][0].z, ar[q][0].w,
+                            ar[q][1].x, ar[q][1].y, ar[q][1].z, ar[q][1].w};
+        split3(v, ap[q]);
+      }
+      lda(t + 4, ar);
+#pragma unroll
+      for (int hb = 0; hb < 4; ++hb) {
+        bf16x8 bp[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bp[p] = W2pT[((t * 4 + hb) * 3 + p) * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+#pragma unroll
+          for (int j = 0; j < 6; ++j) pacc[q][hb] = mfma16(ap[q][I[j]], bp[J[j]], pacc[q][hb]);
+      }
+    }
+  } else {
   load_t(w, bq[0], aq[0]);
   for (int t = w; t < T; t += 8) {
     load_t(t + 4, bq[1], aq[1]);
@@ -314,6 +364,7 @@ __global__ __launch_bounds__(256) void k_mlp_bwd(int E, int W, const float* __re
     if (t + 4 >= T) break;
     load_t(t + 8, bq[0], aq[0]);
     mul_t(bq[1], aq[1]);
+  }
   }
 #pragma unroll
   for (int q = 0; q < NS; ++q)
@@ -428,7 +479,7 @@ hipError_t launch_mlp_fwd(int E, int W, const float* emb, const float* W0, const
                        H1, A2, H2, WT, c, p);
   return hipGetLastError();
 }
-int64_t mlp_w2_piece_bytes(int W) { return (int64_t)(W / 16) * 6 * 1024; }
+int64_t mlp_w2_piece_bytes(int W) { return 2 * (int64_t)W * 384; }   // img, then imgT
 hipError_t launch_mlp_w2_pieces(int n, const float* const* W2, const int* W, void* const* img, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (n > 8) return hipErrorInvalidValue;
@@ -439,6 +490,7 @@ hipError_t launch_mlp_w2_pieces(int n, const float* const* W2, const int* W, voi
     if (W[i] <= 0 || W[i] % 16) return hipErrorInvalidValue;
     a.W2[i] = W2[i];
     a.img[i] = reinterpret_cast<bf16x8*>(img[i]);
+    a.imgT[i] = reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(img[i]) + (int64_t)W[i] * 384);
     a.W[i] = W[i];
     a.begin[i + 1] = a.begin[i] + (W[i] / 16) * 2 * 64;
   }
@@ -450,15 +502,19 @@ hipError_t launch_mlp_w2_pieces(int n, const float* const* W2, const int* W, voi
 hipError_t launch_mlp_bwd(int E, int W, const float* WB, const float* W0, const float* W1,
                           const float* W2, const float* A1, const float* A2, const float* A1d,
                           const float* A2d, float* A2B, float* A1B, float* EB, float c,
-                          hipStream_t s) {
+                          hipStream_t s, const void* W2p) {
   if (E <= 0) return hipSuccess;
   const dim3 grid((E + 15) / 16);
+  // the transposed image follows the forward one (W * 384 bytes each, W2Pieces)
+  const bf16x8* pT = (W2p && W % 32 == 0)
+                         ? reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(W2p) + (int64_t)W * 384)
+                         : nullptr;
   if (A1d)
     hipLaunchKernelGGL(k_mlp_bwd<true>, grid, dim3(256), 0, s, E, W, WB, W0, W1, W2, A1, A2, A1d, A2d,
-                       A2B, A1B, EB, c);
+                       A2B, A1B, EB, c, pT);
   else
     hipLaunchKernelGGL(k_mlp_bwd<false>, grid, dim3(256), 0, s, E, W, WB, W0, W1, W2, A1, A2, A1d,
-                       A2d, A2B, A1B, EB, c);
+                       A2d, A2B, A1B, EB, c, pT);
   return hipGetLastError();
 }
 

@@ -33,7 +33,7 @@ hipError_t launch_mlp_w2_pieces(int n, const float* const* W2, const int* W, voi
 hipError_t launch_mlp_bwd(int E, int W, const float* WB, const float* W0, const float* W1,
                           const float* W2, const float* A1, const float* A2, const float* A1d,
                           const float* A2d, float* A2B, float* A1B, float* EB, float c,
-                          hipStream_t s);
+                          hipStream_t s, const void* W2p = nullptr);
 // the explicit step's loss (MSE / Huber, mean over labelled entries) and its
 // cotangents: terms[0..2] = weighted energy-per-atom / force / stress terms
 struct LossArgs {

@@ -1016,10 +1016,10 @@ class ExplicitStep:
         W0, W1, W2 = Ws
         if self._mlp_hip(wb) and W2.shape[1] % 16 == 0:
             from . import _lib
-            _lib.check(self.p.lib.e3gnn_radial_mlp_backward(
+            _lib.check(self.p.lib.e3gnn_radial_mlp_backward_p(
                 int(wb.shape[0]), int(W2.shape[1]), wb.contiguous().data_ptr(), W0.data_ptr(),
-                W1.data_ptr(), W2.data_ptr(), a1.data_ptr(), a2.data_ptr(), None, None, None, None,
-                embb.data_ptr(), self.p.c, self._stream(wb)))
+                W1.data_ptr(), W2.data_ptr(), self._w2p_of.get(W2.data_ptr()), a1.data_ptr(), a2.data_ptr(),
+                None, None, None, None, embb.data_ptr(), self.p.c, self._stream(wb)))
             return
         a2b = self.p.act_jvp(a2, wb @ W2.t())
         a1b = self.p.act_jvp(a1, a2b @ W1.t())
@@ -1032,10 +1032,11 @@ class ExplicitStep:
         E = A1.shape[0] // 2
         if self._mlp_hip(WB) and W2.shape[1] % 16 == 0:
             from . import _lib
-            _lib.check(self.p.lib.e3gnn_radial_mlp_backward(
+            _lib.check(self.p.lib.e3gnn_radial_mlp_backward_p(
                 E, int(W2.shape[1]), WB.data_ptr(), W0.data_ptr(), W1.data_ptr(), W2.data_ptr(),
-                A1[:E].data_ptr(), A2[:E].data_ptr(), A1[E:].data_ptr(), A2[E:].data_ptr(),
-                A2B.data_ptr(), A1B.data_ptr(), EMBB.data_ptr(), self.p.c, self._stream(WB)))
+                self._w2p_of.get(W2.data_ptr()), A1[:E].data_ptr(), A2[:E].data_ptr(), A1[E:].data_ptr(),
+                A2[E:].data_ptr(), A2B.data_ptr(), A1B.data_ptr(), EMBB.data_ptr(), self.p.c,
+                self._stream(WB)))
             return
         H2B = WB @ W2.t()
         self.p.act_dual(A2[:E], A2[E:], H2B[:E], H2B[E:], out0=A2B[:E], out1=A2B[E:])
