@@ -260,13 +260,15 @@ int e3gnn_conv_graph(int64_t n_nodes, int64_t n_edges, const int32_t* edge_cente
                      int32_t* src_perm, int32_t* scratch, void* stream);
 /* The same build from int64 edge indices (a batch's edge_index rows), also
  * writing their int32 copies center_out / nbr_out [E]; graphs of at most
- * e3gnn_conv_graph_small_max_nodes() nodes (one workgroup, one launch -- the
- * per-step rebuild of a captured fine-tune step). */
+ * e3gnn_conv_graph_small_max_nodes() nodes and e3gnn_conv_graph_small_max_edges()
+ * edges (one workgroup, one launch -- the per-step rebuild of a captured
+ * fine-tune step). */
 int e3gnn_conv_graph_i64(int64_t n_nodes, int64_t n_edges, const int64_t* edge_center,
                          const int64_t* edge_nbr, int32_t* center_out, int32_t* nbr_out,
                          int32_t* row_ptr, int32_t* src_ptr, int32_t* src_perm, int32_t* scratch,
                          void* stream);
 int e3gnn_conv_graph_small_max_nodes(void);
+int e3gnn_conv_graph_small_max_edges(void);
 /* agg[n_nodes x agg_dim] = segmented sum of TP(h[nbr], Y, w); Y [E x 9],
  * w [E x w_dim], h [n_nodes x h_dim]. */
 int e3gnn_conv_forward(int kind, int64_t n_nodes, const int32_t* row_ptr, const int32_t* edge_nbr,

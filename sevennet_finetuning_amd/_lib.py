@@ -54,6 +54,7 @@ SIGNATURES = {
     'e3gnn_conv_graph': (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_conv_graph_i64': (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_conv_graph_small_max_nodes': (_c_int, []),
+    'e3gnn_conv_graph_small_max_edges': (_c_int, []),
     'e3gnn_conv_forward': (_c_int, [_c_int, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'e3gnn_conv_backward': (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -62,6 +62,7 @@ class HipConvBackend:
     def __init__(self):
         self.lib = _lib.load()
         self.small_max = int(self.lib.e3gnn_conv_graph_small_max_nodes())
+        self.small_max_e = int(self.lib.e3gnn_conv_graph_small_max_edges())
         self.dims = {}
         for kind in (0, 1, 2):
             a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
@@ -88,7 +89,7 @@ class HipConvBackend:
             aux = into
             c, j = g.edge_center, g.edge_nbr
             if (c.dtype == torch.int64 and j.dtype == torch.int64 and c.is_contiguous() and j.is_contiguous()
-                    and c.device == dev and n <= self.small_max):
+                    and c.device == dev and n <= self.small_max and E <= self.small_max_e):
                 # one launch: the int32 copies, the CSRs and the validation
                 _lib.check(self.lib.e3gnn_conv_graph_i64(
                     n, E, c.data_ptr(), j.data_ptr(), aux['center'].data_ptr(), aux['nbr'].data_ptr(),

@@ -1803,7 +1803,7 @@ int e3gnn_conv_graph(int64_t n_nodes, int64_t n_edges, const int32_t* edge_cente
     return fail(E3GNN_ERR_ARG, "null conv graph buffer");
   hipStream_t s = (hipStream_t)stream;
   int* err_d = scratch + n_nodes;
-  if (n_nodes <= graph_small_max_nodes()) {   // one workgroup, one launch
+  if (n_nodes <= graph_small_max_nodes() && n_edges <= graph_small_max_edges()) {   // one workgroup, one launch
     HIPCHK(launch_build_graph_small(n_edges, (int)n_nodes, edge_center, edge_nbr, nullptr, nullptr, nullptr,
                                     nullptr, row_ptr, src_ptr, src_perm, err_d, s));
   } else {
@@ -1819,9 +1819,10 @@ int e3gnn_conv_graph_i64(int64_t n_nodes, int64_t n_edges, const int64_t* edge_c
                          int32_t* src_ptr, int32_t* src_perm, int32_t* scratch, void* stream) {
   if (n_nodes < 0 || n_edges < 0 || n_nodes >= (int64_t)1 << 31 || n_edges >= (int64_t)1 << 31)
     return fail(E3GNN_ERR_ARG, "conv graph size out of int32 range");
-  if (n_nodes > graph_small_max_nodes())
+  if (n_nodes > graph_small_max_nodes() || n_edges > graph_small_max_edges())
     return fail(E3GNN_ERR_ARG, "e3gnn_conv_graph_i64: more than " + std::to_string(graph_small_max_nodes()) +
-                                   " nodes (convert the indices and use e3gnn_conv_graph)");
+                                   " nodes or " + std::to_string(graph_small_max_edges()) +
+                                   " edges (convert the indices and use e3gnn_conv_graph)");
   if (!row_ptr || !src_ptr || !scratch ||
       (n_edges > 0 && (!edge_center || !edge_nbr || !center_out || !nbr_out || !src_perm)))
     return fail(E3GNN_ERR_ARG, "null conv graph buffer");
@@ -1833,6 +1834,7 @@ int e3gnn_conv_graph_i64(int64_t n_nodes, int64_t n_edges, const int64_t* edge_c
 }
 
 int e3gnn_conv_graph_small_max_nodes(void) { return graph_small_max_nodes(); }
+int e3gnn_conv_graph_small_max_edges(void) { return graph_small_max_edges(); }
 
 static int graph_check(int* err_d, hipStream_t s) {
   int err = 0;

@@ -23,13 +23,15 @@ hipError_t launch_atom_force(int n_nodes, int n_centers, const int* row_ptr, con
 hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* center,
                               const int* nbr, int* row_ptr, int* src_ptr, int* src_perm, int* cnt,
                               int* err, hipStream_t s, int n_interior = 0);
-// the whole build in one workgroup (n <= graph_small_max_nodes()); int64
+// the whole build in one workgroup (n <= graph_small_max_nodes(), E <=
+// graph_small_max_edges()); int64
 // indices (c64 / j64, converted into cout / jout) or int32 ones (c32 / j32);
 // writes *err (no memset needed)
 hipError_t launch_build_graph_small(int64_t E, int n, const int* c32, const int* j32, const int64_t* c64,
                                     const int64_t* j64, int* cout, int* jout, int* row_ptr, int* src_ptr,
                                     int* src_perm, int* err, hipStream_t s);
 int graph_small_max_nodes();
+int graph_small_max_edges();
 hipError_t launch_embed(int n, int D, const int* type, int nsp, const float* W, float* x, int* err,
                         hipStream_t s);
 // e3nn Gate of the SevenNet-0-shaped family: y = [ns scalars | g1 + g2 gates |

@@ -438,7 +438,7 @@ __global__ __launch_bounds__(256) void k_sort_segments(int n, const int* __restr
 // of the launches above (eleven launches and a memset, each mostly launch
 // latency at this size).  Optionally converts int64 edge indices (the
 // batch's edge_index rows) into the int32 copies the kernels read.
-constexpr int GRAPH_SMALL_N = 6144;
+constexpr int GRAPH_SMALL_N = 3072, GRAPH_SMALL_E = 16384;   // LDS: 24.6 KB of counts / offsets + 64 KB of edges (gfx950: 160 KB per workgroup)
 template <typename T>
 __global__ __launch_bounds__(1024) void k_build_graph_small(int E, int n, const T* __restrict__ cin,
                                                             const T* __restrict__ jin, int* __restrict__ cout,
@@ -447,6 +447,7 @@ __global__ __launch_bounds__(1024) void k_build_graph_small(int E, int n, const 
                                                             int* __restrict__ err) {
   __shared__ int cnt[GRAPH_SMALL_N];
   __shared__ int ptr[GRAPH_SMALL_N + 1];
+  __shared__ int lperm[GRAPH_SMALL_E];   // the transposed CSR's edge list, sorted here, then stored
   __shared__ int wsum[16];
   __shared__ int errl;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -454,9 +455,23 @@ __global__ __launch_bounds__(1024) void k_build_graph_small(int E, int n, const 
   for (int i = t; i <= n; i += 1024) row_ptr[i] = 0;
   if (t == 0) errl = 0;
   __syncthreads();
+  // the thread's edges e = t + 1024 u, all loads in flight at once (a loop
+  // that waited for each edge's loads took ~1 us per edge of the thread)
+  constexpr int EPT = GRAPH_SMALL_E / 1024;
+  int cv[EPT], pv[EPT], jv[EPT];
+#pragma unroll
+  for (int u = 0; u < EPT; ++u) {
+    const int e = t + 1024 * u;
+    cv[u] = e < E ? (int)cin[e] : 0;
+    pv[u] = (e < E && e > 0) ? (int)cin[e - 1] : -1;
+    jv[u] = e < E ? (int)jin[e] : 0;
+  }
   // validation, row_ptr (as k_row_ptr) and the per-neighbour counts
-  for (int e = t; e < E; e += 1024) {
-    const int c = (int)cin[e], j = (int)jin[e];
+#pragma unroll
+  for (int u = 0; u < EPT; ++u) {
+    const int e = t + 1024 * u;
+    if (e >= E) continue;
+    const int c = cv[u], j = jv[u];
     if (cout) cout[e] = c;
     if (jout) jout[e] = j;
     if (j < 0 || j >= n) atomicOr(&errl, 4);
@@ -465,7 +480,7 @@ __global__ __launch_bounds__(1024) void k_build_graph_small(int E, int n, const 
       atomicOr(&errl, 2);
       continue;
     }
-    const int prev = e ? (int)cin[e - 1] : -1;
+    const int prev = pv[u];
     if (c < prev) {
       atomicOr(&errl, 1);
       continue;
@@ -497,34 +512,49 @@ __global__ __launch_bounds__(1024) void k_build_graph_small(int E, int n, const 
   for (int i = t; i <= n; i += 1024) src_ptr[i] = ptr[i];
   for (int i = t; i < n; i += 1024) cnt[i] = 0;
   __syncthreads();
-  for (int e = t; e < E; e += 1024) {
-    const int j = (int)jin[e];
-    if (j < 0 || j >= n) continue;
-    perm[ptr[j] + atomicAdd(&cnt[j], 1)] = e;
+#pragma unroll
+  for (int u = 0; u < EPT; ++u) {
+    const int e = t + 1024 * u, j = jv[u];
+    if (e >= E || j < 0 || j >= n) continue;
+    lperm[ptr[j] + atomicAdd(&cnt[j], 1)] = e;
   }
-  __threadfence_block();
   __syncthreads();
-  // each neighbour's edges ascending (as k_sort_segments; one wave per node)
+  // each neighbour's edges ascending (as k_sort_segments; one wave per node),
+  // in LDS: a global round trip per node made this phase ~50 us
   for (int j = w; j < n; j += 16) {
     const int b = ptr[j], len = ptr[j + 1] - b;
     if (len <= 1) continue;
     if (len <= 64) {
-      const int v = lane < len ? perm[b + lane] : INT_MAX;
-      int rank = 0;
-      for (int k = 0; k < len; ++k) rank += __shfl(v, k) < v;
-      if (lane < len) perm[b + rank] = v;
+      // rank = the segment's smaller ids, read as LDS broadcasts eight at a
+      // time (a cross-lane shuffle per element waited ~100 cycles each)
+      const int v = lane < len ? lperm[b + lane] : INT_MAX;
+      int rank = 0, k = 0;
+      for (; k + 8 <= len; k += 8) {
+        int x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = lperm[b + k + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) rank += x[u] < v;
+      }
+      for (; k < len; ++k) rank += lperm[b + k] < v;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < len) lperm[b + rank] = v;
+      __builtin_amdgcn_wave_barrier();
     } else if (lane == 0) {
       for (int i = b + 1; i < b + len; ++i) {
-        const int v = perm[i];
+        const int v = lperm[i];
         int k = i - 1;
-        while (k >= b && perm[k] > v) {
-          perm[k + 1] = perm[k];
+        while (k >= b && lperm[k] > v) {
+          lperm[k + 1] = lperm[k];
           --k;
         }
-        perm[k + 1] = v;
+        lperm[k + 1] = v;
       }
     }
   }
+  __syncthreads();
+  const int ne = ptr[n];
+  for (int i = t; i < ne; i += 1024) perm[i] = lperm[i];
   if (t == 0) *err = errl;
 }
 
@@ -838,7 +868,7 @@ hipError_t launch_build_graph(int64_t E, int n_centers, int n_nodes, const int* 
 hipError_t launch_build_graph_small(int64_t E, int n, const int* c32, const int* j32, const int64_t* c64,
                                     const int64_t* j64, int* cout, int* jout, int* row_ptr, int* src_ptr,
                                     int* src_perm, int* err, hipStream_t s) {
-  if (n < 0 || n > GRAPH_SMALL_N || E < 0 || E >= ((int64_t)1 << 30)) return hipErrorInvalidValue;
+  if (n < 0 || n > GRAPH_SMALL_N || E < 0 || E > GRAPH_SMALL_E) return hipErrorInvalidValue;
   if (c64)
     hipLaunchKernelGGL(k_build_graph_small<int64_t>, dim3(1), dim3(1024), 0, s, (int)E, n, c64, j64, cout,
                        jout, row_ptr, src_ptr, src_perm, err);
@@ -848,6 +878,7 @@ hipError_t launch_build_graph_small(int64_t E, int n, const int* c32, const int*
   return hipGetLastError();
 }
 int graph_small_max_nodes() { return GRAPH_SMALL_N; }
+int graph_small_max_edges() { return GRAPH_SMALL_E; }
 hipError_t launch_embed(int n, int D, const int* type, int nsp, const float* W, float* x, int* err,
                         hipStream_t s) {
   LAUNCH(k_embed, nblk((int64_t)n * D), n, D, type, nsp, W, x, err);

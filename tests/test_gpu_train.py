@@ -259,12 +259,15 @@ def test_radial_mlp_chain_kernels_vs_fp64(width, pieces):
         assert _rel(a, b) < 2e-5, nm
 
 
-@pytest.mark.parametrize('n,mean_deg,hub', [(5, 2, 0), (3000, 0.0005, 0), (3000, 6, 150), (20000, 28, 90)])
+@pytest.mark.parametrize('n,mean_deg,hub', [(5, 2, 0), (3000, 0.0005, 0), (1000, 6, 150), (3000, 6, 150),
+                                             (20000, 28, 90)])
 def test_conv_graph_csr_matches_numpy(hip_backend, n, mean_deg, hub):
     """row_ptr / src_ptr / src_perm of e3gnn_conv_graph against numpy: the
     transposed CSR lists each neighbour's edges in ascending edge id.  Sizes
     span one and several 1,024-count scan blocks, nodes without edges, and a
-    hub neighbour with more than 64 incoming edges (the long-segment sort)."""
+    hub neighbour with more than 64 incoming edges (the long-segment sort);
+    the one-workgroup build (<= 3,072 nodes, <= 16,384 edges: n = 5, 1,000 and
+    the sparse 3,000) and the multi-launch one (the rest)."""
     rng = np.random.default_rng(n)
     deg = rng.poisson(mean_deg, n)
     deg[::11] = 0
