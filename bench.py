@@ -43,6 +43,12 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 matrix = vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E peak
+# what the step computes in: f32 data and accumulation everywhere; the radial
+# MLP's matrix products (and the wide node linears) on bf16 MFMA with f32
+# operands split into bf16 pieces -- six piece products (f32-grade) where the
+# energy is formed, three (~2^-16 relative) for the backward's dH2 = dw W2^T
+# and its w recompute
+DTYPE = 'f32 (MLP / linear products on bf16 MFMA pieces: bf16x6 fwd, bf16x3 bwd)'
 
 
 def log(msg):
@@ -559,7 +565,7 @@ def main():
             'metric': metric,
             'value': round(value, 2), 'unit': 'atoms/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
-            'higher_is_better': True, 'scaling': scaling, 'vs_baseline': None, 'dtype': 'f32',
+            'higher_is_better': True, 'scaling': scaling, 'vs_baseline': None, 'dtype': DTYPE,
             'data': 'synthetic Si diamond box, default_rng(0) 0.05 A displacements; '
                     + ('SevenNet-0 weights (reference opt_params_sevenn.pt)' if model_dir is None else
                        f'{label}: e3nn initialisation (model_build, seed 0), fused-kernel family '

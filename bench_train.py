@@ -163,7 +163,8 @@ def main():
             'metric': 'structures/sec fine-tune step (rehearsal + EWC), SevenNet-0',
             'value': round(structs / dt, 2), 'unit': 'structures/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': 'f32 (radial-MLP W2 products on bf16x6 MFMA pieces: f32-grade)',
             'data': 'synthetic 54-atom mixed-species diamond cells, synthetic labels/Fisher',
             'config': {'workload': f'rehearsal step: 2 x {args.batch} structures per rank '
                                    f'({atoms_per_step} atoms), force+stress+energy Huber + EWC, '
@@ -171,7 +172,12 @@ def main():
                        'atoms_per_rank_step': atoms_per_step, 'edges_per_batch': edges,
                        'parallelism': f'dp{world}',
                        'hip_graph': bool(tr.hip_graph),
-                       'explicit_grad': tr.explicit is not None, 'blas': args.blas},
+                       'explicit_grad': tr.explicit is not None,
+                       # which GEMMs ran: the library's grouped GEMM (no vendor
+                       # BLAS kernel in the step) or torch's with the --blas choice
+                       'gemm': ('libe3gnn_hip e3gnn_gemm_grouped (no rocBLAS / hipBLASLt kernel)'
+                                if tr.explicit is not None and tr.explicit.gm.lib is not None
+                                else f'torch ({args.blas})')},
             'atoms_per_s': round(atoms_per_step * world * args.steps / dt, 1),
             'loss': float(loss), 'mem_loss': float(mloss), 'cpu_baseline': cpu}), flush=True)
     if world > 1:

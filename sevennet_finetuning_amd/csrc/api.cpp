@@ -1073,6 +1073,29 @@ static int gemm_prob(const e3gnn_gemm_desc& q, int i, TgProb& p) {
     p.B2 = lay(q.b2, q.ldb2, q.trans_b2, q.k2);
     p.ldc = q.ldc; p.crep = 1; p.crs = 0; p.cns = 1;
   }
+  // the kernel addresses each operand through one buffer descriptor with
+  // 32-bit byte offsets (TG_RECORDS, ~2 GB): refuse what would wrap
+  {
+    auto fits = [](const TgLay& L, int64_t rows, int64_t K, const e3gnn_gemm_layout* g) {
+      if (g && (g->ld < 0 || g->kst < 0 || g->sst < 0 || g->rs < 0 || g->ld > INT32_MAX ||
+                g->kst > INT32_MAX || g->sst > INT32_MAX))
+        return false;
+      if (L.ld < 0 || L.kst < 0 || L.sst < 0 || L.rs < 0) return false;
+      if (rows <= 0 || K <= 0) return true;
+      const int64_t rep = std::max(L.rep, 1), ks = L.ks > 0 ? L.ks : K;
+      const int64_t off = (rows - 1) / rep * L.ld + std::min<int64_t>(rows - 1, rep - 1) * L.rs +
+                          std::min<int64_t>(K - 1, ks - 1) * L.kst + (K - 1) / ks * L.sst;
+      return off >= 0 && (off + 1) * 4 <= (int64_t)0x7fff0000;
+    };
+    const e3gnn_gemm_layouts* G = q.layout;
+    const int64_t lds[4] = {q.lda, q.ldb, q.lda2, q.ldb2};
+    for (int64_t v : lds)
+      if (v < 0 || v > INT32_MAX) return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: leading dimension beyond int32");
+    if (!fits(p.A1, q.m, q.k, G ? &G->a : nullptr) || !fits(p.B1, q.n, q.k, G ? &G->b : nullptr) ||
+        (q.k2 > 0 && (!fits(p.A2, q.m, q.k2, G ? &G->a2 : nullptr) || !fits(p.B2, q.n, q.k2, G ? &G->b2 : nullptr))))
+      return fail(E3GNN_ERR_ARG, "e3gnn_gemm_grouped: problem " + std::to_string(i) +
+                                     " addresses an operand beyond 2 GB (32-bit buffer offsets)");
+  }
   p.C = q.c;
   p.M = q.m; p.N = q.n; p.K1 = q.k; p.K2 = q.k2;
   p.alpha = q.alpha; p.beta = q.beta;

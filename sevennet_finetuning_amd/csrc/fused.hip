@@ -1129,9 +1129,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // 2 x 16 x 32 on f32 MFMA.  Middle blocks: two workgroups per CU (LDS), 2 waves
 // per SIMD; the first block: 3 waves per SIMD.
 
+// The staged image holds only the pieces the backward's products read: with
+// the three-product forms (E3GNN_BWD_W_X3, E3GNN_DH2_X3) pieces 0 and 1 of
+// each operand, 16 KB per pair instead of 24 (E3GNN_LS_LEAN=0: all three)
+#ifndef E3GNN_LS_LEAN
+#define E3GNN_LS_LEAN 1
+#endif
+constexpr int LS_WPC = (E3GNN_LS_LEAN && E3GNN_BWD_W_X3) ? 2 : 3;   // staged pieces of a w-recompute block
+constexpr int LS_DPC = (E3GNN_LS_LEAN && E3GNN_DH2_X3) ? 2 : 3;     // of the pair's dH2 operand
+constexpr int LS_IBLK = LS_WPC * 2048;   // image bytes of one w-recompute block (pieces x 2 halves x 1 KB)
+constexpr int LS_IW = 2 * LS_IBLK;       // the pair's w-recompute part
+constexpr int LS_IMG = LS_IW + LS_DPC * 4096;   // + the dH2 part (pieces x 4 bh x 1 KB)
+
+template <int NPC = 3>
 __device__ __forceinline__ void lds_op3(Op3& o, const char* blk, int lane) {
 #pragma unroll
-  for (int pc = 0; pc < 3; ++pc)
+  for (int pc = 0; pc < NPC; ++pc)
 #pragma unroll
     for (int m = 0; m < 2; ++m)
       o.v[pc][m] = *reinterpret_cast<const bf16x8*>(blk + ((pc * 2 + m) * 64 + lane) * 16);
@@ -1220,6 +1233,42 @@ template <class L>
 struct BwdWpg {
   static constexpr int v = L::KIND == 1 ? E3GNN_BWD_WPG : 4;
 };
+// LDS-DMA staging (E3GNN_LS_DMA, default on where it fits): the pair image is
+// written by global_load_lds_dwordx4 straight from L2 (no staging registers,
+// no ds_write) into one of TWO images, so a pair costs ONE barrier: at pair P
+// each wave waits for its own DMA of P (issued at P - 1), the barrier makes
+// all of P visible and retires every read of P - 1's image, then the DMA of
+// P + 1 goes into that image.  The two images need 16 KB more LDS; in the
+// middle blocks the 0e x 0e -> 0e path's dE/dagg (C0 floats, moff 0) is then
+// read from L2 with the neighbour-row prefetch instead of staged, so two
+// workgroups still fit a CU (2 x 80.9 KB of 160 KB).
+#ifndef E3GNN_LS_DMA
+#define E3GNN_LS_DMA 0
+#endif
+template <class L>
+struct LsDma {
+  static constexpr int WPG = BwdWpg<L>::v;
+  static constexpr bool lean = LS_WPC == 2 && LS_DPC == 2;   // 16 x 1 KB chunks: 4 per wave
+  static constexpr bool drop0 = L::KIND == 1;
+  static constexpr int OFF0 = drop0 ? L::P[0].mul : 0;       // path 0 (l 0 0 0, moff 0): C0 floats
+  static constexpr int DMS = L::DM - OFF0;                    // staged dE/dagg floats per centre
+  static constexpr int bytes = WPG * DMS * 4 + 2 * LS_IMG;
+  static constexpr bool v = E3GNN_LS_DMA && lean && WPG == 4 && BwdLsWaves<L>::v * bytes <= 163840;
+};
+// one wave-instruction of LDS-DMA: 64 lanes x 16 bytes from per-lane global
+// addresses to the wave-uniform LDS byte address lds_dst (+ lane x 16); M0
+// set and restored inside the statement.  hipcc does not count it: the
+// consumer waits with an explicit vmcnt before the barrier that publishes it.
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
+}
 #ifndef E3GNN_ABL_NOBAR
 #define E3GNN_ABL_NOBAR 0
 #endif
@@ -1236,22 +1285,46 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
   static_assert(NBLK % 2 == 0, "weight blocks come in pairs");
   constexpr int WPG = BwdWpg<L>::v, NT = 64 * WPG;
   // staging pieces (b128) of a pair: the w-recompute operands, then the dH2 ones
-  constexpr int NWP = LS_PAIR_W / 16, NST = (LS_PAIR_W + LS_PAIR_D) / 16 / NT;
-  static_assert((LS_PAIR_W + LS_PAIR_D) / 16 % NT == 0 && NWP % 64 == 0, "staging pieces per thread");
-  __shared__ __attribute__((aligned(16))) float smem[WPG * L::DM + (LS_PAIR_W + LS_PAIR_D) / 4];
+  constexpr int NWP = LS_IW / 16, NST = LS_IMG / 16 / NT, PB = LS_IBLK / 16;
+  static_assert(LS_IMG / 16 % NT == 0 && NWP % 64 == 0 && PB % 64 == 0, "staging pieces per thread");
+  using DM_ = LsDma<L>;
+  constexpr bool DMA = DM_::v;
+  constexpr int OFF0 = DMA ? DM_::OFF0 : 0, DMS = L::DM - OFF0;   // dE/dagg floats staged per centre
+  static_assert(!DMA || (L::P[0].l1 == 0 && L::P[0].l2 == 0 && L::P[0].l3 == 0 && L::P[0].moff == 0 &&
+                         OFF0 % 4 == 0), "path 0 is the 0e x 0e -> 0e slice at the row start");
+  __shared__ __attribute__((aligned(16))) float smem[WPG * DMS + (DMA ? 2 : 1) * LS_IMG / 4];
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int cb = c_begin + blockIdx.x * WPG;
   const int c = cb + wid;
   const bool valid = c < c_end;
   const int beg = valid ? row_ptr[c] : 0, end = valid ? row_ptr[c + 1] : 0;
   const int T = ls_tiles(row_ptr, cb, c_end, false, WPG);
-  float* dacc = smem + wid * L::DM;
-  char* img = reinterpret_cast<char*>(smem + WPG * L::DM);
+  float* dacc = smem + wid * DMS - OFF0;   // dacc[m] for m >= OFF0
+  char* img = reinterpret_cast<char*>(smem + WPG * DMS);
   if (valid && end > beg) {
-    const float4* s4 = reinterpret_cast<const float4*>(gagg + (int64_t)c * L::DM);
-    float4* d4 = reinterpret_cast<float4*>(dacc);
-    for (int k = lane; k < L::DM / 4; k += 64) d4[k] = s4[k];
+    const float4* s4 = reinterpret_cast<const float4*>(gagg + (int64_t)c * L::DM + OFF0);
+    float4* d4 = reinterpret_cast<float4*>(dacc + OFF0);
+    for (int k = lane; k < DMS / 4; k += 64) d4[k] = s4[k];
   }
+  // DMA mode: the image the current pair reads (0 / 1), its byte base in LDS,
+  // and path 0's dE/dagg row of this centre through a descriptor (invalid
+  // centres: empty, reads 0)
+  int rb = 0;
+  const unsigned img_lds = lds_addr(img);
+  const __amdgpu_buffer_rsrc_t Rg0 =
+      rsrc_bytes(gagg + (valid ? (int64_t)c * L::DM : 0), valid ? (int64_t)OFF0 * 4 : 0);
+  auto issue_dma = [&](int P, int buf) {
+    // chunk k = 4 wid + i of the image: k < 8 the w-recompute blocks (block
+    // k / 4, piece-half k % 4 of w2v), then the dH2 operand's 8 KB (w2d)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = 4 * wid + i;   // wave-uniform
+      const char* src = k < 8 ? reinterpret_cast<const char*>(W.w2v) + (int64_t)P * LS_PAIR_W + (k >> 2) * LS_BLK +
+                                    (k & 3) * 1024
+                              : reinterpret_cast<const char*>(W.w2d) + (int64_t)P * LS_PAIR_D + (k - 8) * 1024;
+      glds16(src + lane * 16, img_lds + buf * LS_IMG + k * 1024);
+    }
+  };
   const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
   f32x4 st[NST];
@@ -1259,10 +1332,13 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
 #if E3GNN_ABL_NOSTAGE
     return;
 #endif
+    // image piece idx: w-recompute block idx / PB (its first LS_WPC pieces
+    // in the w2v order), then the dH2 operand's first LS_DPC pieces (w2d)
+    auto wsrc = [&](int idx) { return (idx / PB) * LS_BLK + (idx % PB) * 16; };
     if constexpr (NWP % NT == 0) {  // (4 waves: each thread's pieces all W, then all D)
       constexpr int NW = NWP / NT;
 #pragma unroll
-      for (int i = 0; i < NW; ++i) st[i] = ldw4(R.w2v, (tid + NT * i) * 16, P * LS_PAIR_W);
+      for (int i = 0; i < NW; ++i) st[i] = ldw4(R.w2v, wsrc(tid + NT * i), P * LS_PAIR_W);
 #pragma unroll
       for (int i = NW; i < NST; ++i) st[i] = ldw4(R.w2d, (tid + NT * i - NWP) * 16, P * LS_PAIR_D);
     } else {
@@ -1270,7 +1346,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
       for (int i = 0; i < NST; ++i) {
         const int idx = tid + NT * i;
         const bool isw = idx < NWP;  // wave-uniform (NWP % 64 == 0)
-        st[i] = isw ? ldw4(R.w2v, idx * 16, P * LS_PAIR_W) : ldw4(R.w2d, (idx - NWP) * 16, P * LS_PAIR_D);
+        st[i] = isw ? ldw4(R.w2v, wsrc(idx), P * LS_PAIR_W) : ldw4(R.w2d, (idx - NWP) * 16, P * LS_PAIR_D);
       }
     }
   };
@@ -1289,7 +1365,8 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
   };
   constexpr bool STAMPED = std::is_same<L, LayerMid>::value;   // SevenNet-0's
   STAMP_DECL
-  issue(0);
+  if constexpr (DMA) issue_dma(0, 0);
+  else issue(0);
   for (int t = 0; t < T; ++t) {
     if constexpr (STAMPED) STAMP(0);
     const int q0 = beg + 16 * t;
@@ -1297,10 +1374,12 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
     const int er = (act && q0 + col < end) ? q0 + col : -1;
     const int vx = (er >= 0 ? nbr[er] : 0) * L::DX * 4;
     float xpf[20];   // the lane's 4 channels x D1 of the next channel group
+    float g0pf[4];   // DMA mode: path 0's dE/dagg of that group (l1 = 0 groups)
     auto load_group = [&](auto Iq, int jq) {
       constexpr int D1q = 2 * Iq + 1;
       constexpr int XOq = iblock_xoff<L, Iq>();
       ldv<4 * D1q>(Rx, vx + 4 * g * D1q * 4, (XOq + 16 * jq * D1q) * 4, xpf);
+      if constexpr (OFF0 > 0 && Iq == 0) ldv<4>(Rg0, 4 * g * 4, 16 * jq * 4, g0pf);
     };
     float y[9];
     Op3 hq;
@@ -1350,11 +1429,15 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
         for (int j2 = 0; j2 < MUL / 16; j2 += U) {
           sfor<U>([&](auto hh) {
             const int jj = j2 + hh;
-            float x[4 * D1], dx[4 * D1];
+            float x[4 * D1], dx[4 * D1], g0[4];
 #pragma unroll
             for (int i = 0; i < 4 * D1; ++i) {
               x[i] = xpf[i];
               dx[i] = 0.f;
+            }
+            if constexpr (OFF0 > 0 && I == 0) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) g0[i] = g0pf[i];
             }
             if (jj + 1 < MUL / 16) {
               load_group(I, jj + 1);
@@ -1368,17 +1451,26 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                 constexpr int D3 = 2 * p.l3 + 1;
                 constexpr int ODD = (NB0 + hh * NPI + path_rank<L>(pi)) & 1;
                 const int nb = NB0 + jj * NPI + path_rank<L>(pi);
+                const char* pimg = img + (DMA ? rb * LS_IMG : 0);   // this pair's image
                 if constexpr (!ODD) {   // pair start: stage it, fetch the next one
                   if constexpr (STAMPED) STAMP(5);
-                  commit();
-                  issue((nb >> 1) + 1 < NPAIR ? (nb >> 1) + 1 : 0);
+                  const int nextP = (nb >> 1) + 1 < NPAIR ? (nb >> 1) + 1 : 0;
+                  if constexpr (DMA) {
+                    // this wave's DMA of the pair has landed; after the barrier
+                    // every wave's has, and nobody reads the other image any more
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                    issue_dma(nextP, rb ^ 1);
+                  } else {
+                    commit();
+                    issue(nextP);
+                  }
                   if constexpr (STAMPED) STAMP(2);   // barriers + staging
                   if (act) {
                     __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
                     Op3 wq;
-                    lds_op3(wq, img, lane);
+                    lds_op3<LS_WPC>(wq, pimg, lane);
                     wv0 = w2_block_bwd<false>(hq, wq);
-                    lds_op3(wq, img + LS_BLK, lane);
+                    lds_op3<LS_WPC>(wq, pimg + LS_IBLK, lane);
                     wv1 = w2_block_bwd<false>(hq, wq);
                     __builtin_amdgcn_s_setprio(0);
                   }
@@ -1387,9 +1479,14 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                 if (act) {
                   const f32x4 wv = ODD ? wv1 : wv0;
                   float gm[4 * D3];
-                  const float* gl = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
+                  if constexpr (OFF0 > 0 && pi == 0) {   // (DMA mode: from L2, prefetched)
 #pragma unroll
-                  for (int k = 0; k < 4 * D3; ++k) gm[k] = gl[k];
+                    for (int k = 0; k < 4; ++k) gm[k] = g0[k];
+                  } else {
+                    const float* gl = dacc + p.moff + 16 * jj * D3 + 4 * g * D3;
+#pragma unroll
+                    for (int k = 0; k < 4 * D3; ++k) gm[k] = gl[k];
+                  }
                   float dwr[4];
                   // padded slots: y = 0, so dE/dx = dE/dw = 0 there
                   tp_bwd_xw4<p.l1, p.l2, p.l3>(x, y + yoff(p.l2), wv, gm, dx, dYa + yoff(p.l2), dwr);
@@ -1398,7 +1495,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                   if constexpr (ODD) {
                     if constexpr (STAMPED) STAMP(5);   // tensor product (+ stores)
                     __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
-                    dh2_pair(dh2, dwp, dwr, img + LS_PAIR_W, lane);
+                    dh2_pair(dh2, dwp, dwr, pimg + LS_IW, lane);
                     __builtin_amdgcn_s_setprio(0);
                     if constexpr (STAMPED) STAMP(4);   // dH2 (split + MFMA)
                   } else {
@@ -1406,6 +1503,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                     for (int r = 0; r < 4; ++r) dwp[r] = dwr[r];
                   }
                 }
+                if constexpr (DMA && ODD) rb ^= 1;   // the next pair reads the other image
               }
             });
             // per-edge dE/dx[nbr]; the first block's inputs are the species
@@ -1442,6 +1540,8 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
     if constexpr (STAMPED) STAMP(6);   // tile end: dE/dY sums, MLP chain backward
   }
   if constexpr (STAMPED) STAMP_FLUSH(blockIdx.x * WPG + wid);
+  // the last pair's DMA (pair 0 of a next tile) lands before the wave ends
+  if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 }  // namespace

@@ -275,7 +275,9 @@ __global__ void k_row_ptr(int64_t E, int n_centers, int n_nodes, int n_interior,
   }
   if (j < 0 || j >= n_nodes) atomicOr(err, 4);
   if (c < n_interior && j >= n_centers) atomicOr(err, 16);  // interior centre with a ghost neighbour
-  const int prev = e ? center[e - 1] : -1;
+  // an invalid (negative) predecessor is reported by its own thread; the
+  // fill never starts below row_ptr[0]
+  const int prev = e ? max(center[e - 1], -1) : -1;
   if (c < prev) {
     atomicOr(err, 1);
     return;
@@ -459,12 +461,15 @@ __global__ __launch_bounds__(1024) void k_build_graph_small(int E, int n, const 
   // that waited for each edge's loads took ~1 us per edge of the thread)
   constexpr int EPT = GRAPH_SMALL_E / 1024;
   int cv[EPT], pv[EPT], jv[EPT];
+  // validated in the input's own type before narrowing (an int64 index
+  // 2^32 + 3 must not pass as 3): out of range -> -1, reported below
+  auto idx = [n](T v) { return (v < (T)0 || v >= (T)n) ? -1 : (int)v; };
 #pragma unroll
   for (int u = 0; u < EPT; ++u) {
     const int e = t + 1024 * u;
-    cv[u] = e < E ? (int)cin[e] : 0;
-    pv[u] = (e < E && e > 0) ? (int)cin[e - 1] : -1;
-    jv[u] = e < E ? (int)jin[e] : 0;
+    cv[u] = e < E ? idx(cin[e]) : 0;
+    pv[u] = (e < E && e > 0) ? idx(cin[e - 1]) : -1;
+    jv[u] = e < E ? idx(jin[e]) : 0;
   }
   // validation, row_ptr (as k_row_ptr) and the per-neighbour counts
 #pragma unroll

@@ -170,6 +170,30 @@ def handshake(rg, group=None, device='cpu'):
     return rg
 
 
+def local_handshake(rgs):
+    """``handshake`` for ALL ranks' graphs held by one process (the rank
+    emulation of bench.py --rank-emulation, tests): every owner's send lists
+    from its peers' requests, without a process group."""
+    world = len(rgs)
+    for r, rg in enumerate(rgs):
+        counts, rows = np.zeros(world, dtype=np.int64), []
+        srt = np.argsort(rg.owned)
+        for p, q in enumerate(rgs):
+            if p == r or q.req_ids.size == 0:
+                rows.append(np.zeros(0, dtype=np.int64))
+                continue
+            lo = int(q.recv_counts[:r].sum())
+            ids = q.req_ids[lo:lo + int(q.recv_counts[r])]   # q's ghosts owned by r, by id
+            rr = srt[np.searchsorted(rg.owned, ids, sorter=srt)].astype(np.int64) if ids.size else \
+                np.zeros(0, dtype=np.int64)
+            if ids.size and not np.array_equal(rg.owned[rr], ids):
+                raise RuntimeError('local handshake: a peer asked for an atom this rank does not own')
+            counts[p] = ids.size
+            rows.append(rr)
+        rg.send_counts, rg.send_rows = counts, np.concatenate(rows)
+    return rgs
+
+
 # ------------------------------------------------------------------ halo
 class Halo:
     """Forward (owner rows -> ghost rows) and reverse (ghost rows -> owner rows,
@@ -253,6 +277,56 @@ class Halo:
 
     def reverse(self, kind, t):
         self.reverse_finish(self.reverse_start(kind, t))
+
+
+class LocalHalo(Halo):
+    """A rank's exchanges emulated inside one process (bench.py
+    --rank-emulation: one rank of a decomposition timed on one GPU): the
+    packs and unpacks of the real Halo run unchanged on the rank's own rows,
+    and each all_to_all is replaced by a device copy of the receive buffer's
+    size from the send buffer (rows the rank does not have are left as they
+    were).  The ghost VALUES are therefore not the peers': a timing rehearsal
+    of one rank's compute and halo kernels, not a physics result."""
+
+    staged = False
+
+    def __init__(self, rg, engine, group=None):
+        super().__init__(rg, engine, group)
+        self.staged = False
+
+    def _a2a_start(self, out, inp, out_splits, in_splits):
+        n = min(out.shape[0], inp.shape[0])
+        if n:
+            out[:n].copy_(inp[:n])
+        return [None, None, out]
+
+    def forward_start(self, kind, t):
+        # (world > 1 by construction: the emulated rank belongs to a grid)
+        dim = self.eng.dim(kind, t)
+        sbuf = self.eng.empty(sum(self.sc), dim)
+        rbuf = self.eng.empty(sum(self.rc), dim)
+        self.eng.pack(kind, t, self.send_rows, sbuf)
+        return (kind, t, rbuf, sbuf, self._a2a_start(rbuf, sbuf, self.rc, self.sc))
+
+    def reverse_start(self, kind, t):
+        dim = self.eng.dim(kind, t)
+        sbuf = self.eng.empty(sum(self.rc), dim)
+        rbuf = self.eng.empty(sum(self.sc), dim)
+        self.eng.pack(kind, t, self.recv_rows, sbuf)
+        return (kind, t, rbuf, sbuf, self._a2a_start(rbuf, sbuf, self.sc, self.rc))
+
+    def bytes_per_step(self, num_layers):
+        """(sent, received) bytes of one evaluation's exchanges: the forward
+        feature halos of layers 1..L-1, the reverse gradient halos of the same
+        layers and the ghost forces"""
+        s = r = 0
+        for t in range(1, num_layers):
+            d = self.eng.dim('x', t)
+            s += sum(self.sc) * d * 4 + sum(self.rc) * d * 4      # forward + reverse
+            r += sum(self.rc) * d * 4 + sum(self.sc) * d * 4
+        s += sum(self.rc) * 3 * 4
+        r += sum(self.sc) * 3 * 4
+        return s, r
 
 
 # ------------------------------------------------------------------ engines
@@ -358,13 +432,18 @@ class ParallelE3GNN:
         self.rg = None
         self.halo = None
 
-    def set_graph(self, rg):
+    def set_graph(self, rg, emulate=False):
         """New neighbour list: handshake, halo index lists and the one-time
-        upload of the rank graph; ``evaluate`` then moves no host data."""
-        if rg.send_rows is None:
+        upload of the rank graph; ``evaluate`` then moves no host data.
+        ``emulate``: one rank of a decomposition in a single process (send
+        lists from ``local_handshake``, exchanges as ``LocalHalo`` copies)."""
+        if emulate:
+            if rg.send_rows is None:
+                raise ValueError('rank emulation: run local_handshake over all ranks first')
+        elif rg.send_rows is None:
             handshake(rg, self.group, self._comm_device())
         self.rg = rg
-        self.halo = Halo(rg, self.eng, self.group)
+        self.halo = (LocalHalo if emulate else Halo)(rg, self.eng, self.group)
         self.eng.upload(rg)
 
     def _comm_device(self):

@@ -426,7 +426,6 @@ def collate(graphs, device=None, dtype=None):
         for k in (KEY.EDGE_VEC, KEY.CELL_SHIFT):
             if k in out:
                 out[k] = out[k][perm]
-    out[KEY.EDGE_SORTED] = torch.tensor(True)
     for k, v in pg.items():
         if v:
             t = torch.cat(v, 0)
@@ -437,7 +436,26 @@ def collate(graphs, device=None, dtype=None):
         out = {k: v.to(dtype) if v.is_floating_point() else v for k, v in out.items()}
     if device is not None:
         out = {k: v.to(device, non_blocking=True) for k, v in out.items()}
+    mark_edges_sorted(out)
     return out
+
+
+def mark_edges_sorted(b):
+    """Record that b's edge_index is CSR-sorted by centre: the flag (a host
+    tensor) names the edge_index storage and its version counter, so
+    replacing or editing the edges afterwards makes it stale by itself"""
+    ei = b[KEY.EDGE_IDX]
+    b[KEY.EDGE_SORTED] = torch.tensor([ei.data_ptr(), ei._version], dtype=torch.int64)
+
+
+def edges_marked_sorted(b):
+    """True only when b's EDGE_SORTED flag still describes its edge_index
+    (a stale flag -- edges reordered or modified after collate -- is ignored
+    and the callers sort as for an unflagged batch)"""
+    f, ei = b.get(KEY.EDGE_SORTED), b.get(KEY.EDGE_IDX)
+    if f is None or ei is None or not torch.is_tensor(f) or f.numel() != 2 or f.is_cuda:
+        return False
+    return int(f[0]) == ei.data_ptr() and int(f[1]) == ei._version
 
 
 # ------------------------------------------------------------------ trainer
@@ -603,6 +621,8 @@ class Trainer:
         st = torch.cuda.current_stream(self.device).cuda_stream
         E, F = output[KEY.PRED_TOTAL_ENERGY].detach(), output[KEY.PRED_FORCE].detach()
         S = output.get(KEY.PRED_STRESS) if P['stress'] else None
+        if P['stress'] and S is None:   # the autograd path's KeyError, not a silent zero term
+            raise KeyError(f'stress loss configured but the output has no {KEY.PRED_STRESS}')
         S = S.detach().contiguous() if S is not None else None
         nb, n = int(E.numel()), int(F.shape[0])
         ref = lambda k, like: batch[k].to(like.device, like.dtype).contiguous()   # noqa: E731
@@ -825,7 +845,7 @@ class GraphedRehearsalStep:
         are sorted on the host already (EDGE_SORTED); anything else gets a
         stable device argsort of the per-edge entries, no host sync."""
         ei = b.get(KEY.EDGE_IDX)
-        if ei is None or ei.shape[1] < 2 or KEY.EDGE_SORTED in b:   # (collate sorted it)
+        if ei is None or ei.shape[1] < 2 or edges_marked_sorted(b):   # (collate sorted it)
             return b
         perm = torch.argsort(ei[0], stable=True)
         out = dict(b)

@@ -134,6 +134,10 @@ class _Gemms:
         self.defer = None
         self.dws = []              # workspace chunks (one after the first step)
         self.dws_total = 0
+        # a captured HIP graph keeps the raw addresses of the workspaces it
+        # used: a buffer replaced by a larger one stays allocated for the
+        # lifetime of this object (and so of every graph that captured it)
+        self.retired = []
 
     def _hip(self, *ts):
         return self.lib is not None and all(t.is_cuda and t.dtype == torch.float32 for t in ts)
@@ -150,12 +154,31 @@ class _Gemms:
             return x.data_ptr(), (s1 if k > 1 else max(r, 1)), 1
         return None
 
+    # the library's GEMM reads each operand through one buffer descriptor with
+    # 32-bit byte offsets (csrc/tgemm.hip TG_RECORDS): larger operands take
+    # the torch path (e3gnn_gemm_grouped refuses them with E3GNN_ERR_ARG)
+    MAX_OPERAND_BYTES = 0x7fff0000
+
+    @classmethod
+    def _fits(cls, *ts):
+        for t in ts:
+            if t is None:
+                continue
+            if any(st < 0 for st in t.stride()):
+                return False
+            span = 1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride()) if n > 0)
+            if span * t.element_size() > cls.MAX_OPERAND_BYTES:
+                return False
+        return True
+
     def add(self, C, A, B, alpha=1.0, beta=0, A2=None, B2=None, kr=None, wgrad=False):
         """kr: (int32 device tensor, row-tile stride) of per-tile k ranges (the
         dense matrices' block sparsity, e3gnn_gemm_desc::krange) or None;
         wgrad: C is a weight gradient read only after finish_defer (its split-K
         reduction may be deferred)"""
-        if not self._hip(C, A, B, *(t for t in (A2, B2) if t is not None)):
+        if not self._hip(C, A, B, *(t for t in (A2, B2) if t is not None)) or \
+                not self._fits(A, B, A2, B2):
+            self.flush()   # (queued problems may produce this one's operands)
             # straight into C (no temporaries / copy kernels)
             torch.addmm(C, A, B, beta=1 if beta else 0, alpha=alpha, out=C)
             if A2 is not None:
@@ -190,6 +213,11 @@ class _Gemms:
         """one problem in the general layouts (e3gnn_gemm_layouts ``lay``); C, A,
         B, A2, B2 = (tensor, element offset) of the operand bases"""
         from . import _lib
+        L = [(A, lay.a, M, K), (B, lay.b, N, K)] + ([(A2, lay.a2, M, K2), (B2, lay.b2, N, K2)] if K2 else [])
+        if self.lib is None or not all(self._lay_fits(t[0], t[1], g, r, k) for t, g, r, k in L):
+            self.flush()
+            self._lay_torch(M, N, K, C, A, B, lay, A2, B2, K2, alpha, beta)
+            return
         d = _lib.GemmDesc()
         ptr = lambda t: t[0].data_ptr() + 4 * t[1]   # noqa: E731 (float32)
         d.a, d.b, d.c = ptr(A), ptr(B), ptr(C)
@@ -199,6 +227,44 @@ class _Gemms:
         d.alpha, d.beta = float(alpha), int(bool(beta))
         d.layout = ctypes.addressof(lay)
         self._push(d, (C[0], A[0], B[0], A2, B2, lay), C[0].device, None, wgrad)
+
+    @classmethod
+    def _lay_fits(cls, x, off, g, rows, K):
+        """largest byte offset of operand layout g (e3gnn_gemm_layout) over
+        rows x K elements from element `off` of x, within one descriptor"""
+        if rows <= 0 or K <= 0:
+            return True
+        if min(g.ld, g.kst, g.sst, g.rs) < 0 or max(g.ld, g.kst, g.sst) > 0x7fffffff:
+            return False
+        rep, ks = max(g.rep, 1), g.ks if g.ks > 0 else K
+        top = ((rows - 1) // rep * g.ld + min(rows - 1, rep - 1) * g.rs + min(K - 1, ks - 1) * g.kst
+               + (K - 1) // ks * g.sst)
+        return (top + 1) * x.element_size() <= cls.MAX_OPERAND_BYTES
+
+    @staticmethod
+    def _lay_view(x, off, g, rows, K):
+        """the (rows x K) operand of layout g as a torch view: element (i, k)
+        at (i / rep) ld + (i % rep) rs + (k % ks) kst + (k / ks) sst"""
+        rep, ks = max(g.rep, 1), g.ks if g.ks > 0 else K
+        assert rows % rep == 0 and K % ks == 0
+        v = x.as_strided((rows // rep, rep, K // ks, ks), (g.ld, g.rs, g.sst, g.kst), x.storage_offset() + off)
+        return v.reshape(rows, K)
+
+    def _lay_torch(self, M, N, K, C, A, B, lay, A2, B2, K2, alpha, beta):
+        """add_lay's problem with torch GEMMs (operands the library's 32-bit
+        descriptors cannot address, or no library): same sums, written into
+        C's layout"""
+        prod = self._lay_view(*A, lay.a, M, K) @ self._lay_view(*B, lay.b, N, K).t()
+        if K2:
+            prod = prod + self._lay_view(*A2, lay.a2, M, K2) @ self._lay_view(*B2, lay.b2, N, K2).t()
+        Ct, co = C
+        crep = max(lay.crep, 1)
+        cv = Ct.as_strided((M // crep, crep, N), (lay.ldc, lay.crs, lay.cns), Ct.storage_offset() + co)
+        prod = (alpha * prod).view(M // crep, crep, N)
+        if beta:
+            cv.add_(prod)
+        else:
+            cv.copy_(prod)
 
     def _push(self, d, keep, dev, info, wgrad=False):
         if len(self.q) == self.max_probs:
@@ -228,6 +294,8 @@ class _Gemms:
             self.q = []
             return
         if need > 0 and (self.ws is None or self.ws.numel() < need):
+            if self.ws is not None:
+                self.retired.append(self.ws)
             self.ws = torch.empty(max(need, 1 << 20), device=dev)
         ws = self.ws.data_ptr() if self.ws is not None else None
         _lib.check(self.lib.e3gnn_gemm_grouped(n, descs, ws, self.ws.numel() if self.ws is not None else 0,
@@ -251,6 +319,7 @@ class _Gemms:
         self.flush()
         if len(self.dws) > 1:     # last step needed several chunks: one of the total
             self.dws_total = sum(u for _, u in self.dws)
+            self.retired.extend(b for b, _ in self.dws)
             self.dws = []
         for c in self.dws:
             c[1] = 0
@@ -1075,7 +1144,8 @@ class ExplicitStep:
         center, nbr = ei[0], ei[1]
         perm = None
         if graph is None:
-            if (KEY.EDGE_SORTED not in data and center.numel() > 1
+            from .train import edges_marked_sorted
+            if (not edges_marked_sorted(data) and center.numel() > 1
                     and bool((center[1:] < center[:-1]).any())):
                 perm = torch.argsort(center, stable=True)
                 center, nbr = center[perm], nbr[perm]

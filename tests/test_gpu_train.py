@@ -313,6 +313,17 @@ def test_conv_graph_rejects_unsorted(hip_backend):
         g.rebuild(torch.tensor([0, 2, 1], device=DEV), torch.tensor([1, 1, 1], device=DEV))
     with pytest.raises(E3GNNError, match='out of'):
         g.rebuild(torch.tensor([0, 1, 2], device=DEV), torch.tensor([1, -1, 1], device=DEV))
+    # int64 indices are range-checked before narrowing: 2^32 + 1 is not 1
+    with pytest.raises(E3GNNError, match='out of'):
+        g.rebuild(torch.tensor([0, 1, 2], device=DEV), torch.tensor([1, (1 << 32) + 1, 1], device=DEV))
+    with pytest.raises(E3GNNError, match='edge_center out of'):
+        g.rebuild(torch.tensor([0, (1 << 32) + 1, 2], device=DEV), torch.tensor([1, 2, 1], device=DEV))
+    # a negative centre before a valid one: reported, and the row_ptr fill of
+    # the next edge stays inside the buffer (the graph still rebuilds after)
+    with pytest.raises(E3GNNError, match='edge_center out of'):
+        g.rebuild(torch.tensor([-7, 1, 2], device=DEV), torch.tensor([1, 2, 1], device=DEV))
+    g.rebuild(torch.tensor([0, 1, 2], device=DEV), torch.tensor([1, 2, 1], device=DEV))
+    assert g.aux['row_ptr'].cpu().tolist() == [0, 1, 2, 3, 3]
 
 
 @pytest.fixture(scope='module')
@@ -568,7 +579,9 @@ def test_graphed_rehearsal_step_equals_eager():
                            device=DEV)
     for k in (KEY.EDGE_IDX, KEY.EDGE_VEC):
         b2[k] = b2[k][:, perm] if k == KEY.EDGE_IDX else b2[k][perm]
-    del b2[KEY.EDGE_SORTED]   # (collate's promise no longer holds)
+    # collate's EDGE_SORTED flag is left in place: it names the old edge_index
+    # storage, so it is stale by itself and the steps sort the edges again
+    assert not train.edges_marked_sorted(b2)
     third = (coll([12], (2, 2, 1)), coll([13], (2, 2, 1)))
     theta0 = SevenNetTrainable(device=DEV).flat.detach().double().cpu()
     fe, le = run(False, batches, third)
@@ -625,6 +638,43 @@ def test_graphed_step_replays_of_equal_shapes_equal_eager():
     d = (me.flat - mg.flat).abs()
     assert float(d.max()) <= 2 * 1e-5 * 5
     assert float((d > 1e-6).float().mean()) < 1e-3
+
+
+def test_graphed_small_shape_replayed_after_workspace_growth():
+    """A graph captured on a small batch shape, then a larger shape whose
+    grouped-GEMM workspaces outgrow the first ones (the old buffers are
+    replaced), then the small graph replayed: its captured workspace
+    addresses must still be owned by the trainer, so the replays equal the
+    eager trainer's steps."""
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+
+    def make(graph):
+        m = SevenNetTrainable(device=DEV)
+        cfg = {'loss': 'mse', 'force_loss_weight': 1.0, 'stress_loss_weight': 0.01,
+               'is_train_stress': True, 'optimizer': 'adam', 'optim_param': {'lr': 1e-5},
+               'scheduler': 'exponentiallr', 'scheduler_param': {'gamma': 0.99}, 'device': DEV,
+               'hip_graph': graph}
+        tr = train.Trainer(m, cfg)
+        m.train(True)
+        return m, tr
+
+    def coll(seeds, cells):
+        return train.collate(_batch(seeds, cells), device=DEV, dtype=torch.float32)
+    small = (coll([1], (2, 2, 1)), coll([2], (2, 2, 1)))
+    large = (coll([3, 4, 5], (3, 3, 3)), coll([6, 7], (3, 3, 3)))
+    seq = [small, large, small, large, small]
+    me, te = make(False)
+    le = [[float(x) for x in te.rehearsal_step(*b)] for b in seq]
+    mg, tg = make(True)
+    gm = tg.explicit.gm
+    lg = [[float(x) for x in tg.rehearsal_step(*b)] for b in seq]
+    assert len(tg._graphed.cache) == 2
+    for i in range(len(seq)):
+        for a, c in zip(le[i], lg[i]):
+            assert abs(a - c) <= 1e-5 * abs(a) + 1e-12, (i, le[i], lg[i])
+    assert gm.lib is not None   # the library's grouped GEMM ran (its workspaces are what is tested)
+    d = (me.flat - mg.flat).abs()
+    assert float(d.max()) <= 2 * 1e-5 * len(seq)
 
 
 def test_graphed_ewc_step_interleaved_with_eager_trainer():

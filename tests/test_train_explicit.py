@@ -173,3 +173,35 @@ def test_block_sparsity_tables_cover_every_nonzero(model):
             for b in range(stride):
                 if nz[a * T:(a + 1) * T, b * T:(b + 1) * T].any():
                     assert tab[a, b, 1] > 0, (key, a, b)
+
+
+def test_gemm_layout_torch_fallback_matches_dense():
+    """_Gemms' torch form of a general-layout problem (used when an operand
+    is beyond the library's 32-bit buffer offsets): the linear weight
+    gradient's layout -- K summed over (m, node) segments of the irreps rows
+    -- equals the dense product, and a 2 GB+ layout is detected"""
+    from sevennet_finetuning_amd import _lib
+    from sevennet_finetuning_amd.train_explicit import _Gemms
+    g = torch.Generator().manual_seed(0)
+    rows, d, mi, mo = 7, 3, 4, 5
+    X = torch.randn(rows, 2 + mi * d, generator=g, dtype=torch.float64)
+    Y = torch.randn(rows, 1 + mo * d, generator=g, dtype=torch.float64)
+    G = torch.randn(mi * 10, generator=g, dtype=torch.float64)
+    lay = _lib.GemmLayouts()
+    lay.a.ld, lay.a.rep, lay.a.rs, lay.a.kst, lay.a.ks, lay.a.sst = d, 1, 0, X.stride(0), rows, 1
+    lay.b.ld, lay.b.rep, lay.b.rs, lay.b.kst, lay.b.ks, lay.b.sst = d, 1, 0, Y.stride(0), rows, 1
+    lay.ldc, lay.crep, lay.crs, lay.cns = 10, 1, 0, 2
+    gm = _Gemms.__new__(_Gemms)
+    G0 = G.clone()
+    gm._lay_torch(mi, mo, d * rows, (G, 0), (X, 2), (Y, 1), lay, None, None, 0, 0.5, 1)
+    Xs = X[:, 2:].reshape(rows, mi, d)
+    Ys = Y[:, 1:].reshape(rows, mo, d)
+    ref = 0.5 * torch.einsum('num,nvm->uv', Xs, Ys)
+    Gv = G0.view(mi, 10)[:, 0:2 * mo:2] + ref
+    assert torch.allclose(G.view(mi, 10)[:, 0:2 * mo:2], Gv)
+    assert torch.equal(G.view(mi, 10)[:, 1::2], G0.view(mi, 10)[:, 1::2])
+    assert _Gemms._lay_fits(X, 2, lay.a, mi, d * rows)
+    lay.a.sst = 1 << 29
+    assert not _Gemms._lay_fits(X, 2, lay.a, mi, d * rows)
+    big = torch.empty((1 << 30) + 4, device='meta').as_strided((1 << 20, 4), (1 << 10, 1))
+    assert not _Gemms._fits(big) and _Gemms._fits(torch.empty(64, 64))

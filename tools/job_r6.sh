@@ -1,0 +1,32 @@
+#!/bin/bash
+# round-6 GPU job: parity of the current tree, then same-box A/B benches
+set -u
+export PYTHONUNBUFFERED=1
+mkdir -p gpurun_out
+P=${JOB_PREFIX:-j}
+run() {  # run <name> <secs> <cmd...>: stop the job on a crash-like exit
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/${P}_$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 4 "gpurun_out/${P}_$name.log"
+  if [ $rc -gt 1 ]; then echo "ABORT after $name"; exit $rc; fi
+  return 0
+}
+summ() {
+  for f in gpurun_out/${P}_bench*.log; do
+    echo "$f"; tail -1 "$f" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['roofline']['ms_per_launch'], {k:v['ms'] for k,v in d['kernels'].items() if v['ms']>0.4})" || true
+  done
+}
+for s in "$@"; do
+  case $s in
+    parity) run parity 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread ;;
+    graphs) run graphs 600 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread -k "graph or rejects" ;;
+    tests) run tests 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    bench) run bench 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    benchfull) run benchfull 400 python bench.py ;;
+    bv_*) v=${s#bv_}; run bench_$v 300 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
+    pv_*) v=${s#pv_}; run parity_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread ;;
+    summ) summ ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
