@@ -76,6 +76,17 @@ def parse():
                     help='N > 1 rehearsal: every rank on cuda:0, gloo instead of RCCL')
     ap.add_argument('--profile-only', action='store_true',
                     help='warmup + steps only, no stats pass (for rocprofv3)')
+    ap.add_argument('--system', default='si', choices=['si', 'hfo2'],
+                    help='si: the displaced Si diamond box (BASELINE config 3); hfo2: the '
+                         "reference's example HfO2 snapshot (res.dat, 96 atoms, non-uniform "
+                         'degree) tiled --cells^3 times (default 10^3 = 96,000 atoms), N = 1')
+    ap.add_argument('--rank-emulation', default=None, metavar='R[,R...]',
+                    help='N = 1 only: build every rank graph of the --strong box (default 46^3 '
+                         'cells = 778,688 atoms) split over --emulate-world ranks, time the listed '
+                         'ranks one at a time on this GPU (ParallelE3GNN.evaluate with each '
+                         'all_to_all replaced by a same-size local copy: compute + halo kernels, '
+                         'no network) and the whole box on this GPU; prints one JSON line')
+    ap.add_argument('--emulate-world', type=int, default=8)
     ap.add_argument('--model-config', default=None, metavar='cCHlL',
                     help='instead of SevenNet-0: the SevenNet-0 preset with channel CH and L '
                          'blocks (e.g. c64l4), built by model_build (e3nn init, seed 0) and '
@@ -103,6 +114,69 @@ def make_box(cells, device, si=69):
         'nbr': torch.tensor(ei[1], dtype=torch.int32, device=device),
         'vec': torch.tensor(vec, dtype=torch.float32, device=device),
     }
+
+
+HFO2_RESDAT = os.path.join(ROOT, 'sevennet_finetuning_amd', 'assets', 'structures', 'hfo2_resdat.npz')
+
+
+def make_box_hfo2(k, device, symbols):
+    """The reference's HfO2 example snapshot (example_inputs/md_serial_example
+    res.dat: 96 atoms of a triclinic cell, 44.5 edges per atom at 5 A with a
+    spread) tiled k^3 times: a box whose per-atom degree is NOT uniform, so the
+    fused kernels' 16-edge tile padding and the lock-step backward's
+    max-of-four tile counts are exercised as on a real MD configuration."""
+    from sevennet_finetuning_amd.neighbor import neighbor_list
+    from sevennet_finetuning_amd.structures import tile
+    d = np.load(HFO2_RESDAT)
+    types1 = np.array([symbols.index(str(x)) for x in d['symbols']], dtype=np.int64)
+    pos, cell = tile(d['pos'], d['cell'], (k, k, k))
+    types = np.tile(types1, k ** 3)
+    t0 = time.perf_counter()
+    ei, sh = neighbor_list(pos, cell, 5.0)
+    host_nl_s = time.perf_counter() - t0
+    vec = pos[ei[1]] + sh @ cell - pos[ei[0]]
+    e1, s1 = neighbor_list(d['pos'], d['cell'], 5.0)
+    return {
+        'pos': pos, 'cell': cell, 'host_nl_ms': host_nl_s * 1e3, 'n': len(pos), 'E': ei.shape[1],
+        'types': torch.tensor(types, dtype=torch.int32, device=device),
+        'center': torch.tensor(ei[0], dtype=torch.int32, device=device),
+        'nbr': torch.tensor(ei[1], dtype=torch.int32, device=device),
+        'vec': torch.tensor(vec, dtype=torch.float32, device=device),
+        'k': k, 'cell1': (d['pos'], d['cell'], types1, e1, s1), 'center_np': ei[0],
+    }
+
+
+def degree_stats(center, n, wpg=4):
+    """Per-atom degree spread and what it costs the fused kernels: every
+    centre's edges run in 16-edge tiles (padding = tile slots / edges), and
+    the lock-step backward runs each workgroup of `wpg` consecutive centres
+    for the max of their tile counts (imbalance = workgroup tile slots /
+    the centres' own tiles)."""
+    deg = np.bincount(np.asarray(center), minlength=n)
+    tiles = (deg + 15) // 16
+    m = (n // wpg) * wpg
+    wg = tiles[:m].reshape(-1, wpg).max(axis=1).sum() * wpg + (tiles[m:].max() * (n - m) if n > m else 0)
+    return {'edges_per_atom_mean': round(float(deg.mean()), 3), 'min': int(deg.min()),
+            'max': int(deg.max()), 'std': round(float(deg.std()), 3),
+            'tile_padding': round(float(tiles.sum() * 16 / max(deg.sum(), 1)), 4),
+            'lockstep_imbalance': round(float(wg / max(tiles.sum(), 1)), 4)}
+
+
+def parity_check_tiled(model, box, device):
+    """E(k^3-tiled box) = k^3 E(cell) and per-image forces equal, on the box
+    the bench times (make_box_hfo2)."""
+    pos1, cell1, types1, ei, sh = box['cell1']
+    vec1 = pos1[ei[1]] + sh @ cell1 - pos1[ei[0]]
+    t = lambda a, dt=torch.int32: torch.as_tensor(a, dtype=dt, device=device)
+    one = model.energy_forces(t(types1), t(ei[0]), t(ei[1]), t(vec1, torch.float32))
+    e1, f1 = float(one['energy']), one['forces'].cpu().numpy()
+    big = model.energy_forces(box['types'], box['center'], box['nbr'], box['vec'])
+    k3 = box['k'] ** 3
+    de = abs(float(big['energy']) - k3 * e1) / abs(k3 * e1)
+    df = float(np.abs(big['forces'].cpu().numpy().reshape(k3, len(pos1), 3) - f1[None]).max())
+    return {'property': f'res.dat tiled {box["k"]}^3, {box["n"]} atoms: E = k^3 E_cell, '
+                        'per-image forces equal', 'energy_rel_err': de, 'max_force_err': df,
+            'ok': bool(de <= 2e-6 and df <= 1e-4)}
 
 
 def device_nl_timing(box, device, reps=5):
@@ -420,6 +494,79 @@ def model_config_deployment(spec):
     return d, f'SevenNet-0 preset with channel {ch}, {nl} blocks'
 
 
+def rank_emulation(args, model, device, si):
+    """One-GPU rehearsal of a decomposed --strong step (north_star config 4):
+    the per-rank compute a W-GPU run would do, measured rank by rank, next to
+    the whole box on this GPU.  Compute-bound ceiling of the strong-scaling
+    speedup = (whole box ms) / (slowest emulated rank ms); the real W-GPU step
+    adds whatever part of the exchanges the interior work does not hide (the
+    bytes per exchange are reported; no link rate is assumed here)."""
+    from sevennet_finetuning_amd.parallel import (HipSegmentEngine, ParallelE3GNN, brick_grid,
+                                                  build_rank_graph, local_handshake)
+    from sevennet_finetuning_amd.structures import si_diamond
+    world = args.emulate_world
+    cells = args.cells or 46
+    grid = tuple(brick_grid(world))
+    pos, cell = si_diamond((cells,) * 3, sigma=0.05)
+    n = len(pos)
+    t0 = time.perf_counter()
+    rgs = [build_rank_graph(pos, cell, np.full(n, si), 5.0, grid, r) for r in range(world)]
+    local_handshake(rgs)
+    log(f'rank graphs: {world} ranks {grid} of {n} atoms in {time.perf_counter() - t0:.1f} s')
+    counts = [{'rank': rg.rank, 'owned': rg.n_local, 'ghosts': rg.n_ghost, 'interior': rg.n_interior,
+               'edges': int(len(rg.center)), 'send_rows': int(rg.send_counts.sum()),
+               'recv_rows': int(rg.recv_counts.sum())} for rg in rgs]
+
+    def timed(fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / steps * 1e3
+
+    # the whole box on this GPU (the 1-GPU point of the strong-scaling curve)
+    box = make_box(cells, device, si)
+    whole_ms = timed(lambda: model.energy_forces(box['types'], box['center'], box['nbr'], box['vec']),
+                     max(1, min(args.steps, 3)), 1)
+    del box
+    log(f'whole box: {whole_ms:.2f} ms/step')
+    ranks = [int(r) for r in args.rank_emulation.split(',')]
+    per = []
+    for r in ranks:
+        rg = rgs[r]
+        drv = ParallelE3GNN(HipSegmentEngine(model))
+        drv.set_graph(rg, emulate=True)
+        ms = timed(drv.evaluate, args.steps, args.warmup)
+        tm = {}
+        drv.evaluate(timing=tm)   # every exchange (pack + local copy + unpack) serialised
+        sent, recv = drv.halo.bytes_per_step(model.num_layers)
+        per.append({**counts[r], 'ms': round(ms, 3),
+                    'exchange_kernels_ms': round(tm.get('exchange_s', 0.0) * 1e3, 3),
+                    'exchanges_per_step': tm.get('exchanges', 0),
+                    'halo_bytes_sent_per_step': sent, 'halo_bytes_received_per_step': recv,
+                    'largest_exchange_bytes': max(sum(drv.halo.sc), sum(drv.halo.rc)) *
+                    max(model.lib.e3gnn_feature_dim(model._ctx, t) for t in range(1, model.num_layers)) * 4})
+        log(f'rank {r}: {per[-1]}')
+    worst = max(p['ms'] for p in per)
+    return {
+        'metric': f'one-GPU rank emulation of the {n:,}-atom box split {"x".join(map(str, grid))} '
+                  f'over {world} GPUs: per-rank ms and the compute-bound strong-scaling ceiling',
+        'value': round(whole_ms / worst, 3), 'unit': 'x (whole-box ms / slowest emulated rank ms)',
+        'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup, 'higher_is_better': True,
+        'dtype': DTYPE, 'data': 'synthetic Si diamond box, default_rng(0) 0.05 A displacements',
+        'config': {'workload': f'SevenNet-0 energy+force+virial, {n:,}-atom periodic Si box '
+                               f'({cells}^3 cells), rank graphs of a {world}-rank brick decomposition',
+                   'total_atoms': n, 'grid': list(grid)},
+        'whole_box_ms': round(whole_ms, 3), 'emulated_ranks': per,
+        'all_ranks': counts,
+        'note': 'each all_to_all is a same-size device copy (no peer data, no link): ms = one rank\'s '
+                'compute + halo pack/unpack kernels; a W-GPU step adds the exchange time the interior '
+                'work does not hide'}
+
+
 def main():
     args = parse()
     rc = maybe_launch(args, sys.argv[1:])
@@ -450,13 +597,30 @@ def main():
     cells, grid, total = box_plan(args, world)
     scaling = 'strong' if args.strong else 'weak'
     parity = None
+    if args.rank_emulation is not None:
+        if world != 1:
+            raise SystemExit('--rank-emulation runs on one GPU (N = 1)')
+        print(json.dumps(rank_emulation(args, model, device, si)), flush=True)
+        return
+    degrees = None
+    if args.system == 'hfo2' and world != 1:
+        raise SystemExit('--system hfo2 runs on one GPU (N = 1)')
     if world == 1:
-        box = make_box(cells, device, si)
+        if args.system == 'hfo2':
+            cells = args.cells or 10
+            box = make_box_hfo2(cells, device, model.chemical_symbols)
+            degrees = degree_stats(box['center_np'], box['n'])
+            label = f'{label} on HfO2'
+        else:
+            box = make_box(cells, device, si)
         n, E = box['n'], box['E']
         n_rank, parallelism = n, 'single'
         log(f'box: {n} atoms, {E} edges; workspace after first step follows')
+        if degrees:
+            log(f'degrees: {degrees}')
         if not args.no_parity_check:
-            parity = parity_check_serial(model, cells, device, si)
+            parity = parity_check_tiled(model, box, device) if args.system == 'hfo2' else \
+                parity_check_serial(model, cells, device, si)
             log(f'parity check: {parity}')
 
         def step():
@@ -561,12 +725,17 @@ def main():
 
     if rank == 0:
         metric, workload = describe(n, world, cells, args.strong, grid, label)
+        if args.system == 'hfo2':
+            metric = f'atoms/sec energy+force, {label} lmax=2, {n:,}-atom box @1 GPU'
+            workload = (f'SevenNet-0 energy+force+virial, {n:,}-atom periodic HfO2 box (the reference '
+                        f"example's res.dat, 96 atoms, tiled {cells}^3), 1 GPU")
         line = {
             'metric': metric,
             'value': round(value, 2), 'unit': 'atoms/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
             'higher_is_better': True, 'scaling': scaling, 'vs_baseline': None, 'dtype': DTYPE,
-            'data': 'synthetic Si diamond box, default_rng(0) 0.05 A displacements; '
+            'data': ('synthetic Si diamond box, default_rng(0) 0.05 A displacements; '
+                     if args.system == 'si' else "reference example HfO2 snapshot (res.dat) tiled; ")
                     + ('SevenNet-0 weights (reference opt_params_sevenn.pt)' if model_dir is None else
                        f'{label}: e3nn initialisation (model_build, seed 0), fused-kernel family '
                        f'{model.family}'),
@@ -578,6 +747,7 @@ def main():
             'roofline': roofline,
             'cpu_baseline': cpu,
             'neighbor_list': nl,
+            'degrees': degrees,
             'distributed': distributed,
             'kernels': kernels,
         }

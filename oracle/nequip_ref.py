@@ -29,7 +29,12 @@ Reference modules (pipeline order, sevenn/model_build.py:186-445):
     IrrepsLinear si2, SelfConnectionOutro :106-109
     EquivariantGate         nn/equivariant_gate.py:13-61 (scalars: act_scalar by
                             parity; gates: act_gate)
-  readout linears           model_build.py:374-408
+  readout linears           model_build.py:374-395, or FCN_e3nn
+                            (readout_as_fcn, :396-408; nn/linear.py:94-129)
+  biases (use_bias_in_linear) e3nn o3.Linear(biases=True): + b on 0e outputs of
+                            the embedding, si1, si2 and readout linears
+                            (model_build.py:194, :386, :393;
+                            interaction_blocks.py:58, :80)
   (SpeciesWise)Rescale      nn/scale.py:12-73, AtomReduce nn/linear.py:53-90
   ForceStressOutput         nn/force_output.py:74-130
 
@@ -154,6 +159,25 @@ def e3nn_linear(x, irreps_in, irreps_out, w_flat):
     return torch.cat([o.reshape(n, -1) for o in outs], dim=1)
 
 
+def add_bias(y, irreps_out, b):
+    """e3nn o3.Linear(biases=True) (IrrepsLinear biases=use_bias_in_linear,
+    model_build.py:194, :237, :386, :393): + b on the channels of every 0e
+    output irrep, in output order"""
+    if b is None:
+        return y
+    b = torch.as_tensor(b, dtype=y.dtype).reshape(-1)
+    oo = offsets(irreps_out)
+    parts, k = [], 0
+    for j, (m, l, p) in enumerate(irreps_out):
+        blk = y[:, oo[j]:oo[j + 1]]
+        if (l, p) == (0, 1):
+            blk = blk + b[k:k + m]
+            k += m
+        parts.append(blk)
+    assert k == b.numel(), (k, b.numel())
+    return torch.cat(parts, dim=1)
+
+
 def fctp_scalar(x, irreps_in, onehot, irreps_out, w_flat):
     """FullyConnectedTensorProduct(x, nsp x 0e -> irreps_out)
     (self_connection.py:11-38): per (i_x, i_out) of equal irrep a
@@ -213,12 +237,35 @@ class NequIPRef:
     def t(self, name):
         return torch.as_tensor(self.p[name], dtype=self.dtype)
 
+    def lin(self, x, irreps_in, irreps_out, name):
+        """IrrepsLinear `name` (weight, + bias when the deployment has one)"""
+        y = e3nn_linear(x, irreps_in, irreps_out, self.p[f'{name}.linear.weight'])
+        return add_bias(y, irreps_out, self.p.get(f'{name}.linear.bias'))
+
     def act(self, name, x):
         if name == 'silu':
             return torch.nn.functional.silu(x) * self.silu_norm
         if name == 'tanh':
             return torch.tanh(x) * self.tanh_norm
         raise ValueError(name)
+
+    def readout_fcn(self, x):
+        """FCN_e3nn readout (nn/linear.py:94-129): e3nn FullyConnectedNet
+        [dim] + hidden + [1], h <- c act(h W_k / sqrt(fan_in)) between layers
+        (c = normalize2mom(act), the manifest's act_norm), no activation last"""
+        ro = self.man['readout']
+        f = {'relu': torch.relu, 'silu': torch.nn.functional.silu, 'tanh': torch.tanh,
+             'sigmoid': torch.sigmoid, 'abs': torch.abs,
+             'elu': torch.nn.functional.elu}[ro['act']]
+        c = float(ro['act_norm'])
+        h = x
+        nh = len(ro['hidden'])
+        for k in range(nh + 1):
+            w = self.t(f'readout_FCN.fcn.layer{k}.weight')
+            h = h @ (w / math.sqrt(w.shape[0]))
+            if k < nh:
+                h = f(h) * c
+        return h
 
     def edge_embedding(self, r):
         rc = self.cutoff
@@ -299,6 +346,7 @@ class NequIPRef:
         onehot = torch.nn.functional.one_hot(types, self.nsp).to(dt)
         x = (onehot @ self.t('onehot_to_feature_x.linear.weight').reshape(self.nsp, -1)) \
             / math.sqrt(self.nsp)
+        x = add_bias(x, self.irreps[0], self.p.get('onehot_to_feature_x.linear.bias'))
         for t in range(self.nlayer):
             irr_x, irr_out = self.irreps[t], self.irreps[t + 1]
             gin = gate_irreps(irr_out)[0]
@@ -307,17 +355,18 @@ class NequIPRef:
                                  self.p[f'{t}_self_connection_intro.fc_tensor_product.weight'])
             else:
                 sc = e3nn_linear(x, irr_x, gin, self.p[f'{t}_self_connection_intro.linear.weight'])
-            h = e3nn_linear(x, irr_x, irr_x, self.p[f'{t}_self_interaction_1.linear.weight'])
+            h = self.lin(x, irr_x, irr_x, f'{t}_self_interaction_1')
             # edge_index[1] is the gathered source, [0] the target (convolution.py:111-113)
             # the convolution's output irreps (model_build.py:303-315); without
             # the key (sevenn < 0.9 deployments) the block's irreps_manual
             agg, mid = self.convolution(t, h, emb, sh, dst, src, irr_x, self.conv_out[t])
-            y = e3nn_linear(agg, mid, gin, self.p[f'{t}_self_interaction_2.linear.weight']) + sc
+            y = self.lin(agg, mid, gin, f'{t}_self_interaction_2') + sc
             x = self.gate(y, irr_out)
-        hid = e3nn_linear(x, self.irreps[-1], [(self.hidden, 0, 1)],
-                          self.p['reduce_input_to_hidden.linear.weight'])
-        e_s = e3nn_linear(hid, [(self.hidden, 0, 1)], [(1, 0, 1)],
-                          self.p['reduce_hidden_to_energy.linear.weight'])
+        if self.man.get('readout', {}).get('type', 'linear') == 'fcn':
+            e_s = self.readout_fcn(x)
+        else:
+            hid = self.lin(x, self.irreps[-1], [(self.hidden, 0, 1)], 'reduce_input_to_hidden')
+            e_s = self.lin(hid, [(self.hidden, 0, 1)], [(1, 0, 1)], 'reduce_hidden_to_energy')
         atomic = e_s[:, 0] * self.t('rescale_atomic_energy.scale')[types] + \
             self.t('rescale_atomic_energy.shift')[types]
         return {'energy': atomic.sum(), 'atomic_energy': atomic, 'strain': strain}

@@ -657,6 +657,10 @@ int fused_family(const minijson::Value& man) {
   if (lmax != 2) return -1;
   if (man.has("self_connection_type") && man["self_connection_type"].str() != "linear") return -1;
   if (!man.has("cutoff_function") || man["cutoff_function"]["name"].str() != "XPLOR") return -1;
+  // linear biases / the FCN readout (model_build.py:194-240, :396-408): the
+  // generic engine applies them
+  if (man.has("use_bias_in_linear") && man["use_bias_in_linear"].boolean()) return -1;
+  if (man.has("readout") && man["readout"].has("type") && man["readout"]["type"].str() != "linear") return -1;
   const int L = (int)man["num_convolution_layer"].num();
   if (L < 2) return -1;
   if (man.has("weight_nn_hidden_neurons")) {

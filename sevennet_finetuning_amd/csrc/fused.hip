@@ -936,26 +936,55 @@ __device__ __forceinline__ void dh2_pair_g(f32x4 (&dh2)[4], const float (&da)[4]
 #ifndef E3GNN_NBR_DH2_BF16
 #define E3GNN_NBR_DH2_BF16 E3GNN_DH2_X3
 #endif
+// Nodes per wave (E3GNN_NBR_NPW; 1: one node per wave).  With more, a wave
+// walks NPW nodes of its workgroup's block (node base + 4 k + wave) and hides
+// the per-node dependent chain src_ptr -> src_perm -> centre / SH / basis of
+// the NEXT node behind the current one: the next node's edge ids are fetched
+// when the current node starts, its centre rows, SH and basis values when the
+// current node's tensor-product loop is done (its MLP-chain backward runs
+// while they land).
+#ifndef E3GNN_NBR_NPW
+#define E3GNN_NBR_NPW 1
+#endif
 template <class L>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_bwd_nbr(
     const int* __restrict__ src_ptr, const int* __restrict__ src_perm, const int* __restrict__ center,
     const float* __restrict__ emb, const float* __restrict__ Y, const float* __restrict__ h,
     const float* __restrict__ gagg, MlpW W, float* __restrict__ dh, float* __restrict__ dgu, int n_centers,
     int r_begin, int r_end, float* __restrict__ demb) {
+  constexpr int NPW = E3GNN_NBR_NPW;
   __shared__ __attribute__((aligned(16))) float lds[4][L::DX];
   const int wid = threadIdx.x >> 6;
-  const int jn = __builtin_amdgcn_readfirstlane(r_begin + xcd_block() * 4 + wid);
-  if (jn >= r_end) return;
+  const int base = r_begin + xcd_block() * 4 * NPW;
   float* dacc = lds[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
-  const int qb = src_ptr[jn], qe = src_ptr[jn + 1];
   const WRes R = make_wres(W, L::W);
-  const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
   const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
+  // the next node's first-pass edge data (NPW > 1)
+  int nx_er[2] = {-1, -1}, nx_vg[2] = {0, 0};
+  float nx_y[2][9], nx_b[2][2];
+  bool have_nx = false;
+  for (int kn = 0; kn < NPW; ++kn) {
+  const int jn = __builtin_amdgcn_readfirstlane(base + 4 * kn + wid);
+  if (jn >= r_end) break;
+  const int qb = src_ptr[jn], qe = src_ptr[jn + 1];
+  const int jn2 = base + 4 * (kn + 1) + wid;
+  const bool next = NPW > 1 && kn + 1 < NPW && jn2 < r_end;   // wave-uniform
+  int er2[2] = {-1, -1};
+  if (next) {
+    const int qb2 = src_ptr[jn2], qe2 = src_ptr[jn2 + 1];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = qb2 + 16 * u + col;
+      er2[u] = q < qe2 ? src_perm[q] : -1;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
   for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
 
   for (int q0 = qb; q0 < qe; q0 += 32) {
     const bool two = q0 + 16 < qe;   // wave-uniform
+    const bool pre = have_nx && q0 == qb;   // wave-uniform: this pass's edge data is prefetched
     phase();
     Op3 wq;
     load_w2b(wq, R.w2b, lane, L::P[0].woff);
@@ -965,14 +994,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int q = q0 + 16 * u + col;
-      er[u] = q < qe ? src_perm[q] : -1;   // edge of slot c
-      vg[u] = (er[u] >= 0 ? center[er[u]] * L::DM : n_centers * L::DM) * 4;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) y[u][k] = er[u] >= 0 ? Y[(int64_t)er[u] * 9 + k] : 0.f;
-      if (u == 1 && !two) continue;
       float b[2];
+      if (pre) {
+        er[u] = nx_er[u];
+        vg[u] = nx_vg[u];
 #pragma unroll
-      for (int k = 0; k < 2; ++k) b[k] = er[u] >= 0 ? emb[(int64_t)er[u] * 8 + 4 * k + g] : 0.f;
+        for (int k = 0; k < 9; ++k) y[u][k] = nx_y[u][k];
+        b[0] = nx_b[u][0];
+        b[1] = nx_b[u][1];
+      } else {
+        er[u] = q < qe ? src_perm[q] : -1;   // edge of slot c
+        vg[u] = (er[u] >= 0 ? center[er[u]] * L::DM : n_centers * L::DM) * 4;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) y[u][k] = er[u] >= 0 ? Y[(int64_t)er[u] * 9 + k] : 0.f;
+        if (u == 1 && !two) continue;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) b[k] = er[u] >= 0 ? emb[(int64_t)er[u] * 8 + 4 * k + g] : 0.f;
+      }
+      if (u == 1 && !two) continue;
       MlpT m;
       mlp_chain(R, b, lane, m);
       f32x4 h2[4];
@@ -1086,6 +1125,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
     });
 
+    if (next && q0 + 32 >= qe) {
+      // the node's last pass: the next node's centre rows, SH and basis
+      // values go out now (its edge ids came at this node's start) and land
+      // under the MLP-chain backward below
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        nx_er[u] = er2[u];
+        nx_vg[u] = (er2[u] >= 0 ? center[er2[u]] * L::DM : n_centers * L::DM) * 4;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) nx_y[u][k] = er2[u] >= 0 ? Y[(int64_t)er2[u] * 9 + k] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) nx_b[u][k] = er2[u] >= 0 ? emb[(int64_t)er2[u] * 8 + 4 * k + g] : 0.f;
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (u == 1 && !two) break;
@@ -1115,6 +1168,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __builtin_amdgcn_s_waitcnt(0);
   float* dhj = dh + (int64_t)jn * L::DX;
   for (int t = lane; t < L::DX; t += 64) dhj[t] = dacc[t];
+  have_nx = next;
+  }
 }
 
 // ================================================================ lock-step kernels
@@ -1567,7 +1622,8 @@ static hipError_t fwd_impl(const FusedArgs& a, hipStream_t s) {
 template <class L>
 static hipError_t bwd_nbr_impl(const FusedArgs& a, hipStream_t s) {
   const int nn = a.node_end - a.node_begin;
-  hipLaunchKernelGGL(k_conv_bwd_nbr<L>, dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr, a.src_perm,
+  hipLaunchKernelGGL(k_conv_bwd_nbr<L>, dim3((nn + 4 * E3GNN_NBR_NPW - 1) / (4 * E3GNN_NBR_NPW)), dim3(256), 0, s,
+                     a.src_ptr, a.src_perm,
                      a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu, a.n_centers, a.node_begin,
                      a.node_end, a.demb);
   return hipGetLastError();

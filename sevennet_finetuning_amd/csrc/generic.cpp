@@ -115,6 +115,22 @@ struct GLin {
   int din = 0, dout = 0;
   DBuf W, WT;
 };
+// e3nn o3.Linear(biases=True) (use_bias_in_linear): the bias over the full
+// output row -- b on the channels of every 0e output irrep, in output order,
+// zero elsewhere
+std::vector<float> bias_row(const GIrreps& out, const float* b, size_t numel) {
+  const auto oo = goffsets(out);
+  std::vector<float> v(oo.back(), 0.f);
+  size_t k = 0;
+  for (size_t j = 0; j < out.size(); ++j)
+    if (out[j].l == 0 && out[j].p == 1)
+      for (int u = 0; u < out[j].mul; ++u) {
+        if (k >= numel) throw std::runtime_error("linear bias size mismatch");
+        v[oo[j] + u] = b[k++];
+      }
+  if (k != numel) throw std::runtime_error("linear bias size mismatch");
+  return v;
+}
 void make_lin(GLin& L, const std::vector<float>& W, int din, int dout) {
   L.din = din;
   L.dout = dout;
@@ -168,6 +184,7 @@ struct GenLayer {
   e3gnn_gtp* gtp = nullptr;
   DBuf gate_cols;
   GenGateArgs gate{};
+  DBuf b1, b2;                 // si1 / si2 biases (full rows; empty without biases)
 };
 
 struct GenModel {
@@ -177,6 +194,14 @@ struct GenModel {
   DBuf coeffs, embed, readout_v, scale, shift;
   std::vector<int> dims;  // x[t] dims, t = 0..L
   std::vector<GenLayer> L;
+  // readout_as_fcn (FCN_e3nn): widths dims[L], hidden..., 1; layer k's
+  // weight / sqrt(fan_in); activation kind / normalize2mom constant
+  bool fcn = false;
+  std::vector<int> fcn_w;
+  std::vector<GLin> fcn_l;
+  int fcn_kind = 0;
+  float fcn_c = 1.f;
+  DBuf one;
   ~GenModel() {
     for (auto& l : L)
       if (l.gtp) e3gnn_gtp_free(l.gtp);
@@ -187,6 +212,8 @@ struct GenCtx {
   int64_t n = 0, nl = 0, E = 0;
   std::vector<DBuf> x, grad, h, y, w;
   std::vector<std::vector<DBuf>> pre, act;  // radial MLP hidden layers per block
+  std::vector<DBuf> fz, fa;                   // readout FCN pre-activations / activations
+  DBuf fes, fgs, fg0, fg1;                    // its output, dE/d(output), backward rows
   DBuf Y, emb, agg, dagg, dy, dh, dxc, dw, dYt, dA0, dA1, dYacc, demb, fe, vpart, eat, part, scratch;
 };
 
@@ -265,6 +292,13 @@ GenModel* gen_load(const minijson::Value& man, const std::vector<float>& flat) {
     if (we.second != (size_t)m->nsp * m->d0) throw std::runtime_error("bad size onehot_to_feature_x");
     std::vector<float> e(we.second);
     for (size_t i = 0; i < e.size(); ++i) e[i] = (float)(we.first[i] / std::sqrt((double)m->nsp));
+    // the embedding's bias (use_bias_in_linear): the same for every species row
+    if (T.count("onehot_to_feature_x.linear.bias")) {
+      auto b = get("onehot_to_feature_x.linear.bias");
+      const auto row = bias_row(irr[0], b.first, b.second);
+      for (int sp = 0; sp < m->nsp; ++sp)
+        for (int c = 0; c < m->d0; ++c) e[(size_t)sp * m->d0 + c] += row[c];
+    }
     if (upload(m->embed, e) != hipSuccess) throw std::runtime_error("upload");
   }
   std::vector<int> hidden;
@@ -382,6 +416,14 @@ GenModel* gen_load(const minijson::Value& man, const std::vector<float>& flat) {
       make_lin(G.si1, dense_linear(xi, xi, w.first, w.second, 1.0), G.dx, G.dx);
       w = get(p + "_self_interaction_2.linear.weight");
       make_lin(G.si2, dense_linear(mid, gin, w.first, w.second, 1.0 / den), G.dm, G.dg);
+      if (T.count(p + "_self_interaction_1.linear.bias")) {
+        auto b = get(p + "_self_interaction_1.linear.bias");
+        if (upload(G.b1, bias_row(xi, b.first, b.second)) != hipSuccess) throw std::runtime_error("upload");
+      }
+      if (T.count(p + "_self_interaction_2.linear.bias")) {
+        auto b = get(p + "_self_interaction_2.linear.bias");
+        if (upload(G.b2, bias_row(gin, b.first, b.second)) != hipSuccess) throw std::runtime_error("upload");
+      }
     }
     if (sc_type == "linear") {
       auto w = get(p + "_self_connection_intro.linear.weight");
@@ -437,29 +479,69 @@ GenModel* gen_load(const minijson::Value& man, const std::vector<float>& flat) {
       make_lin(G.mlp[k], v, a, b);
     }
   }
-  // ---- readout: two linears without activation = one vector; rescale
+  // ---- readout: two linears without activation = one vector (their biases
+  // a constant, folded into the shift); or the FCN readout; rescale
   {
-    const int hid = man.has("readout_hidden") ? (int)man["readout_hidden"].num() : irr[L][0].mul / 2;
-    GIrreps hir{{hid, 0, 1}}, one{{1, 0, 1}};
-    auto w1 = get("reduce_input_to_hidden.linear.weight");
-    auto w2 = get("reduce_hidden_to_energy.linear.weight");
-    const auto A = dense_linear(irr[L], hir, w1.first, w1.second, 1.0);
-    const auto B = dense_linear(hir, one, w2.first, w2.second, 1.0);
-    const int dl = m->dims[L];
-    std::vector<float> v(dl, 0.f);
-    for (int c = 0; c < dl; ++c) {
-      double s = 0;
-      for (int k = 0; k < hid; ++k) s += (double)A[(size_t)c * hid + k] * B[k];
-      v[c] = (float)s;
-    }
-    if (upload(m->readout_v, v) != hipSuccess) throw std::runtime_error("upload");
     auto sc = get("rescale_atomic_energy.scale");
     auto sh = get("rescale_atomic_energy.shift");
     if (sc.second != sh.second || (sc.second != 1 && sc.second != (size_t)m->nsp))
       throw std::runtime_error("rescale_atomic_energy: one value or one per species");
     m->per_species = sc.second == 1 ? 0 : 1;
+    std::vector<float> shift(sh.first, sh.first + sh.second);
+    const int dl = m->dims[L];
+    const bool fcn = man.has("readout") && man["readout"].has("type") && man["readout"]["type"].str() == "fcn";
+    if (fcn) {
+      // FCN_e3nn (nn/linear.py:94-129, model_build.py:396-408)
+      for (auto& i : irr[L])
+        if (i.l != 0) throw std::runtime_error("readout_as_fcn needs a scalar-only last block");
+      const auto& ro = man["readout"];
+      static const char* kinds[] = {"relu", "silu", "tanh", "sigmoid", "abs", "elu"};
+      m->fcn_kind = -1;
+      for (int k = 0; k < 6; ++k)
+        if (ro["act"].str() == kinds[k]) m->fcn_kind = k;
+      if (m->fcn_kind < 0) throw std::runtime_error("readout activation " + ro["act"].str() + " is not built");
+      m->fcn_c = (float)ro["act_norm"].num();
+      m->fcn_w = {dl};
+      for (auto& h : ro["hidden"].arr()) m->fcn_w.push_back((int)h.num());
+      m->fcn_w.push_back(1);
+      m->fcn_l.resize(m->fcn_w.size() - 1);
+      for (size_t k = 0; k + 1 < m->fcn_w.size(); ++k) {
+        auto w = get("readout_FCN.fcn.layer" + std::to_string(k) + ".weight");
+        const int a = m->fcn_w[k], b = m->fcn_w[k + 1];
+        if (w.second != (size_t)a * b) throw std::runtime_error("readout FCN layer size");
+        std::vector<float> v(w.second);
+        for (size_t i = 0; i < v.size(); ++i) v[i] = (float)(w.first[i] / std::sqrt((double)a));
+        make_lin(m->fcn_l[k], v, a, b);
+      }
+      m->fcn = true;
+      if (upload(m->one, std::vector<float>(1, 1.f)) != hipSuccess) throw std::runtime_error("upload");
+    } else {
+      const int hid = man.has("readout_hidden") ? (int)man["readout_hidden"].num() : irr[L][0].mul / 2;
+      GIrreps hir{{hid, 0, 1}}, one{{1, 0, 1}};
+      auto w1 = get("reduce_input_to_hidden.linear.weight");
+      auto w2 = get("reduce_hidden_to_energy.linear.weight");
+      const auto A = dense_linear(irr[L], hir, w1.first, w1.second, 1.0);
+      const auto B = dense_linear(hir, one, w2.first, w2.second, 1.0);
+      std::vector<float> v(dl, 0.f);
+      for (int c = 0; c < dl; ++c) {
+        double s = 0;
+        for (int k = 0; k < hid; ++k) s += (double)A[(size_t)c * hid + k] * B[k];
+        v[c] = (float)s;
+      }
+      if (upload(m->readout_v, v) != hipSuccess) throw std::runtime_error("upload");
+      // biases: e = (x A + bA) B + bB = x v + (bA . B + bB), per atom before
+      // the rescale: shift += (bA . B + bB) scale
+      double cst = 0;
+      if (T.count("reduce_input_to_hidden.linear.bias")) {
+        auto b = get("reduce_input_to_hidden.linear.bias");
+        const auto row = bias_row(hir, b.first, b.second);
+        for (int k = 0; k < hid; ++k) cst += (double)row[k] * B[k];
+      }
+      if (T.count("reduce_hidden_to_energy.linear.bias")) cst += *get("reduce_hidden_to_energy.linear.bias").first;
+      for (size_t i = 0; i < shift.size(); ++i) shift[i] = (float)(shift[i] + cst * sc.first[i]);
+    }
     if (upload(m->scale, std::vector<float>(sc.first, sc.first + sc.second)) != hipSuccess ||
-        upload(m->shift, std::vector<float>(sh.first, sh.first + sh.second)) != hipSuccess)
+        upload(m->shift, shift) != hipSuccess)
       throw std::runtime_error("upload");
   }
   (void)hipGetLastError();
@@ -485,6 +567,10 @@ GenCtx* gen_ctx_create(const GenModel* m) {
   for (int t = 0; t < L; ++t) {
     c->pre[t].resize(m->L[t].width.size() - 2);
     c->act[t].resize(m->L[t].width.size() - 2);
+  }
+  if (m->fcn) {
+    c->fz.resize(m->fcn_w.size() - 2);
+    c->fa.resize(m->fcn_w.size() - 2);
   }
   return c;
 }
@@ -538,6 +624,18 @@ hipError_t gen_graph_set(GenCtx* c, const GenModel* m, const GenGraph& g, hipStr
   GCHK(c->eat.ensure(nl1 * F));
   GCHK(c->part.ensure(((int64_t)sum_blocks(nl) + 1) * F));
   GCHK(c->scratch.ensure(8 * F));
+  if (m->fcn) {
+    int wmax = 1;
+    for (size_t k = 0; k + 2 < m->fcn_w.size(); ++k) {
+      GCHK(c->fz[k].ensure(nl1 * m->fcn_w[k + 1] * F));
+      GCHK(c->fa[k].ensure(nl1 * m->fcn_w[k + 1] * F));
+    }
+    for (int w : m->fcn_w) wmax = std::max(wmax, w);
+    GCHK(c->fes.ensure(nl1 * F));
+    GCHK(c->fgs.ensure(nl1 * F));
+    GCHK(c->fg0.ensure(nl1 * wmax * F));
+    GCHK(c->fg1.ensure(nl1 * wmax * F));
+  }
   GCHK(launch_gen_embed((int)n, m->d0, g.type, m->nsp, m->embed.f(), c->x[0].f(), g.err, s));
   if (E > 0) GCHK(launch_gen_edge_embed(m->edge, E, g.vec, c->Y.f(), c->emb.f(), s));
   return hipSuccess;
@@ -548,6 +646,7 @@ hipError_t gen_layer_forward(GenCtx* c, const GenModel* m, const GenGraph& g, in
   const int64_t n = c->n, nl = c->nl, E = c->E;
   // self_interaction_1 on every row (ghost rows are gathered as neighbours)
   GCHK(gemm(c->x[t].f(), G.dx, G.si1.W.f(), G.dx, c->h[t].f(), G.dx, n, G.dx, G.dx, 0, nullptr, nullptr, 0, s));
+  if (G.b1.p) GCHK(launch_gen_bias(n, G.dx, G.b1.f(), c->h[t].f(), s));
   // radial MLP: hidden layers keep their pre-activations (the backward's act')
   const float* a = c->emb.f();
   int wa = m->nb;
@@ -565,6 +664,7 @@ hipError_t gen_layer_forward(GenCtx* c, const GenModel* m, const GenGraph& g, in
                         c->agg.f(), s));
   // self_interaction_2 (/ denominator, folded) + self-connection, gate
   GCHK(gemm(c->agg.f(), G.dm, G.si2.W.f(), G.dg, c->y[t].f(), G.dg, nl, G.dm, G.dg, 0, nullptr, nullptr, 0, s));
+  if (G.b2.p) GCHK(launch_gen_bias(nl, G.dg, G.b2.f(), c->y[t].f(), s));
   if (G.sc_species)
     GCHK(launch_gen_species_linear((int)nl, G.dx, G.dg, g.type, c->x[t].f(), G.scs.f(), c->y[t].f(), 1, s));
   else
@@ -577,8 +677,37 @@ hipError_t gen_readout(GenCtx* c, const GenModel* m, const GenGraph& g, float* e
                        hipStream_t s) {
   const int L = m->nlayer;
   const int64_t nl = c->nl;
-  GCHK(launch_gen_readout((int)nl, m->dims[L], c->x[L].f(), m->readout_v.f(), g.type, m->scale.f(),
-                          m->shift.f(), m->per_species, c->eat.f(), c->grad[L].f(), s));
+  if (m->fcn) {
+    // FCN_e3nn forward over the owned rows, the rescale, and its backward down
+    // to dE/dx[L] (the readout is the only consumer of x[L])
+    const int nh = (int)m->fcn_w.size() - 2;
+    const float* a = c->x[L].f();
+    int wa = m->fcn_w[0];
+    for (int k = 0; k < nh; ++k) {
+      const int wb = m->fcn_w[k + 1];
+      GCHK(gemm(a, wa, m->fcn_l[k].W.f(), wb, c->fz[k].f(), wb, nl, wa, wb, 0, nullptr, nullptr, 0, s));
+      GCHK(launch_gen_fcn_act(nl * wb, m->fcn_kind, m->fcn_c, 0, c->fz[k].f(), nullptr, c->fa[k].f(), s));
+      a = c->fa[k].f();
+      wa = wb;
+    }
+    GCHK(gemm(a, wa, m->fcn_l[nh].W.f(), 1, c->fes.f(), 1, nl, wa, 1, 0, nullptr, nullptr, 0, s));
+    GCHK(launch_gen_readout((int)nl, 1, c->fes.f(), m->one.f(), g.type, m->scale.f(), m->shift.f(),
+                            m->per_species, c->eat.f(), c->fgs.f(), s));
+    // dE/da_nh = g W_nh^T (K = 1); then dz = da c f'(z), da_k = dz W_k^T
+    float* bufs[2] = {c->fg0.f(), c->fg1.f()};
+    float* cur = nh == 0 ? c->grad[L].f() : bufs[0];
+    GCHK(gemm(c->fgs.f(), 1, m->fcn_l[nh].WT.f(), wa, cur, wa, nl, 1, wa, 0, nullptr, nullptr, 0, s));
+    for (int k = nh - 1; k >= 0; --k) {
+      const int wb = m->fcn_w[k + 1], wk = m->fcn_w[k];
+      GCHK(launch_gen_fcn_act(nl * wb, m->fcn_kind, m->fcn_c, 1, c->fz[k].f(), cur, cur, s));
+      float* out = k == 0 ? c->grad[L].f() : bufs[(nh - k) & 1];
+      GCHK(gemm(cur, wb, m->fcn_l[k].WT.f(), wk, out, wk, nl, wb, wk, 0, nullptr, nullptr, 0, s));
+      cur = out;
+    }
+  } else {
+    GCHK(launch_gen_readout((int)nl, m->dims[L], c->x[L].f(), m->readout_v.f(), g.type, m->scale.f(),
+                            m->shift.f(), m->per_species, c->eat.f(), c->grad[L].f(), s));
+  }
   GCHK(launch_sum(nl, c->eat.f(), c->part.f(), energy ? energy : c->scratch.f(), s));
   if (atomic_energy && nl > 0)
     GCHK(hipMemcpyAsync(atomic_energy, c->eat.p, nl * 4, hipMemcpyDeviceToDevice, s));

@@ -50,6 +50,9 @@ hipError_t launch_gen_readout(int n, int d, const float* x, const float* v, cons
                               const float* scale, const float* shift, int per_species, float* eat,
                               float* dx, hipStream_t s);
 hipError_t launch_gen_add(int64_t n, const float* a, float* acc, hipStream_t s);
+hipError_t launch_gen_bias(int64_t n, int d, const float* b, float* y, hipStream_t s);
+hipError_t launch_gen_fcn_act(int64_t n, int kind, float c, int mode, const float* z, const float* gin,
+                              float* out, hipStream_t s);
 
 // ---------------------------------------------------------------- host engine
 struct GenModel;

@@ -258,6 +258,53 @@ __global__ void k_gen_readout(int n, int d, const float* __restrict__ x, const f
   for (int c = 0; c < d; ++c) g[c] = v[c] * scale[t];
 }
 
+// ------------------------------------------------------------ linear biases
+// e3nn o3.Linear(biases=True) (use_bias_in_linear): + b[c] on every row; b is
+// the full-width vector (zero on the columns of non-0e output irreps)
+__global__ void k_gen_bias(int64_t n, int d, const float* __restrict__ b, float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n * d) y[i] += b[i % d];
+}
+
+// ------------------------------------------------------------ readout FCN
+// FCN_e3nn (nn/linear.py:94-129): e3nn FullyConnectedNet's activation
+// c f(z) (c = normalize2mom(f)) and its derivative c f'(z).  kind: 0 relu,
+// 1 silu, 2 tanh, 3 sigmoid, 4 abs, 5 elu (sevenn/_const.py ACTIVATION)
+__device__ __forceinline__ void gen_act(int kind, float z, float& f, float& df) {
+  switch (kind) {
+    case 0: f = z > 0.f ? z : 0.f; df = z > 0.f ? 1.f : 0.f; break;
+    case 1: {
+      const float sg = 1.f / (1.f + __expf(-z));
+      f = z * sg;
+      df = sg * (1.f + z * (1.f - sg));
+      break;
+    }
+    case 2: {
+      const float t = tanhf(z);
+      f = t;
+      df = 1.f - t * t;
+      break;
+    }
+    case 3: {
+      const float sg = 1.f / (1.f + __expf(-z));
+      f = sg;
+      df = sg * (1.f - sg);
+      break;
+    }
+    case 4: f = fabsf(z); df = z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f); break;
+    default: f = z > 0.f ? z : expm1f(z); df = z > 0.f ? 1.f : __expf(z); break;
+  }
+}
+// mode 0: a = c f(z); mode 1: g = g_in * c f'(z)
+__global__ void k_gen_fcn_act(int64_t n, int kind, float c, int mode, const float* __restrict__ z,
+                              const float* __restrict__ gin, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float f, df;
+  gen_act(kind, z[i], f, df);
+  out[i] = mode == 0 ? c * f : gin[i] * c * df;
+}
+
 __global__ void k_gen_add(int64_t n, const float* __restrict__ a, float* __restrict__ acc) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) acc[i] += a[i];
@@ -304,6 +351,15 @@ hipError_t launch_gen_readout(int n, int d, const float* x, const float* v, cons
                               const float* scale, const float* shift, int per_species, float* eat,
                               float* dx, hipStream_t s) {
   GLAUNCH(k_gen_readout, nblk(n), n, d, x, v, type, scale, shift, per_species, eat, dx);
+  return hipGetLastError();
+}
+hipError_t launch_gen_bias(int64_t n, int d, const float* b, float* y, hipStream_t s) {
+  GLAUNCH(k_gen_bias, nblk(n * d), n, d, b, y);
+  return hipGetLastError();
+}
+hipError_t launch_gen_fcn_act(int64_t n, int kind, float c, int mode, const float* z, const float* gin,
+                              float* out, hipStream_t s) {
+  GLAUNCH(k_gen_fcn_act, nblk(n), n, kind, c, mode, z, gin, out);
   return hipGetLastError();
 }
 hipError_t launch_gen_add(int64_t n, const float* a, float* acc, hipStream_t s) {

@@ -58,6 +58,8 @@ DEFAULTS = {
     'train_shift_scale': False,
     'use_bias_in_linear': False,
     'readout_as_fcn': False,
+    'readout_fcn_hidden_neurons': [30, 30],
+    'readout_fcn_activation': 'relu',
     'self_connection_type': 'nequip',
     'interaction_type': 'nequip',
     'act_scalar': {'e': 'silu', 'o': 'tanh'},
@@ -197,6 +199,28 @@ def _linear_numel(irreps_in, irreps_out):
                if (li, pi) == (lo, po))
 
 
+def _bias_numel(irreps_out):
+    """e3nn o3.Linear(biases=True): a bias per channel of every 0e output
+    irrep (``biases and ir.is_scalar()``)"""
+    return sum(m for m, l, p in irreps_out if (l, p) == (0, 1))
+
+
+def act_norm(name):
+    """e3nn normalize2mom(act): 1 / sqrt(E[act(z)^2]) over e3nn's fixed
+    sample (1e6 float64 normals from a CPU generator seeded 0) -- reproduces
+    the frozen constants of the reference deployments (silu 1.6791767923989418,
+    tanh 1.5937334472592695)"""
+    f = {'relu': torch.relu, 'silu': torch.nn.functional.silu, 'tanh': torch.tanh,
+         'sigmoid': torch.sigmoid, 'abs': torch.abs, 'elu': torch.nn.functional.elu}.get(name)
+    if f is None:
+        raise ValueError(f'activation {name!r} (reference _const.ACTIVATION: relu silu tanh abs '
+                         'ssp sigmoid elu; ssp is not built)')
+    gen = torch.Generator(device='cpu').manual_seed(0)
+    z = torch.randn(1_000_000, generator=gen, dtype=torch.float64)
+    c = float(f(z).pow(2).mean().pow(-0.5))
+    return 1.0 if abs(c - 1.0) < 1e-4 else c
+
+
 def model_manifest(cfg):
     """The deployment manifest (parameter table in the reference's
     named_parameters order) of a resolved config."""
@@ -208,15 +232,29 @@ def model_manifest(cfg):
     parity = -1 if cfg['is_parity'] else 1
     sc_type = cfg['self_connection_type']
     if sc_type not in ('linear', 'nequip'):
-        raise NotImplementedError(f'self_connection_type {sc_type!r}')
-    if cfg['readout_as_fcn'] or cfg['use_bias_in_linear']:
-        raise NotImplementedError('readout_as_fcn / use_bias_in_linear are not built')
+        # the reference accepts exactly these (_const.py:13 IMPLEMENTED_SELF_CONNECTION_TYPE,
+        # checked at :153 / :207); 'none' passes init_self_connection (model_build.py:48)
+        # but its interaction block then calls the missing intro (interaction_blocks.py:44-49)
+        raise ValueError(f'self_connection_type {sc_type!r}: the reference implements '
+                         "'nequip' and 'linear' only (sevenn/_const.py IMPLEMENTED_SELF_CONNECTION_TYPE)")
+    bias = bool(cfg['use_bias_in_linear'])
+    fcn = bool(cfg['readout_as_fcn'])
     tensors = []
 
     def add(name, shape):
         tensors.append({'name': name, 'shape': list(shape)})
+
+    def add_linear(name, irreps_in, irreps_out, biases=bias):
+        """e3nn o3.Linear's parameters in registration order: the flat
+        weight, then (biases=True) one bias per scalar 0e output channel,
+        zero-initialised (IrrepsLinear(..., biases=use_bias_in_linear),
+        model_build.py:194, :237, :386, :393; interaction_blocks.py:58, :80)"""
+        add(f'{name}.linear.weight', [_linear_numel(irreps_in, irreps_out)])
+        nbias = _bias_numel(irreps_out) if biases else 0
+        if nbias:
+            add(f'{name}.linear.bias', [nbias])
     add('edge_embedding.basis_function.coeffs', [nb])
-    add('onehot_to_feature_x.linear.weight', [_linear_numel([(nsp, 0, 1)], irreps[0])])
+    add_linear('onehot_to_feature_x', [(nsp, 0, 1)], irreps[0])
     conv_out = []
     for t in range(L):
         last = t == L - 1
@@ -240,20 +278,33 @@ def model_manifest(cfg):
             mid[(l3, p3)] = mid.get((l3, p3), 0) + mul
         mid_irreps = [(m, l, p) for (l, p), m in sorted(mid.items())]
         W = sum(i[0] for i in ins)
-        if sc_type == 'linear':
-            add(f'{t}_self_connection_intro.linear.weight', [_linear_numel(xin, gin)])
+        if sc_type == 'linear':   # SelfConnectionLinearIntro: o3.Linear without biases
+            add_linear(f'{t}_self_connection_intro', xin, gin, biases=False)
         else:   # FullyConnectedTensorProduct(x, nsp x 0e -> gin), self_connection.py:11-38
             add(f'{t}_self_connection_intro.fc_tensor_product.weight',
                 [_linear_numel(xin, gin) * nsp])
-        add(f'{t}_self_interaction_1.linear.weight', [_linear_numel(xin, xin)])
+        add_linear(f'{t}_self_interaction_1', xin, xin)
         add(f'{t}_convolution.denominator', [1])
         dims = [nb] + hid + [W]
         for k in range(len(dims) - 1):
             add(f'{t}_convolution.weight_nn.layer{k}.weight', [dims[k], dims[k + 1]])
-        add(f'{t}_self_interaction_2.linear.weight', [_linear_numel(mid_irreps, gin)])
+        add_linear(f'{t}_self_interaction_2', mid_irreps, gin)
     hidden = sum(m for m, l, p in irreps[-1] if (l, p) == (0, 1)) // 2
-    add('reduce_input_to_hidden.linear.weight', [_linear_numel(irreps[-1], [(hidden, 0, 1)])])
-    add('reduce_hidden_to_energy.linear.weight', [hidden])
+    readout = {'type': 'linear'}
+    if fcn:
+        # FCN_e3nn (nn/linear.py:94-129): e3nn FullyConnectedNet([dim] + hidden
+        # + [1], act) on the last block's scalars (model_build.py:396-408)
+        if any(l != 0 for _, l, _ in irreps[-1]):
+            raise ValueError('readout_as_fcn: the last block must output scalars only')
+        rh = [int(h) for h in cfg['readout_fcn_hidden_neurons']]
+        ract = str(cfg['readout_fcn_activation'])
+        fdims = [_dim(irreps[-1])] + rh + [1]
+        for k in range(len(fdims) - 1):
+            add(f'readout_FCN.fcn.layer{k}.weight', [fdims[k], fdims[k + 1]])
+        readout = {'type': 'fcn', 'hidden': rh, 'act': ract, 'act_norm': act_norm(ract)}
+    else:
+        add_linear('reduce_input_to_hidden', irreps[-1], [(hidden, 0, 1)])
+        add_linear('reduce_hidden_to_energy', [(hidden, 0, 1)], [(1, 0, 1)])
     add('rescale_atomic_energy.shift', [nsp])
     add('rescale_atomic_energy.scale', [nsp])
     off = 0
@@ -294,6 +345,8 @@ def model_manifest(cfg):
         'lmax_edge': int(cfg['_lmax_edge']),
         'readout_hidden': hidden,
         'self_connection_type': sc_type,
+        'use_bias_in_linear': bias,
+        'readout': readout,
         'conv_denominator': cfg['_conv_denominator'],
         'species_wise_rescale': True,
         'num_params': off,
@@ -335,6 +388,8 @@ def init_weights(man, cfg, seed=0):
         name = t['name']
         if name == 'edge_embedding.basis_function.coeffs':
             v = np.arange(1, n + 1) * math.pi / rc
+        elif name.endswith('.linear.bias'):   # e3nn: zeros
+            v = np.zeros(n)
         elif name.endswith('.denominator'):
             v = np.array([den[int(name.split('_')[0])]])
         elif name == 'rescale_atomic_energy.shift':

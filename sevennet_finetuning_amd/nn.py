@@ -303,7 +303,8 @@ def sevennet0_kinds(manifest, conv_only=False):
         return None
     cf = man.get('cutoff_function', {}) or {}
     if not conv_only and (man.get('self_connection_type', 'linear') != 'linear' or
-                          cf.get('name', 'XPLOR') != 'XPLOR'):
+                          cf.get('name', 'XPLOR') != 'XPLOR' or bool(man.get('use_bias_in_linear')) or
+                          (man.get('readout') or {}).get('type', 'linear') != 'linear'):
         return None
     irreps = [parse_irreps(s) for s in man['irreps_manual']]
     L = int(man['num_convolution_layer'])
@@ -357,6 +358,10 @@ class SevenNetTrainable(torch.nn.Module):
         self.sh_normalize = bool(man.get('sh_normalize', True))
         self.sc_type = man.get('self_connection_type', 'linear')
         self.readout_hidden = int(man.get('readout_hidden', self.irreps[-1][0][0] // 2))
+        # use_bias_in_linear (e3nn Linear biases on 0e outputs) and the
+        # readout_as_fcn readout (FCN_e3nn): model_build.py:194-240, :396-408
+        self.use_bias = bool(man.get('use_bias_in_linear', False))
+        self.readout_cfg = dict(man.get('readout') or {'type': 'linear'})
         self.conv_backend = conv_backend
         flat_host = np.fromfile(os.path.join(model_dir, 'weights.bin'), dtype='<f4') \
             if weights is None else np.ascontiguousarray(weights, dtype='<f4').reshape(-1)
@@ -467,8 +472,44 @@ class SevenNetTrainable(torch.nn.Module):
                 raise ValueError(f'block {blk["kind"]}: backend dims {be.dims[blk["kind"]]} != '
                                  f'{(dx, dw, dm)}')
         hid = self.readout_hidden
+        if self.readout_cfg.get('type', 'linear') == 'fcn' and any(l != 0 for _, l, _ in irr[-1]):
+            raise ValueError('readout_as_fcn needs a scalar-only last block')
         self.readout1 = _Linear(irr[-1], [(hid, 0, 1)])
         self.readout2 = _Linear([(hid, 0, 1)], [(1, 0, 1)])
+
+    def bias(self, y, irreps_out, name):
+        """+ the IrrepsLinear's bias (its 0e output channels) when the model
+        has biases (use_bias_in_linear)"""
+        if f'{name}.linear.bias' not in self.slices:
+            return y
+        b = self.param(f'{name}.linear.bias')
+        parts, off, k = [], 0, 0
+        for m, l, p in irreps_out:
+            d = m * (2 * l + 1)
+            blk = y[:, off:off + d]
+            if (l, p) == (0, 1):
+                blk = blk + b[k:k + m]
+                k += m
+            parts.append(blk)
+            off += d
+        return torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
+
+    def readout_fcn(self, x):
+        """FCN_e3nn (nn/linear.py:94-129): e3nn FullyConnectedNet on the
+        last block's scalars, c act(h W / sqrt(fan_in)) between layers"""
+        ro = self.readout_cfg
+        f = {'relu': torch.relu, 'silu': torch.nn.functional.silu, 'tanh': torch.tanh,
+             'sigmoid': torch.sigmoid, 'abs': torch.abs,
+             'elu': torch.nn.functional.elu}[ro['act']]
+        c = float(ro['act_norm'])
+        nh = len(ro['hidden'])
+        h = x
+        for k in range(nh + 1):
+            w = self.param(f'readout_FCN.fcn.layer{k}.weight')
+            h = h @ (w / math.sqrt(w.shape[0]))
+            if k < nh:
+                h = f(h) * c
+        return h[:, 0]
 
     def act(self, x):
         # HIP kernels on the GPU (one launch per derivative order); the CPU
@@ -597,9 +638,11 @@ class SevenNetTrainable(torch.nn.Module):
         Y = spherical_harmonics(vec_k, self.lmax_edge, self.sh_normalize)
         P = self.param
         x = P('onehot_to_feature_x.linear.weight').view(self.nsp, -1)[types] / math.sqrt(self.nsp)
+        x = self.bias(x, self.irreps[0], 'onehot_to_feature_x')
         for t, blk in enumerate(self.blocks):
             sc = self.self_connection(t, blk, x, types)
-            h = blk['si1'](x, P(f'{t}_self_interaction_1.linear.weight'))
+            h = self.bias(blk['si1'](x, P(f'{t}_self_interaction_1.linear.weight')), self.irreps[t],
+                          f'{t}_self_interaction_1')
             pre = f'{t}_convolution'
             w0 = P(f'{pre}.weight_nn.layer0.weight')
             hid = self.act(emb @ (w0 / math.sqrt(w0.shape[0])))
@@ -608,10 +651,17 @@ class SevenNetTrainable(torch.nn.Module):
             w2 = P(f'{pre}.weight_nn.layer2.weight')
             w = hid @ (w2 / math.sqrt(w2.shape[0]))
             agg = conv_ops.conv(h, Y, w, blk['kind'], graph) / P(f'{pre}.denominator')
-            y = blk['si2'](agg, P(f'{t}_self_interaction_2.linear.weight')) + sc
+            y = self.bias(blk['si2'](agg, P(f'{t}_self_interaction_2.linear.weight')),
+                          blk['sc_irreps'][1], f'{t}_self_interaction_2') + sc
             x = self.gate(y, blk['gate'])
-        hidden = self.readout1(x, P('reduce_input_to_hidden.linear.weight'))
-        e_s = self.readout2(hidden, P('reduce_hidden_to_energy.linear.weight'))[:, 0]
+        if self.readout_cfg.get('type', 'linear') == 'fcn':
+            e_s = self.readout_fcn(x)
+        else:
+            hid = self.readout_hidden
+            hidden = self.bias(self.readout1(x, P('reduce_input_to_hidden.linear.weight')),
+                               [(hid, 0, 1)], 'reduce_input_to_hidden')
+            e_s = self.bias(self.readout2(hidden, P('reduce_hidden_to_energy.linear.weight')),
+                            [(1, 0, 1)], 'reduce_hidden_to_energy')[:, 0]
         atomic = e_s * P('rescale_atomic_energy.scale')[types] + \
             P('rescale_atomic_energy.shift')[types]
         nb = int(data[KEY.NUM_ATOMS].numel()) if KEY.NUM_ATOMS in data else 1

@@ -59,6 +59,10 @@ def supported(model):
         return False
     if model.sc_type != 'linear' or model.cut.get('name', 'XPLOR') != 'XPLOR':
         return False
+    # linear biases / the FCN readout: the autograd path (their derivatives
+    # are not in the hand-scheduled sweep)
+    if getattr(model, 'use_bias', False) or model.readout_cfg.get('type', 'linear') != 'linear':
+        return False
     if model.lmax_edge != 2 or model.filter_parity != 1:
         return False
     for blk in model.blocks:

@@ -324,3 +324,74 @@ def test_odd_and_unsorted_gates_on_the_native_engine_vs_oracle(tmp_path):
         assert abs(got['energy'] - float(ref['energy'])) <= 2e-6 * abs(float(ref['energy']))
         assert np.abs(got['forces'] - F).max() <= 2e-5 * np.abs(F).max()
         assert np.abs(got['stress'] - S).max() <= 1e-4 * np.abs(S).max()
+
+
+def _option_deployment(out_dir, **opts):
+    """A config-built model with the reference options this build used to
+    refuse: use_bias_in_linear (random nonzero biases, as after training) and
+    readout_as_fcn (FCN_e3nn readout)."""
+    from _conv_cpu import GenericCpuConvBackend
+    from sevennet_finetuning_amd import model_build as mb
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    cfg = {'chemical_species': ['Hf', 'O'], 'cutoff': 4.5, 'channel': 16, 'lmax': 2,
+           'is_parity': False, 'num_convolution_layer': 3, 'conv_denominator': 12.0,
+           'weight_nn_hidden_neurons': [32, 32], 'self_connection_type': 'linear',
+           'cutoff_function': {'cutoff_function_name': 'XPLOR', 'cutoff_on': 4.0}}
+    cfg.update(opts)
+    c = mb.resolve_config(cfg)
+    man = mb.model_manifest(c)
+    flat = mb.init_weights(man, c, 11)
+    g = np.random.default_rng(2)
+    for t in man['tensors']:
+        if t['name'].endswith('.bias'):
+            flat[t['offset']:t['offset'] + t['numel']] = g.normal(0, 0.5, t['numel'])
+        if t['name'] == 'rescale_atomic_energy.scale':
+            flat[t['offset']:t['offset'] + t['numel']] = 5.0
+    m = SevenNetTrainable(device='cpu', conv_backend=GenericCpuConvBackend(), manifest=man, weights=flat)
+    m.config = c
+    return mb.deploy(m, out_dir)
+
+
+@pytest.mark.parametrize('opts', [{'use_bias_in_linear': True}, {'readout_as_fcn': True},
+                                  {'readout_as_fcn': True, 'use_bias_in_linear': True,
+                                   'readout_fcn_activation': 'silu', 'readout_fcn_hidden_neurons': [24],
+                                   'self_connection_type': 'nequip', 'is_parity': True}],
+                         ids=['bias', 'fcn', 'bias_fcn_nequip_parity'])
+def test_bias_and_fcn_readout_models_on_the_native_engine_vs_oracle(tmp_path, opts):
+    """model_build's use_bias_in_linear / readout_as_fcn deployments
+    (model_build.py:194-240, :396-408) served by the C-ABI generic engine
+    (biases added after the dense linears, the readout biases folded into the
+    shift; the FCN readout's forward and backward on the library's GEMM and
+    activation kernels), the torch-side model and the ASE calculator (deploy
+    -> serve round trip), against the fp64 oracle: E 2e-6 relative, forces
+    1e-4 eV/A, stress 2e-6 eV/A^3."""
+    from oracle.neighbor import neighbor_list
+    from oracle.nequip_ref import NequIPRef
+    from sevennet_finetuning_amd.model import E3GNNModel, load_model
+    from sevennet_finetuning_amd.sevennet_calculator import SevenNetCalculator
+    from sevennet_finetuning_amd.structures import si_diamond
+    dep = _option_deployment(str(tmp_path / 'dep'), **opts)
+    pos, cell = si_diamond((2, 2, 2), sigma=0.08, seed=7)
+    types = np.arange(len(pos)) % 2
+    ref_m = NequIPRef(dep)
+    ei, sh = neighbor_list(pos, cell, ref_m.cutoff)
+    ref = ref_m(torch.tensor(pos), torch.tensor(types), torch.tensor(ei), torch.tensor(sh),
+                torch.tensor(cell))
+    E, F, S = float(ref['energy']), ref['forces'].numpy(), ref['stress'].numpy()
+    assert np.abs(F).max() > 0.05
+    native = E3GNNModel(dep, device=DEV)
+    assert native.family == -1           # the generic engine, not the fused kernels
+    assert isinstance(load_model(dep, device=DEV), E3GNNModel)
+    for model in (native, load_model(dep, device=DEV, engine='torch')):
+        got = _run(model, pos, cell, types)
+        assert abs(got['energy'] - E) <= 2e-6 * abs(E), (got['energy'], E)
+        assert np.abs(got['forces'] - F).max() <= 1e-4
+        assert np.abs(got['stress'] - S).max() <= 2e-6
+    # the calculator surface on the deployment directory (deploy -> serve)
+    from sevennet_finetuning_amd.structures import Atoms
+    calc = SevenNetCalculator(dep, device=DEV)
+    atoms = Atoms(symbols=[['Hf', 'O'][t] for t in types], positions=pos, cell=cell)
+    calc.calculate(atoms)
+    assert abs(calc.results['energy'] - E) <= 2e-6 * abs(E)
+    assert np.abs(calc.results['forces'] - F).max() <= 1e-4
+    assert np.abs(calc.results['stress'] - (-S[[0, 1, 2, 4, 5, 3]])).max() <= 2e-6

@@ -68,10 +68,13 @@ def test_derived_irreps_and_refusals():
     assert man['family'] == 'nequip'
     assert any(t['name'] == '0_self_connection_intro.fc_tensor_product.weight'
                for t in man['tensors'])
-    c = ft_config()
-    c['self_connection_type'] = 'mace'
-    with pytest.raises(NotImplementedError, match='mace'):
-        mb.model_manifest(mb.resolve_config(c))
+    # the reference implements 'nequip' and 'linear' (_const.py:13, checked at
+    # :153); 'none' cannot build there either (interaction_blocks.py:44-49)
+    for bad in ('mace', 'none'):
+        c = ft_config()
+        c['self_connection_type'] = bad
+        with pytest.raises(ValueError, match="'nequip' and 'linear'"):
+            mb.model_manifest(mb.resolve_config(c))
     c = ft_config()
     c['irreps_manual'] = ['128x0e'] + ['128x0e+64x1e+32x3e'] * 4 + ['128x0e']
     with pytest.raises(NotImplementedError, match='l > 2'):
@@ -309,3 +312,85 @@ def test_convolution_irreps_follow_the_current_reference():
         assert {(l, p) for _, l, p in si2.irreps_in} == \
             {(l, p) for _, l, p in mb._parse(man['conv_irreps_out'][-1])}
         assert si2.numel == m.slices['3_self_interaction_2.linear.weight'][1]
+
+
+def _small_option_config(**kw):
+    c = {'chemical_species': ['Hf', 'O'], 'cutoff': 4.0, 'channel': 8, 'lmax': 2,
+         'is_parity': False, 'num_convolution_layer': 3, 'conv_denominator': 7.0,
+         'weight_nn_hidden_neurons': [16, 16], 'self_connection_type': 'linear',
+         'cutoff_function': {'cutoff_function_name': 'XPLOR', 'cutoff_on': 3.5}}
+    c.update(kw)
+    return c
+
+
+@pytest.mark.parametrize('opts', [{'use_bias_in_linear': True},
+                                  {'readout_as_fcn': True},
+                                  {'readout_as_fcn': True, 'readout_fcn_activation': 'tanh',
+                                   'readout_fcn_hidden_neurons': [12], 'use_bias_in_linear': True,
+                                   'self_connection_type': 'nequip', 'is_parity': True}])
+def test_bias_and_fcn_readout_options_build_and_match_the_oracle(opts, tmp_path):
+    """use_bias_in_linear (e3nn Linear biases on every 0e output of the
+    embedding, si1, si2 and readout linears; model_build.py:194, :237, :386,
+    :393, interaction_blocks.py:58, :80) and readout_as_fcn (FCN_e3nn,
+    model_build.py:396-408): the parameter table in the reference's order
+    (weight, then bias; readout_FCN.fcn.layer{k}.weight), e3nn's zero bias
+    initialisation, the normalize2mom constant of the readout activation, and
+    the trainable model (CPU double) = the fp64 oracle (oracle/nequip_ref.py)
+    on a deployment with random nonzero biases -- energy, forces, stress."""
+    from _conv_cpu import GenericCpuConvBackend
+    from _systems import oracle_eval  # noqa: F401  (fixtures module on the path)
+    from oracle.nequip_ref import NequIPRef
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    from sevennet_finetuning_amd.structures import si_diamond
+    cfg = mb.resolve_config(_small_option_config(**opts))
+    man = mb.model_manifest(cfg)
+    names = [t['name'] for t in man['tensors']]
+    bias = opts.get('use_bias_in_linear', False)
+    fcn = opts.get('readout_as_fcn', False)
+    assert man['use_bias_in_linear'] == bias and man['readout']['type'] == ('fcn' if fcn else 'linear')
+    assert man['family'] == 'nequip'   # never the SevenNet-0 kernels' predicate
+    if bias:
+        i = names.index('0_self_interaction_1.linear.weight')
+        assert names[i + 1] == '0_self_interaction_1.linear.bias'
+        assert names[names.index('onehot_to_feature_x.linear.weight') + 1] == 'onehot_to_feature_x.linear.bias'
+        assert not any(n.startswith('0_self_connection_intro') and n.endswith('bias') for n in names)
+        shapes = {t['name']: t['shape'] for t in man['tensors']}
+        assert shapes['onehot_to_feature_x.linear.bias'] == [8]
+        flat0 = mb.init_weights(man, cfg, 0)
+        for t in man['tensors']:
+            if t['name'].endswith('.bias'):
+                assert not flat0[t['offset']:t['offset'] + t['numel']].any()
+    if fcn:
+        assert 'reduce_input_to_hidden.linear.weight' not in names
+        act = opts.get('readout_fcn_activation', 'relu')
+        hid = opts.get('readout_fcn_hidden_neurons', [30, 30])
+        assert man['readout']['hidden'] == hid
+        assert abs(man['readout']['act_norm'] - {'relu': 1.4163393446331367,
+                                                 'tanh': 1.5937334472592695}[act]) < 1e-9
+        assert [t['shape'] for t in man['tensors'] if t['name'].startswith('readout_FCN')] == \
+            [[8, hid[0]]] + [[a, b] for a, b in zip(hid, hid[1:])] + [[hid[-1], 1]]
+    flat = mb.init_weights(man, cfg, 3)
+    g = np.random.default_rng(5)
+    for t in man['tensors']:   # a "trained" model: nonzero biases
+        if t['name'].endswith('.bias'):
+            flat[t['offset']:t['offset'] + t['numel']] = g.normal(0, 0.5, t['numel'])
+    m = SevenNetTrainable(device='cpu', conv_backend=GenericCpuConvBackend(), manifest=man,
+                          weights=flat, dtype=torch.float64)
+    m.config = cfg
+    out = mb.deploy(m, str(tmp_path / 'dep'))
+    ref = NequIPRef(out)
+    pos, cell = si_diamond((1, 1, 2), sigma=0.1, seed=4)
+    types = np.arange(len(pos)) % 2
+    from oracle.neighbor import neighbor_list
+    ei, sh = neighbor_list(pos, cell, 4.0)
+    r = ref(torch.tensor(pos), torch.tensor(types), torch.tensor(ei), torch.tensor(sh, dtype=torch.float64),
+            torch.tensor(cell))
+    vec = torch.tensor(pos[ei[1]] + sh @ cell - pos[ei[0]], dtype=torch.float64)
+    from sevennet_finetuning_amd import _keys as KEY
+    data = {KEY.NODE_FEATURE: torch.tensor(types), KEY.EDGE_IDX: torch.tensor(ei), KEY.EDGE_VEC: vec,
+            KEY.NUM_ATOMS: torch.tensor([len(pos)]),
+            KEY.CELL_VOLUME: torch.tensor([abs(np.linalg.det(cell))], dtype=torch.float64)}
+    o = m(data)
+    assert abs(float(o[KEY.PRED_TOTAL_ENERGY][0]) - float(r['energy'])) <= 1e-10 * abs(float(r['energy']))
+    assert torch.allclose(o[KEY.PRED_FORCE], r['forces'], atol=1e-10)
+    assert torch.allclose(o[KEY.PRED_STRESS][0], r['stress'], atol=1e-10)

@@ -125,3 +125,41 @@ def test_decomposed_hip_matches_single_device(tmp_path, name):
     assert np.abs(got['virial'] - one['virial'].cpu().numpy()).max() < 2e-5 * max(1, abs(e1))
     ref = oracle_eval(pos, cell, types)
     assert np.abs(got['forces'] - ref['forces']).max() < 1e-4
+
+
+def test_local_handshake_and_rank_emulation_plumbing():
+    """bench.py --rank-emulation: every rank graph built in one process,
+    send lists from local_handshake (no process group) -- each owner sends
+    exactly the atoms its peers' ghost blocks ask for, in their order -- and
+    one rank's evaluate with LocalHalo (each all_to_all a same-size local
+    copy) runs the full segment sequence: 2 (L - 1) + 1 exchanges, every
+    pack/unpack on real index lists, outputs of the rank's shapes."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from _segment_cpu import make_engine
+    from sevennet_finetuning_amd.parallel import LocalHalo, ParallelE3GNN, local_handshake
+    pos, cell, types = system('si_rng0_6x2x2', SYMS)
+    grid = brick_grid(2)
+    rgs = local_handshake([build_rank_graph(pos, cell, types, 5.0, grid, r) for r in range(2)])
+    for r, rg in enumerate(rgs):
+        assert rg.send_counts[r] == 0
+        off = np.concatenate([[0], np.cumsum(rg.send_counts)])
+        for p, q in enumerate(rgs):
+            lo = int(q.recv_counts[:r].sum())
+            want = q.req_ids[lo:lo + int(q.recv_counts[r])]
+            assert np.array_equal(rg.owned[rg.send_rows[off[p]:off[p + 1]]], want)
+    eng = make_engine(rgs[0])
+    drv = ParallelE3GNN(eng)
+    with pytest.raises(ValueError):
+        drv.set_graph(build_rank_graph(pos, cell, types, 5.0, grid, 0), emulate=True)
+    drv.set_graph(rgs[0], emulate=True)
+    assert isinstance(drv.halo, LocalHalo)
+    tm = {}
+    out = drv.evaluate(timing=tm)
+    L = eng.num_layers
+    assert tm['exchanges'] == 2 * (L - 1) + 1
+    assert out['forces'].shape == (rgs[0].n_local, 3) and np.isfinite(float(out['energy']))
+    sent, recv = drv.halo.bytes_per_step(L)
+    sc, rc = int(rgs[0].send_counts.sum()), int(rgs[0].recv_counts.sum())
+    dims = sum(eng.dim('x', t) for t in range(1, L))
+    assert sent == 4 * (dims * (sc + rc) + 3 * rc) and recv == 4 * (dims * (rc + sc) + 3 * sc)

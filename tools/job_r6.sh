@@ -26,6 +26,13 @@ for s in "$@"; do
     benchfull) run benchfull 400 python bench.py ;;
     bv_*) v=${s#bv_}; run bench_$v 300 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity-check ;;
     pv_*) v=${s#pv_}; run parity_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread ;;
+    fv_*) v=${s#fv_}; run full_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -u -m pytest tests/test_gpu_fullsize.py -x -q --timeout 400 --timeout-method thread -k "v1 or determin or supercell"
+          run family_$v 600 env E3GNN_LIB=sevennet_finetuning_amd/variants/$v.so python -u -m pytest tests/test_gpu_family.py -x -q --timeout 400 --timeout-method thread ;;
+    nve) run nve 900 python -u tools/nve_drift.py --cells 3 --steps 2000 --dt 1.0 --temp 600 ;;
+    hfo2) run bench_hfo2 600 python bench.py --system hfo2 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    rankemu) run rankemu 900 python -u bench.py --rank-emulation 0,7 --steps 3 --warmup 1 ;;
+    newtests) run newtests 900 python -u -m pytest tests/test_gpu_generic.py tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread -k "bias_and_fcn or workspace or rejects" ;;
+    gtrain) run gtrain 900 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread ;;
     summ) summ ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
