@@ -936,55 +936,26 @@ __device__ __forceinline__ void dh2_pair_g(f32x4 (&dh2)[4], const float (&da)[4]
 #ifndef E3GNN_NBR_DH2_BF16
 #define E3GNN_NBR_DH2_BF16 E3GNN_DH2_X3
 #endif
-// Nodes per wave (E3GNN_NBR_NPW; 1: one node per wave).  With more, a wave
-// walks NPW nodes of its workgroup's block (node base + 4 k + wave) and hides
-// the per-node dependent chain src_ptr -> src_perm -> centre / SH / basis of
-// the NEXT node behind the current one: the next node's edge ids are fetched
-// when the current node starts, its centre rows, SH and basis values when the
-// current node's tensor-product loop is done (its MLP-chain backward runs
-// while they land).
-#ifndef E3GNN_NBR_NPW
-#define E3GNN_NBR_NPW 1
-#endif
 template <class L>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_conv_bwd_nbr(
     const int* __restrict__ src_ptr, const int* __restrict__ src_perm, const int* __restrict__ center,
     const float* __restrict__ emb, const float* __restrict__ Y, const float* __restrict__ h,
     const float* __restrict__ gagg, MlpW W, float* __restrict__ dh, float* __restrict__ dgu, int n_centers,
     int r_begin, int r_end, float* __restrict__ demb) {
-  constexpr int NPW = E3GNN_NBR_NPW;
   __shared__ __attribute__((aligned(16))) float lds[4][L::DX];
   const int wid = threadIdx.x >> 6;
-  const int base = r_begin + xcd_block() * 4 * NPW;
+  const int jn = __builtin_amdgcn_readfirstlane(r_begin + xcd_block() * 4 + wid);
+  if (jn >= r_end) return;
   float* dacc = lds[wid];
   const int lane = threadIdx.x & 63, g = lane >> 4, col = lane & 15;
-  const WRes R = make_wres(W, L::W);
-  const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
-  // the next node's first-pass edge data (NPW > 1)
-  int nx_er[2] = {-1, -1}, nx_vg[2] = {0, 0};
-  float nx_y[2][9], nx_b[2][2];
-  bool have_nx = false;
-  for (int kn = 0; kn < NPW; ++kn) {
-  const int jn = __builtin_amdgcn_readfirstlane(base + 4 * kn + wid);
-  if (jn >= r_end) break;
   const int qb = src_ptr[jn], qe = src_ptr[jn + 1];
-  const int jn2 = base + 4 * (kn + 1) + wid;
-  const bool next = NPW > 1 && kn + 1 < NPW && jn2 < r_end;   // wave-uniform
-  int er2[2] = {-1, -1};
-  if (next) {
-    const int qb2 = src_ptr[jn2], qe2 = src_ptr[jn2 + 1];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = qb2 + 16 * u + col;
-      er2[u] = q < qe2 ? src_perm[q] : -1;
-    }
-  }
+  const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rx = rsrc_bytes(h + (int64_t)jn * L::DX, L::DX * 4);
+  const __amdgpu_buffer_rsrc_t Rg = rsrc_bytes(gagg, (int64_t)n_centers * L::DM * 4);
   for (int t = lane; t < L::DX; t += 64) dacc[t] = 0.f;
 
   for (int q0 = qb; q0 < qe; q0 += 32) {
     const bool two = q0 + 16 < qe;   // wave-uniform
-    const bool pre = have_nx && q0 == qb;   // wave-uniform: this pass's edge data is prefetched
     phase();
     Op3 wq;
     load_w2b(wq, R.w2b, lane, L::P[0].woff);
@@ -994,24 +965,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int q = q0 + 16 * u + col;
-      float b[2];
-      if (pre) {
-        er[u] = nx_er[u];
-        vg[u] = nx_vg[u];
+      er[u] = q < qe ? src_perm[q] : -1;   // edge of slot c
+      vg[u] = (er[u] >= 0 ? center[er[u]] * L::DM : n_centers * L::DM) * 4;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) y[u][k] = nx_y[u][k];
-        b[0] = nx_b[u][0];
-        b[1] = nx_b[u][1];
-      } else {
-        er[u] = q < qe ? src_perm[q] : -1;   // edge of slot c
-        vg[u] = (er[u] >= 0 ? center[er[u]] * L::DM : n_centers * L::DM) * 4;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) y[u][k] = er[u] >= 0 ? Y[(int64_t)er[u] * 9 + k] : 0.f;
-        if (u == 1 && !two) continue;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) b[k] = er[u] >= 0 ? emb[(int64_t)er[u] * 8 + 4 * k + g] : 0.f;
-      }
+      for (int k = 0; k < 9; ++k) y[u][k] = er[u] >= 0 ? Y[(int64_t)er[u] * 9 + k] : 0.f;
       if (u == 1 && !two) continue;
+      float b[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) b[k] = er[u] >= 0 ? emb[(int64_t)er[u] * 8 + 4 * k + g] : 0.f;
       MlpT m;
       mlp_chain(R, b, lane, m);
       f32x4 h2[4];
@@ -1125,20 +1086,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
     });
 
-    if (next && q0 + 32 >= qe) {
-      // the node's last pass: the next node's centre rows, SH and basis
-      // values go out now (its edge ids came at this node's start) and land
-      // under the MLP-chain backward below
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        nx_er[u] = er2[u];
-        nx_vg[u] = (er2[u] >= 0 ? center[er2[u]] * L::DM : n_centers * L::DM) * 4;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) nx_y[u][k] = er2[u] >= 0 ? Y[(int64_t)er2[u] * 9 + k] : 0.f;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) nx_b[u][k] = er2[u] >= 0 ? emb[(int64_t)er2[u] * 8 + 4 * k + g] : 0.f;
-      }
-    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (u == 1 && !two) break;
@@ -1168,8 +1115,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __builtin_amdgcn_s_waitcnt(0);
   float* dhj = dh + (int64_t)jn * L::DX;
   for (int t = lane; t < L::DX; t += 64) dhj[t] = dacc[t];
-  have_nx = next;
-  }
 }
 
 // ================================================================ lock-step kernels
@@ -1288,7 +1233,10 @@ template <class L>
 struct BwdWpg {
   static constexpr int v = L::KIND == 1 ? E3GNN_BWD_WPG : 4;
 };
-// LDS-DMA staging (E3GNN_LS_DMA, default on where it fits): the pair image is
+// LDS-DMA staging (E3GNN_LS_DMA=1; measured and not kept: middle backward
+// 5.68 -> 5.77 ms per launch, the explicit vmcnt(0) before each pair's
+// barrier also drains the neighbour-row prefetch and the dE/dx stores that
+// the compiler's counted waits leave in flight): the pair image is
 // written by global_load_lds_dwordx4 straight from L2 (no staging registers,
 // no ds_write) into one of TWO images, so a pair costs ONE barrier: at pair P
 // each wave waits for its own DMA of P (issued at P - 1), the barrier makes
@@ -1308,8 +1256,20 @@ struct LsDma {
   static constexpr int OFF0 = drop0 ? L::P[0].mul : 0;       // path 0 (l 0 0 0, moff 0): C0 floats
   static constexpr int DMS = L::DM - OFF0;                    // staged dE/dagg floats per centre
   static constexpr int bytes = WPG * DMS * 4 + 2 * LS_IMG;
-  static constexpr bool v = E3GNN_LS_DMA && lean && WPG == 4 && BwdLsWaves<L>::v * bytes <= 163840;
+  static constexpr bool fits = lean && WPG == 4 && BwdLsWaves<L>::v * bytes <= 163840;
+  static constexpr bool v = E3GNN_LS_DMA && fits;
 };
+// Double-buffered REGISTER staging (E3GNN_LS_DB, default on where two images
+// fit: middle backward 5.66 -> 5.53 ms per launch, same box; =0 the single
+// image with two barriers per pair): the same two images and one
+// barrier per pair as the DMA form, the pair's pieces still loaded into
+// registers a pair ahead (loads the compiler counts: no drain of the other
+// loads in flight) and written into the pair's image before the barrier --
+// the other image is the one the previous pair read, retired by the previous
+// pair's barrier.
+#ifndef E3GNN_LS_DB
+#define E3GNN_LS_DB 1
+#endif
 // one wave-instruction of LDS-DMA: 64 lanes x 16 bytes from per-lane global
 // addresses to the wave-uniform LDS byte address lds_dst (+ lane x 16); M0
 // set and restored inside the statement.  hipcc does not count it: the
@@ -1344,10 +1304,12 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
   static_assert(LS_IMG / 16 % NT == 0 && NWP % 64 == 0 && PB % 64 == 0, "staging pieces per thread");
   using DM_ = LsDma<L>;
   constexpr bool DMA = DM_::v;
-  constexpr int OFF0 = DMA ? DM_::OFF0 : 0, DMS = L::DM - OFF0;   // dE/dagg floats staged per centre
-  static_assert(!DMA || (L::P[0].l1 == 0 && L::P[0].l2 == 0 && L::P[0].l3 == 0 && L::P[0].moff == 0 &&
+  constexpr bool RDB = !DMA && E3GNN_LS_DB && DM_::fits;   // double-buffered register staging
+  constexpr bool TWO = DMA || RDB;                         // two images, one barrier per pair
+  constexpr int OFF0 = TWO ? DM_::OFF0 : 0, DMS = L::DM - OFF0;   // dE/dagg floats staged per centre
+  static_assert(!TWO || (L::P[0].l1 == 0 && L::P[0].l2 == 0 && L::P[0].l3 == 0 && L::P[0].moff == 0 &&
                          OFF0 % 4 == 0), "path 0 is the 0e x 0e -> 0e slice at the row start");
-  __shared__ __attribute__((aligned(16))) float smem[WPG * DMS + (DMA ? 2 : 1) * LS_IMG / 4];
+  __shared__ __attribute__((aligned(16))) float smem[WPG * DMS + (TWO ? 2 : 1) * LS_IMG / 4];
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, g = lane >> 4, col = lane & 15;
   const int cb = c_begin + blockIdx.x * WPG;
   const int c = cb + wid;
@@ -1506,7 +1468,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                 constexpr int D3 = 2 * p.l3 + 1;
                 constexpr int ODD = (NB0 + hh * NPI + path_rank<L>(pi)) & 1;
                 const int nb = NB0 + jj * NPI + path_rank<L>(pi);
-                const char* pimg = img + (DMA ? rb * LS_IMG : 0);   // this pair's image
+                const char* pimg = img + (TWO ? rb * LS_IMG : 0);   // this pair's image
                 if constexpr (!ODD) {   // pair start: stage it, fetch the next one
                   if constexpr (STAMPED) STAMP(5);
                   const int nextP = (nb >> 1) + 1 < NPAIR ? (nb >> 1) + 1 : 0;
@@ -1515,6 +1477,14 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                     // every wave's has, and nobody reads the other image any more
                     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
                     issue_dma(nextP, rb ^ 1);
+                  } else if constexpr (RDB) {
+                    // this pair's image (the one two pairs back read, retired
+                    // by the previous pair's barrier), then the one barrier
+#pragma unroll
+                    for (int i = 0; i < NST; ++i)
+                      *reinterpret_cast<f32x4*>(img + rb * LS_IMG + (tid + NT * i) * 16) = st[i];
+                    __syncthreads();
+                    issue(nextP);
                   } else {
                     commit();
                     issue(nextP);
@@ -1558,7 +1528,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                     for (int r = 0; r < 4; ++r) dwp[r] = dwr[r];
                   }
                 }
-                if constexpr (DMA && ODD) rb ^= 1;   // the next pair reads the other image
+                if constexpr (TWO && ODD) rb ^= 1;   // the next pair reads the other image
               }
             });
             // per-edge dE/dx[nbr]; the first block's inputs are the species
@@ -1622,8 +1592,7 @@ static hipError_t fwd_impl(const FusedArgs& a, hipStream_t s) {
 template <class L>
 static hipError_t bwd_nbr_impl(const FusedArgs& a, hipStream_t s) {
   const int nn = a.node_end - a.node_begin;
-  hipLaunchKernelGGL(k_conv_bwd_nbr<L>, dim3((nn + 4 * E3GNN_NBR_NPW - 1) / (4 * E3GNN_NBR_NPW)), dim3(256), 0, s,
-                     a.src_ptr, a.src_perm,
+  hipLaunchKernelGGL(k_conv_bwd_nbr<L>, dim3((nn + 3) / 4), dim3(256), 0, s, a.src_ptr, a.src_perm,
                      a.center, a.emb, a.Y, a.h, a.gagg, a.W, a.dh, a.dgu, a.n_centers, a.node_begin,
                      a.node_end, a.demb);
   return hipGetLastError();

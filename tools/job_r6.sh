@@ -32,6 +32,7 @@ for s in "$@"; do
     hfo2) run bench_hfo2 600 python bench.py --system hfo2 --steps 5 --warmup 1 --no-cpu-baseline ;;
     rankemu) run rankemu 900 python -u bench.py --rank-emulation 0,7 --steps 3 --warmup 1 ;;
     newtests) run newtests 900 python -u -m pytest tests/test_gpu_generic.py tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread -k "bias_and_fcn or workspace or rejects" ;;
+    nvetest) run nvetest 600 python -u -m pytest tests/test_gpu_native.py -x -q -s --timeout 400 --timeout-method thread -k nve_drift ;;
     gtrain) run gtrain 900 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread ;;
     summ) summ ;;
     *) echo "unknown step $s"; exit 2 ;;
