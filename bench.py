@@ -68,8 +68,8 @@ def parse():
                     help='strong scaling: one --cells^3 box (default 46^3 = 778,688 atoms, '
                          'north_star config 4) split over the N ranks')
     ap.add_argument('--no-parity-check', action='store_true')
-    ap.add_argument('--cpu-cells', type=int, default=6,
-                    help='cpu_baseline sample: n^3 cells (6 -> 1,728 atoms)')
+    ap.add_argument('--cpu-cells', type=int, default=11,
+                    help='cpu_baseline sample: n^3 cells (11 -> 10,648 atoms, SURVEY.md 8d)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--same-device', action='store_true',
@@ -87,6 +87,9 @@ def parse():
                          'all_to_all replaced by a same-size local copy: compute + halo kernels, '
                          'no network) and the whole box on this GPU; prints one JSON line')
     ap.add_argument('--emulate-world', type=int, default=8)
+    ap.add_argument('--no-fine-tune', action='store_true',
+                    help='skip the fine_tune leg (N = 1: the fine-tune rehearsal step of '
+                         'BASELINE config 5, bench_train.step_bench, timed after the main line)')
     ap.add_argument('--model-config', default=None, metavar='cCHlL',
                     help='instead of SevenNet-0: the SevenNet-0 preset with channel CH and L '
                          'blocks (e.g. c64l4), built by model_build (e3nn init, seed 0) and '
@@ -278,11 +281,13 @@ def pmc_traffic(kernel, cells):
 
 def cpu_baseline(seconds, cells, model_dir=None):
     """Oracle (plain-PyTorch CPU restatement of the reference) on a bounded
-    sample of the same workload: a cells^3 Si box (default 6^3 = 1,728 atoms,
-    where the reference CPU path is already at its flat large-box throughput,
-    SURVEY.md 6), the same recipe as the bench box: one untimed warm-up call,
-    then >= 3 timed evaluations and >= `seconds` of CPU work on the host's
-    thread share."""
+    sample of the same workload: a cells^3 Si box (default 11^3 = 10,648
+    atoms, SURVEY.md 8d's sample; the CPU path is NOT flat in box size --
+    1,728 atoms ran at 65 and 10,648 at 115 atoms/s on 8 threads, so the
+    smaller sample understated it), the same recipe as the bench box: one
+    untimed warm-up call on a 64-atom box of the same lattice (allocator,
+    thread pool, kernel selection), then >= 1 timed evaluation and >=
+    `seconds` of CPU work on the host's thread share."""
     from oracle.neighbor import neighbor_list
     from oracle.nequip_ref import NequIPRef
     from oracle.sevennet_ref import SevenNet0Ref
@@ -301,9 +306,12 @@ def cpu_baseline(seconds, cells, model_dir=None):
     args = (torch.tensor(pos, dtype=torch.float32), torch.full((len(pos),), si),
             torch.tensor(ei), torch.tensor(sh, dtype=torch.float32),
             torch.tensor(cell, dtype=torch.float32))
-    ref(*args)   # warm-up call (allocator, thread pool, kernel selection): not timed
+    pw, cw = si_diamond((2, 2, 2), sigma=0.05)
+    ew, sw = neighbor_list(pw, cw, 5.0)
+    ref(torch.tensor(pw, dtype=torch.float32), torch.full((len(pw),), si), torch.tensor(ew),
+        torch.tensor(sw, dtype=torch.float32), torch.tensor(cw, dtype=torch.float32))   # warm-up: not timed
     t0, n = time.perf_counter(), 0
-    while n < 3 or time.perf_counter() - t0 < seconds:
+    while n < 1 or time.perf_counter() - t0 < seconds:
         ref(*args)
         n += 1
     dt = time.perf_counter() - t0
@@ -311,7 +319,7 @@ def cpu_baseline(seconds, cells, model_dir=None):
             'kind': 'port',
             'sample': f'{n} energy+force+stress evals of a {len(pos)}-atom Si box ({cells}^3 '
                       f'cells, {ei.shape[1]} edges) in {dt:.1f} s, oracle/sevennet_ref.py fp32, '
-                      f'torch CPU, after one untimed warm-up call',
+                      f'torch CPU, after an untimed warm-up call on a 64-atom box',
             'reference_context': 'the reference frozen TorchScript CPU path measured in the '
                                  'survey container: 272 atoms/s at 10,648 atoms, 8 threads '
                                  '(SURVEY.md 8d); not re-run here (a shipped program), not '
@@ -722,6 +730,20 @@ def main():
     cpu = None
     if rank == 0 and not args.no_cpu_baseline and world == 1 and not args.profile_only:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_cells, model_dir)
+    fine_tune = None
+    if world == 1 and not args.profile_only and not args.no_fine_tune and model_dir is None:
+        # BASELINE config 5 measured in the same run (bench_train.py's step,
+        # same recipe and timing contract): the driver records it with the line
+        import bench_train
+        r = bench_train.step_bench(device, 10, 3)
+        fine_tune = {'workload': 'rehearsal step (RehearsalTrainer.run_one_epoch_rehearsal, FT_w_reEWC '
+                                 'recipe): 2 x 8 synthetic 54-atom structures, forward + forces/stress + '
+                                 'loss gradient + EWC + Adam, twice; HIP graph per batch shape',
+                     'ms_per_step': round(r['ms_per_step'], 3),
+                     'structures_per_s': round(r['structures_per_s'], 2),
+                     'atoms_per_s': round(r['atoms_per_s'], 1), 'steps': 10, 'warmup': 3,
+                     'gemm': r['gemm'], 'loss': r['loss']}
+        log(f'fine-tune step: {fine_tune}')
 
     if rank == 0:
         metric, workload = describe(n, world, cells, args.strong, grid, label)
@@ -747,6 +769,7 @@ def main():
             'roofline': roofline,
             'cpu_baseline': cpu,
             'neighbor_list': nl,
+            'fine_tune': fine_tune,
             'degrees': degrees,
             'distributed': distributed,
             'kernels': kernels,

@@ -79,6 +79,66 @@ def cpu_baseline(batches, cfg, seconds):
                       'trainable model + oracle uvu TP (tests/_conv_cpu.py), torch CPU fp32'}
 
 
+def step_bench(device, steps, warmup, batch=8, rank=0, world=1, eager=False, autograd=False,
+               blas='rocblas'):
+    """The timed rehearsal step (module docstring) on `device`: builds the
+    model, the synthetic batches and the trainer, runs `warmup` untimed and
+    `steps` timed steps (barrier + synchronize around the timed region, max
+    over ranks).  Returns a dict of the measurement (bench.py's fine_tune
+    leg uses it too)."""
+    from sevennet_finetuning_amd import train
+    from sevennet_finetuning_amd.nn import SevenNetTrainable
+    model = SevenNetTrainable(device=device)
+    fisher = {n: torch.full_like(p, 1e-3) for n, p in model.named_parameters()}
+    opt = {n: p.detach().clone() for n, p in model.named_parameters()}
+    cfg = {'loss': 'huber', 'loss_param': {'delta': 0.01}, 'force_loss_weight': 1.0,
+           'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
+           'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
+           'scheduler_param': {'gamma': 0.99}, 'is_ddp': world > 1, 'device': device,
+           'hip_graph': not eager, 'explicit_grad': not autograd, 'blas': blas,
+           'continue': {'fisher_information': fisher, 'opt_params': opt, 'ewc_lambda': 1e5}}
+    tr = train.Trainer(model, cfg)
+    n_b = 4
+    batches = make_batches(rank, 2 * n_b, batch, model.chemical_symbols)
+    dev_batches = [train.collate(b, device=device, dtype=torch.float32) for b in batches]
+    atoms_per_step = sum(int(b['num_atoms'].sum()) for b in dev_batches[:2])
+    edges = int(dev_batches[0]['edge_index'].shape[1])
+    log(f'{batch} x 54-atom structures per batch, {edges} edges; rank {rank}/{world}')
+    model.train(True)
+
+    def step(i):
+        b, m = dev_batches[(2 * i) % (2 * n_b)], dev_batches[(2 * i + 1) % (2 * n_b)]
+        return tr.rehearsal_step(b, m)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    for i in range(warmup):
+        step(i)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss, mloss = step(i)
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t)
+    structs = 2 * batch * world * steps
+    return {'ms_per_step': dt / steps * 1e3, 'structures_per_s': structs / dt,
+            'atoms_per_s': atoms_per_step * world * steps / dt, 'atoms_per_rank_step': atoms_per_step,
+            'edges_per_batch': edges, 'loss': float(loss), 'mem_loss': float(mloss),
+            'hip_graph': bool(tr.hip_graph), 'explicit_grad': tr.explicit is not None,
+            'gemm': ('libe3gnn_hip e3gnn_gemm_grouped (no rocBLAS / hipBLASLt kernel)'
+                     if tr.explicit is not None and tr.explicit.gm.lib is not None
+                     else f'torch ({blas})'),
+            'batches': batches, 'cfg': cfg}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -111,49 +171,9 @@ def main():
         rank, local, device = 0, 0, torch.device('cuda', 0)
         torch.cuda.set_device(device)
 
-    from sevennet_finetuning_amd.nn import SevenNetTrainable
-    model = SevenNetTrainable(device=device)
-    fisher = {n: torch.full_like(p, 1e-3) for n, p in model.named_parameters()}
-    opt = {n: p.detach().clone() for n, p in model.named_parameters()}
-    cfg = {'loss': 'huber', 'loss_param': {'delta': 0.01}, 'force_loss_weight': 1.0,
-           'stress_loss_weight': 0.01, 'is_train_stress': True, 'optimizer': 'adam',
-           'optim_param': {'lr': 1e-5}, 'scheduler': 'exponentiallr',
-           'scheduler_param': {'gamma': 0.99}, 'is_ddp': world > 1, 'device': device,
-           'hip_graph': not args.eager, 'explicit_grad': not args.autograd, 'blas': args.blas,
-           'continue': {'fisher_information': fisher, 'opt_params': opt, 'ewc_lambda': 1e5}}
-    tr = train.Trainer(model, cfg)
-    n_b = 4
-    batches = make_batches(rank, 2 * n_b, args.batch, model.chemical_symbols)
-    dev_batches = [train.collate(b, device=device, dtype=torch.float32) for b in batches]
-    atoms_per_step = sum(int(b['num_atoms'].sum()) for b in dev_batches[:2])
-    edges = int(dev_batches[0]['edge_index'].shape[1])
-    log(f'{args.batch} x 54-atom structures per batch, {edges} edges; rank {rank}/{world}')
-    model.train(True)
-
-    def step(i):
-        b, m = dev_batches[(2 * i) % (2 * n_b)], dev_batches[(2 * i + 1) % (2 * n_b)]
-        return tr.rehearsal_step(b, m)
-
-    def barrier():
-        if world > 1:
-            torch.distributed.barrier()
-
-    for i in range(args.warmup):
-        step(i)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss, mloss = step(i)
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=device)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t)
-    ms = dt / args.steps * 1e3
-    structs = 2 * args.batch * world * args.steps
+    r = step_bench(device, args.steps, args.warmup, args.batch, rank, world, args.eager,
+                   args.autograd, args.blas)
+    ms, batches, cfg = r['ms_per_step'], r['batches'], r['cfg']
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log('cpu baseline ...')
@@ -161,25 +181,23 @@ def main():
     if rank == 0:
         print(json.dumps({
             'metric': 'structures/sec fine-tune step (rehearsal + EWC), SevenNet-0',
-            'value': round(structs / dt, 2), 'unit': 'structures/s', 'n_gpus': world,
+            'value': round(r['structures_per_s'], 2), 'unit': 'structures/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
             'dtype': 'f32 (radial-MLP W2 products on bf16x6 MFMA pieces: f32-grade)',
             'data': 'synthetic 54-atom mixed-species diamond cells, synthetic labels/Fisher',
             'config': {'workload': f'rehearsal step: 2 x {args.batch} structures per rank '
-                                   f'({atoms_per_step} atoms), force+stress+energy Huber + EWC, '
+                                   f'({r["atoms_per_rank_step"]} atoms), force+stress+energy Huber + EWC, '
                                    'Adam, grad all-reduce',
-                       'atoms_per_rank_step': atoms_per_step, 'edges_per_batch': edges,
+                       'atoms_per_rank_step': r['atoms_per_rank_step'],
+                       'edges_per_batch': r['edges_per_batch'],
                        'parallelism': f'dp{world}',
-                       'hip_graph': bool(tr.hip_graph),
-                       'explicit_grad': tr.explicit is not None,
+                       'hip_graph': r['hip_graph'], 'explicit_grad': r['explicit_grad'],
                        # which GEMMs ran: the library's grouped GEMM (no vendor
                        # BLAS kernel in the step) or torch's with the --blas choice
-                       'gemm': ('libe3gnn_hip e3gnn_gemm_grouped (no rocBLAS / hipBLASLt kernel)'
-                                if tr.explicit is not None and tr.explicit.gm.lib is not None
-                                else f'torch ({args.blas})')},
-            'atoms_per_s': round(atoms_per_step * world * args.steps / dt, 1),
-            'loss': float(loss), 'mem_loss': float(mloss), 'cpu_baseline': cpu}), flush=True)
+                       'gemm': r['gemm']},
+            'atoms_per_s': round(r['atoms_per_s'], 1),
+            'loss': r['loss'], 'mem_loss': r['mem_loss'], 'cpu_baseline': cpu}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

@@ -929,6 +929,53 @@ __device__ __forceinline__ void dh2_pair_g(f32x4 (&dh2)[4], const float (&da)[4]
   }
 }
 
+// both tiles of a pass at once: each W2 piece block is loaded once and feeds
+// the two tiles' products (the one-tile form above loaded the pair's pieces
+// per tile: half of the last block's dH2 operand stream)
+__device__ __forceinline__ void dh2_pair_g2(f32x4 (&dh2)[2][4], const float (&dp)[2][4], const float (&dr)[2][4],
+                                            bool two, __amdgpu_buffer_rsrc_t w2d, int pair, int lane) {
+  constexpr int NPC = E3GNN_DH2_X3 ? 2 : 3;
+  bf16x8 d[2][3];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = t < 4 ? dp[u][t] : dr[u][t - 4];
+    if constexpr (NPC == 2) {
+      bf16x8 e[2];
+      split2x8(v, e);
+      d[u][0] = e[0];
+      d[u][1] = e[1];
+    } else {
+      split3x8(v, d[u]);
+    }
+  }
+#pragma unroll
+  for (int bh = 0; bh < 4; ++bh) {
+    bf16x8 a[NPC];
+#pragma unroll
+    for (int pc = 0; pc < NPC; ++pc)
+      a[pc] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2d, lane * 16, pair * LS_PAIR_D + (pc * 4 + bh) * 1024, 0));
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      if constexpr (NPC == 2) {
+        dh2[u][bh] = mfma16(a[1], d[u][0], dh2[u][bh]);
+        dh2[u][bh] = mfma16(a[0], d[u][1], dh2[u][bh]);
+        dh2[u][bh] = mfma16(a[0], d[u][0], dh2[u][bh]);
+      } else {
+        constexpr int I[6] = {2, 1, 0, 1, 0, 0}, J[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int q = 0; q < 6; ++q) dh2[u][bh] = mfma16(a[I[q]], d[u][J[q]], dh2[u][bh]);
+      }
+    }
+  }
+}
+#ifndef E3GNN_NBR_DH2_SHARED
+#define E3GNN_NBR_DH2_SHARED 1
+#endif
+
 // the last block's dH2 on bf16 MFMA from global (L2) W2 pieces: with the
 // three-product form its operand traffic equals the f32 form's (two pieces x 4
 // hidden blocks per pair) and the MFMA cycles drop ~5x (2.60 -> 2.41 ms, same
@@ -1031,6 +1078,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 wnxt[1] = two ? w2_block_bwd<false>(hq[1], wq) : zero4();
               }
               if (nb + 2 < NBLK) load_w2b(wq, R.w2v, lane, 16 * (nb + 2));
+              float dwr2[2][4];   // both tiles' dE/dw (the shared dH2 form)
 #pragma unroll
               for (int u = 0; u < 2; ++u) {
                 if (u == 1 && !two) break;
@@ -1051,7 +1099,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                   pin<D1>(dx + r * D1);
                   pin<8>(dYa[u] + 1);
                 }
-#if E3GNN_NBR_DH2_BF16
+#if E3GNN_NBR_DH2_BF16 && E3GNN_NBR_DH2_SHARED
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dwr2[u][r] = u == 1 && !two ? 0.f : dwr[r];
+#elif E3GNN_NBR_DH2_BF16
                 // dH2^T += W2[:, pair] dw^T on bf16x6 over the block pair (K = 32
                 // channels: the pair's first block is held in dwp)
                 if (nb & 1) {
@@ -1068,6 +1119,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                   for (int r = 0; r < 4; ++r) dh2[u][bh] = mfma(bq[bh][r], dwr[r], dh2[u][bh]);
 #endif
               }
+#if E3GNN_NBR_DH2_BF16 && E3GNN_NBR_DH2_SHARED
+              if (!two) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dwr2[1][r] = 0.f;
+              }
+              // dH2^T += W2[:, pair] dw^T over the block pair for both tiles,
+              // each W2 piece loaded once (the pair's first block held in dwp)
+              if (nb & 1) {
+                dh2_pair_g2(dh2, dwp, dwr2, two, R.w2d, nb >> 1, lane);
+              } else {
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) dwp[u][r] = dwr2[u][r];
+              }
+#endif
               pin<4 * D1>(dx);
               wcur[0] = wnxt[0];
               wcur[1] = wnxt[1];

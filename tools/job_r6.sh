@@ -34,6 +34,12 @@ for s in "$@"; do
     newtests) run newtests 900 python -u -m pytest tests/test_gpu_generic.py tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread -k "bias_and_fcn or workspace or rejects" ;;
     nvetest) run nvetest 600 python -u -m pytest tests/test_gpu_native.py -x -q -s --timeout 400 --timeout-method thread -k nve_drift ;;
     gtrain) run gtrain 900 python -u -m pytest tests/test_gpu_train.py -x -q --timeout 300 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    smoke_nl0) run smoke_nl0 300 env E3GNN_NL_BF16=0 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --profile-only --no-parity-check ;;
+    pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
+    pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
+    pmcmops) run pmcmops 600 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU --kernel-trace --output-format csv -d gpurun_out/pmc_mops -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     summ) summ ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
