@@ -5,7 +5,8 @@ edges) and the 778,688-atom box (46^3 cells, 21.8M edges) on one device.
 The oracle cannot evaluate these sizes in test time, so parity is carried by
 size-independent properties (force_output.py:74-130 defines
 the quantities):
-* supercell property: a displaced 8-atom cell tiled k^3 times has
+* supercell property: a displaced 8-atom cell (and the reference's 96-atom
+  HfO2 snapshot, non-uniform degree, tiled to 96,000 atoms) tiled k^3 times has
   E = k^3 E_cell, per-image forces equal to the cell's and the same stress;
   the 8-atom cell itself is checked against the fp64 oracle here, so the
   property ties the full-size result to the oracle;
@@ -18,11 +19,15 @@ the quantities):
   block, only the centres later blocks still need) and must reproduce the
   HIP values.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
 from _systems import load_manifest_symbols, oracle_eval
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 SYMS = load_manifest_symbols()
@@ -95,6 +100,32 @@ def test_supercell_property(model, cell8, k):
     # and against the fp64 oracle directly
     assert np.abs(fk - ref['forces'][None]).max() <= F_TOL
     assert abs(big['energy'] / k ** 3 - ref['energy']) <= E_RTOL * abs(ref['energy'])
+
+
+def test_hfo2_resdat_tiled_to_96k_non_uniform_degree(model):
+    """bench.py --system hfo2's box: the reference example's HfO2 snapshot
+    (res.dat, 96 atoms, 41-49 edges per atom: the fused kernels' partial
+    tiles and lock-step tile counts vary per centre) tiled 10^3 = 96,000
+    atoms.  E = k^3 E_cell, forces repeat per image, stress equal; the cell
+    itself against the fp64 oracle."""
+    from sevennet_finetuning_amd.structures import tile
+    d = np.load(os.path.join(ROOT, 'sevennet_finetuning_amd', 'assets', 'structures', 'hfo2_resdat.npz'))
+    types = np.array([model.chemical_symbols.index(str(x)) for x in d['symbols']])
+    pos, cell = d['pos'], d['cell']
+    ref = oracle_eval(pos, cell, types)
+    one = small(model, pos, cell, types)
+    assert abs(one['energy'] - ref['energy']) <= E_RTOL * abs(ref['energy'])
+    assert np.abs(one['forces'] - ref['forces']).max() <= F_TOL
+    k = 10
+    posk, cellk = tile(pos, cell, (k, k, k))
+    big = eval_box(model, posk, cellk, np.tile(types, k ** 3))
+    deg = big['n_edges'] / len(posk)
+    assert big['n_edges'] == 4274 * k ** 3 and 44 < deg < 45
+    assert abs(big['energy'] - k ** 3 * one['energy']) <= E_RTOL * abs(big['energy'])
+    fk = big['forces'].reshape(k ** 3, len(pos), 3)
+    assert np.abs(fk - one['forces'][None]).max() <= F_TOL
+    assert np.abs(big['stress'] - one['stress']).max() <= S_TOL
+    assert np.abs(fk - ref['forces'][None]).max() <= F_TOL
 
 
 @pytest.fixture(scope='module')
