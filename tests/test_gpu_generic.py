@@ -395,3 +395,31 @@ def test_bias_and_fcn_readout_models_on_the_native_engine_vs_oracle(tmp_path, op
     assert abs(calc.results['energy'] - E) <= 2e-6 * abs(E)
     assert np.abs(calc.results['forces'] - F).max() <= 1e-4
     assert np.abs(calc.results['stress'] - (-S[[0, 1, 2, 4, 5, 3]])).max() <= 2e-6
+
+
+def test_bias_and_fcn_readout_model_decomposed_matches_serial(tmp_path):
+    """The use_bias_in_linear + readout_as_fcn deployment through the segment
+    API over two ranks (gloo, both on the box's GPU; halo exchanges of
+    parallel.py) equals its serial native evaluation: the biases and the FCN
+    readout live in the per-rank layer / readout segments."""
+    import socket
+
+    import torch.multiprocessing as mp
+    from _parallel_workers import worker
+    from sevennet_finetuning_amd.model import E3GNNModel
+    from sevennet_finetuning_amd.structures import tile
+    dep = _option_deployment(str(tmp_path / 'dep'), use_bias_in_linear=True, readout_as_fcn=True)
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / 'opt_2.npz')
+    mp.spawn(worker, args=(2, port, 'hfo2_resdat', 'hip', out, dep, (2, 2, 1)), nprocs=2, join=True)
+    got = np.load(out)
+    model = E3GNNModel(dep, device=DEV)
+    d = np.load(f'{GOLD}/hfo2_resdat.npz')
+    types = np.array([model.chemical_symbols.index(str(s)) for s in d['symbols']])
+    pos4, cell4 = tile(d['pos'], d['cell'], (2, 2, 1))
+    one = _run(model, pos4, cell4, np.tile(types, 4))
+    assert got['n_ghost'][0] > 0 and got['repeat_same'][0]
+    assert abs(float(got['energy']) - one['energy']) <= 2e-6 * abs(one['energy'])
+    assert np.abs(got['forces'] - one['forces']).max() <= 2e-5
