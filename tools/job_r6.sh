@@ -40,6 +40,10 @@ for s in "$@"; do
     pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
     pmcmops) run pmcmops 600 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU --kernel-trace --output-format csv -d gpurun_out/pmc_mops -o run -- python bench.py --steps 1 --warmup 1 --profile-only --no-parity-check ;;
+    proftraint) run proftraint 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_traint -o run -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    trainops) run trainops 300 python tools/prof_train_ops.py ;;
+    opttests) run opttests 900 python -u -m pytest tests/test_gpu_generic.py tests/test_gpu_fullsize.py -x -q --timeout 400 --timeout-method thread -k "bias_and_fcn or hfo2_resdat" ;;
+    profbench) run profbench 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_profbench -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fine-tune ;;
     summ) summ ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
