@@ -736,6 +736,9 @@ __global__ void k_gather_rows(int j_begin, int n, int D, const int* __restrict__
 // in flight -- 85 VGPRs, 5 waves per SIMD: 1.39 vs 0.94 ms per 480-wide
 // launch; the occupancy of this 20-register form hides the row latency better;
 // rows in flight U = 2 / 4 / 8 and non-temporal loads measured the same.)
+#ifndef E3GNN_GATHER_V2
+#define E3GNN_GATHER_V2 0
+#endif
 #ifndef E3GNN_GATHER_U
 #define E3GNN_GATHER_U 4
 #endif
@@ -759,6 +762,33 @@ __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict
     s.z += v.z;
     s.w += v.w;
   };
+#if E3GNN_GATHER_V2
+  // the node's row ids once per 64 (lane i holds perm[b + i]), each row id
+  // broadcast from its lane (v_readlane: a scalar, no dependent index load
+  // per batch of rows), the same ascending order as below
+  if (en - b <= 64) {
+    const int myidx = b + lane < en ? perm[b + lane] : 0;
+    const int cnt = en - b;
+    for (int c = lane; c < D4; c += 64) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      int k = 0;
+      for (; k + U <= cnt; k += U) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int row = __builtin_amdgcn_readlane(myidx, k + u);
+          v[u] = src[(int64_t)row * D4 + c];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) add(s, v[u]);
+      }
+      for (; k < cnt; ++k) add(s, src[(int64_t)__builtin_amdgcn_readlane(myidx, k) * D4 + c]);
+      if (acc) add(s, dst[(int64_t)j * D4 + c]);
+      dst[(int64_t)j * D4 + c] = s;
+    }
+    return;
+  }
+#endif
   for (int c = lane; c < D4; c += 64) {
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     int q = b;
