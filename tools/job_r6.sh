@@ -43,7 +43,8 @@ for s in "$@"; do
     proftraint) run proftraint 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_traint -o run -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     trainops) run trainops 300 python tools/prof_train_ops.py ;;
     opttests) run opttests 900 python -u -m pytest tests/test_gpu_generic.py tests/test_gpu_fullsize.py -x -q --timeout 400 --timeout-method thread -k "bias_and_fcn or hfo2_resdat" ;;
-    profbench) run profbench 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_profbench -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fine-tune ;;
+    profbench) run profbench 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_profbench -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fine-tune --no-parity-check ;;
+    stamps_*) v=${s#stamps_}; run stamps_$v 300 python tools/stamps.py sevennet_finetuning_amd/variants/$v.so ;;
     summ) summ ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
