@@ -1357,6 +1357,9 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 #ifndef E3GNN_ABL_NOSTAGE
 #define E3GNN_ABL_NOSTAGE 0
 #endif
+#ifndef E3GNN_ABL_XLOCAL
+#define E3GNN_ABL_XLOCAL 0
+#endif
 template <class L>
 __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_eu(BwdLsWaves<L>::v, BwdLsWaves<L>::v))) void k_conv_bwd_ls(
     const int* __restrict__ row_ptr, const int* __restrict__ nbr, const float* __restrict__ emb,
@@ -1456,7 +1459,11 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
     const int q0 = beg + 16 * t;
     const bool act = q0 < end;   // wave-uniform
     const int er = (act && q0 + col < end) ? q0 + col : -1;
+#if E3GNN_ABL_XLOCAL   // timing-only: every edge reads the centre's own row (L2-hot)
+    const int vx = (er >= 0 ? c : 0) * L::DX * 4;
+#else
     const int vx = (er >= 0 ? nbr[er] : 0) * L::DX * 4;
+#endif
     float xpf[20];   // the lane's 4 channels x D1 of the next channel group
     float g0pf[4];   // DMA mode: path 0's dE/dagg of that group (l1 = 0 groups)
     auto load_group = [&](auto Iq, int jq) {

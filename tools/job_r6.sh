@@ -45,6 +45,10 @@ for s in "$@"; do
     opttests) run opttests 900 python -u -m pytest tests/test_gpu_generic.py tests/test_gpu_fullsize.py -x -q --timeout 400 --timeout-method thread -k "bias_and_fcn or hfo2_resdat" ;;
     profbench) run profbench 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_profbench -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fine-tune --no-parity-check ;;
     stamps_*) v=${s#stamps_}; run stamps_$v 300 python tools/stamps.py sevennet_finetuning_amd/variants/$v.so ;;
+    tb) run tb 300 python bench_train.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+    tb_noside) run tb_noside 300 env E3GNN_TRAIN_SIDE=0 python bench_train.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+    tbs_*) v=${s#tbs_}; run tbs_$v 300 env E3GNN_TRAIN_SIDE=$v python bench_train.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+    tbsprof_*) v=${s#tbsprof_}; run tbsprof_$v 300 env E3GNN_TRAIN_SIDE=$v rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${P}_tbsprof_$v -o run -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     summ) summ ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
