@@ -879,6 +879,17 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
 #ifndef E3GNN_DH2_X3
 #define E3GNN_DH2_X3 1
 #endif
+// operand pieces requested before the MFMAs that consume them (default;
+// =0 the per-block interleaved order the compiler chose): the middle
+// backward's pair images from LDS (E3GNN_LDS_EARLY: 5.56 -> 5.46 ms per launch,
+// same box) and the last block's dH2 pieces from L2 (E3GNN_NBR_EARLY: 2.21 ->
+// 2.10 ms; profiles/r06_s10_*)
+#ifndef E3GNN_LDS_EARLY
+#define E3GNN_LDS_EARLY 1
+#endif
+#ifndef E3GNN_NBR_EARLY
+#define E3GNN_NBR_EARLY 1
+#endif
 constexpr int LS_BLK = 6144;            // bytes of one w2v column block (3 pieces x 2 halves x 1 KB)
 constexpr int LS_PAIR_W = 2 * LS_BLK;   // the pair's two w-recompute operand blocks
 constexpr int LS_PAIR_D = 12288;        // the pair's dH2 operand (w2d: 3 pieces x 4 bh x 1 KB)
@@ -950,13 +961,27 @@ __device__ __forceinline__ void dh2_pair_g2(f32x4 (&dh2)[2][4], const float (&dp
       split3x8(v, d[u]);
     }
   }
+#if E3GNN_NBR_EARLY
+  // every piece of the pair requested first (one L2 latency per pair)
+  bf16x8 aa[4][NPC];
+#pragma unroll
+  for (int bh = 0; bh < 4; ++bh)
+#pragma unroll
+    for (int pc = 0; pc < NPC; ++pc)
+      aa[bh][pc] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2d, lane * 16, pair * LS_PAIR_D + (pc * 4 + bh) * 1024, 0));
+#endif
 #pragma unroll
   for (int bh = 0; bh < 4; ++bh) {
     bf16x8 a[NPC];
 #pragma unroll
     for (int pc = 0; pc < NPC; ++pc)
+#if E3GNN_NBR_EARLY
+      a[pc] = aa[bh][pc];
+#else
       a[pc] = __builtin_bit_cast(
           bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w2d, lane * 16, pair * LS_PAIR_D + (pc * 4 + bh) * 1024, 0));
+#endif
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (u == 1 && !two) break;
@@ -1231,6 +1256,23 @@ __device__ __forceinline__ void dh2_pair(f32x4 (&dh2)[4], const float (&da)[4], 
       for (int t = 0; t < 8; ++t) v[t] = t < 4 ? da[t] : db[t - 4];
       split2x8(v, d);
     }
+#if E3GNN_LDS_EARLY
+    // every piece read first, fenced from the MFMAs (one exposed LDS latency
+    // for the pair, not one per hidden block)
+    bf16x8 a[4][2];
+#pragma unroll
+    for (int bh = 0; bh < 4; ++bh)
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc)
+        a[bh][pc] = *reinterpret_cast<const bf16x8*>(pimg + ((pc * 4 + bh) * 64 + lane) * 16);
+    phase();
+#pragma unroll
+    for (int bh = 0; bh < 4; ++bh) {
+      dh2[bh] = mfma16(a[bh][1], d[0], dh2[bh]);
+      dh2[bh] = mfma16(a[bh][0], d[1], dh2[bh]);
+      dh2[bh] = mfma16(a[bh][0], d[0], dh2[bh]);
+    }
+#else
 #pragma unroll
     for (int bh = 0; bh < 4; ++bh) {
       bf16x8 a[2];
@@ -1241,6 +1283,7 @@ __device__ __forceinline__ void dh2_pair(f32x4 (&dh2)[4], const float (&da)[4], 
       dh2[bh] = mfma16(a[0], d[1], dh2[bh]);
       dh2[bh] = mfma16(a[0], d[0], dh2[bh]);
     }
+#endif
     return;
   }
   bf16x8 d[3];
@@ -1566,11 +1609,20 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                   if constexpr (STAMPED) STAMP(2);   // barriers + staging
                   if (act) {
                     __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
+#if E3GNN_LDS_EARLY
+                    Op3 wq, wq1;   // both blocks' pieces read first
+                    lds_op3<LS_WPC>(wq, pimg, lane);
+                    lds_op3<LS_WPC>(wq1, pimg + LS_IBLK, lane);
+                    phase();
+                    wv0 = w2_block_bwd<false>(hq, wq);
+                    wv1 = w2_block_bwd<false>(hq, wq1);
+#else
                     Op3 wq;
                     lds_op3<LS_WPC>(wq, pimg, lane);
                     wv0 = w2_block_bwd<false>(hq, wq);
                     lds_op3<LS_WPC>(wq, pimg + LS_IBLK, lane);
                     wv1 = w2_block_bwd<false>(hq, wq);
+#endif
                     __builtin_amdgcn_s_setprio(0);
                   }
                   if constexpr (STAMPED) STAMP(3);   // w recompute

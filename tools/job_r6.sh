@@ -6,9 +6,11 @@ mkdir -p gpurun_out
 P=${JOB_PREFIX:-j}
 run() {  # run <name> <secs> <cmd...>: stop the job on a crash-like exit
   local name=$1 secs=$2; shift 2
-  timeout -k 10 "$secs" "$@" > "gpurun_out/${P}_$name.log" 2>&1
+  local f="gpurun_out/${P}_$name.log" n=2   # a repeated step keeps every log
+  while [ -e "$f" ]; do f="gpurun_out/${P}_${name}_r$n.log"; n=$((n + 1)); done
+  timeout -k 10 "$secs" "$@" > "$f" 2>&1
   local rc=$?
-  echo "=== $name rc=$rc"; tail -n 4 "gpurun_out/${P}_$name.log"
+  echo "=== $name rc=$rc"; tail -n 4 "$f"
   if [ $rc -gt 1 ]; then echo "ABORT after $name"; exit $rc; fi
   return 0
 }
