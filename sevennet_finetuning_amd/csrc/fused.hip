@@ -799,7 +799,7 @@ __device__ __forceinline__ void load_gm(float* gmN, __amdgpu_buffer_rsrc_t Rg, i
 // demb += (rows < 8).  `er`: the edge of the lane's slot c (-1: padded slot).
 __device__ __forceinline__ void mlp_bwd_chain_ids(const WRes& R, const float* __restrict__ emb, int er,
                                                   int lane, const f32x4 (&dh2)[4],
-                                                  float* __restrict__ demb) {
+                                                  float* __restrict__ demb, const float* dold = nullptr) {
   const int g = lane >> 4;
   MlpT m;
   {
@@ -841,16 +841,21 @@ __device__ __forceinline__ void mlp_bwd_chain_ids(const WRes& R, const float* __
     de = w2_block<false>(dq, wq);   // rows 4g + r < 8: the embedding dims
   }
   if (g < 2 && er >= 0) {
+    if (dold) {   // (the caller read the old values at the tile start)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) demb[(int64_t)er * 8 + 4 * g + r] += de[r];
+      for (int r = 0; r < 4; ++r) demb[(int64_t)er * 8 + 4 * g + r] = dold[r] + de[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) demb[(int64_t)er * 8 + 4 * g + r] += de[r];
+    }
   }
 }
 // the same for the CSR edge tile [e0, min(e0 + 16, end))
 __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __restrict__ emb, int e0,
                                               int end, int lane, const f32x4 (&dh2)[4],
-                                              float* __restrict__ demb) {
+                                              float* __restrict__ demb, const float* dold = nullptr) {
   const int e = e0 + (lane & 15);
-  mlp_bwd_chain_ids(R, emb, e < end ? e : -1, lane, dh2, demb);
+  mlp_bwd_chain_ids(R, emb, e < end ? e : -1, lane, dh2, demb, dold);
 }
 
 // Backward of the last block (224 message channels), one wave per NEIGHBOUR
@@ -884,6 +889,12 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
 // backward's pair images from LDS (E3GNN_LDS_EARLY: 5.56 -> 5.46 ms per launch,
 // same box) and the last block's dH2 pieces from L2 (E3GNN_NBR_EARLY: 2.21 ->
 // 2.10 ms; profiles/r06_s10_*)
+// the middle blocks' tile-end read-modify-writes of dE/du and dE/demb: the
+// old values read at the tile start (E3GNN_RMW_PF: 5.39 -> 5.34 ms per launch,
+// same box; profiles/r06_s12_*)
+#ifndef E3GNN_RMW_PF
+#define E3GNN_RMW_PF 1
+#endif
 #ifndef E3GNN_LDS_EARLY
 #define E3GNN_LDS_EARLY 1
 #endif
@@ -1419,6 +1430,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
   constexpr bool DMA = DM_::v;
   constexpr bool RDB = !DMA && E3GNN_LS_DB && DM_::fits;   // double-buffered register staging
   constexpr bool TWO = DMA || RDB;                         // two images, one barrier per pair
+  constexpr bool RPF = E3GNN_RMW_PF && L::KIND == 1;       // (the first block: no VGPRs to spare)
   constexpr int OFF0 = TWO ? DM_::OFF0 : 0, DMS = L::DM - OFF0;   // dE/dagg floats staged per centre
   static_assert(!TWO || (L::P[0].l1 == 0 && L::P[0].l2 == 0 && L::P[0].l3 == 0 && L::P[0].moff == 0 &&
                          OFF0 % 4 == 0), "path 0 is the 0e x 0e -> 0e slice at the row start");
@@ -1516,6 +1528,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
       if constexpr (OFF0 > 0 && Iq == 0) ldv<4>(Rg0, 4 * g * 4, 16 * jq * 4, g0pf);
     };
     float y[9];
+    float gu_old[3] = {0.f, 0.f, 0.f}, de_old[4] = {0.f, 0.f, 0.f, 0.f};   // E3GNN_RMW_PF
     Op3 hq;
     // neighbour rows (lanes without an edge read row 0: harmless, their y
     // and w are 0); issued unconditionally, like every vector-memory op
@@ -1534,6 +1547,18 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
       float b[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) b[s] = er >= 0 ? emb[(int64_t)er * 8 + 4 * s + g] : 0.f;
+      if constexpr (RPF) {
+        // the tile end's read-modify-writes (dE/du, dE/demb of the lane's
+        // edge): old values read here, their latency under the whole tile
+        if (g == 0 && er >= 0) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k) gu_old[k] = dgu[(int64_t)er * 3 + k];
+        }
+        if (g < 2 && er >= 0) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) de_old[k] = demb[(int64_t)er * 8 + 4 * g + k];
+        }
+      }
       MlpT m;
       mlp_chain(R, b, lane, m);
       f32x4 h2[4];
@@ -1681,12 +1706,18 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
         const float gy = s3 * d[1] + c15 * (ux * d[4] + uz * d[6]) + 2.f * s5 * uy * d[5];
         const float gz = s3 * d[2] + c15 * (ux * d[3] + uy * d[6]) - s5 * uz * d[5] + c15 * uz * d[7];
         float* o = dgu + (int64_t)er * 3;
-        o[0] += gx;
-        o[1] += gy;
-        o[2] += gz;
+        if constexpr (RPF) {
+          o[0] = gu_old[0] + gx;
+          o[1] = gu_old[1] + gy;
+          o[2] = gu_old[2] + gz;
+        } else {
+          o[0] += gx;
+          o[1] += gy;
+          o[2] += gz;
+        }
       }
       if constexpr (STAMPED) STAMP(5);
-      mlp_bwd_chain(R, emb, q0, end, lane, dh2, demb);
+      mlp_bwd_chain(R, emb, q0, end, lane, dh2, demb, RPF ? de_old : nullptr);
     }
     if constexpr (STAMPED) STAMP(6);   // tile end: dE/dY sums, MLP chain backward
   }
