@@ -898,6 +898,11 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
 #ifndef E3GNN_LDS_EARLY
 #define E3GNN_LDS_EARLY 1
 #endif
+// the same for the last block's per-pass dE/du and dE/demb (E3GNN_NBR_RMW_PF:
+// 2.13 -> 2.09-2.12 ms, same box; profiles/r06_s12_*)
+#ifndef E3GNN_NBR_RMW_PF
+#define E3GNN_NBR_RMW_PF 1
+#endif
 #ifndef E3GNN_NBR_EARLY
 #define E3GNN_NBR_EARLY 1
 #endif
@@ -1044,6 +1049,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     load_w2b(wq, R.w2b, lane, L::P[0].woff);
     int er[2], vg[2];
     float y[2][9];
+    // E3GNN_NBR_RMW_PF: the pass end's dE/du and dE/demb old values, read here
+    float gu_old[2][3], de_old[2][4];
     Op3 hq[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1052,6 +1059,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       vg[u] = (er[u] >= 0 ? center[er[u]] * L::DM : n_centers * L::DM) * 4;
 #pragma unroll
       for (int k = 0; k < 9; ++k) y[u][k] = er[u] >= 0 ? Y[(int64_t)er[u] * 9 + k] : 0.f;
+      if constexpr (E3GNN_NBR_RMW_PF) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) gu_old[u][k] = (g == 0 && er[u] >= 0) ? dgu[(int64_t)er[u] * 3 + k] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) de_old[u][k] = (g < 2 && er[u] >= 0) ? demb[(int64_t)er[u] * 8 + 4 * g + k] : 0.f;
+      }
       if (u == 1 && !two) continue;
       float b[2];
 #pragma unroll
@@ -1206,12 +1219,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const float gy = s3 * d[1] + c15 * (ux * d[4] + uz * d[6]) + 2.f * s5 * uy * d[5];
         const float gz = s3 * d[2] + c15 * (ux * d[3] + uy * d[6]) - s5 * uz * d[5] + c15 * uz * d[7];
         float* o = dgu + (int64_t)er[u] * 3;
-        o[0] += gx;
-        o[1] += gy;
-        o[2] += gz;
+        if constexpr (E3GNN_NBR_RMW_PF) {
+          o[0] = gu_old[u][0] + gx;
+          o[1] = gu_old[u][1] + gy;
+          o[2] = gu_old[u][2] + gz;
+        } else {
+          o[0] += gx;
+          o[1] += gy;
+          o[2] += gz;
+        }
       }
       phase();
-      mlp_bwd_chain_ids(R, emb, er[u], lane, dh2[u], demb);
+      mlp_bwd_chain_ids(R, emb, er[u], lane, dh2[u], demb, E3GNN_NBR_RMW_PF ? de_old[u] : nullptr);
     }
   }
   phase();
