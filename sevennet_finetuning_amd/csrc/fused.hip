@@ -1358,8 +1358,8 @@ __device__ __forceinline__ int ls_tiles(const int* __restrict__ row_ptr, int cb,
 // group's neighbour rows prefetched); dH2 of the pair on bf16x6 at its end.
 // waves per SIMD: the first block (128 input channels, 1,152 message channels:
 // 42 KB of LDS per workgroup) runs three (168 VGPRs with a few spills
-// measured 2.57 -> 2.27 ms against two), the middle blocks two (244 VGPRs;
-// their 75 KB of LDS allows no more)
+// measured 2.57 -> 2.27 ms against two), the middle blocks two (225 VGPRs;
+// their 80.9 KB of LDS allows no more)
 template <class L>
 struct BwdLsWaves {
   static constexpr int v = L::KIND == 0 ? 3 : 2;

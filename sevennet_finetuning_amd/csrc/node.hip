@@ -739,6 +739,15 @@ __global__ void k_gather_rows(int j_begin, int n, int D, const int* __restrict__
 #ifndef E3GNN_GATHER_V2
 #define E3GNN_GATHER_V2 0
 #endif
+// rows of 65..128 float4 (SevenNet-0's middle blocks: 120): both halves of a
+// row per pass, 8 rows in flight (E3GNN_GATHER_2H: 3.22 -> 3.13-3.15 ms for
+// the three launches of a step, same box; profiles/r06_s14_*)
+#ifndef E3GNN_GATHER_2H
+#define E3GNN_GATHER_2H 1
+#endif
+#ifndef E3GNN_GATHER_U2
+#define E3GNN_GATHER_U2 8
+#endif
 #ifndef E3GNN_GATHER_U
 #define E3GNN_GATHER_U 4
 #endif
@@ -786,6 +795,43 @@ __global__ void k_gather_rows4(int j_begin, int n, int D4, const int* __restrict
       if (acc) add(s, dst[(int64_t)j * D4 + c]);
       dst[(int64_t)j * D4 + c] = s;
     }
+    return;
+  }
+#endif
+#if E3GNN_GATHER_2H
+  // rows of 65..128 float4: both halves of each row in the same pass (twice
+  // the loads in flight per lane, one pass over the row indices)
+  if (D4 > 64 && D4 <= 128) {
+    constexpr int U2 = E3GNN_GATHER_U2;
+    const int c0 = lane, c1 = lane + 64;
+    const bool h1 = c1 < D4;
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+    int q = b;
+    for (; q + U2 <= en; q += U2) {
+      float4 v0[U2], v1[U2];
+#pragma unroll
+      for (int u = 0; u < U2; ++u) {
+        const int64_t row = (int64_t)perm[q + u] * D4;
+        v0[u] = src[row + c0];
+        v1[u] = h1 ? src[row + c1] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U2; ++u) {
+        add(s0, v0[u]);
+        add(s1, v1[u]);
+      }
+    }
+    for (; q < en; ++q) {
+      const int64_t row = (int64_t)perm[q] * D4;
+      add(s0, src[row + c0]);
+      if (h1) add(s1, src[row + c1]);
+    }
+    if (acc) {
+      add(s0, dst[(int64_t)j * D4 + c0]);
+      if (h1) add(s1, dst[(int64_t)j * D4 + c1]);
+    }
+    dst[(int64_t)j * D4 + c0] = s0;
+    if (h1) dst[(int64_t)j * D4 + c1] = s1;
     return;
   }
 #endif
