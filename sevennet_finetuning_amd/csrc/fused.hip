@@ -1424,6 +1424,19 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const char*)p;
 }
+// wave priority around the lock-step backward's MFMA bursts (E3GNN_LS_PRIO:
+// 1 raise it there, 0 never)
+#ifndef E3GNN_LS_PRIO
+#define E3GNN_LS_PRIO 1
+#endif
+template <int P>
+__device__ __forceinline__ void ls_prio_c() { __builtin_amdgcn_s_setprio(P); }
+__device__ __forceinline__ void ls_prio(int p) {
+  if constexpr (E3GNN_LS_PRIO) {
+    if (p) ls_prio_c<1>();
+    else ls_prio_c<0>();
+  }
+}
 #ifndef E3GNN_ABL_NOBAR
 #define E3GNN_ABL_NOBAR 0
 #endif
@@ -1652,7 +1665,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                   }
                   if constexpr (STAMPED) STAMP(2);   // barriers + staging
                   if (act) {
-                    __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
+                    ls_prio(1);   // MFMA bursts first
 #if E3GNN_LDS_EARLY
                     Op3 wq, wq1;   // both blocks' pieces read first
                     lds_op3<LS_WPC>(wq, pimg, lane);
@@ -1667,7 +1680,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                     lds_op3<LS_WPC>(wq, pimg + LS_IBLK, lane);
                     wv1 = w2_block_bwd<false>(hq, wq);
 #endif
-                    __builtin_amdgcn_s_setprio(0);
+                    ls_prio(0);
                   }
                   if constexpr (STAMPED) STAMP(3);   // w recompute
                 }
@@ -1689,9 +1702,9 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
                   pin<8>(dYa + 1);
                   if constexpr (ODD) {
                     if constexpr (STAMPED) STAMP(5);   // tensor product (+ stores)
-                    __builtin_amdgcn_s_setprio(1);   // MFMA bursts first
+                    ls_prio(1);   // MFMA bursts first
                     dh2_pair(dh2, dwp, dwr, pimg + LS_IW, lane);
-                    __builtin_amdgcn_s_setprio(0);
+                    ls_prio(0);
                     if constexpr (STAMPED) STAMP(4);   // dH2 (split + MFMA)
                   } else {
 #pragma unroll
