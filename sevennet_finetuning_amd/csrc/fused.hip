@@ -318,7 +318,7 @@ struct MlpT {
 // (w2_block: act(a1) split in three bf16 pieces in its accumulator layout, W1
 // pre-split in the same operand order, MlpW::w1b): 48 MFMAs x 16 cycles
 // instead of 64 x 32 on v_mfma_f32_16x16x4_f32, f32-grade.
-__device__ __forceinline__ void mlp_chain(const WRes& R, const float (&b)[2], int lane, MlpT& m) {
+__device__ __forceinline__ void mlp_layer0(const WRes& R, const float (&b)[2], int lane, f32x4 (&a1)[4]) {
   const int g = lane >> 4, c = lane & 15;
   const int v0 = (g * 64 + c) * 4;  // W0s[4s + g][16 bh + c]
 #pragma unroll
@@ -326,8 +326,11 @@ __device__ __forceinline__ void mlp_chain(const WRes& R, const float (&b)[2], in
     f32x4 acc = zero4();
 #pragma unroll
     for (int s = 0; s < 2; ++s) acc = mfma(ldw(R.w0, v0, (4 * s * 64 + 16 * bh) * 4), b[s], acc);
-    m.a1[bh] = acc;
+    a1[bh] = acc;
   }
+}
+__device__ __forceinline__ void mlp_chain(const WRes& R, const float (&b)[2], int lane, MlpT& m) {
+  mlp_layer0(R, b, lane, m.a1);
   Op3 hq;
   {
     f32x4 h1[4];
@@ -799,10 +802,16 @@ __device__ __forceinline__ void load_gm(float* gmN, __amdgpu_buffer_rsrc_t Rg, i
 // demb += (rows < 8).  `er`: the edge of the lane's slot c (-1: padded slot).
 __device__ __forceinline__ void mlp_bwd_chain_ids(const WRes& R, const float* __restrict__ emb, int er,
                                                   int lane, const f32x4 (&dh2)[4],
-                                                  float* __restrict__ demb, const float* dold = nullptr) {
+                                                  float* __restrict__ demb, const float* dold = nullptr,
+                                                  const float* bk = nullptr, const f32x4* a2k = nullptr) {
   const int g = lane >> 4;
   MlpT m;
-  {
+  if (a2k) {   // (the tile start's layer-1 pre-activations kept: layer 0 only)
+    const float b[2] = {bk[0], bk[1]};
+    mlp_layer0(R, b, lane, m.a1);
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) m.a2[bb] = a2k[bb];
+  } else {
     float b[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) b[s] = er >= 0 ? emb[(int64_t)er * 8 + 4 * s + g] : 0.f;
@@ -853,9 +862,10 @@ __device__ __forceinline__ void mlp_bwd_chain_ids(const WRes& R, const float* __
 // the same for the CSR edge tile [e0, min(e0 + 16, end))
 __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __restrict__ emb, int e0,
                                               int end, int lane, const f32x4 (&dh2)[4],
-                                              float* __restrict__ demb, const float* dold = nullptr) {
+                                              float* __restrict__ demb, const float* dold = nullptr,
+                                              const float* bk = nullptr, const f32x4* a2k = nullptr) {
   const int e = e0 + (lane & 15);
-  mlp_bwd_chain_ids(R, emb, e < end ? e : -1, lane, dh2, demb, dold);
+  mlp_bwd_chain_ids(R, emb, e < end ? e : -1, lane, dh2, demb, dold, bk, a2k);
 }
 
 // Backward of the last block (224 message channels), one wave per NEIGHBOUR
@@ -892,6 +902,13 @@ __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __rest
 // the middle blocks' tile-end read-modify-writes of dE/du and dE/demb: the
 // old values read at the tile start (E3GNN_RMW_PF: 5.39 -> 5.34 ms per launch,
 // same box; profiles/r06_s12_*)
+// the middle blocks' tile-start layer-1 pre-activations (a2) and embedding
+// values kept to the tile end, whose MLP chain backward then recomputes layer
+// 0 only (E3GNN_KEEP_A2: 5.38-5.39 -> 5.21-5.27 ms per launch, same box;
+// profiles/r06_s16_*)
+#ifndef E3GNN_KEEP_A2
+#define E3GNN_KEEP_A2 1
+#endif
 #ifndef E3GNN_RMW_PF
 #define E3GNN_RMW_PF 1
 #endif
@@ -1463,6 +1480,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
   constexpr bool RDB = !DMA && E3GNN_LS_DB && DM_::fits;   // double-buffered register staging
   constexpr bool TWO = DMA || RDB;                         // two images, one barrier per pair
   constexpr bool RPF = E3GNN_RMW_PF && L::KIND == 1;       // (the first block: no VGPRs to spare)
+  constexpr bool KA2 = E3GNN_KEEP_A2 && L::KIND == 1;
   constexpr int OFF0 = TWO ? DM_::OFF0 : 0, DMS = L::DM - OFF0;   // dE/dagg floats staged per centre
   static_assert(!TWO || (L::P[0].l1 == 0 && L::P[0].l2 == 0 && L::P[0].l3 == 0 && L::P[0].moff == 0 &&
                          OFF0 % 4 == 0), "path 0 is the 0e x 0e -> 0e slice at the row start");
@@ -1561,6 +1579,8 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
     };
     float y[9];
     float gu_old[3] = {0.f, 0.f, 0.f}, de_old[4] = {0.f, 0.f, 0.f, 0.f};   // E3GNN_RMW_PF
+    f32x4 a2k[4];   // E3GNN_KEEP_A2: layer-1 pre-activations of the tile, kept to its end
+    float bk[2];
     Op3 hq;
     // neighbour rows (lanes without an edge read row 0: harmless, their y
     // and w are 0); issued unconditionally, like every vector-memory op
@@ -1593,6 +1613,12 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
       }
       MlpT m;
       mlp_chain(R, b, lane, m);
+      if constexpr (KA2) {
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) a2k[bb] = m.a2[bb];
+        bk[0] = b[0];
+        bk[1] = b[1];
+      }
       f32x4 h2[4];
 #pragma unroll
       for (int bb = 0; bb < 4; ++bb)
@@ -1749,7 +1775,8 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
         }
       }
       if constexpr (STAMPED) STAMP(5);
-      mlp_bwd_chain(R, emb, q0, end, lane, dh2, demb, RPF ? de_old : nullptr);
+      mlp_bwd_chain(R, emb, q0, end, lane, dh2, demb, RPF ? de_old : nullptr, KA2 ? bk : nullptr,
+                    KA2 ? a2k : nullptr);
     }
     if constexpr (STAMPED) STAMP(6);   // tile end: dE/dY sums, MLP chain backward
   }
