@@ -803,12 +803,18 @@ __device__ __forceinline__ void load_gm(float* gmN, __amdgpu_buffer_rsrc_t Rg, i
 __device__ __forceinline__ void mlp_bwd_chain_ids(const WRes& R, const float* __restrict__ emb, int er,
                                                   int lane, const f32x4 (&dh2)[4],
                                                   float* __restrict__ demb, const float* dold = nullptr,
-                                                  const float* bk = nullptr, const f32x4* a2k = nullptr) {
+                                                  const float* bk = nullptr, const f32x4* a2k = nullptr,
+                                                  const f32x4* a1k = nullptr) {
   const int g = lane >> 4;
   MlpT m;
   if (a2k) {   // (the tile start's layer-1 pre-activations kept: layer 0 only)
-    const float b[2] = {bk[0], bk[1]};
-    mlp_layer0(R, b, lane, m.a1);
+    if (a1k) {   // (and layer 0's: nothing recomputed)
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) m.a1[bb] = a1k[bb];
+    } else {
+      const float b[2] = {bk[0], bk[1]};
+      mlp_layer0(R, b, lane, m.a1);
+    }
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) m.a2[bb] = a2k[bb];
   } else {
@@ -863,9 +869,10 @@ __device__ __forceinline__ void mlp_bwd_chain_ids(const WRes& R, const float* __
 __device__ __forceinline__ void mlp_bwd_chain(const WRes& R, const float* __restrict__ emb, int e0,
                                               int end, int lane, const f32x4 (&dh2)[4],
                                               float* __restrict__ demb, const float* dold = nullptr,
-                                              const float* bk = nullptr, const f32x4* a2k = nullptr) {
+                                              const float* bk = nullptr, const f32x4* a2k = nullptr,
+                                              const f32x4* a1k = nullptr) {
   const int e = e0 + (lane & 15);
-  mlp_bwd_chain_ids(R, emb, e < end ? e : -1, lane, dh2, demb, dold, bk, a2k);
+  mlp_bwd_chain_ids(R, emb, e < end ? e : -1, lane, dh2, demb, dold, bk, a2k, a1k);
 }
 
 // Backward of the last block (224 message channels), one wave per NEIGHBOUR
@@ -1377,9 +1384,12 @@ __device__ __forceinline__ int ls_tiles(const int* __restrict__ row_ptr, int cb,
 // 42 KB of LDS per workgroup) runs three (168 VGPRs with a few spills
 // measured 2.57 -> 2.27 ms against two), the middle blocks two (225 VGPRs;
 // their 80.9 KB of LDS allows no more)
+#ifndef E3GNN_LS_FIRST_WAVES
+#define E3GNN_LS_FIRST_WAVES 3
+#endif
 template <class L>
 struct BwdLsWaves {
-  static constexpr int v = L::KIND == 0 ? 3 : 2;
+  static constexpr int v = L::KIND == 0 ? E3GNN_LS_FIRST_WAVES : 2;
 };
 // centres (waves) per workgroup: 4; E3GNN_BWD_WPG = 8 (A/B) gives the middle
 // block one 8-wave workgroup per CU sharing each staged W2 pair (124 KB LDS)
@@ -1479,8 +1489,9 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
   constexpr bool DMA = DM_::v;
   constexpr bool RDB = !DMA && E3GNN_LS_DB && DM_::fits;   // double-buffered register staging
   constexpr bool TWO = DMA || RDB;                         // two images, one barrier per pair
-  constexpr bool RPF = E3GNN_RMW_PF && L::KIND == 1;       // (the first block: no VGPRs to spare)
-  constexpr bool KA2 = E3GNN_KEEP_A2 && L::KIND == 1;
+  // (the first block at three waves per SIMD: no VGPRs to spare)
+  constexpr bool RPF = E3GNN_RMW_PF && (L::KIND == 1 || BwdLsWaves<L>::v == 2);
+  constexpr bool KA2 = E3GNN_KEEP_A2 && (L::KIND == 1 || BwdLsWaves<L>::v == 2);
   constexpr int OFF0 = TWO ? DM_::OFF0 : 0, DMS = L::DM - OFF0;   // dE/dagg floats staged per centre
   static_assert(!TWO || (L::P[0].l1 == 0 && L::P[0].l2 == 0 && L::P[0].l3 == 0 && L::P[0].moff == 0 &&
                          OFF0 % 4 == 0), "path 0 is the 0e x 0e -> 0e slice at the row start");
@@ -1580,6 +1591,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
     float y[9];
     float gu_old[3] = {0.f, 0.f, 0.f}, de_old[4] = {0.f, 0.f, 0.f, 0.f};   // E3GNN_RMW_PF
     f32x4 a2k[4];   // E3GNN_KEEP_A2: layer-1 pre-activations of the tile, kept to its end
+    f32x4 a1k[E3GNN_KEEP_A2 >= 2 ? 4 : 1];   // (= 2: layer 0's as well)
     float bk[2];
     Op3 hq;
     // neighbour rows (lanes without an edge read row 0: harmless, their y
@@ -1616,6 +1628,10 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
       if constexpr (KA2) {
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) a2k[bb] = m.a2[bb];
+        if constexpr (E3GNN_KEEP_A2 >= 2) {
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb) a1k[bb] = m.a1[bb];
+        }
         bk[0] = b[0];
         bk[1] = b[1];
       }
@@ -1776,7 +1792,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
       }
       if constexpr (STAMPED) STAMP(5);
       mlp_bwd_chain(R, emb, q0, end, lane, dh2, demb, RPF ? de_old : nullptr, KA2 ? bk : nullptr,
-                    KA2 ? a2k : nullptr);
+                    KA2 ? a2k : nullptr, (KA2 && E3GNN_KEEP_A2 >= 2) ? a1k : nullptr);
     }
     if constexpr (STAMPED) STAMP(6);   // tile end: dE/dY sums, MLP chain backward
   }
