@@ -329,6 +329,20 @@ __device__ __forceinline__ void mlp_layer0(const WRes& R, const float (&b)[2], i
     a1[bh] = acc;
   }
 }
+// The backward kernels' MLP-chain products (the layer-1 recompute and the
+// chain backward's dH1 / dE/demb) on three bf16 products like dH2 and the w
+// recompute (E3GNN_CHAIN_X3, default; =0 six); the forward, whose chain gives
+// the energy, keeps six.  Same box: step 39.8 -> 39.2 ms (first / middle /
+// last backward 1.68 / 5.28 / 2.06 -> 1.56 / 5.20 / 1.92 ms); parity, full-size
+// and family tests green; NVE drift over 2,000 steps 1.67e-4 meV/atom/ps
+// against 1.38e-4 (six-product chains) and 1.19e-4 (exact-gradient generic
+// engine), excursions identical (profiles/r06_s18_*)
+#ifndef E3GNN_CHAIN_X3
+#define E3GNN_CHAIN_X3 1
+#endif
+constexpr bool CX3 = E3GNN_CHAIN_X3 != 0;
+// X3: layer 1 on three bf16 products
+template <bool X3 = false>
 __device__ __forceinline__ void mlp_chain(const WRes& R, const float (&b)[2], int lane, MlpT& m) {
   mlp_layer0(R, b, lane, m.a1);
   Op3 hq;
@@ -345,7 +359,7 @@ __device__ __forceinline__ void mlp_chain(const WRes& R, const float (&b)[2], in
     phase();
     Op3 wq;
     load_w2b(wq, R.w1b, lane, 16 * bo);
-    m.a2[bo] = w2_block<false>(hq, wq);
+    m.a2[bo] = X3 ? w2_block3<false>(hq, wq) : w2_block<false>(hq, wq);
   }
 }
 
@@ -821,7 +835,7 @@ __device__ __forceinline__ void mlp_bwd_chain_ids(const WRes& R, const float* __
     float b[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) b[s] = er >= 0 ? emb[(int64_t)er * 8 + 4 * s + g] : 0.f;
-    mlp_chain(R, b, lane, m);
+    mlp_chain<CX3>(R, b, lane, m);
   }
 
   // dH1^T = W1 dA2^T and demb^T = W0 dA1^T on bf16x6 (operands W1^T and W0^T
@@ -840,7 +854,7 @@ __device__ __forceinline__ void mlp_bwd_chain_ids(const WRes& R, const float* __
       phase();
       Op3 wq;
       load_w2b(wq, R.w1tb, lane, 16 * bi);
-      dh1[bi] = w2_block<false>(dq, wq);
+      dh1[bi] = CX3 ? w2_block3<false>(dq, wq) : w2_block<false>(dq, wq);
     }
   }
   f32x4 de;
@@ -853,7 +867,7 @@ __device__ __forceinline__ void mlp_bwd_chain_ids(const WRes& R, const float* __
     Op3 dq, wq;
     split_h2(da1, dq);
     load_w2b(wq, R.w0tb, lane, 0);
-    de = w2_block<false>(dq, wq);   // rows 4g + r < 8: the embedding dims
+    de = CX3 ? w2_block3<false>(dq, wq) : w2_block<false>(dq, wq);   // rows 4g + r < 8: the embedding dims
   }
   if (g < 2 && er >= 0) {
     if (dold) {   // (the caller read the old values at the tile start)
@@ -1094,7 +1108,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int k = 0; k < 2; ++k) b[k] = er[u] >= 0 ? emb[(int64_t)er[u] * 8 + 4 * k + g] : 0.f;
       MlpT m;
-      mlp_chain(R, b, lane, m);
+      mlp_chain<CX3>(R, b, lane, m);
       f32x4 h2[4];
 #pragma unroll
       for (int bb = 0; bb < 4; ++bb)
@@ -1624,7 +1638,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
         }
       }
       MlpT m;
-      mlp_chain(R, b, lane, m);
+      mlp_chain<CX3>(R, b, lane, m);
       if constexpr (KA2) {
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) a2k[bb] = m.a2[bb];

@@ -70,10 +70,11 @@ def main():
     ap.add_argument('--temp', type=float, default=600.0)
     ap.add_argument('--seeds', default='0')
     ap.add_argument('--variant', default=os.path.join(ROOT, 'sevennet_finetuning_amd', 'variants', 'six.so'))
+    ap.add_argument('--label', default='six_product', help='name of the variant leg')
     a = ap.parse_args()
     legs = [('shipped', None, EXE), ('generic_f32', {'E3GNN_GENERIC': '1'}, EXE)]
     if os.path.exists(a.variant):
-        legs.append(('six_product', None, variant_exe(a.variant)))
+        legs.append((a.label, None, variant_exe(a.variant)))
     for seed in [int(s) for s in a.seeds.split(',')]:
         for name, env, exe in legs:
             st = drift_stats(run(a.cells, a.steps, a.dt, a.temp, seed, env, exe), a.dt)
