@@ -3,7 +3,8 @@ over the C ABI) for the shipped fused kernels against reference force fields
 of the same model: the generic engine (E3GNN_GENERIC=1: independent f32
 kernels, plain f32 radial-MLP GEMMs, forces the exact gradient of its energy
 to f32 rounding) and, when present, an in-tree variant library built with the
-six-product backward (E3GNN_DH2_X3=0 E3GNN_BWD_W_X3=0).
+six-product backward (E3GNN_DH2_X3=0 E3GNN_BWD_W_X3=0
+E3GNN_CHAIN_X3=0).
 
     python tools/nve_drift.py [--cells 3] [--steps 2000] [--dt 1.0] [--temp 600]
                               [--variant sevennet_finetuning_amd/variants/six.so]
