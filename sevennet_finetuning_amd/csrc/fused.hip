@@ -66,6 +66,10 @@ __device__ __forceinline__ void phase() { __builtin_amdgcn_sched_barrier(0); }
 // Diagnostic build only (-DE3GNN_STAMPS, never the shipped library): per-wave
 // s_memtime totals of the middle backward's phases, written by lane 0 to a
 // buffer of their own (e3gnn_debug_stamps) that no other code reads.
+// E3GNN_STAMPS_FWD=1 (with E3GNN_STAMPS): the middle FORWARD's phases instead
+#ifndef E3GNN_STAMPS_FWD
+#define E3GNN_STAMPS_FWD 0
+#endif
 #ifdef E3GNN_STAMPS
 __device__ unsigned long long* g_stamp_buf = nullptr;
 #define STAMP_N 8
@@ -666,7 +670,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Fwd2Waves<L
   const WRes R = make_wres(W, L::W);
   const __amdgpu_buffer_rsrc_t Rh = rsrc_bytes(h, (int64_t)n_nodes * L::DX * 4);
   const float rden = 1.0f / denom;
+  constexpr bool STAMPED = std::is_same<L, LayerMid>::value && E3GNN_STAMPS_FWD;
+  STAMP_DECL
   for (int e0 = beg; e0 < end || e0 == beg; e0 += 32) {
+    if constexpr (STAMPED) STAMP(0);
     const bool first_tile = e0 == beg;
     const bool two = e0 + 16 < end;   // wave-uniform: the second tile has edges
     int src[2][4];
@@ -700,6 +707,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Fwd2Waves<L
         for (int r = 0; r < 4; ++r) h2[b][r] = act_fwd(m.a2[b][r]);
       split_h2(h2, hq[u]);
     }
+    if constexpr (STAMPED) STAMP(1);   // edge loads, MLP chain, H2 split
     sfor<3>([&](auto I) {
       constexpr int MUL = iblock_mul<L, I>();
       if constexpr (MUL > 0) {
@@ -721,6 +729,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Fwd2Waves<L
             if constexpr (p.l1 == I) {
               constexpr int D3 = 2 * p.l3 + 1;
               phase();
+              if constexpr (STAMPED) STAMP(4);   // (group start: row copies / loads)
               const f32x4 wv0 = w2_block<true>(hq[0], wq);
               const f32x4 wv1 = two ? w2_block<true>(hq[1], wq) : zero4();
               {  // operands of the next block load under this block's tensor product
@@ -728,12 +737,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Fwd2Waves<L
                 if (nc >= 0) load_w2b(wq, R.w2b, lane, nc);
               }
               phase();
+              if constexpr (STAMPED) STAMP(2);   // w MFMAs
               float acc[D3];
 #pragma unroll
               for (int k = 0; k < D3; ++k) acc[k] = -0.f;
               // the lane's 4 edges of each tile (padded edges have Y = 0)
               tp_acc4<p.l1, p.l2, p.l3>(x[0], lds[wid][0] + 4 * g * 9 + yoff(p.l2), 9, wv0, acc);
               if (two) tp_acc4<p.l1, p.l2, p.l3>(x[1], lds[wid][1] + 4 * g * 9 + yoff(p.l2), 9, wv1, acc);
+              if constexpr (STAMPED) STAMP(3);   // tensor product
 #pragma unroll
               for (int k = 0; k < D3; ++k) {
                 float v = acc[k];
@@ -743,6 +754,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Fwd2Waves<L
                   *a = first_tile ? v : *a + v;
                 }
               }
+              if constexpr (STAMPED) STAMP(5);   // row sums + LDS accumulation
             }
           });
         }
@@ -757,6 +769,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Fwd2Waves<L
     const float4* src = reinterpret_cast<const float4*>(acl);
     float4* dst = reinterpret_cast<float4*>(out);
     for (int t = lane; t < L::DM / 4; t += 64) dst[t] = src[t];
+  }
+  if constexpr (STAMPED) {
+    STAMP(6);   // copy-out
+    STAMP_FLUSH(c - c_begin);
   }
 }
 
@@ -1580,7 +1596,7 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
     __syncthreads();
 #endif
   };
-  constexpr bool STAMPED = std::is_same<L, LayerMid>::value;   // SevenNet-0's
+  constexpr bool STAMPED = std::is_same<L, LayerMid>::value && !E3GNN_STAMPS_FWD;   // SevenNet-0's
   STAMP_DECL
   if constexpr (DMA) issue_dma(0, 0);
   else issue(0);

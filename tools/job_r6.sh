@@ -52,6 +52,7 @@ for s in "$@"; do
     tbs_*) v=${s#tbs_}; run tbs_$v 300 env E3GNN_TRAIN_SIDE=$v python bench_train.py --steps 20 --warmup 3 --no-cpu-baseline ;;
     tbsprof_*) v=${s#tbsprof_}; run tbsprof_$v 300 env E3GNN_TRAIN_SIDE=$v rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${P}_tbsprof_$v -o run -- python bench_train.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     nvev_*) v=${s#nvev_}; run nvev_$v 900 python -u tools/nve_drift.py --cells 3 --steps 2000 --dt 1.0 --temp 600 --variant sevennet_finetuning_amd/variants/$v.so --label $v ;;
+    fstamps_*) v=${s#fstamps_}; run fstamps_$v 300 python tools/stamps.py sevennet_finetuning_amd/variants/$v.so 23 fwd ;;
     summ) summ ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

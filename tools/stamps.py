@@ -2,7 +2,7 @@
 DIAGNOSTIC build of the library (-DE3GNN_STAMPS: s_memtime stamps per phase,
 per wave, written to a buffer of their own; the shipped library has none).
 
-    python tools/stamps.py <variant.so> [cells]
+    python tools/stamps.py <variant.so> [cells] [fwd]
 
 Builds nothing: the variant is made beforehand on the CPU with
 ``build_lib.build(out=..., defines=['E3GNN_STAMPS'])``.  Prints, over all
@@ -22,11 +22,15 @@ sys.path.insert(0, ROOT)
 
 PHASES = ['tile start', 'setup+MLP chain', 'barriers+staging', 'w recompute', 'dH2',
           'TP (+dxc stores)', 'tile end', 'TOTAL']
+# a variant built with E3GNN_STAMPS_FWD=1 stamps the middle FORWARD instead
+PHASES_FWD = ['pass start', 'setup+MLP chain', 'w MFMAs', 'tensor product', 'path start (rows)',
+              'row sums + LDS acc', 'copy-out', 'TOTAL']
 
 
 def main():
     lib_path = os.path.abspath(sys.argv[1])
-    cells = int(sys.argv[2]) if len(sys.argv) > 2 else 23
+    cells = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 23
+    names = PHASES_FWD if 'fwd' in sys.argv[2:] else PHASES
     os.environ['E3GNN_LIB'] = lib_path
     import bench
     from sevennet_finetuning_amd import _lib
@@ -51,7 +55,7 @@ def main():
     print(f'waves {len(a)}, mean cycles/wave {a[:, 7].mean():.0f}, '
           f'max {a[:, 7].max():.0f}')
     for k in range(7):
-        print(f'  {PHASES[k]:18s} {a[:, k].sum() / tot:6.3f}   {a[:, k].mean():10.0f} cyc/wave')
+        print(f'  {names[k]:18s} {a[:, k].sum() / tot:6.3f}   {a[:, k].mean():10.0f} cyc/wave')
     print(f'  unaccounted        {1 - a[:, :7].sum() / tot:6.3f}')
     del _lib
 
