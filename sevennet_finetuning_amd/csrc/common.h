@@ -33,6 +33,61 @@ __device__ __forceinline__ float sum_rows4(float v) {
   return s + t;
 }
 
+// the same for N values at once (N <= 5): each stage's N swaps back to back
+// inside ONE asm statement, one hazard pad before and after the group instead
+// of around every swap, and the N reductions' adds free to interleave
+template <int N>
+__device__ __forceinline__ void permlane_swap_n32(float (&a)[N], float (&b)[N]);
+template <int N>
+__device__ __forceinline__ void permlane_swap_n16(float (&a)[N], float (&b)[N]);
+#define E3GNN_PL_SWAPS(W)                                                                             \
+  template <>                                                                                         \
+  __device__ __forceinline__ void permlane_swap_n##W<1>(float (&a)[1], float (&b)[1]) {               \
+    asm volatile("s_nop 1\n\tv_permlane" #W "_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a[0]), "+v"(b[0]));    \
+  }                                                                                                   \
+  template <>                                                                                         \
+  __device__ __forceinline__ void permlane_swap_n##W<2>(float (&a)[2], float (&b)[2]) {               \
+    asm volatile("s_nop 1\n\tv_permlane" #W "_swap_b32 %0, %1\n\tv_permlane" #W "_swap_b32 %2, %3\n\ts_nop 1" \
+                 : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]));                                   \
+  }                                                                                                   \
+  template <>                                                                                         \
+  __device__ __forceinline__ void permlane_swap_n##W<3>(float (&a)[3], float (&b)[3]) {               \
+    asm volatile("s_nop 1\n\tv_permlane" #W "_swap_b32 %0, %1\n\tv_permlane" #W "_swap_b32 %2, %3"     \
+                 "\n\tv_permlane" #W "_swap_b32 %4, %5\n\ts_nop 1"                                      \
+                 : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]));           \
+  }                                                                                                   \
+  template <>                                                                                         \
+  __device__ __forceinline__ void permlane_swap_n##W<4>(float (&a)[4], float (&b)[4]) {               \
+    asm volatile("s_nop 1\n\tv_permlane" #W "_swap_b32 %0, %1\n\tv_permlane" #W "_swap_b32 %2, %3"     \
+                 "\n\tv_permlane" #W "_swap_b32 %4, %5\n\tv_permlane" #W "_swap_b32 %6, %7\n\ts_nop 1"  \
+                 : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), \
+                   "+v"(b[3]));                                                                       \
+  }                                                                                                   \
+  template <>                                                                                         \
+  __device__ __forceinline__ void permlane_swap_n##W<5>(float (&a)[5], float (&b)[5]) {               \
+    asm volatile("s_nop 1\n\tv_permlane" #W "_swap_b32 %0, %1\n\tv_permlane" #W "_swap_b32 %2, %3"     \
+                 "\n\tv_permlane" #W "_swap_b32 %4, %5\n\tv_permlane" #W "_swap_b32 %6, %7"              \
+                 "\n\tv_permlane" #W "_swap_b32 %8, %9\n\ts_nop 1"                                      \
+                 : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), \
+                   "+v"(b[3]), "+v"(a[4]), "+v"(b[4]));                                               \
+  }
+E3GNN_PL_SWAPS(32)
+E3GNN_PL_SWAPS(16)
+#undef E3GNN_PL_SWAPS
+template <int N>
+__device__ __forceinline__ void sum_rows4_n(float (&v)[N]) {
+  static_assert(N >= 1 && N <= 5, "up to five values per group");
+  float a[N], b[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) a[i] = b[i] = v[i];
+  permlane_swap_n32<N>(a, b);
+#pragma unroll
+  for (int i = 0; i < N; ++i) a[i] = b[i] = a[i] + b[i];
+  permlane_swap_n16<N>(a, b);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = a[i] + b[i];
+}
+
 // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs
 // (b and b + 8 share one, MI355X_MICROARCH.md "Workgroup dispatch"), so
 // consecutive blocks land on different L2s.  This bijection gives each XCD a

@@ -649,6 +649,15 @@ __device__ __forceinline__ void load_tile_edges(const int* __restrict__ nbr,
 // 3 waves <= 168 registers, 2 <= 256; without the hint the compiler parks
 // MFMA accumulators in AGPRs and lands just above a boundary): the first
 // block (128 input channels) fits three, the others two
+// row sums over the four lane groups as groups of permlane swaps (the
+// forward's D3 values per path, the lock-step backward's 8 dE/dY values per
+// edge; E3GNN_ROWSUM_GROUPED, default) instead of one hazard-padded pair of
+// swaps per value: middle forward 9.21 -> 9.01-9.11 ms for the three launches,
+// same box (profiles/r06_s20_*); in the last block's backward it measured
+// neutral to slower and stays per value
+#ifndef E3GNN_ROWSUM_GROUPED
+#define E3GNN_ROWSUM_GROUPED 1
+#endif
 template <class L>
 struct Fwd2Waves {
   static constexpr int v = L::KIND == 0 ? 3 : 2;
@@ -745,10 +754,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Fwd2Waves<L
               tp_acc4<p.l1, p.l2, p.l3>(x[0], lds[wid][0] + 4 * g * 9 + yoff(p.l2), 9, wv0, acc);
               if (two) tp_acc4<p.l1, p.l2, p.l3>(x[1], lds[wid][1] + 4 * g * 9 + yoff(p.l2), 9, wv1, acc);
               if constexpr (STAMPED) STAMP(3);   // tensor product
+              if constexpr (E3GNN_ROWSUM_GROUPED) sum_rows4_n<D3>(acc);
 #pragma unroll
               for (int k = 0; k < D3; ++k) {
                 float v = acc[k];
-                v = sum_rows4(v) * rden;
+                v = (E3GNN_ROWSUM_GROUPED ? v : sum_rows4(v)) * rden;
                 if (g == 0) {
                   float* a = acl + p.moff + (16 * j + col) * D3 + k;
                   *a = first_tile ? v : *a + v;
@@ -1799,8 +1809,19 @@ __global__ __launch_bounds__(64 * BwdWpg<L>::v) __attribute__((amdgpu_waves_per_
     if (act) {
       // dE/dY of edge c: sum over the 4 lane groups, then dE/du through the SH
       // polynomials (serial_code.py:50-70)
+      if constexpr (E3GNN_ROWSUM_GROUPED) {   // (the same grouped sums)
+        float d4a[4] = {dYa[1], dYa[2], dYa[3], dYa[4]}, d4b[4] = {dYa[5], dYa[6], dYa[7], dYa[8]};
+        sum_rows4_n<4>(d4a);
+        sum_rows4_n<4>(d4b);
 #pragma unroll
-      for (int q = 1; q < 9; ++q) dYa[q] = sum_rows4(dYa[q]);
+        for (int q = 0; q < 4; ++q) {
+          dYa[1 + q] = d4a[q];
+          dYa[5 + q] = d4b[q];
+        }
+      } else {
+#pragma unroll
+        for (int q = 1; q < 9; ++q) dYa[q] = sum_rows4(dYa[q]);
+      }
       if (g == 0 && er >= 0) {
         const float s3 = 1.7320508075688772f, s5 = 2.23606797749979f, c15 = s3 * s5;
         const float is3 = 0.57735026918962576f;  // 1 / sqrt(3)
