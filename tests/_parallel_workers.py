@@ -26,8 +26,11 @@ def worker(rank, world, port, name, engine, out, model_dir=None, tile=None):
     ``model_dir``: another deployment (HIP engine; its species list), ``tile``:
     replicate the system's cell (nx, ny, nz) first."""
     import torch
-    if engine == 'cpu':  # the ranks share the host's cores (no oversubscription)
-        torch.set_num_threads(max(1, (os.cpu_count() or 1) // world))
+    if engine == 'cpu':
+        # one thread per rank: the repeated-evaluation check compares bits, and
+        # a multi-threaded CPU BLAS may split its sums differently from call to
+        # call when the ranks compete for the host's cores (seen once, 4 ranks)
+        torch.set_num_threads(1)
     dist = _init(rank, world, port)
     from _systems import load_manifest_symbols, system
     from sevennet_finetuning_amd.parallel import (ParallelE3GNN, brick_grid, build_rank_graph,
