@@ -377,6 +377,38 @@ __device__ __forceinline__ void mlp_pre(const WRes& R, const float* __restrict__
   mlp_chain(R, b, lane, m);
 }
 
+// both tiles of a forward pass (E3GNN_FWD_CHAIN2): layer 1's W1 operand
+// blocks loaded once for the two tiles' products (the same six products per
+// tile as mlp_chain, the same sums)
+__device__ __forceinline__ void mlp_pre2(const WRes& R, const float* __restrict__ emb, int e0, int e1,
+                                         bool two, int lane, f32x4 (&a2)[2][4]) {
+  const int g = lane >> 4, c = lane & 15;
+  Op3 hq[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = e0 + 16 * u + c;
+    float b[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) b[s] = (e < e1 && (u == 0 || two)) ? emb[(int64_t)e * 8 + 4 * s + g] : 0.f;
+    f32x4 a1[4];
+    mlp_layer0(R, b, lane, a1);
+    f32x4 h1[4];
+#pragma unroll
+    for (int bh = 0; bh < 4; ++bh)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h1[bh][r] = act_fwd(a1[bh][r]);
+    split_h2(h1, hq[u]);
+  }
+#pragma unroll
+  for (int bo = 0; bo < 4; ++bo) {
+    phase();
+    Op3 wq;
+    load_w2b(wq, R.w1b, lane, 16 * bo);
+    a2[0][bo] = w2_block<false>(hq[0], wq);
+    a2[1][bo] = two ? w2_block<false>(hq[1], wq) : zero4();
+  }
+}
+
 // ---------------------------------------------------------------- TP pieces
 // CG entries grouped by (i, j): each pair's partial sum over k is formed and
 // consumed at once (short live ranges, one product per pair)
@@ -658,6 +690,13 @@ __device__ __forceinline__ void load_tile_edges(const int* __restrict__ nbr,
 #ifndef E3GNN_ROWSUM_GROUPED
 #define E3GNN_ROWSUM_GROUPED 1
 #endif
+// the forward pass's two tiles through the radial MLP together, each W1
+// operand block loaded once for both (E3GNN_FWD_CHAIN2; same products, same
+// bits): last-block forward 1.05-1.06 -> 1.00-1.01 ms, middle 9.13 -> 9.02 ms
+// averaged over two runs each (noisy box; profiles/r06_s23_*)
+#ifndef E3GNN_FWD_CHAIN2
+#define E3GNN_FWD_CHAIN2 1
+#endif
 template <class L>
 struct Fwd2Waves {
   static constexpr int v = L::KIND == 0 ? 3 : 2;
@@ -704,17 +743,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Fwd2Waves<L
     auto load_group = [&](auto Iq, int jq) { load_rows(Iq, jq, 0, xpf); };
     load_group(std::integral_constant<int, first_I<L>()>{}, 0);
     Op3 hq[2];
+    if constexpr (E3GNN_FWD_CHAIN2 && L::KIND != 0) {   // (the first block: three waves, no room)
+      f32x4 a2[2][4];
+      mlp_pre2(R, emb, e0, end, two, lane, a2);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (u == 1 && !two) break;
-      MlpT m;
-      mlp_pre(R, emb, e0 + 16 * u, end, lane, m);
-      f32x4 h2[4];
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+        f32x4 h2[4];
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < 4; ++b)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h2[b][r] = act_fwd(m.a2[b][r]);
-      split_h2(h2, hq[u]);
+          for (int r = 0; r < 4; ++r) h2[b][r] = act_fwd(a2[u][b][r]);
+        split_h2(h2, hq[u]);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+        MlpT m;
+        mlp_pre(R, emb, e0 + 16 * u, end, lane, m);
+        f32x4 h2[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h2[b][r] = act_fwd(m.a2[b][r]);
+        split_h2(h2, hq[u]);
+      }
     }
     if constexpr (STAMPED) STAMP(1);   // edge loads, MLP chain, H2 split
     sfor<3>([&](auto I) {
